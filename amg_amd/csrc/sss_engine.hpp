@@ -1,0 +1,101 @@
+// sss_engine.hpp — internal declarations of the gfx950 engine (not part of any public ABI).
+//
+// Layout in HBM (DESIGN.md §Data layout): every level keeps the reference's CSR arrays
+// (int32 row_ptr / col_idx, fp64 val) for A, P and R, plus b, x, wp (fp64, length n_l) and
+// the C/F marker.  Index arrays are int32 exactly as in SSS_main.h:95-105; all arithmetic is
+// fp64 without contraction (-ffp-contract=off) so the parity kernels reproduce the host
+// reference bit for bit.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <vector>
+
+#include "../../include/sss_hip.h"
+
+namespace sss {
+
+constexpr int kBlock = 256;        // threads per workgroup for streaming kernels (4 waves)
+constexpr int kTileEntries = 2048; // CSR entries staged in LDS per SpMV row block (24 KiB)
+constexpr int kMaxLevels = max_AMG_LVL;
+
+int hip_fail(hipError_t e, const char *what, const char *file, int line);
+#define SSS_HIP(call)                                                                    \
+    do {                                                                                 \
+        hipError_t e_ = (call);                                                          \
+        if (e_ != hipSuccess) return ::sss::hip_fail(e_, #call, __FILE__, __LINE__);    \
+    } while (0)
+
+template <class T>
+inline T *dev_alloc(size_t count)
+{
+    void *p = nullptr;
+    if (count == 0) count = 1;
+    if (hipMalloc(&p, count * sizeof(T)) != hipSuccess) return nullptr;
+    return static_cast<T *>(p);
+}
+inline void dev_free(void *p)
+{
+    if (p) (void)hipFree(p);
+}
+
+// CSR matrix resident in HBM, plus its CSR-adaptive row blocking for SpMV.
+struct DevCSR {
+    int n = 0, ncols = 0, nnz = 0;
+    int *rp = nullptr, *ci = nullptr;
+    double *v = nullptr;
+    int nblk = 0;          // SpMV row blocks
+    int *blk = nullptr;    // block -> first row (nblk + 1 entries)
+};
+int devcsr_upload(DevCSR &d, const SSS_MAT &h);
+void devcsr_free(DevCSR &d);
+int build_row_blocks(const int *h_rp, int n, std::vector<int> &blk);
+
+// y <- op(A x) on `stream` (see SSS_HIP_SPMV_*).  `partial` (optional, RESID only): one
+// sum-of-squares of the written y per row block, for a deterministic fused norm.
+int launch_spmv(const DevCSR &A, int op, double alpha, const double *x, const double *b, double *y,
+                int cap, double *partial, hipStream_t stream);
+
+// ---- smoother schedules -------------------------------------------------------------------
+struct PassSchedule {          // rows of one class (F or C), grouped by DAG depth
+    int depth = 0;
+    std::vector<int> h_off;    // depth + 1 offsets into rows
+    int *rows = nullptr;       // device
+    int nrows = 0;
+    int max_width = 0;
+};
+struct SmootherPlan {
+    int kind = SSS_HIP_SMOOTH_EXACT;
+    PassSchedule pass[2];      // [0] = F pass (mark != 1), [1] = C pass (mark == 1)
+    double *d_first = nullptr; // effective divisor for the first sweep of a call
+    double *d_later = nullptr; // ... for later sweeps (aliases d_first when all rows have a diagonal)
+    int *cls = nullptr;        // per row: 1 if mark == 1 else 0
+    bool long_rows = false;    // wave-per-row kernels
+    double *x_tmp = nullptr;   // Jacobi ping-pong buffer
+};
+int smoother_build(SmootherPlan &sp, const SSS_MAT &A, const int *mark, int kind);
+void smoother_free(SmootherPlan &sp);
+int smoother_run(const SmootherPlan &sp, const DevCSR &A, const double *b, double *x, int sweeps,
+                 hipStream_t stream);
+
+// ---- reductions ----------------------------------------------------------------------------
+// Deterministic sum of `n` partials -> *out (device); optionally sqrt.
+int launch_final_sum(const double *partials, int n, double *out, bool take_sqrt, hipStream_t s);
+
+// ---- coarse solvers ------------------------------------------------------------------------
+struct CoarseDirect {
+    int n = 0;
+    double *inv = nullptr;     // row-major explicit inverse
+};
+int coarse_direct_build(CoarseDirect &cd, const SSS_MAT &A, hipStream_t stream);
+void coarse_direct_free(CoarseDirect &cd);
+int coarse_direct_apply(const CoarseDirect &cd, const double *b, double *x, hipStream_t stream);
+
+struct CoarseKrylov;           // reference CG(beta==1)+GMRES(30) on device
+CoarseKrylov *coarse_krylov_create(const DevCSR &A, int row_cap, hipStream_t stream);
+void coarse_krylov_destroy(CoarseKrylov *k);
+int coarse_krylov_solve(CoarseKrylov *k, const DevCSR &A, const double *b, double *x, double ctol,
+                        hipStream_t stream);
+
+}  // namespace sss

@@ -1,0 +1,407 @@
+// sss_hier.hip — HBM mirror of an SSS_AMG hierarchy and the device V-cycle.
+//
+// The V/W-cycle control flow of SSS_amg_cycle (Solve/SSS_cycle.cu:848-967) is static given
+// cycle_type, so the host walks it and enqueues kernels on one stream without synchronising:
+//   descent  : smoother_pre(l); wp_l = b_l - A_l x_l (one fused kernel, SSS_cycle.cu:916-917);
+//              b_{l+1} = R_l wp_l (:921); x_{l+1} = 0 (:929)
+//   coarsest : SSS_amg_coarest_solve (:933) -> Krylov (parity) or explicit inverse (direct)
+//   ascent   : x_l += P_l x_{l+1} (:942); smoother_post(l) (:958)
+// The outer residual r = b - A0 x and ||r|| (Solve/SSS_SOLVE.c:59-64) are one fused kernel
+// writing per-block sums of squares plus a one-block deterministic reduction; the 8-byte
+// norm is the only per-iteration device->host transfer.
+#include "sss_engine.hpp"
+
+#include <cstdlib>
+#include <cstring>
+#include <string>
+
+using namespace sss;
+
+struct sss_hip_hier {
+    int nl = 0;
+    SSS_AMG_PARS pars{};
+    sss_hip_opts opts{};
+    hipStream_t stream = nullptr;
+    struct Level {
+        DevCSR A, P, R;
+        double *b = nullptr, *x = nullptr, *wp = nullptr;
+        SmootherPlan sm;
+    } L[kMaxLevels];
+    int coarse_mode = SSS_HIP_COARSE_DIRECT;
+    CoarseDirect direct;
+    CoarseKrylov *krylov = nullptr;
+    double *partial = nullptr;   // per-row-block partial sums for the level-0 norm
+    double *d_norm = nullptr;
+    double *h_norm = nullptr;    // pinned
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    int owns_device = 0;
+};
+
+static int env_int(const char *name, int dflt)
+{
+    const char *s = getenv(name);
+    return (s && *s) ? atoi(s) : dflt;
+}
+
+extern "C" void sss_hip_opts_default(sss_hip_opts *o)
+{
+    std::memset(o, 0, sizeof(*o));
+    o->device = env_int("SSS_HIP_DEVICE", -1);
+    o->smoother = SSS_HIP_SMOOTH_EXACT;
+    o->coarse = SSS_HIP_COARSE_KRYLOV;
+    o->row_cap = env_int("SSS_HIP_ROWCAP", 0);
+    o->use_graph = env_int("SSS_HIP_GRAPH", 0);
+    o->verbose = env_int("SSS_HIP_VERBOSE", 0);
+    if (const char *s = getenv("SSS_HIP_SMOOTHER")) {
+        std::string v(s);
+        if (v == "hybrid") o->smoother = SSS_HIP_SMOOTH_HYBRID;
+        else if (v == "jacobi") o->smoother = SSS_HIP_SMOOTH_JACOBI;
+    }
+    if (const char *s = getenv("SSS_HIP_COARSE")) {
+        std::string v(s);
+        if (v == "direct") o->coarse = SSS_HIP_COARSE_DIRECT;
+    }
+}
+
+extern "C" int sss_hip_device_count(void)
+{
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+}
+
+static int level_smoother_kind(const sss_hip_opts &o, int l)
+{
+    if (o.smoother == SSS_HIP_SMOOTH_JACOBI) return SSS_HIP_SMOOTH_JACOBI;
+    if (o.smoother == SSS_HIP_SMOOTH_HYBRID && l > 0) return SSS_HIP_SMOOTH_JACOBI;
+    return SSS_HIP_SMOOTH_EXACT;
+}
+
+static void hier_release(sss_hip_hier *h)
+{
+    if (!h) return;
+    if (h->stream) (void)hipStreamSynchronize(h->stream);
+    for (int l = 0; l < h->nl; ++l) {
+        auto &L = h->L[l];
+        devcsr_free(L.A);
+        devcsr_free(L.P);
+        devcsr_free(L.R);
+        dev_free(L.b);
+        dev_free(L.x);
+        dev_free(L.wp);
+        smoother_free(L.sm);
+    }
+    coarse_direct_free(h->direct);
+    coarse_krylov_destroy(h->krylov);
+    dev_free(h->partial);
+    dev_free(h->d_norm);
+    if (h->h_norm) (void)hipHostFree(h->h_norm);
+    if (h->ev0) (void)hipEventDestroy(h->ev0);
+    if (h->ev1) (void)hipEventDestroy(h->ev1);
+    if (h->stream) (void)hipStreamDestroy(h->stream);
+    delete h;
+}
+
+extern "C" sss_hip_hier *sss_hip_hier_create(const SSS_AMG *mg, const sss_hip_opts *o)
+{
+    if (sss_hip_device_count() <= 0) {
+        fprintf(stderr, "### ERROR: no HIP device available for the AMG solve phase\n");
+        return nullptr;
+    }
+    auto *h = new sss_hip_hier();
+    h->nl = mg->num_levels;
+    h->pars = mg->pars;
+    if (o) h->opts = *o;
+    else sss_hip_opts_default(&h->opts);
+    if (h->opts.device >= 0 && hipSetDevice(h->opts.device) != hipSuccess) { delete h; return nullptr; }
+    auto fail = [&](const char *what) {
+        fprintf(stderr, "### ERROR: sss_hip_hier_create: %s\n", what);
+        hier_release(h);
+        return (sss_hip_hier *)nullptr;
+    };
+    if (hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess) return fail("stream");
+    if (hipEventCreate(&h->ev0) != hipSuccess || hipEventCreate(&h->ev1) != hipSuccess) return fail("events");
+
+    for (int l = 0; l < h->nl; ++l) {
+        const SSS_AMG_COMP &C = mg->cg[l];
+        auto &L = h->L[l];
+        const int n = C.A.num_rows;
+        if (devcsr_upload(L.A, C.A)) return fail("upload A");
+        if (l < h->nl - 1) {
+            if (devcsr_upload(L.P, C.P) || devcsr_upload(L.R, C.R)) return fail("upload P/R");
+            if (smoother_build(L.sm, C.A, C.cfmark.d, level_smoother_kind(h->opts, l))) return fail("smoother plan");
+        }
+        L.b = dev_alloc<double>((size_t)n);
+        L.x = dev_alloc<double>((size_t)n);
+        L.wp = dev_alloc<double>((size_t)n);
+        if (!L.b || !L.x || !L.wp) return fail("vectors");
+        if (hipMemset(L.b, 0, sizeof(double) * n) != hipSuccess || hipMemset(L.x, 0, sizeof(double) * n) != hipSuccess ||
+            hipMemset(L.wp, 0, sizeof(double) * n) != hipSuccess)
+            return fail("memset");
+    }
+    h->partial = dev_alloc<double>((size_t)h->L[0].A.nblk);
+    h->d_norm = dev_alloc<double>(1);
+    if (!h->partial || !h->d_norm || hipHostMalloc((void **)&h->h_norm, sizeof(double)) != hipSuccess)
+        return fail("norm buffers");
+
+    const SSS_MAT &Ac = mg->cg[h->nl - 1].A;
+    h->coarse_mode = h->opts.coarse;
+    if (h->coarse_mode == SSS_HIP_COARSE_DIRECT && Ac.num_rows > 20000) h->coarse_mode = SSS_HIP_COARSE_KRYLOV;
+    if (h->coarse_mode == SSS_HIP_COARSE_DIRECT) {
+        if (coarse_direct_build(h->direct, Ac, h->stream)) return fail("coarse inverse");
+    } else {
+        h->krylov = coarse_krylov_create(h->L[h->nl - 1].A, h->opts.row_cap, h->stream);
+        if (!h->krylov) return fail("coarse Krylov workspace");
+    }
+    if (hipStreamSynchronize(h->stream) != hipSuccess) return fail("sync");
+    if (h->opts.verbose) {
+        for (int l = 0; l < h->nl; ++l)
+            fprintf(stderr, "[sss_hip] level %d: n=%d nnz=%d blocks=%d dagF=%d dagC=%d kind=%d\n", l, h->L[l].A.n,
+                    h->L[l].A.nnz, h->L[l].A.nblk, h->L[l].sm.pass[0].depth, h->L[l].sm.pass[1].depth,
+                    h->L[l].sm.kind);
+    }
+    return h;
+}
+
+extern "C" void sss_hip_hier_destroy(sss_hip_hier *h) { hier_release(h); }
+
+static double *level_vec(sss_hip_hier *h, int level, int which)
+{
+    if (!h || level < 0 || level >= h->nl) return nullptr;
+    auto &L = h->L[level];
+    return which == SSS_HIP_VEC_B ? L.b : which == SSS_HIP_VEC_X ? L.x : which == SSS_HIP_VEC_WP ? L.wp : nullptr;
+}
+
+extern "C" int sss_hip_upload_vec(sss_hip_hier *h, int level, int which, const double *src, int n)
+{
+    double *d = level_vec(h, level, which);
+    if (!d || n > h->L[level].A.n) return ERROR_INPUT_PAR;
+    SSS_HIP(hipMemcpyAsync(d, src, sizeof(double) * (size_t)n, hipMemcpyHostToDevice, h->stream));
+    SSS_HIP(hipStreamSynchronize(h->stream));
+    return 0;
+}
+
+extern "C" int sss_hip_download_vec(sss_hip_hier *h, int level, int which, double *dst, int n)
+{
+    double *d = level_vec(h, level, which);
+    if (!d || n > h->L[level].A.n) return ERROR_INPUT_PAR;
+    SSS_HIP(hipMemcpyAsync(dst, d, sizeof(double) * (size_t)n, hipMemcpyDeviceToHost, h->stream));
+    SSS_HIP(hipStreamSynchronize(h->stream));
+    return 0;
+}
+
+static int coarse_tol(const sss_hip_hier *h, double *tol)
+{
+    *tol = h->pars.ctol;
+    if (*tol > h->pars.tol) *tol = h->pars.tol * 0.1;
+    return 0;
+}
+
+extern "C" int sss_hip_coarse_solve(sss_hip_hier *h)
+{
+    auto &C = h->L[h->nl - 1];
+    double tol;
+    coarse_tol(h, &tol);
+    if (h->coarse_mode == SSS_HIP_COARSE_DIRECT) return coarse_direct_apply(h->direct, C.b, C.x, h->stream);
+    return coarse_krylov_solve(h->krylov, C.A, C.b, C.x, tol, h->stream);
+}
+
+extern "C" int sss_hip_smooth(sss_hip_hier *h, int level, int post)
+{
+    auto &L = h->L[level];
+    const int sweeps = post ? h->pars.post_iter : h->pars.pre_iter;
+    return smoother_run(L.sm, L.A, L.b, L.x, sweeps, h->stream);
+}
+
+extern "C" int sss_hip_cycle(sss_hip_hier *h)
+{
+    const int nl = h->nl;
+    int cycle_type = h->pars.cycle_type <= 0 ? 1 : h->pars.cycle_type;
+    int visits[kMaxLevels] = {0};
+    int l = 0, rc;
+    hipStream_t s = h->stream;
+    for (;;) {
+        while (l < nl - 1) {
+            auto &L = h->L[l];
+            visits[l]++;
+            if ((rc = sss_hip_smooth(h, l, 0))) return rc;
+            if ((rc = launch_spmv(L.A, SSS_HIP_SPMV_RESID, -1.0, L.x, L.b, L.wp, 0, nullptr, s))) return rc;
+            if ((rc = launch_spmv(L.R, SSS_HIP_SPMV_MXY, 1.0, L.wp, nullptr, h->L[l + 1].b, 0, nullptr, s))) return rc;
+            l++;
+            SSS_HIP(hipMemsetAsync(h->L[l].x, 0, sizeof(double) * (size_t)h->L[l].A.n, s));
+        }
+        if ((rc = sss_hip_coarse_solve(h))) return rc;
+        while (l > 0) {
+            l--;
+            auto &L = h->L[l];
+            if ((rc = launch_spmv(L.P, SSS_HIP_SPMV_AMXPY, 1.0, h->L[l + 1].x, nullptr, L.x, 0, nullptr, s))) return rc;
+            if ((rc = sss_hip_smooth(h, l, 1))) return rc;
+            if (visits[l] < cycle_type) break;
+            visits[l] = 0;
+        }
+        if (l <= 0) break;
+    }
+    return 0;
+}
+
+static int enqueue_residual_norm(sss_hip_hier *h)
+{
+    auto &L = h->L[0];
+    int rc = launch_spmv(L.A, SSS_HIP_SPMV_RESID, -1.0, L.x, L.b, L.wp, 0, h->partial, h->stream);
+    if (rc) return rc;
+    return launch_final_sum(h->partial, L.A.nblk, h->d_norm, true, h->stream);
+}
+
+extern "C" int sss_hip_residual_norm(sss_hip_hier *h, double *absres)
+{
+    int rc = enqueue_residual_norm(h);
+    if (rc) return rc;
+    SSS_HIP(hipMemcpyAsync(h->h_norm, h->d_norm, sizeof(double), hipMemcpyDeviceToHost, h->stream));
+    SSS_HIP(hipStreamSynchronize(h->stream));
+    *absres = *h->h_norm;
+    return 0;
+}
+
+extern "C" int sss_hip_sync(sss_hip_hier *h)
+{
+    SSS_HIP(hipStreamSynchronize(h->stream));
+    return 0;
+}
+
+extern "C" int sss_hip_num_levels(sss_hip_hier *h) { return h ? h->nl : 0; }
+
+extern "C" int sss_hip_level_info_get(sss_hip_hier *h, int level, sss_hip_level_info *out)
+{
+    if (!h || level < 0 || level >= h->nl) return ERROR_INPUT_PAR;
+    auto &L = h->L[level];
+    out->rows = L.A.n;
+    out->nnz = L.A.nnz;
+    out->nnz_p = L.P.nnz;
+    out->dag_f = L.sm.pass[0].depth;
+    out->dag_c = L.sm.pass[1].depth;
+    out->smoother_kind = L.sm.kind;
+    return 0;
+}
+
+extern "C" int sss_hip_time_level0_spmv(sss_hip_hier *h, int reps, double *avg_ms)
+{
+    auto &L = h->L[0];
+    SSS_HIP(hipStreamSynchronize(h->stream));
+    SSS_HIP(hipEventRecord(h->ev0, h->stream));
+    for (int r = 0; r < reps; ++r) {
+        int rc = launch_spmv(L.A, SSS_HIP_SPMV_RESID, -1.0, L.x, L.b, L.wp, 0, nullptr, h->stream);
+        if (rc) return rc;
+    }
+    SSS_HIP(hipEventRecord(h->ev1, h->stream));
+    SSS_HIP(hipEventSynchronize(h->ev1));
+    float ms = 0.f;
+    SSS_HIP(hipEventElapsedTime(&ms, h->ev0, h->ev1));
+    *avg_ms = (double)ms / reps;
+    return 0;
+}
+
+extern "C" int sss_hip_time_iterations(sss_hip_hier *h, int reps, double *avg_ms, double *absres)
+{
+    SSS_HIP(hipStreamSynchronize(h->stream));
+    SSS_HIP(hipEventRecord(h->ev0, h->stream));
+    for (int r = 0; r < reps; ++r) {
+        int rc = sss_hip_cycle(h);
+        if (!rc) rc = sss_hip_residual_norm(h, absres);
+        if (rc) return rc;
+    }
+    SSS_HIP(hipEventRecord(h->ev1, h->stream));
+    SSS_HIP(hipEventSynchronize(h->ev1));
+    float ms = 0.f;
+    SSS_HIP(hipEventElapsedTime(&ms, h->ev0, h->ev1));
+    *avg_ms = (double)ms / reps;
+    return 0;
+}
+
+// ---- host-memory convenience wrappers for the exported reference entry points ----------------
+namespace {
+struct HostCSR {
+    DevCSR d;
+    ~HostCSR() { devcsr_free(d); }
+};
+}  // namespace
+
+extern "C" int sss_hip_host_spmv(int op, double alpha, const SSS_MAT *A, const double *x, const double *b,
+                                 double *y, int cap)
+{
+    if (sss_hip_device_count() <= 0) return ERROR_MISC;
+    HostCSR M;
+    if (devcsr_upload(M.d, *A)) return ERROR_MISC;
+    const size_t ny = (size_t)A->num_rows, nx = (size_t)A->num_cols;
+    double *dx = dev_alloc<double>(nx), *dy = dev_alloc<double>(ny), *db = dev_alloc<double>(ny);
+    int rc = 0;
+    if (!dx || !dy || !db) rc = ERROR_ALLOC_MEM;
+    if (!rc && hipMemcpy(dx, x, sizeof(double) * nx, hipMemcpyHostToDevice) != hipSuccess) rc = ERROR_MISC;
+    if (!rc && hipMemcpy(dy, y, sizeof(double) * ny, hipMemcpyHostToDevice) != hipSuccess) rc = ERROR_MISC;
+    if (!rc && b && hipMemcpy(db, b, sizeof(double) * ny, hipMemcpyHostToDevice) != hipSuccess) rc = ERROR_MISC;
+    if (!rc) rc = launch_spmv(M.d, op, alpha, dx, db, dy, cap, nullptr, nullptr);
+    if (!rc && hipMemcpy(y, dy, sizeof(double) * ny, hipMemcpyDeviceToHost) != hipSuccess) rc = ERROR_MISC;
+    dev_free(dx);
+    dev_free(dy);
+    dev_free(db);
+    return rc;
+}
+
+extern "C" int sss_hip_host_smooth(const SSS_SMTR *s, int post)
+{
+    if (sss_hip_device_count() <= 0) return ERROR_MISC;
+    const int n = s->A->num_rows;
+    const int use_cf = s->cf_order && s->ordering;
+    if (!use_cf && s->smoother == SSS_SM_GS) {
+        fprintf(stderr, "### ERROR: natural-order Gauss-Seidel (cf_order = 0) is not offered by the GPU engine\n");
+        return ERROR_INPUT_PAR;
+    }
+    HostCSR M;
+    SmootherPlan sp;
+    if (devcsr_upload(M.d, *s->A)) return ERROR_MISC;
+    if (smoother_build(sp, *s->A, use_cf ? s->ordering : nullptr,
+                       s->smoother == SSS_SM_JACOBI ? SSS_HIP_SMOOTH_JACOBI : SSS_HIP_SMOOTH_EXACT)) {
+        smoother_free(sp);
+        return ERROR_MISC;
+    }
+    (void)post;
+    double *dx = dev_alloc<double>((size_t)n), *db = dev_alloc<double>((size_t)n);
+    int rc = (!dx || !db) ? ERROR_ALLOC_MEM : 0;
+    if (!rc && hipMemcpy(dx, s->x->d, sizeof(double) * n, hipMemcpyHostToDevice) != hipSuccess) rc = ERROR_MISC;
+    if (!rc && hipMemcpy(db, s->b->d, sizeof(double) * n, hipMemcpyHostToDevice) != hipSuccess) rc = ERROR_MISC;
+    if (!rc) rc = smoother_run(sp, M.d, db, dx, s->nsweeps, nullptr);
+    if (!rc && hipMemcpy(s->x->d, dx, sizeof(double) * n, hipMemcpyDeviceToHost) != hipSuccess) rc = ERROR_MISC;
+    dev_free(dx);
+    dev_free(db);
+    smoother_free(sp);
+    return rc;
+}
+
+extern "C" int sss_hip_host_coarse_solve(SSS_MAT *A, SSS_VEC *b, SSS_VEC *x, double ctol, int coarse_mode,
+                                         int row_cap)
+{
+    if (sss_hip_device_count() <= 0) return ERROR_MISC;
+    const int n = A->num_rows;
+    HostCSR M;
+    if (devcsr_upload(M.d, *A)) return ERROR_MISC;
+    double *dx = dev_alloc<double>((size_t)n), *db = dev_alloc<double>((size_t)n);
+    int rc = (!dx || !db) ? ERROR_ALLOC_MEM : 0;
+    if (!rc && hipMemcpy(dx, x->d, sizeof(double) * n, hipMemcpyHostToDevice) != hipSuccess) rc = ERROR_MISC;
+    if (!rc && hipMemcpy(db, b->d, sizeof(double) * n, hipMemcpyHostToDevice) != hipSuccess) rc = ERROR_MISC;
+    if (!rc) {
+        if (coarse_mode == SSS_HIP_COARSE_DIRECT && n <= 20000) {
+            CoarseDirect cd;
+            rc = coarse_direct_build(cd, *A, nullptr);
+            if (!rc) rc = coarse_direct_apply(cd, db, dx, nullptr);
+            if (!rc && hipDeviceSynchronize() != hipSuccess) rc = ERROR_MISC;
+            coarse_direct_free(cd);
+        } else {
+            CoarseKrylov *k = coarse_krylov_create(M.d, row_cap, nullptr);
+            rc = k ? coarse_krylov_solve(k, M.d, db, dx, ctol, nullptr) : ERROR_ALLOC_MEM;
+            coarse_krylov_destroy(k);
+        }
+    }
+    if (!rc && hipMemcpy(x->d, dx, sizeof(double) * n, hipMemcpyDeviceToHost) != hipSuccess) rc = ERROR_MISC;
+    dev_free(dx);
+    dev_free(db);
+    return rc;
+}

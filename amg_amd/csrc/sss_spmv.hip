@@ -1,0 +1,195 @@
+// sss_spmv.hip — CSR SpMV family for every level (gfx950, wave64, fp64, no contraction).
+//
+// Replaces SSS_blas_mv_amxpy / SSS_blas_mv_mxy (SSS_utils.c:161-201) and the coarse-grid
+// spmv_kernel / alpha_spmv_kernel (Solve/SSS_cuda.cu:77-118, which launch <<<64,64>>> and
+// re-upload the whole CSR per call).  Here the CSR lives in HBM for the whole solve.
+//
+// Kernel: CSR-adaptive.  At upload each matrix is cut into row blocks of <= 256 rows holding
+// <= kTileEntries nonzeros.  A workgroup stages its block's val/col slice into LDS with
+// coalesced loads (the slice is contiguous in CSR), then each thread walks ONE row from LDS
+// and accumulates in stored CSR order starting from 0.0 — the reference's exact summation
+// order, so results are bitwise identical to the host reference.  A row longer than the
+// tile forms a block on its own: the workgroup computes the products a_k*x_{c_k} in parallel
+// (identically rounded), stages them in LDS and one lane adds them in order (bitwise again).
+//
+// Roofline: HBM-bound, 12 B/nnz (fp64 value + int32 column) + 4 B/row (row_ptr) + 8 B/row
+// per vector stream (x compulsory, y, b); no MFMA (≈0.13 flop/byte).
+#include "sss_engine.hpp"
+#include "sss_spmv_dev.hpp"
+
+#include <algorithm>
+
+namespace sss {
+
+int hip_fail(hipError_t e, const char *what, const char *file, int line)
+{
+    fprintf(stderr, "### ERROR: HIP call %s failed at %s:%d: %s\n", what, file, line, hipGetErrorString(e));
+    return ERROR_MISC;
+}
+
+int build_row_blocks(const int *h_rp, int n, std::vector<int> &blk)
+{
+    blk.clear();
+    int r = 0;
+    while (r < n) {
+        blk.push_back(r);
+        const int base = h_rp[r];
+        int e = r + 1;
+        if (h_rp[e] - base <= kTileEntries) {
+            while (e < n && e - r < kBlock && h_rp[e + 1] - base <= kTileEntries) ++e;
+        }
+        r = e;
+    }
+    blk.push_back(n);
+    return (int)blk.size() - 1;
+}
+
+int devcsr_upload(DevCSR &d, const SSS_MAT &h)
+{
+    d.n = h.num_rows;
+    d.ncols = h.num_cols;
+    d.nnz = h.num_nnzs;
+    d.rp = dev_alloc<int>((size_t)d.n + 1);
+    d.ci = dev_alloc<int>((size_t)d.nnz);
+    d.v = dev_alloc<double>((size_t)d.nnz);
+    if (!d.rp || !d.ci || !d.v) return hip_fail(hipErrorOutOfMemory, "hipMalloc(CSR)", __FILE__, __LINE__);
+    SSS_HIP(hipMemcpy(d.rp, h.row_ptr, sizeof(int) * ((size_t)d.n + 1), hipMemcpyHostToDevice));
+    if (d.nnz > 0) {
+        SSS_HIP(hipMemcpy(d.ci, h.col_idx, sizeof(int) * (size_t)d.nnz, hipMemcpyHostToDevice));
+        SSS_HIP(hipMemcpy(d.v, h.val, sizeof(double) * (size_t)d.nnz, hipMemcpyHostToDevice));
+    }
+    std::vector<int> blk;
+    d.nblk = build_row_blocks(h.row_ptr, d.n, blk);
+    d.blk = dev_alloc<int>(blk.size());
+    if (!d.blk) return hip_fail(hipErrorOutOfMemory, "hipMalloc(blk)", __FILE__, __LINE__);
+    SSS_HIP(hipMemcpy(d.blk, blk.data(), sizeof(int) * blk.size(), hipMemcpyHostToDevice));
+    return 0;
+}
+
+void devcsr_free(DevCSR &d)
+{
+    dev_free(d.rp);
+    dev_free(d.ci);
+    dev_free(d.v);
+    dev_free(d.blk);
+    d = DevCSR();
+}
+
+// ---- kernel -------------------------------------------------------------------------------
+template <int OP, bool NORM>
+__global__ __launch_bounds__(kBlock) void spmv_adaptive(const int *__restrict__ blk, const int *__restrict__ rp,
+                                                        const int *__restrict__ ci, const double *__restrict__ v,
+                                                        const double *__restrict__ x, const double *__restrict__ b,
+                                                        double *__restrict__ y, double alpha, int cap,
+                                                        double *__restrict__ partial)
+{
+    __shared__ SpmvSmem sm;
+    const double sq = csr_block_rows(blk, rp, ci, v, x, sm, [&](int r, double s) -> double {
+        double out;
+        if constexpr (OP == SSS_HIP_SPMV_MXY) out = s;
+        else if constexpr (OP == SSS_HIP_SPMV_AMXPY) out = y[r] + s * alpha;
+        else if constexpr (OP == SSS_HIP_SPMV_RESID) out = b[r] + s * alpha;
+        else {
+            if (cap > 0 && r >= cap) return 0.0;   // as-shipped <<<64,64>>> row cap
+            out = y[r] + s;
+        }
+        y[r] = out;
+        return NORM ? out * out : 0.0;
+    });
+    if (NORM) {
+        const double t = block_sum(sq, sm.red);
+        if (threadIdx.x == 0) partial[blockIdx.x] = t;
+    }
+}
+
+template <int OP, bool NORM>
+static void launch_op(const DevCSR &A, double alpha, const double *x, const double *b, double *y, int cap,
+                      double *partial, hipStream_t s)
+{
+    hipLaunchKernelGGL((spmv_adaptive<OP, NORM>), dim3(A.nblk), dim3(kBlock), 0, s, A.blk, A.rp, A.ci, A.v, x, b,
+                       y, alpha, cap, partial);
+}
+
+int launch_spmv(const DevCSR &A, int op, double alpha, const double *x, const double *b, double *y, int cap,
+                double *partial, hipStream_t stream)
+{
+    if (A.n == 0 || A.nblk == 0) return 0;
+    switch (op) {
+    case SSS_HIP_SPMV_MXY: launch_op<SSS_HIP_SPMV_MXY, false>(A, alpha, x, b, y, cap, nullptr, stream); break;
+    case SSS_HIP_SPMV_AMXPY: launch_op<SSS_HIP_SPMV_AMXPY, false>(A, alpha, x, b, y, cap, nullptr, stream); break;
+    case SSS_HIP_SPMV_RESID:
+        if (partial) launch_op<SSS_HIP_SPMV_RESID, true>(A, alpha, x, b, y, cap, partial, stream);
+        else launch_op<SSS_HIP_SPMV_RESID, false>(A, alpha, x, b, y, cap, nullptr, stream);
+        break;
+    case SSS_HIP_SPMV_ACC: launch_op<SSS_HIP_SPMV_ACC, false>(A, alpha, x, b, y, cap, nullptr, stream); break;
+    default: return ERROR_INPUT_PAR;
+    }
+    SSS_HIP(hipGetLastError());
+    return 0;
+}
+
+// ---- deterministic final reduction ----------------------------------------------------------
+__global__ __launch_bounds__(1024) void final_sum_kernel(const double *__restrict__ partials, int n,
+                                                         double *__restrict__ out, int take_sqrt)
+{
+    __shared__ double red[1024 / 64];
+    double v = 0.0;
+    for (int i = threadIdx.x; i < n; i += 1024) v += partials[i];
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        double t = 0.0;
+        for (int w = 0; w < 1024 / 64; ++w) t += red[w];
+        *out = take_sqrt ? sqrt(t) : t;
+    }
+}
+
+int launch_final_sum(const double *partials, int n, double *out, bool take_sqrt, hipStream_t s)
+{
+    hipLaunchKernelGGL(final_sum_kernel, dim3(1), dim3(1024), 0, s, partials, n, out, take_sqrt ? 1 : 0);
+    SSS_HIP(hipGetLastError());
+    return 0;
+}
+
+}  // namespace sss
+
+// ---- C ABI: plans over caller-owned device CSR ----------------------------------------------
+struct sss_hip_spmv_plan {
+    sss::DevCSR csr;   // rp/ci/v borrowed from the caller (not owned); blk owned
+};
+
+extern "C" sss_hip_spmv_plan *sss_hip_spmv_plan_create(int n, int nnz, const int *d_rp, const int *h_rp)
+{
+    auto *p = new sss_hip_spmv_plan();
+    std::vector<int> blk;
+    p->csr.n = n;
+    p->csr.nnz = nnz;
+    p->csr.rp = const_cast<int *>(d_rp);
+    p->csr.nblk = sss::build_row_blocks(h_rp, n, blk);
+    p->csr.blk = sss::dev_alloc<int>(blk.size());
+    if (!p->csr.blk || hipMemcpy(p->csr.blk, blk.data(), sizeof(int) * blk.size(), hipMemcpyHostToDevice) != hipSuccess) {
+        sss::dev_free(p->csr.blk);
+        delete p;
+        return nullptr;
+    }
+    return p;
+}
+
+extern "C" void sss_hip_spmv_plan_destroy(sss_hip_spmv_plan *p)
+{
+    if (!p) return;
+    sss::dev_free(p->csr.blk);
+    delete p;
+}
+
+extern "C" int sss_hip_spmv(const sss_hip_spmv_plan *p, int op, double alpha, const int *d_rp, const int *d_ci,
+                            const double *d_v, const double *d_x, const double *d_b, double *d_y, int cap,
+                            void *stream)
+{
+    sss::DevCSR A = p->csr;
+    A.rp = const_cast<int *>(d_rp);
+    A.ci = const_cast<int *>(d_ci);
+    A.v = const_cast<double *>(d_v);
+    return sss::launch_spmv(A, op, alpha, d_x, d_b, d_y, cap, nullptr, (hipStream_t)stream);
+}

@@ -1,0 +1,723 @@
+/*
+ * sss_setup.c — AMG setup phase (host C).  Out of the GPU hot-path scope (SURVEY.md §2 rows
+ * 10-12), but it builds the hierarchy the hot path consumes, so it reproduces the reference's
+ * setup semantics exactly ("uncapped" reference):
+ *
+ *   strong couplings ............ Setup/SSS_coarsen.c:106-181
+ *   weak-coupling compression ... Setup/SSS_coarsen.c:185-212
+ *   classical RS C/F split ...... Setup/SSS_coarsen.c:294-498 (bucketed measure lists)
+ *   F-F cleanup ................. Setup/SSS_coarsen.c:501-574
+ *   direct P pattern ............ Setup/SSS_coarsen.c:577-630
+ *   direct interpolation ........ Setup/SSS_inter.cu:400-547 (the host twin interp_DIR)
+ *   truncation .................. Setup/SSS_inter.cu:16-102
+ *   Galerkin RAP ................ SSS_matvec.c:398-534
+ *   level loop .................. Setup/SSS_SETUP.cu:36-178
+ *
+ * The measure lists are kept as an array of buckets indexed by measure instead of the
+ * reference's heap-allocated sorted list of list nodes; the element-level linked lists
+ * (lists/where) and the order of every insert/remove are the same, so the head of the
+ * maximal bucket — the next C point — is the same.  RAP runs the reference's row-by-row
+ * marker algorithm independently per coarse row (OpenMP), which yields identical rows
+ * (diagonal first, then discovery order; identical summation order).
+ */
+#include "sss_internal.h"
+
+#include <math.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <sys/time.h>
+#ifdef _OPENMP
+#include <omp.h>
+#endif
+
+/* ======================================================================================
+ * Strength of connection
+ * ====================================================================================== */
+static void strong_couplings(const SSS_MAT *A, SSS_IMAT *S, const SSS_AMG_PARS *pars)
+{
+    const int n = A->num_rows;
+    const double theta = pars->strong_threshold;
+    const double row_sum_bound = 2.0 - pars->max_row_sum;
+    const int *ia = A->row_ptr, *ja = A->col_idx;
+    const double *a = A->val;
+
+    S->num_rows = n;
+    S->num_cols = A->num_cols;
+    S->num_nnzs = A->num_nnzs;
+    S->val = NULL;
+    S->row_ptr = (int *)SSS_calloc((size_t)n + 1, sizeof(int));
+    S->col_idx = (int *)SSS_calloc((size_t)A->num_nnzs, sizeof(int));
+    memcpy(S->row_ptr, ia, ((size_t)n + 1) * sizeof(int));
+    memcpy(S->col_idx, ja, (size_t)A->num_nnzs * sizeof(int));
+
+#pragma omp parallel for schedule(static)
+    for (int i = 0; i < n; ++i) {
+        double abs_sum = 0.0, max_off = 0.0, dii = 0.0;
+        int have_diag = 0;
+        for (int k = ia[i]; k < ia[i + 1]; ++k) {
+            double m = SSS_ABS(a[k]);
+            abs_sum += m;
+            if (ja[k] != i) max_off = SSS_max(max_off, m);
+            else if (!have_diag) { dii = a[k]; have_diag = 1; }
+        }
+        max_off *= theta;
+        for (int k = ia[i]; k < ia[i + 1]; ++k)     /* first diagonal entry is never strong */
+            if (ja[k] == i) { S->col_idx[k] = -1; break; }
+        if (abs_sum < row_sum_bound * SSS_ABS(dii)) {
+            for (int k = ia[i]; k < ia[i + 1]; ++k) S->col_idx[k] = -1;
+        } else {
+            for (int k = ia[i]; k < ia[i + 1]; ++k)
+                if (-a[k] <= max_off) S->col_idx[k] = -1;
+        }
+    }
+}
+
+/* Drops entries marked -1; returns -99 when nothing strong is left (reference's ERROR_UNKNOWN). */
+static int drop_weak(SSS_IMAT *S)
+{
+    int out = 0;
+    for (int i = 0; i < S->num_rows; ++i) {
+        int lo = S->row_ptr[i], hi = S->row_ptr[i + 1];
+        S->row_ptr[i] = out;
+        for (int k = lo; k < hi; ++k)
+            if (S->col_idx[k] > -1) S->col_idx[out++] = S->col_idx[k];
+    }
+    S->row_ptr[S->num_rows] = out;
+    S->num_nnzs = out;
+    return out > 0 ? 0 : -99;
+}
+
+/* ======================================================================================
+ * Measure buckets.  bucket_first/last[m] play the role of the reference list node with
+ * data == m (node->head / node->tail); next/prev are the reference's lists/where arrays.
+ * ====================================================================================== */
+typedef struct {
+    int *first, *last;   /* per measure; first == LIST_TAIL marks an absent bucket */
+    int cap;             /* allocated measures */
+    int top;             /* upper bound on the largest non-empty measure */
+    int *next, *prev;    /* per point: successor / predecessor inside its bucket */
+} measure_buckets;
+
+static void buckets_grow(measure_buckets *B, int m)
+{
+    int old = B->cap, cap = B->cap;
+    while (cap <= m) cap = cap * 2 + 16;
+    B->first = (int *)realloc(B->first, sizeof(int) * (size_t)cap);
+    B->last = (int *)realloc(B->last, sizeof(int) * (size_t)cap);
+    for (int k = old; k < cap; ++k) B->first[k] = B->last[k] = LIST_TAIL;
+    B->cap = cap;
+}
+
+static void bucket_insert(measure_buckets *B, int m, int pt)
+{
+    if (m >= B->cap) buckets_grow(B, m);
+    if (B->first[m] == LIST_TAIL) {               /* new bucket: point is alone */
+        B->first[m] = B->last[m] = pt;
+        B->next[pt] = LIST_TAIL;
+        B->prev[pt] = LIST_HEAD;
+    } else {                                      /* append at the bucket tail */
+        int t = B->last[m];
+        B->next[t] = pt;
+        B->prev[pt] = t;
+        B->next[pt] = LIST_TAIL;
+        B->last[m] = pt;
+    }
+    if (m > B->top) B->top = m;
+}
+
+static void bucket_remove(measure_buckets *B, int m, int pt)
+{
+    if (m < 0 || m >= B->cap || B->first[m] == LIST_TAIL) {
+        printf("### ERROR: This list is empty! %s : %d\n", __FILE__, __LINE__);
+        return;
+    }
+    if (B->first[m] == pt && B->last[m] == pt) {
+        B->first[m] = B->last[m] = LIST_TAIL;
+    } else if (B->first[m] == pt) {
+        B->first[m] = B->next[pt];
+        B->prev[B->next[pt]] = LIST_HEAD;
+    } else if (B->last[m] == pt) {
+        B->last[m] = B->prev[pt];
+        B->next[B->prev[pt]] = LIST_TAIL;
+    } else {
+        B->next[B->prev[pt]] = B->next[pt];
+        B->prev[B->next[pt]] = B->prev[pt];
+    }
+}
+
+/* Head point of the largest non-empty bucket, or -1 if every bucket is empty. */
+static int bucket_max_head(measure_buckets *B)
+{
+    while (B->top > 0 && B->first[B->top] == LIST_TAIL) B->top--;
+    return (B->top > 0 && B->first[B->top] != LIST_TAIL) ? B->first[B->top] : -1;
+}
+
+/* Classical Ruge-Stueben first pass + C1 fix-up.  Returns the C-point count (or <0). */
+static int rs_split(const SSS_MAT *A, SSS_IMAT *S, SSS_IVEC *vertices)
+{
+    const int n = A->num_rows;
+    int *mark = vertices->d;
+    int ncoarse, undecided = 0;
+    int *lambda, *owner;
+    SSS_IMAT ST;
+    measure_buckets B;
+
+    ncoarse = drop_weak(S);
+    if (ncoarse < 0) return ncoarse;
+    ST = SSS_imat_trans(S);
+
+    memset(&B, 0, sizeof(B));
+    B.next = (int *)SSS_calloc((size_t)n, sizeof(int));
+    B.prev = (int *)SSS_calloc((size_t)n, sizeof(int));
+    lambda = (int *)SSS_calloc((size_t)n, sizeof(int));
+    buckets_grow(&B, 64);
+
+    for (int i = 0; i < n; ++i) lambda[i] = ST.row_ptr[i + 1] - ST.row_ptr[i];
+    for (int i = 0; i < n; ++i) {
+        if (S->row_ptr[i + 1] == S->row_ptr[i]) {
+            mark[i] = ISPT;
+            lambda[i] = 0;
+        } else {
+            mark[i] = UNPT;
+            undecided++;
+        }
+    }
+
+    /* Initial lists; points with no influence become F immediately. */
+    for (int i = 0; i < n; ++i) {
+        if (mark[i] == ISPT) continue;
+        if (lambda[i] > 0) {
+            bucket_insert(&B, lambda[i], i);
+            continue;
+        }
+        if (lambda[i] < 0) printf("### WARNING: Negative lambda[%d]!\n", i);
+        mark[i] = FGPT;
+        undecided--;
+        for (int k = S->row_ptr[i]; k < S->row_ptr[i + 1]; ++k) {
+            int j = S->col_idx[k];
+            if (mark[j] == ISPT) continue;
+            if (j < i) {
+                if (lambda[j] > 0) bucket_remove(&B, lambda[j], j);
+                lambda[j]++;
+                bucket_insert(&B, lambda[j], j);
+            } else {
+                lambda[j]++;
+            }
+        }
+    }
+
+    while (undecided > 0) {
+        int c = bucket_max_head(&B);
+        int mc;
+        if (c < 0) {
+            printf("### ERROR: RS coarsening ran out of candidates (%d undecided)\n", undecided);
+            break;
+        }
+        mc = lambda[c];
+        if (mc == 0) printf("### WARNING: Head of the list has measure 0!\n");
+        mark[c] = CGPT;
+        lambda[c] = 0;
+        undecided--;
+        bucket_remove(&B, mc, c);
+        ncoarse++;
+
+        /* points that c strongly influences become F */
+        for (int q = ST.row_ptr[c]; q < ST.row_ptr[c + 1]; ++q) {
+            int j = ST.col_idx[q];
+            if (mark[j] != UNPT) continue;
+            mark[j] = FGPT;
+            bucket_remove(&B, lambda[j], j);
+            undecided--;
+            for (int r = S->row_ptr[j]; r < S->row_ptr[j + 1]; ++r) {
+                int k = S->col_idx[r];
+                if (mark[k] != UNPT) continue;
+                bucket_remove(&B, lambda[k], k);
+                lambda[k]++;
+                bucket_insert(&B, lambda[k], k);
+            }
+        }
+        /* points that strongly influence c lose one unit of measure */
+        for (int q = S->row_ptr[c]; q < S->row_ptr[c + 1]; ++q) {
+            int j = S->col_idx[q], m;
+            if (mark[j] != UNPT) continue;
+            m = lambda[j];
+            bucket_remove(&B, m, j);
+            lambda[j] = --m;
+            if (m > 0) {
+                bucket_insert(&B, m, j);
+                continue;
+            }
+            mark[j] = FGPT;
+            undecided--;
+            for (int r = S->row_ptr[j]; r < S->row_ptr[j + 1]; ++r) {
+                int k = S->col_idx[r];
+                if (mark[k] != UNPT) continue;
+                bucket_remove(&B, lambda[k], k);
+                lambda[k]++;
+                bucket_insert(&B, lambda[k], k);
+            }
+        }
+    }
+
+    /* C1 criterion: two strongly coupled F points must share a strong C point. */
+    owner = lambda;
+    for (int i = 0; i < n; ++i) owner[i] = -1;
+    for (int i = 0; i < n; ++i) {
+        int promoted = -1, have_promoted = 0;
+        if (mark[i] != FGPT) continue;
+        for (int q = S->row_ptr[i]; q < S->row_ptr[i + 1]; ++q)
+            if (mark[S->col_idx[q]] == CGPT) owner[S->col_idx[q]] = i;
+        for (int q = S->row_ptr[i]; q < S->row_ptr[i + 1]; ++q) {
+            int j = S->col_idx[q], shares = 0;
+            if (mark[j] != FGPT) continue;
+            for (int r = S->row_ptr[j]; r < S->row_ptr[j + 1]; ++r)
+                if (owner[S->col_idx[r]] == i) { shares = 1; break; }
+            if (shares) continue;
+            if (!have_promoted) {
+                mark[j] = CGPT;
+                ncoarse++;
+                owner[j] = i;
+                promoted = j;
+                have_promoted = 1;
+            } else {
+                mark[i] = CGPT;
+                mark[promoted] = FGPT;
+                break;
+            }
+        }
+    }
+
+    SSS_imat_destroy(&ST);
+    free(B.first);
+    free(B.last);
+    free(B.next);
+    free(B.prev);
+    free(lambda);
+    return ncoarse;
+}
+
+/* Setup/SSS_coarsen.c:501-574.  Note: the tentative-C state (pending, pending_owner,
+ * tentative) deliberately persists across rows exactly as in the reference. */
+static int cleanup_ff(const SSS_IMAT *S, SSS_IVEC *vertices, int n, int ncoarse)
+{
+    int *mark = vertices->d;
+    int *tag = (int *)SSS_calloc((size_t)n, sizeof(int));
+    int pending = FALSE, pending_owner = -1, tentative = -1;
+
+    for (int i = 0; i < n; ++i) tag[i] = -1;
+    for (int i = 0; i < n; ++i) {
+        if (mark[i] != FGPT) continue;
+        for (int q = S->row_ptr[i]; q < S->row_ptr[i + 1]; ++q) {
+            int j = S->col_idx[q];
+            tag[j] = (mark[j] == CGPT) ? i : -1;
+        }
+        if (pending_owner != i) tentative = -1;
+        for (int q = S->row_ptr[i]; q < S->row_ptr[i + 1]; ++q) {
+            int j = S->col_idx[q], linked = 0;
+            if (mark[j] != FGPT) continue;
+            for (int r = S->row_ptr[j]; r < S->row_ptr[j + 1]; ++r)
+                if (tag[S->col_idx[r]] == i) { linked = 1; break; }
+            if (linked) continue;
+            if (pending) {
+                mark[i] = CGPT;
+                ncoarse++;
+                if (tentative > -1) {
+                    mark[tentative] = FGPT;
+                    ncoarse--;
+                    tentative = -1;
+                }
+                pending = FALSE;
+            } else {
+                mark[j] = CGPT;
+                ncoarse++;
+                tentative = j;
+                pending_owner = i;
+                pending = TRUE;
+                i--;                    /* revisit i with j as a C point */
+            }
+            break;
+        }
+    }
+    free(tag);
+    return ncoarse;
+}
+
+/* Setup/SSS_coarsen.c:577-630: F rows take their strong C neighbours, C rows themselves. */
+static void direct_pattern(SSS_MAT *P, const SSS_IMAT *S, const SSS_IVEC *vertices, int n, int ncoarse)
+{
+    const int *mark = vertices->d;
+    int pos = 0;
+    P->num_rows = n;
+    P->num_cols = ncoarse;
+    P->row_ptr = (int *)SSS_calloc((size_t)n + 1, sizeof(int));
+    for (int i = 0; i < n; ++i) {
+        int cnt = 0;
+        if (mark[i] == FGPT) {
+            for (int q = S->row_ptr[i]; q < S->row_ptr[i + 1]; ++q)
+                if (mark[S->col_idx[q]] == CGPT) cnt++;
+        } else if (mark[i] == CGPT) {
+            cnt = 1;
+        }
+        P->row_ptr[i + 1] = P->row_ptr[i] + cnt;
+    }
+    P->num_nnzs = P->row_ptr[n] - P->row_ptr[0];
+    P->col_idx = (int *)SSS_calloc((size_t)P->num_nnzs, sizeof(int));
+    P->val = (double *)SSS_calloc((size_t)P->num_nnzs, sizeof(double));
+    for (int i = 0; i < n; ++i) {
+        if (mark[i] == FGPT) {
+            for (int q = S->row_ptr[i]; q < S->row_ptr[i + 1]; ++q)
+                if (mark[S->col_idx[q]] == CGPT) P->col_idx[pos++] = S->col_idx[q];
+        } else if (mark[i] == CGPT) {
+            P->col_idx[pos++] = i;
+        }
+    }
+}
+
+int SSS_amg_coarsen(SSS_MAT *A, SSS_IVEC *vertices, SSS_MAT *P, SSS_IMAT *S, SSS_AMG_PARS *pars)
+{
+    int ncoarse = 0;
+    strong_couplings(A, S, pars);
+    if (pars->cs_type == SSS_COARSE_RS) ncoarse = rs_split(A, S, vertices);
+    else if (pars->cs_type != SSS_COARSE_RSP) SSS_exit_on_errcode(ERROR_AMG_COARSE_TYPE, __func__);
+    if (ncoarse <= 0) return ERROR_UNKNOWN;
+    if (pars->interp_type == intERP_DIR) {
+        ncoarse = cleanup_ff(S, vertices, A->num_rows, ncoarse);
+        direct_pattern(P, S, vertices, A->num_rows, ncoarse);
+    } else {
+        /* Standard interpolation (form_P_pattern_std / interp_STD) is not part of this
+         * engine: the reference's default and every BASELINE config use direct. */
+        SSS_exit_on_errcode(ERROR_AMG_interp_type, __func__);
+    }
+    return 0;
+}
+
+/* ======================================================================================
+ * Interpolation and truncation
+ * ====================================================================================== */
+void SSS_amg_interp_trunc(SSS_MAT *P, SSS_AMG_PARS *pars)
+{
+    const double eps = pars->trunc_threshold;
+    int kept = 0, wcol = 0, wval = 0;
+    for (int i = 0; i < P->num_rows; ++i) {
+        const int lo = P->row_ptr[i], hi = P->row_ptr[i + 1];
+        double pos_max = 0, neg_min = 0, pos_sum = 0, neg_sum = 0, pos_kept = 0, neg_kept = 0;
+        double pos_fac, neg_fac;
+        P->row_ptr[i] = kept;
+        for (int k = lo; k < hi; ++k) {
+            double v = P->val[k];
+            if (v > 0) { pos_sum += v; pos_max = SSS_max(pos_max, v); }
+            else if (v < 0) { neg_sum += v; neg_min = SSS_MIN(neg_min, v); }
+        }
+        pos_max *= eps;
+        neg_min *= eps;
+        for (int k = lo; k < hi; ++k) {
+            double v = P->val[k];
+            if (v >= pos_max) { kept++; P->col_idx[wcol++] = P->col_idx[k]; pos_kept += v; }
+            else if (v <= neg_min) { kept++; P->col_idx[wcol++] = P->col_idx[k]; neg_kept += v; }
+        }
+        pos_fac = pos_kept > SMALLFLOAT ? pos_sum / pos_kept : 1.0;
+        neg_fac = neg_kept < -SMALLFLOAT ? neg_sum / neg_kept : 1.0;
+        for (int k = lo; k < hi; ++k) {
+            double v = P->val[k];
+            if (v >= pos_max) P->val[wval++] = v * pos_fac;
+            else if (v <= neg_min) P->val[wval++] = v * neg_fac;
+        }
+    }
+    P->num_nnzs = P->row_ptr[P->num_rows] = kept;
+    P->col_idx = (int *)SSS_realloc(P->col_idx, (size_t)kept * sizeof(int));
+    P->val = (double *)SSS_realloc(P->val, (size_t)kept * sizeof(double));
+}
+
+/*
+ * Setup/SSS_inter.cu:400-547.  `aii` is carried from row to row exactly as the host twin
+ * does (a row without a diagonal entry reuses the previous row's value, including the
+ * apN correction) — resolved up front so the weight computation can run row-parallel.
+ */
+void interp_DIR(SSS_MAT *A, SSS_IVEC *vertices, SSS_MAT *P, SSS_AMG_PARS *pars)
+{
+    const int n = A->num_rows;
+    const int *mark = vertices->d;
+    const int *ia = A->row_ptr, *ja = A->col_idx;
+    const double *a = A->val;
+    double *aii_row = (double *)malloc(sizeof(double) * (size_t)(n > 0 ? n : 1));
+    int *diag_pos = (int *)malloc(sizeof(int) * (size_t)(n > 0 ? n : 1));
+    int *cmap;
+    double t0 = SSS_get_time(), carried = 0.0;
+    int ncoarse = 0;
+
+    /* pass 1: diagonal positions; apN corrections are needed only where the chain matters */
+#pragma omp parallel for schedule(static)
+    for (int i = 0; i < n; ++i) {
+        int d = ia[i + 1];
+        for (int k = ia[i]; k < ia[i + 1]; ++k)
+            if (ja[k] == i) { d = k; break; }
+        diag_pos[i] = d;
+    }
+    /* pass 2 (serial, cheap): resolve the carried aii */
+    for (int i = 0; i < n; ++i) {
+        double aii = diag_pos[i] < ia[i + 1] ? a[diag_pos[i]] : carried;
+        if (mark[i] == FGPT) {
+            double apN = 0.0;
+            int npos = 0;
+            for (int k = ia[i]; k < ia[i + 1]; ++k) {
+                if (k == diag_pos[i] || !(a[k] > 0)) continue;
+                apN += a[k];
+                for (int q = P->row_ptr[i]; q < P->row_ptr[i + 1]; ++q)
+                    if (P->col_idx[q] == ja[k]) { npos++; break; }
+            }
+            if (npos == 0) aii += apN;
+        }
+        aii_row[i] = aii;
+        carried = aii;
+    }
+    /* pass 3: weights, row-parallel */
+#pragma omp parallel for schedule(dynamic, 4096)
+    for (int i = 0; i < n; ++i) {
+        const double aii = aii_row[i];
+        if (mark[i] == FGPT) {
+            double amN = 0.0, amP = 0.0, apN = 0.0, apP = 0.0, alpha, beta;
+            int npos = 0;
+            for (int k = ia[i]; k < ia[i + 1]; ++k) {
+                int strong = FALSE;
+                if (k == diag_pos[i]) continue;
+                for (int q = P->row_ptr[i]; q < P->row_ptr[i + 1]; ++q)
+                    if (P->col_idx[q] == ja[k]) { strong = TRUE; break; }
+                if (a[k] > 0) {
+                    apN += a[k];
+                    if (strong) { apP += a[k]; npos++; }
+                } else {
+                    amN += a[k];
+                    if (strong) amP += a[k];
+                }
+            }
+            alpha = amN / amP;
+            beta = npos > 0 ? apN / apP : 0.0;
+            for (int q = P->row_ptr[i]; q < P->row_ptr[i + 1]; ++q) {
+                int k = ia[i];
+                while (k < ia[i + 1] && ja[k] != P->col_idx[q]) ++k;
+                P->val[q] = a[k] > 0 ? -beta * a[k] / aii : -alpha * a[k] / aii;
+            }
+        } else if (mark[i] == CGPT) {
+            P->val[P->row_ptr[i]] = 1.0;
+        }
+    }
+    printf("-------------cpu_step1_time = %f ms -------------------\n", (SSS_get_time() - t0) * 1000.0);
+
+    /* coarse renumbering */
+    cmap = (int *)SSS_calloc((size_t)n, sizeof(int));
+    for (int i = 0; i < n; ++i)
+        if (mark[i] == CGPT) cmap[i] = ncoarse++;
+    P->num_cols = ncoarse;
+#pragma omp parallel for schedule(static)
+    for (int q = 0; q < P->num_nnzs; ++q) P->col_idx[q] = cmap[P->col_idx[q]];
+    free(cmap);
+    free(aii_row);
+    free(diag_pos);
+    SSS_amg_interp_trunc(P, pars);
+}
+
+void SSS_amg_interp(SSS_MAT *A, SSS_IVEC *vertices, SSS_MAT *P, SSS_IMAT *S, SSS_AMG_PARS *pars)
+{
+    (void)S;
+    if (pars->interp_type == intERP_DIR) interp_DIR(A, vertices, P, pars);
+    else SSS_exit_on_errcode(ERROR_AMG_interp_type, __func__);
+}
+
+/* ======================================================================================
+ * Galerkin product A_c = R A P (SSS_matvec.c:398-534), row-parallel.
+ * ====================================================================================== */
+SSS_MAT SSS_blas_mat_rap(const SSS_MAT *R, const SSS_MAT *A, const SSS_MAT *P)
+{
+    const int nc = R->num_rows, nf = A->num_rows;
+    const int *ri = R->row_ptr, *rj = R->col_idx, *ai = A->row_ptr, *aj = A->col_idx;
+    const int *pi = P->row_ptr, *pj = P->col_idx;
+    const double *rv = R->val, *av = A->val, *pv = P->val;
+    int64_t *start = (int64_t *)calloc((size_t)nc + 1, sizeof(int64_t));
+    SSS_MAT C;
+
+    C.num_rows = nc;
+    C.num_cols = nc;
+    C.row_ptr = (int *)SSS_calloc((size_t)nc + 1, sizeof(int));
+
+#pragma omp parallel
+    {
+        int *seen_f = (int *)malloc(sizeof(int) * (size_t)(nf > 0 ? nf : 1));
+        int *seen_c = (int *)malloc(sizeof(int) * (size_t)(nc > 0 ? nc : 1));
+        for (int i = 0; i < nf; ++i) seen_f[i] = -1;
+        for (int i = 0; i < nc; ++i) seen_c[i] = -1;
+#pragma omp for schedule(dynamic, 256)
+        for (int ic = 0; ic < nc; ++ic) {
+            int64_t cnt = 1;
+            seen_c[ic] = ic;
+            for (int q1 = ri[ic]; q1 < ri[ic + 1]; ++q1) {
+                int i1 = rj[q1];
+                for (int q2 = ai[i1]; q2 < ai[i1 + 1]; ++q2) {
+                    int i2 = aj[q2];
+                    if (seen_f[i2] == ic) continue;
+                    seen_f[i2] = ic;
+                    for (int q3 = pi[i2]; q3 < pi[i2 + 1]; ++q3)
+                        if (seen_c[pj[q3]] != ic) { seen_c[pj[q3]] = ic; cnt++; }
+                }
+            }
+            start[ic + 1] = cnt;
+        }
+        free(seen_f);
+        free(seen_c);
+    }
+    for (int ic = 0; ic < nc; ++ic) start[ic + 1] += start[ic];
+    if (start[nc] > INT32_MAX) {
+        printf("### ERROR: RAP product has %lld nonzeros (int32 index limit)\n", (long long)start[nc]);
+        SSS_exit_on_errcode(ERROR_MAT_SIZE, __func__);
+    }
+    C.num_nnzs = (int)start[nc];
+    for (int ic = 0; ic <= nc; ++ic) C.row_ptr[ic] = (int)start[ic];
+    C.col_idx = (int *)SSS_calloc((size_t)C.num_nnzs, sizeof(int));
+    C.val = (double *)SSS_calloc((size_t)C.num_nnzs, sizeof(double));
+
+#pragma omp parallel
+    {
+        int *seen_f = (int *)malloc(sizeof(int) * (size_t)(nf > 0 ? nf : 1));
+        int *seen_c = (int *)malloc(sizeof(int) * (size_t)(nc > 0 ? nc : 1));
+        int *slot = (int *)malloc(sizeof(int) * (size_t)(nc > 0 ? nc : 1));
+        for (int i = 0; i < nf; ++i) seen_f[i] = -1;
+        for (int i = 0; i < nc; ++i) seen_c[i] = -1;
+#pragma omp for schedule(dynamic, 256)
+        for (int ic = 0; ic < nc; ++ic) {
+            int pos = C.row_ptr[ic];
+            seen_c[ic] = ic;
+            slot[ic] = pos;
+            C.col_idx[pos] = ic;
+            C.val[pos] = 0.0;
+            pos++;
+            for (int q1 = ri[ic]; q1 < ri[ic + 1]; ++q1) {
+                const double r = rv[q1];
+                const int i1 = rj[q1];
+                for (int q2 = ai[i1]; q2 < ai[i1 + 1]; ++q2) {
+                    const double ra = r * av[q2];
+                    const int i2 = aj[q2];
+                    if (seen_f[i2] != ic) {
+                        seen_f[i2] = ic;
+                        for (int q3 = pi[i2]; q3 < pi[i2 + 1]; ++q3) {
+                            const double rap = ra * pv[q3];
+                            const int i3 = pj[q3];
+                            if (seen_c[i3] != ic) {
+                                seen_c[i3] = ic;
+                                slot[i3] = pos;
+                                C.val[pos] = rap;
+                                C.col_idx[pos] = i3;
+                                pos++;
+                            } else {
+                                C.val[slot[i3]] += rap;
+                            }
+                        }
+                    } else {
+                        for (int q3 = pi[i2]; q3 < pi[i2 + 1]; ++q3) C.val[slot[pj[q3]]] += ra * pv[q3];
+                    }
+                }
+            }
+        }
+        free(seen_f);
+        free(seen_c);
+        free(slot);
+    }
+    free(start);
+    return C;
+}
+
+/* ======================================================================================
+ * Level loop (Setup/SSS_SETUP.cu:5-178)
+ * ====================================================================================== */
+void SSS_amg_complexity_print(SSS_AMG *mg)
+{
+    static const char *rule = "-----------------------------------------------------------\n";
+    double grid = 0.0, op = 0.0;
+    fputs(rule, stdout);
+    printf("  Level   Num of rows   Num of nonzeros   Avg. NNZ / row   \n");
+    fputs(rule, stdout);
+    for (int l = 0; l < mg->num_levels; ++l) {
+        const SSS_MAT *A = &mg->cg[l].A;
+        printf("%5d %13d %17d %14.2lf\n", l, A->num_rows, A->num_nnzs, (double)A->num_nnzs / A->num_rows);
+        grid += A->num_rows;
+        op += A->num_nnzs;
+    }
+    fputs(rule, stdout);
+    grid /= mg->cg[0].A.num_rows;
+    op /= mg->cg[0].A.num_nnzs;
+    printf("  Grid complexity = %.3lf  |", grid);
+    printf("  Operator complexity = %.3lf\n", op);
+    fputs(rule, stdout);
+}
+
+void SSS_amg_setup(SSS_AMG *mg, SSS_MAT *A, SSS_AMG_PARS *pars)
+{
+    const int min_cdof = SSS_max(pars->coarse_dof, MIN_CDOF);
+    const int max_lvls = pars->max_levels;
+    const int n0 = A->num_rows;
+    const double t0 = SSS_get_time();
+    SSS_IVEC vertices;
+    int lvl = 0;
+
+    *mg = SSS_amg_data_create(pars);
+    vertices = SSS_ivec_create(n0);
+    mg->cg[0].A = SSS_mat_struct_create(n0, n0, A->num_nnzs);
+    SSS_mat_cp(A, &mg->cg[0].A);
+
+    while (mg->cg[lvl].A.num_rows > min_cdof && lvl < max_lvls - 1) {
+        SSS_AMG_COMP *L = &mg->cg[lvl];
+        SSS_IMAT S;
+        int status;
+        memset(&S, 0, sizeof(S));
+
+        status = SSS_amg_coarsen(&L->A, &vertices, &L->P, &S, pars);
+        if (status < 0) {
+            free(S.row_ptr);
+            free(S.col_idx);
+            printf("### WARNING: Could not find any C-variables!\n");
+            printf("### WARNING: RS coarsening on level-%d failed!\n", lvl);
+            break;
+        }
+        if (L->P.num_cols < min_cdof) {
+            free(S.row_ptr);
+            free(S.col_idx);
+            break;
+        }
+        if (L->P.num_rows > L->P.num_cols * 10) {
+            printf("### WARNING: Coarsening might be too aggressive!\n");
+            printf("### WARNING: Lvl = %d ,Fine level = %d, coarse level = %d. Discard!\n", lvl,
+                   L->P.num_rows, L->P.num_cols);
+        }
+        if (L->P.num_cols * 1.5 > L->A.num_rows) pars->cs_type = SSS_COARSE_RS;
+
+        L->cfmark = SSS_ivec_create(L->A.num_rows);
+        memcpy(L->cfmark.d, vertices.d, (size_t)L->A.num_rows * sizeof(int));
+
+        SSS_amg_interp(&L->A, &vertices, &L->P, &S, pars);
+        L->R = SSS_mat_trans(&L->P);
+        mg->cg[lvl + 1].A = SSS_blas_mat_rap(&L->R, &L->A, &L->P);
+        free(S.row_ptr);
+        free(S.col_idx);
+
+        /* "too dense" test on the finer level (integer nnz/rows, SSS_SETUP.cu:142) */
+        if (L->A.num_nnzs / L->A.num_rows > L->A.num_cols * 0.2) {
+            printf("### WARNING: Coarse matrix is too dense!\n");
+            printf("### WARNING: m = n = %d, nnz = %d!\n", L->A.num_cols, L->A.num_nnzs);
+            SSS_mat_destroy(&mg->cg[lvl + 1].A);
+            break;
+        }
+        lvl++;
+    }
+
+    mg->num_levels = lvl + 1;
+    mg->cg[0].wp = SSS_vec_create(n0);
+    for (int l = 1; l < mg->num_levels; ++l) {
+        int m = mg->cg[l].A.num_rows;
+        mg->cg[l].b = SSS_vec_create(m);
+        mg->cg[l].x = SSS_vec_create(m);
+        mg->cg[l].wp = SSS_vec_create(2 * m);
+    }
+    SSS_ivec_destroy(&vertices);
+    SSS_amg_complexity_print(mg);
+    printf("AMG setup time: %g s\n", SSS_get_time() - t0);
+}

@@ -1,0 +1,182 @@
+/*
+ * sss_solve.c — the drop-in solve path (host C driving the gfx950 engine).
+ *
+ *   SSS_amg_solve ........... Solve/SSS_SOLVE.c:4-87  (same loop, prints, stop test, rtn)
+ *   SSS_solver_amg .......... SSS_AMG.c:9-61
+ *   SSS_amg_cycle ........... Solve/SSS_cycle.cu:848-967   (GPU; host state synced back)
+ *   SSS_amg_coarest_solve ... Solve/SSS_cycle.cu:819-846   (GPU)
+ *   SSS_amg_smoother_pre/post Solve/SSS_smooth.c:138-304   (GPU)
+ *   SSS_blas_mv_amxpy/_mxy .. SSS_utils.c:161-201          (GPU)
+ *
+ * There is no CPU fallback: when no HIP device is usable every entry point above prints an
+ * "### ERROR" line and exits with ERROR_MISC, like the reference's fatal paths.
+ */
+#include "sss_internal.h"
+
+#include <math.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+void sss_fatal(const char *where, const char *what)
+{
+    fflush(stdout);
+    fprintf(stderr, "### ERROR: %s -- %s\n", where, what);
+    printf("### ERROR: %s -- Unknown error occurred!\n", where);
+    fflush(stdout);
+    exit(ERROR_MISC);
+}
+
+/* ---- HBM mirror registry, keyed by mg->cg (the SSS_AMG layout cannot carry it) --------- */
+#define MIRROR_SLOTS 16
+static struct {
+    const void *key;
+    sss_hip_hier *h;
+} g_mirrors[MIRROR_SLOTS];
+
+sss_hip_hier *sss_dev_mirror_for(SSS_AMG *mg)
+{
+    sss_hip_opts o;
+    int free_slot = -1;
+    for (int s = 0; s < MIRROR_SLOTS; ++s) {
+        if (g_mirrors[s].key == (const void *)mg->cg && g_mirrors[s].h) return g_mirrors[s].h;
+        if (!g_mirrors[s].h && free_slot < 0) free_slot = s;
+    }
+    if (free_slot < 0) sss_fatal(__func__, "too many live AMG hierarchies");
+    sss_hip_opts_default(&o);
+    g_mirrors[free_slot].h = sss_hip_hier_create(mg, &o);
+    if (!g_mirrors[free_slot].h) sss_fatal(__func__, "cannot mirror the AMG hierarchy to the GPU");
+    g_mirrors[free_slot].key = mg->cg;
+    return g_mirrors[free_slot].h;
+}
+
+void sss_dev_release_mirror(const void *cg_key)
+{
+    for (int s = 0; s < MIRROR_SLOTS; ++s) {
+        if (g_mirrors[s].key == cg_key && g_mirrors[s].h) {
+            sss_hip_hier_destroy(g_mirrors[s].h);
+            g_mirrors[s].h = NULL;
+            g_mirrors[s].key = NULL;
+        }
+    }
+}
+
+static void check(int rc, const char *where)
+{
+    if (rc != 0) sss_fatal(where, "GPU engine call failed");
+}
+
+/* ---- outer loop -------------------------------------------------------------------- */
+SSS_RTN SSS_amg_solve(SSS_AMG *mg, SSS_VEC *x, SSS_VEC *b)
+{
+    const int max_it = mg->pars.max_it;
+    const double tol = mg->pars.tol;
+    const double sumb = SSS_blas_vec_norm2(b);
+    const double t0 = SSS_get_time();
+    double absres0 = sumb;
+    SSS_RTN rtn = {0.0, 0.0, 0};
+    sss_hip_hier *h;
+
+    SSS_print_itinfo(STOP_REL_RES, 0, 1.0, sumb, 0.0);
+    if (fabs(sumb) == 0.0) {
+        SSS_vec_set_value(x, 0);
+        mg->rtn = rtn;
+        return rtn;
+    }
+    mg->cg[0].x = *x;
+    mg->cg[0].b = *b;
+
+    h = sss_dev_mirror_for(mg);
+    check(sss_hip_upload_vec(h, 0, SSS_HIP_VEC_B, b->d, b->n), __func__);
+    check(sss_hip_upload_vec(h, 0, SSS_HIP_VEC_X, x->d, x->n), __func__);
+
+    for (int iter = 1; iter <= max_it; ++iter) {
+        double absres, relres, factor;
+        check(sss_hip_cycle(h), __func__);
+        check(sss_hip_residual_norm(h, &absres), __func__);   /* one 8-byte D2H per iteration */
+        relres = absres / sumb;
+        factor = absres / absres0;
+        absres0 = absres;
+        SSS_print_itinfo(STOP_REL_RES, iter, relres, absres, factor);
+        rtn.ares = absres;
+        rtn.rres = relres;
+        rtn.nits = iter;
+        mg->rtn = rtn;
+        if (relres < tol) break;
+    }
+    /* results back into the caller's x (level-0 x aliases it) and r into cg[0].wp */
+    check(sss_hip_download_vec(h, 0, SSS_HIP_VEC_X, x->d, x->n), __func__);
+    check(sss_hip_download_vec(h, 0, SSS_HIP_VEC_WP, mg->cg[0].wp.d, mg->cg[0].A.num_rows), __func__);
+    printf("AMG solve time: %g s\n", SSS_get_time() - t0);
+    return rtn;
+}
+
+SSS_RTN SSS_solver_amg(SSS_MAT *A, SSS_VEC *x, SSS_VEC *b, SSS_AMG_PARS *pars)
+{
+    SSS_RTN rtn;
+    SSS_AMG mg;
+    const double sumb = SSS_blas_vec_norm2(b);
+    double t0;
+
+    if (fabs(sumb) == 0.0) {
+        SSS_vec_set_value(x, 0);
+        rtn.ares = 0;
+        rtn.rres = 0;
+        rtn.nits = 0;
+        SSS_print_itinfo(STOP_REL_RES, 0, 0., sumb, 0.0);
+        return rtn;
+    }
+    t0 = SSS_get_time();
+    if (A->num_rows != A->num_cols) printf("### ERROR: A is not a square matrix!\n");
+    if (A->num_nnzs <= 0) printf("### ERROR: A has no nonzero entries!\n");
+    SSS_amg_setup(&mg, A, pars);
+    rtn = SSS_amg_solve(&mg, x, b);
+    SSS_amg_data_destroy(&mg);
+    printf("AMG totally time: %g s\n", SSS_get_time() - t0);
+    return rtn;
+}
+
+/* ---- standalone GPU-backed entry points ------------------------------------------------ */
+void SSS_amg_cycle(SSS_AMG *mg)
+{
+    sss_hip_hier *h = sss_dev_mirror_for(mg);
+    const int nl = mg->num_levels;
+    check(sss_hip_upload_vec(h, 0, SSS_HIP_VEC_B, mg->cg[0].b.d, mg->cg[0].A.num_rows), __func__);
+    check(sss_hip_upload_vec(h, 0, SSS_HIP_VEC_X, mg->cg[0].x.d, mg->cg[0].A.num_rows), __func__);
+    check(sss_hip_cycle(h), __func__);
+    for (int l = 0; l < nl; ++l) {
+        const int n = mg->cg[l].A.num_rows;
+        check(sss_hip_download_vec(h, l, SSS_HIP_VEC_X, mg->cg[l].x.d, n), __func__);
+        check(sss_hip_download_vec(h, l, SSS_HIP_VEC_B, mg->cg[l].b.d, n), __func__);
+        if (l < nl - 1) check(sss_hip_download_vec(h, l, SSS_HIP_VEC_WP, mg->cg[l].wp.d, n), __func__);
+    }
+}
+
+void SSS_amg_coarest_solve(SSS_MAT *A, SSS_VEC *b, SSS_VEC *x, const double ctol)
+{
+    sss_hip_opts o;
+    sss_hip_opts_default(&o);
+    check(sss_hip_host_coarse_solve(A, b, x, ctol, o.coarse, o.row_cap), __func__);
+}
+
+static void smoother_entry(SSS_SMTR *s, int post, const char *fname)
+{
+    if (s->smoother != SSS_SM_GS && s->smoother != SSS_SM_JACOBI) {
+        printf("### ERROR: Wrong smoother type %d!\n", s->smoother);
+        SSS_exit_on_errcode(ERROR_INPUT_PAR, fname);
+    }
+    check(sss_hip_host_smooth(s, post), fname);
+}
+
+void SSS_amg_smoother_pre(SSS_SMTR *s) { smoother_entry(s, 0, "SSS_amg_smoother_pre"); }
+void SSS_amg_smoother_post(SSS_SMTR *s) { smoother_entry(s, 1, "SSS_amg_smoother_post"); }
+
+void SSS_blas_mv_amxpy(double alpha, const SSS_MAT *A, const SSS_VEC *x, SSS_VEC *y)
+{
+    check(sss_hip_host_spmv(SSS_HIP_SPMV_AMXPY, alpha, A, x->d, NULL, y->d, 0), __func__);
+}
+
+void SSS_blas_mv_mxy(const SSS_MAT *A, const SSS_VEC *x, SSS_VEC *y)
+{
+    check(sss_hip_host_spmv(SSS_HIP_SPMV_MXY, 1.0, A, x->d, NULL, y->d, 0), __func__);
+}

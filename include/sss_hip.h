@@ -1,0 +1,121 @@
+/*
+ * sss_hip.h — C ABI of the gfx950 device engine behind the drop-in solve path.
+ *
+ * The host C side (amg_amd/host/sss_solve.c) implements the reference's SSS_amg_solve loop
+ * (Solve/SSS_SOLVE.c:53-80) on top of these calls; bench.py and the GPU tests call them
+ * through ctypes.  Plain pointers and sizes only.  All functions return 0 on success and a
+ * negative SSS_ERROR_CODE on failure (ERROR_MISC for HIP/RCCL errors, with a message on
+ * stderr), except where noted.
+ *
+ * Reference interfaces these replace (amg/ tree):
+ *   sss_hip_cycle ............ SSS_amg_cycle                Solve/SSS_cycle.cu:848-967
+ *   sss_hip_residual_norm .... r = b - A*x; ||r||            Solve/SSS_SOLVE.c:59-64
+ *   sss_hip_coarse_solve ..... SSS_amg_coarest_solve        Solve/SSS_cycle.cu:819-846
+ *   sss_hip_smooth ........... SSS_amg_smoother_pre/post    Solve/SSS_smooth.c:138-304
+ *   sss_hip_csr_spmv ......... SSS_blas_mv_amxpy/_mxy, spmv_cuda/alpha_spmv_cuda
+ *                              SSS_utils.c:161-201, Solve/SSS_cuda.cu:77-165
+ */
+#ifndef SSS_HIP_H
+#define SSS_HIP_H
+
+#include "sss_amg.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- engine options ------------------------------------------------------------------ */
+enum {
+    SSS_HIP_SMOOTH_EXACT = 0,    /* reference GS-CF on every level (level-scheduled, bitwise) */
+    SSS_HIP_SMOOTH_HYBRID = 1,   /* exact GS-CF on level 0, C/F-Jacobi below */
+    SSS_HIP_SMOOTH_JACOBI = 2    /* C/F-Jacobi on every level */
+};
+enum {
+    SSS_HIP_COARSE_KRYLOV = 0,   /* reference CG(beta==1)+GMRES(30), on device */
+    SSS_HIP_COARSE_DIRECT = 1    /* explicit inverse of the coarsest operator, one GEMV */
+};
+enum { SSS_HIP_VEC_B = 0, SSS_HIP_VEC_X = 1, SSS_HIP_VEC_WP = 2 };
+
+typedef struct sss_hip_opts {
+    int device;        /* HIP device ordinal; -1 = keep current */
+    int smoother;      /* SSS_HIP_SMOOTH_* */
+    int coarse;        /* SSS_HIP_COARSE_* */
+    int row_cap;       /* 0 = uncapped coarse SpMV; 4096 reproduces <<<64,64>>> (as shipped) */
+    int use_graph;     /* capture the V-cycle into a hipGraph once and replay it */
+    int verbose;       /* engine diagnostics on stderr */
+} sss_hip_opts;
+
+/* Defaults, overridable by environment: SSS_HIP_SMOOTHER=exact|hybrid|jacobi,
+ * SSS_HIP_COARSE=krylov|direct, SSS_HIP_ROWCAP=<n>, SSS_HIP_GRAPH=0|1, SSS_HIP_DEVICE=<n>,
+ * SSS_HIP_VERBOSE=0|1. */
+void sss_hip_opts_default(sss_hip_opts *o);
+
+/* Number of usable HIP devices (0 when none; never exits). */
+int sss_hip_device_count(void);
+
+/* ---- hierarchy mirror -------------------------------------------------------------- */
+typedef struct sss_hip_hier sss_hip_hier;
+
+/* Uploads every level of mg (A, P, R, cfmark; b/x/wp allocated) to HBM and builds the
+ * smoother schedules.  mg->cg[0].x/.b may be unset. Returns NULL on failure. */
+sss_hip_hier *sss_hip_hier_create(const SSS_AMG *mg, const sss_hip_opts *o);
+void sss_hip_hier_destroy(sss_hip_hier *h);
+
+int sss_hip_upload_vec(sss_hip_hier *h, int level, int which, const double *src, int n);
+int sss_hip_download_vec(sss_hip_hier *h, int level, int which, double *dst, int n);
+
+/* One V/W-cycle on the device-resident level vectors (asynchronous on the engine stream). */
+int sss_hip_cycle(sss_hip_hier *h);
+/* wp0 = b0 - A0*x0 and ||wp0||_2, returned to the host (synchronises the stream). */
+int sss_hip_residual_norm(sss_hip_hier *h, double *absres);
+/* The coarsest-level solve alone (on the level vectors of the coarsest level). */
+int sss_hip_coarse_solve(sss_hip_hier *h);
+/* Pre (post = 0) or post (post = 1) smoothing of one level. */
+int sss_hip_smooth(sss_hip_hier *h, int level, int post);
+int sss_hip_sync(sss_hip_hier *h);
+
+/* Per-level statistics for reporting: rows, nnz(A), nnz(P), smoother DAG depths. */
+typedef struct sss_hip_level_info {
+    int rows, nnz, nnz_p, dag_f, dag_c, smoother_kind;
+} sss_hip_level_info;
+int sss_hip_level_info_get(sss_hip_hier *h, int level, sss_hip_level_info *out);
+int sss_hip_num_levels(sss_hip_hier *h);
+
+/* ---- kernel-level entry points on device memory (tests, bench, roofline) ------------- */
+enum {
+    SSS_HIP_SPMV_MXY = 0,    /* y = A*x                         (SSS_blas_mv_mxy)      */
+    SSS_HIP_SPMV_AMXPY = 1,  /* y += (A*x)*alpha                (SSS_blas_mv_amxpy)    */
+    SSS_HIP_SPMV_RESID = 2,  /* y = b + (A*x)*(-1)              (copy + amxpy(-1))     */
+    SSS_HIP_SPMV_ACC = 3     /* y += A*x, rows < cap only       (spmv_cuda)            */
+};
+/* A plan holds the CSR-adaptive row blocking of one matrix (device pointers). */
+typedef struct sss_hip_spmv_plan sss_hip_spmv_plan;
+sss_hip_spmv_plan *sss_hip_spmv_plan_create(int n, int nnz, const int *d_rp, const int *h_rp);
+void sss_hip_spmv_plan_destroy(sss_hip_spmv_plan *p);
+int sss_hip_spmv(const sss_hip_spmv_plan *p, int op, double alpha, const int *d_rp, const int *d_ci,
+                 const double *d_v, const double *d_x, const double *d_b, double *d_y, int cap,
+                 void *stream);
+
+/* Host-memory convenience wrappers (allocate, copy, run, copy back) used by the exported
+ * SSS_blas_mv_* / smoother / coarse-solve entry points. */
+int sss_hip_host_spmv(int op, double alpha, const SSS_MAT *A, const double *x, const double *b,
+                      double *y, int cap);
+int sss_hip_host_smooth(const SSS_SMTR *s, int post);
+int sss_hip_host_coarse_solve(SSS_MAT *A, SSS_VEC *b, SSS_VEC *x, double ctol, int coarse_mode,
+                              int row_cap);
+
+/* Engine event timer around `reps` launches of the level-0 residual SpMV on the engine
+ * stream: average kernel milliseconds (roofline measurement in bench.py). */
+int sss_hip_time_level0_spmv(sss_hip_hier *h, int reps, double *avg_ms);
+/* Average milliseconds of `reps` full iterations (cycle + residual + norm) on the engine
+ * stream, timed with HIP events; absres of the last iteration is returned. */
+int sss_hip_time_iterations(sss_hip_hier *h, int reps, double *avg_ms, double *absres);
+
+/* ---- generators (host) -------------------------------------------------------------- */
+/* kind 7 or 27; rows of z-planes [z0, z1) of an nx*ny*nz grid, global column indices. */
+int sss_gen_stencil(int kind, int nx, int ny, int nz, int z0, int z1, SSS_MAT *A);
+
+#ifdef __cplusplus
+}
+#endif
+#endif
