@@ -9,21 +9,21 @@
 //     best-so-far logic exactly as written; maxit = max(250, min(n*n, 1000)).
 //   * GMRES(30): Arnoldi p[i] += A*r accumulates into a vector that keeps its old content.
 //   * row cap: 0 = every row (the "uncapped" parity definition); 4096 = as shipped.
-// The CSR, vectors and scalars stay in HBM (the reference re-uploads the whole coarse CSR for
-// every one of its ~1,000 SpMVs per V-cycle).
 //
-// CG control flow runs on the device: every iteration is four launches (SpMV+dot, update+
-// norms, checks [+ residual re-computation when a check fires], p-update+commit).  Scalar
-// decisions are recomputed identically by every workgroup from deterministic partial sums;
-// workgroup 0 publishes them into a state double-buffered across iterations, so no kernel
-// reads a word it (or a sibling workgroup of the same launch) writes.  The host only polls the
-// stop flag every 32 iterations.  GMRES is host-steered: one 8-byte-per-entry Hessenberg
-// column read back per Arnoldi step, the Givens recurrences on the host in the reference's
-// exact arithmetic.
+// Bitwise parity.  With beta == 1 the reference CG is not a contraction: it amplifies rounding
+// differences (on 1138_bus it "fails" every cycle and GMRES finishes).  Reordered reductions
+// would therefore not be parity-grade, so every dot product / norm here is summed in the
+// reference's sequential order: the products are formed in parallel (identically rounded) and
+// staged in LDS, then one lane adds them in index order.  Coarse vectors are a few thousand
+// entries, so a sequential sum costs ~10-20 us; the SpMVs are the row-exact CSR-adaptive
+// kernels.  Result: the coarse solution is bitwise identical to the host reference.
 //
-// Dot products / norms use fixed-order (but not sequential) reductions: results match the
-// sequential host reference to ~1e-15 relative per reduction, not bitwise (tolerance ladder,
-// SURVEY.md §8c).
+// Control flow: CG runs device-side — per iteration one multi-workgroup SpMV (t += A*p), one
+// single-workgroup step kernel (alpha, updates, norms, checks; it owns the scalar state), and a
+// gated residual re-computation pair that only does work when a convergence check fires.  The
+// host polls the stop flag every 32 iterations.  GMRES is host-steered: the Hessenberg column
+// of each Arnoldi step is read back (i+1 doubles) and the Givens recurrences run on the host in
+// the reference's exact arithmetic.
 #include "sss_engine.hpp"
 #include "sss_spmv_dev.hpp"
 
@@ -35,301 +35,281 @@ namespace sss {
 
 enum { CG_RUN = 0, CG_STOP = 1 };
 constexpr int kPoll = 32;
+constexpr int kSeqBlock = 1024;       // single-workgroup kernels
+constexpr int kSeqChunk = 4096;       // doubles per sequential-sum LDS region (32 KiB)
 
 struct CgState {
-    int mode, iter, iter_best, stag, more_step, skip_restore;
-    double absres, absres0, absres_best, relres;
-};
-struct CgConst {
-    double temp1, normr0, tol, maxdiff;
-    int maxit, status;
-};
-struct CgMailB {
-    double alpha;
-    int breakdown;
-};
-struct CgMailC {
-    double absres, relres;
-    int copy_best, solstag, stag_fire, conv_check;
+    int mode, iter, iter_best, stag, more_step, skip_restore, flag_resid, stag_fire, status, maxit;
+    double temp1, normr0, tol, maxdiff, alpha, absres, absres0, absres_best, relres;
 };
 
 struct CoarseKrylov {
-    int n = 0, cap = 0, nbe = 0, nblk = 0;
+    int n = 0, cap = 0;
     double *p = nullptr, *r = nullptr, *t = nullptr, *u_best = nullptr;
-    double *P1 = nullptr, *P2 = nullptr, *P3 = nullptr;
     CgState *st = nullptr;
-    CgConst *cst = nullptr;
-    CgMailB *mb = nullptr;
-    CgMailC *mc = nullptr;
     CgState *h_st = nullptr;   // pinned
-    CgConst *h_cst = nullptr;  // pinned
-    // GMRES
-    double *gp = nullptr, *gw = nullptr, *gx_best = nullptr, *hcol = nullptr, *rs_dev = nullptr;
+    double *gp = nullptr, *gw = nullptr, *gx_best = nullptr, *hcol = nullptr, *rs_dev = nullptr, *scal = nullptr;
     double *h_buf = nullptr;   // pinned, >= 64 doubles
 };
 
 // ---------------------------------------------------------------------------------------------
-// reductions over partial arrays, identical in every workgroup
-__device__ __forceinline__ double reduce_all(const double *__restrict__ part, int count, int stride, int off,
-                                             double *red, bool is_max)
+// Sequential-order sums inside one workgroup.  Up to three independent sums run concurrently
+// (lanes 0, 64, 128 — three waves); each region holds one chunk of products.
+struct SeqSmem {
+    double reg[3][kSeqChunk];
+    double bcast[4];
+};
+
+__device__ __forceinline__ double seq_add_chunk(double s, const double *buf, int m)
 {
-    double v = 0.0;
-    for (int i = threadIdx.x; i < count; i += blockDim.x) {
-        const double e = part[(size_t)i * stride + off];
-        v = is_max ? fmax(v, e) : v + e;
+    int k = 0;
+    for (; k + 8 <= m; k += 8) {
+        const double a0 = buf[k], a1 = buf[k + 1], a2 = buf[k + 2], a3 = buf[k + 3];
+        const double a4 = buf[k + 4], a5 = buf[k + 5], a6 = buf[k + 6], a7 = buf[k + 7];
+        s += a0; s += a1; s += a2; s += a3; s += a4; s += a5; s += a6; s += a7;
     }
-    double t = is_max ? block_max(v, red) : block_sum(v, red);
-    __shared__ double bcast;
-    if (threadIdx.x == 0) bcast = t;
+    for (; k < m; ++k) s += buf[k];
+    return s;
+}
+
+// returns sum_i x_i*y_i in index order (valid in every thread)
+template <int NS>
+__device__ void seq_dots(int n, const double *const (&xs)[NS], const double *const (&ys)[NS], double (&out)[NS],
+                         SeqSmem &sm)
+{
+    double s = 0.0;    // lane q*64 owns sum q
+    for (int base = 0; base < n; base += kSeqChunk) {
+        const int m = min(kSeqChunk, n - base);
+        for (int q = 0; q < NS; ++q)
+            for (int i = threadIdx.x; i < m; i += blockDim.x) sm.reg[q][i] = xs[q][base + i] * ys[q][base + i];
+        __syncthreads();
+        for (int q = 0; q < NS; ++q)
+            if ((int)threadIdx.x == q * 64) s = seq_add_chunk(s, sm.reg[q], m);
+        __syncthreads();
+    }
+    for (int q = 0; q < NS; ++q)
+        if ((int)threadIdx.x == q * 64) sm.bcast[q] = s;
     __syncthreads();
-    t = bcast;
+    for (int q = 0; q < NS; ++q) out[q] = sm.bcast[q];
+    __syncthreads();
+}
+
+__device__ double seq_dot1(int n, const double *x, const double *y, SeqSmem &sm)
+{
+    const double *xs[1] = {x}, *ys[1] = {y};
+    double o[1];
+    seq_dots<1>(n, xs, ys, o, sm);
+    return o[0];
+}
+
+__device__ double block_absmax(int n, const double *x, SeqSmem &sm)
+{
+    double m = 0.0;
+    for (int i = threadIdx.x; i < n; i += blockDim.x) m = fmax(m, fabs(x[i]));
+    for (int off = 32; off > 0; off >>= 1) m = fmax(m, __shfl_xor(m, off, 64));
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0) sm.reg[0][threadIdx.x >> 6] = m;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        double t = 0.0;
+        for (int w = 0; w < (int)(blockDim.x >> 6); ++w) t = fmax(t, sm.reg[0][w]);
+        sm.bcast[3] = t;
+    }
+    __syncthreads();
+    const double t = sm.bcast[3];
     __syncthreads();
     return t;
 }
 
-// r = b - A*u on rows < cap (rows >= cap: r = b), sum of squares per block -> part
+// ---------------------------------------------------------------------------------------------
+// r = b - A*u on rows < cap (rows >= cap: r = b).  gate: 0 always; 1 CG check residual (runs
+// only when the step kernel asked for it); 2 CG restore (only when the best-so-far differs).
 __global__ __launch_bounds__(kBlock) void k_resid(const int *blk, const int *rp, const int *ci, const double *v,
                                                   const double *__restrict__ u, const double *__restrict__ b,
-                                                  double *__restrict__ r, int cap, double *__restrict__ part,
-                                                  const CgState *st, int gate)
+                                                  double *__restrict__ r, int cap, const CgState *st, int gate)
 {
     __shared__ SpmvSmem sm;
-    if (gate && (st->skip_restore || st->iter == st->iter_best)) return;
-    const double sq = csr_block_rows(blk, rp, ci, v, u, sm, [&](int row, double s) -> double {
-        const double o = (cap > 0 && row >= cap) ? b[row] : b[row] + s * -1.0;
-        r[row] = o;
-        return o * o;
+    if (gate == 1 && (st->mode != CG_RUN || !st->flag_resid)) return;
+    if (gate == 2 && (st->skip_restore || st->iter == st->iter_best)) return;
+    (void)csr_block_rows(blk, rp, ci, v, u, sm, [&](int row, double s) -> double {
+        r[row] = (cap > 0 && row >= cap) ? b[row] : b[row] + s * -1.0;
+        return 0.0;
     });
-    const double t = block_sum(sq, sm.red);
-    if (threadIdx.x == 0) part[blockIdx.x] = t;
 }
 
-__global__ __launch_bounds__(1024) void k_cg_init(int n, int nblk, const double *__restrict__ part,
-                                                  const double *__restrict__ r, double *__restrict__ p, double tol,
-                                                  int maxit, CgState *st, CgConst *cst)
+// t += A*p (rows < cap)
+__global__ __launch_bounds__(kBlock) void k_acc(const int *blk, const int *rp, const int *ci, const double *v,
+                                                const double *__restrict__ x, double *__restrict__ y, int cap,
+                                                const CgState *st)
 {
-    __shared__ double red[16];
-    const double rr = reduce_all(part, nblk, 1, 0, red, false);
+    __shared__ SpmvSmem sm;
+    if (st && st->mode != CG_RUN) return;
+    (void)csr_block_rows(blk, rp, ci, v, x, sm, [&](int row, double s) -> double {
+        if (!(cap > 0 && row >= cap)) y[row] = y[row] + s;
+        return 0.0;
+    });
+}
+
+__global__ __launch_bounds__(kSeqBlock) void k_cg_init(int n, const double *__restrict__ r, double *__restrict__ p,
+                                                       double tol, int maxit, CgState *st)
+{
+    __shared__ SeqSmem sm;
+    const double rr = seq_dot1(n, r, r, sm);
     const double absres0 = sqrt(rr);
     const double normr0 = fmax(SMALLFLOAT, absres0);
     const double relres = absres0 / normr0;
-    for (int i = threadIdx.x; i < n; i += 1024) p[i] = r[i];
+    for (int i = threadIdx.x; i < n; i += blockDim.x) p[i] = r[i];
     if (threadIdx.x == 0) {
-        CgState s{};
+        CgState s;
+        memset(&s, 0, sizeof(s));
         s.mode = relres < tol ? CG_STOP : CG_RUN;
         s.skip_restore = relres < tol;
-        s.iter = 0;
-        s.iter_best = 0;
         s.stag = 1;
         s.more_step = 1;
+        s.maxit = maxit;
+        s.temp1 = rr;          // (z, r) with z = r; frozen (as compiled)
+        s.normr0 = normr0;
+        s.tol = tol;
+        s.maxdiff = tol * 1e-4;
         s.absres = BIGFLOAT;
         s.absres0 = absres0;
         s.absres_best = BIGFLOAT;
         s.relres = relres;
-        st[1] = s;     // iteration 1 reads st[1]
-        cst->temp1 = rr;   // (z, r) with z = r
-        cst->normr0 = normr0;
-        cst->tol = tol;
-        cst->maxdiff = tol * 1e-4;
-        cst->maxit = maxit;
-        cst->status = 0;
+        *st = s;
     }
 }
 
-// A: t += A*p (rows < cap), partial (t, p)
-__global__ __launch_bounds__(kBlock) void k_cg_spmv(const int *blk, const int *rp, const int *ci, const double *v,
-                                                    const double *__restrict__ p, double *__restrict__ t, int cap,
-                                                    double *__restrict__ P1, const CgState *sin)
+// The CG step after t += A*p: alpha, updates, norms, best-so-far, checks I and II/III triggers.
+__global__ __launch_bounds__(kSeqBlock) void k_cg_step(int n, int k, double *__restrict__ u, double *__restrict__ r,
+                                                       double *__restrict__ p, const double *__restrict__ t,
+                                                       double *__restrict__ u_best, CgState *st)
 {
-    __shared__ SpmvSmem sm;
-    if (sin->mode != CG_RUN) return;
-    const double c = csr_block_rows(blk, rp, ci, v, p, sm, [&](int row, double s) -> double {
-        double tv = t[row];
-        if (!(cap > 0 && row >= cap)) {
-            tv = tv + s;
-            t[row] = tv;
-        }
-        return tv * p[row];
-    });
-    const double sum = block_sum(c, sm.red);
-    if (threadIdx.x == 0) P1[blockIdx.x] = sum;
-}
-
-// B: alpha; u += alpha p; r -= alpha t; partials of |r|^2, |u|^2, |p|^2, max|u|
-__global__ __launch_bounds__(kBlock) void k_cg_update(int n, int nblk, const double *__restrict__ P1,
-                                                      double *__restrict__ u, double *__restrict__ r,
-                                                      const double *__restrict__ p, const double *__restrict__ t,
-                                                      double *__restrict__ P2, const CgState *sin, const CgConst *cst,
-                                                      CgMailB *mb)
-{
-    __shared__ double red[kBlock / 64];
-    if (sin->mode != CG_RUN) return;
-    const double temp2 = reduce_all(P1, nblk, 1, 0, red, false);
-    const bool ok = fabs(temp2) > SMALLFLOAT2;
-    const double alpha = ok ? cst->temp1 / temp2 : 0.0;
-    if (blockIdx.x == 0 && threadIdx.x == 0) {
-        mb->alpha = alpha;
-        mb->breakdown = ok ? 0 : 1;
-    }
-    if (!ok) return;
-    const int i = blockIdx.x * kBlock + threadIdx.x;
-    double rr = 0.0, uu = 0.0, pp = 0.0, um = 0.0;
-    if (i < n) {
-        const double pi = p[i];
-        const double ui = u[i] + alpha * pi;
-        const double ri = r[i] + -alpha * t[i];
-        u[i] = ui;
-        r[i] = ri;
-        rr = ri * ri;
-        uu = ui * ui;
-        pp = pi * pi;
-        um = fabs(ui);
-    }
-    double s0 = block_sum(rr, red);
-    double s1 = block_sum(uu, red);
-    double s2 = block_sum(pp, red);
-    double s3 = block_max(um, red);
-    if (threadIdx.x == 0) {
-        P2[4 * blockIdx.x + 0] = s0;
-        P2[4 * blockIdx.x + 1] = s1;
-        P2[4 * blockIdx.x + 2] = s2;
-        P2[4 * blockIdx.x + 3] = s3;
-    }
-}
-
-// C: checks; best-so-far copy; residual re-computation when a convergence check fires
-__global__ __launch_bounds__(kBlock) void k_cg_check(int nbe, const int *blk, const int *rp, const int *ci,
-                                                     const double *v, const double *__restrict__ u,
-                                                     const double *__restrict__ b, double *__restrict__ r,
-                                                     double *__restrict__ u_best, int cap, const double *__restrict__ P2,
-                                                     double *__restrict__ P3, const CgState *sin, const CgConst *cst,
-                                                     const CgMailB *mb, CgMailC *mc)
-{
-    __shared__ SpmvSmem sm;
-    if (sin->mode != CG_RUN || mb->breakdown) return;
-    const double rr = reduce_all(P2, nbe, 4, 0, sm.red, false);
-    const double uu = reduce_all(P2, nbe, 4, 1, sm.red, false);
-    const double pp = reduce_all(P2, nbe, 4, 2, sm.red, false);
-    const double um = reduce_all(P2, nbe, 4, 3, sm.red, true);
-    const double absres = sqrt(rr);
-    const double relres = absres / cst->normr0;
-    const int copy_best = absres < sin->absres_best - cst->maxdiff;
-    const int solstag = um <= SMALLFLOAT;
-    const double normu = sqrt(uu);
-    const double reldiff = fabs(mb->alpha) * sqrt(pp) / normu;
-    const int stag_fire = !solstag && ((sin->stag <= max_STAG) & (reldiff < cst->maxdiff));
-    const int conv_check = !solstag && (stag_fire || relres < cst->tol);
-    if (blockIdx.x == 0 && threadIdx.x == 0) {
-        mc->absres = absres;
-        mc->relres = relres;
-        mc->copy_best = copy_best;
-        mc->solstag = solstag;
-        mc->stag_fire = stag_fire;
-        mc->conv_check = conv_check;
-    }
-    if (copy_best) {
-        const int r0 = blk[blockIdx.x], r1 = blk[blockIdx.x + 1];
-        for (int i = r0 + threadIdx.x; i < r1; i += kBlock) u_best[i] = u[i];
-    }
-    if (!conv_check) return;
-    const double sq = csr_block_rows(blk, rp, ci, v, u, sm, [&](int row, double s) -> double {
-        const double o = (cap > 0 && row >= cap) ? b[row] : b[row] + s * -1.0;
-        r[row] = o;
-        return o * o;
-    });
-    const double tsum = block_sum(sq, sm.red);
-    if (threadIdx.x == 0) P3[blockIdx.x] = tsum;
-}
-
-// D: decisions of checks II/III, p = z + 1.0*p, commit the state for iteration k+1
-__global__ __launch_bounds__(kBlock) void k_cg_commit(int n, int nblk, int k, const double *__restrict__ r,
-                                                      double *__restrict__ p, const double *__restrict__ P3,
-                                                      const CgState *sin, CgState *sout, const CgConst *cst,
-                                                      const CgMailB *mb, const CgMailC *mc)
-{
-    __shared__ double red[kBlock / 64];
-    CgState s = *sin;
-    if (s.mode != CG_RUN) {
-        if (blockIdx.x == 0 && threadIdx.x == 0) *sout = s;
+    __shared__ SeqSmem sm;
+    __shared__ int s_flags[2];
+    if (st->mode != CG_RUN) return;
+    const double temp2 = seq_dot1(n, t, p, sm);
+    if (!(fabs(temp2) > SMALLFLOAT2)) {                 // possible breakdown: goto RESTORE_BESTSOL
+        if (threadIdx.x == 0) { st->mode = CG_STOP; st->iter = k; }
         return;
     }
-    s.iter = k;
-    bool stop = false, zero_p = false;
-    if (mb->breakdown) {
-        stop = true;              // goto RESTORE_BESTSOL with iter = k
-    } else {
-        if (mc->copy_best) {
-            s.absres_best = mc->absres;
-            s.iter_best = k;
-        }
-        s.absres = mc->absres;
-        s.relres = mc->relres;
-        if (mc->solstag) {
-            stop = true;
-            s.iter = ERROR_SOLVER_SOLSTAG;
-        } else {
-            double a3 = 0.0, r3 = 0.0;
-            if (mc->conv_check) {
-                a3 = sqrt(reduce_all(P3, nblk, 1, 0, red, false));
-                r3 = a3 / cst->normr0;
-            }
-            if (mc->stag_fire) {
-                s.absres = a3;
-                s.relres = r3;
-                if (r3 < cst->tol) stop = true;
-                else if (s.stag >= max_STAG) {
-                    stop = true;
-                    s.iter = ERROR_SOLVER_STAG;
-                } else {
-                    zero_p = true;
-                    s.stag++;
-                }
-            }
-            if (!stop && s.relres < cst->tol) {
-                s.absres = a3;
-                s.relres = r3;
-                if (r3 < cst->tol) stop = true;
-                else if (s.more_step >= max_RESTART) {
-                    stop = true;
-                    s.iter = ERROR_SOLVER_TOLSMALL;
-                } else {
-                    zero_p = true;
-                    s.more_step++;
-                }
-            }
-            if (!stop) {
-                s.absres0 = s.absres;
-                const int i = blockIdx.x * kBlock + threadIdx.x;
-                if (i < n) p[i] = 1.0 * r[i] + 1.0 * (zero_p ? 0.0 : p[i]);
-                if (k >= cst->maxit) {
-                    stop = true;       // while (iter++ < matrix) fails next: iter = matrix + 1
-                    s.iter = cst->maxit + 1;
-                }
-            }
-        }
+    const double alpha = st->temp1 / temp2;
+    for (int i = threadIdx.x; i < n; i += blockDim.x) {
+        u[i] = u[i] + alpha * p[i];
+        r[i] = r[i] + -alpha * t[i];
     }
-    if (stop) s.mode = CG_STOP;
-    if (blockIdx.x == 0 && threadIdx.x == 0) *sout = s;
+    __syncthreads();
+    const double *xs[3] = {r, u, p}, *ys[3] = {r, u, p};
+    double sq[3];
+    seq_dots<3>(n, xs, ys, sq, sm);
+    const double infnormu = block_absmax(n, u, sm);
+    if (threadIdx.x == 0) {
+        CgState s = *st;
+        s.iter = k;
+        s.alpha = alpha;
+        s.absres = sqrt(sq[0]);
+        s.relres = s.absres / s.normr0;
+        int copy_best = 0;
+        if (s.absres < s.absres_best - s.maxdiff) {
+            s.absres_best = s.absres;
+            s.iter_best = k;
+            copy_best = 1;
+        }
+        s.flag_resid = 0;
+        s.stag_fire = 0;
+        if (infnormu <= SMALLFLOAT) {
+            s.iter = ERROR_SOLVER_SOLSTAG;
+            s.mode = CG_STOP;
+        } else {
+            const double normu = sqrt(sq[1]);
+            const double reldiff = fabs(alpha) * sqrt(sq[2]) / normu;
+            s.stag_fire = (s.stag <= max_STAG) & (reldiff < s.maxdiff);
+            s.flag_resid = s.stag_fire || s.relres < s.tol;
+        }
+        const int finish_here = s.mode == CG_RUN && !s.flag_resid;
+        if (finish_here) {
+            s.absres0 = s.absres;
+            if (k >= s.maxit) {               // while (iter++ < matrix) ends: iter = matrix + 1
+                s.mode = CG_STOP;
+                s.iter = s.maxit + 1;
+            }
+        }
+        *st = s;
+        s_flags[0] = copy_best;
+        s_flags[1] = finish_here;
+    }
+    __syncthreads();
+    if (s_flags[0])
+        for (int i = threadIdx.x; i < n; i += blockDim.x) u_best[i] = u[i];
+    if (s_flags[1])
+        for (int i = threadIdx.x; i < n; i += blockDim.x) p[i] = 1.0 * r[i] + 1.0 * p[i];
 }
 
-// restore: if absres > absres_best + maxdiff then u = u_best; publish the return status
-__global__ __launch_bounds__(kBlock) void k_cg_restore(int n, int nblk, double *__restrict__ u,
-                                                       const double *__restrict__ u_best, const double *__restrict__ P3,
-                                                       const CgState *sfin, CgConst *cst)
+// After the gated residual re-computation: checks II (stagnation) and III (false convergence).
+__global__ __launch_bounds__(kSeqBlock) void k_cg_fix(int n, int k, const double *__restrict__ r,
+                                                      double *__restrict__ p, CgState *st)
 {
-    __shared__ double red[kBlock / 64];
-    const CgState s = *sfin;
-    if (blockIdx.x == 0 && threadIdx.x == 0) cst->status = s.iter > cst->maxit ? ERROR_SOLVER_matrix : s.iter;
-    if (s.skip_restore || s.iter == s.iter_best) return;
-    const double best = sqrt(reduce_all(P3, nblk, 1, 0, red, false));
-    if (s.absres > best + cst->maxdiff) {
-        const int i = blockIdx.x * kBlock + threadIdx.x;
-        if (i < n) u[i] = u_best[i];
+    __shared__ SeqSmem sm;
+    __shared__ int s_pmode;   // 0: no p update, 1: p = z + p, 2: p = z + 0
+    if (st->mode != CG_RUN || !st->flag_resid) return;
+    const double a3 = sqrt(seq_dot1(n, r, r, sm));
+    if (threadIdx.x == 0) {
+        CgState s = *st;
+        bool stop = false, zero_p = false;
+        const double r3 = a3 / s.normr0;
+        if (s.stag_fire) {
+            s.absres = a3;
+            s.relres = r3;
+            if (r3 < s.tol) stop = true;
+            else if (s.stag >= max_STAG) { stop = true; s.iter = ERROR_SOLVER_STAG; }
+            else { zero_p = true; s.stag++; }
+        }
+        if (!stop && s.relres < s.tol) {
+            s.absres = a3;
+            s.relres = r3;
+            if (r3 < s.tol) stop = true;
+            else if (s.more_step >= max_RESTART) { stop = true; s.iter = ERROR_SOLVER_TOLSMALL; }
+            else { zero_p = true; s.more_step++; }
+        }
+        s_pmode = 0;
+        if (!stop) {
+            s.absres0 = s.absres;
+            s_pmode = zero_p ? 2 : 1;
+            if (k >= s.maxit) { stop = true; s.iter = s.maxit + 1; }
+        }
+        if (stop) s.mode = CG_STOP;
+        s.flag_resid = 0;
+        *st = s;
     }
+    __syncthreads();
+    if (s_pmode)
+        for (int i = threadIdx.x; i < n; i += blockDim.x) p[i] = 1.0 * r[i] + 1.0 * (s_pmode == 2 ? 0.0 : p[i]);
+}
+
+__global__ __launch_bounds__(kSeqBlock) void k_cg_restore(int n, double *__restrict__ u,
+                                                          const double *__restrict__ u_best,
+                                                          const double *__restrict__ r, CgState *st)
+{
+    __shared__ SeqSmem sm;
+    __shared__ int s_copy;
+    const CgState s0 = *st;
+    if (threadIdx.x == 0) st->status = s0.iter > s0.maxit ? ERROR_SOLVER_matrix : s0.iter;
+    if (s0.skip_restore || s0.iter == s0.iter_best) return;
+    const double best = sqrt(seq_dot1(n, r, r, sm));
+    if (threadIdx.x == 0) s_copy = s0.absres > best + s0.maxdiff;
+    __syncthreads();
+    if (s_copy)
+        for (int i = threadIdx.x; i < n; i += blockDim.x) u[i] = u_best[i];
 }
 
 // ---------------------------------------------------------------------------------------------
-// GMRES helpers
+// GMRES kernels (single workgroup unless noted)
+__global__ __launch_bounds__(kSeqBlock) void k_seq_norm(int n, const double *__restrict__ x, double *out)
+{
+    __shared__ SeqSmem sm;
+    const double s = sqrt(seq_dot1(n, x, x, sm));
+    if (threadIdx.x == 0) *out = s;
+}
+
 __global__ __launch_bounds__(kBlock) void k_scal(int n, double a, double *__restrict__ x)
 {
     const int i = blockIdx.x * kBlock + threadIdx.x;
@@ -342,44 +322,23 @@ __global__ __launch_bounds__(kBlock) void k_copy(int n, const double *__restrict
     if (i < n) y[i] = x[i];
 }
 
-// p[i] += A*p[i-1] (rows < cap)
-__global__ __launch_bounds__(kBlock) void k_acc(const int *blk, const int *rp, const int *ci, const double *v,
-                                                const double *__restrict__ x, double *__restrict__ y, int cap)
+// modified Gram-Schmidt of p[i] against p[0..i-1], then normalisation
+__global__ __launch_bounds__(kSeqBlock) void k_mgs(int n, int i, double *P, double *__restrict__ hcol)
 {
-    __shared__ SpmvSmem sm;
-    (void)csr_block_rows(blk, rp, ci, v, x, sm, [&](int row, double s) -> double {
-        if (!(cap > 0 && row >= cap)) y[row] = y[row] + s;
-        return 0.0;
-    });
-}
-
-// modified Gram-Schmidt of p[i] against p[0..i-1], then normalisation; one workgroup
-__global__ __launch_bounds__(1024) void k_mgs(int n, int i, double *P, double *__restrict__ hcol)
-{
-    __shared__ double red[16];
-    __shared__ double bcast;
+    __shared__ SeqSmem sm;
     double *pi = P + (size_t)i * n;
     for (int j = 0; j < i; ++j) {
         const double *pj = P + (size_t)j * n;
-        double d = 0.0;
-        for (int e = threadIdx.x; e < n; e += 1024) d += pj[e] * pi[e];
-        d = block_sum(d, red);
-        if (threadIdx.x == 0) { bcast = d; hcol[j] = d; }
-        __syncthreads();
-        const double h = bcast;
-        __syncthreads();
-        for (int e = threadIdx.x; e < n; e += 1024) pi[e] += -h * pj[e];
+        const double h = seq_dot1(n, pj, pi, sm);
+        if (threadIdx.x == 0) hcol[j] = h;
+        for (int e = threadIdx.x; e < n; e += blockDim.x) pi[e] += -h * pj[e];
         __syncthreads();
     }
-    double d = 0.0;
-    for (int e = threadIdx.x; e < n; e += 1024) d += pi[e] * pi[e];
-    d = block_sum(d, red);
-    if (threadIdx.x == 0) { bcast = sqrt(d); hcol[i] = bcast; }
-    __syncthreads();
-    const double t = bcast;
+    const double t = sqrt(seq_dot1(n, pi, pi, sm));
+    if (threadIdx.x == 0) hcol[i] = t;
     if (t != 0.0) {
         const double inv = 1.0 / t;
-        for (int e = threadIdx.x; e < n; e += 1024) pi[e] *= inv;
+        for (int e = threadIdx.x; e < n; e += blockDim.x) pi[e] *= inv;
     }
 }
 
@@ -421,28 +380,20 @@ CoarseKrylov *coarse_krylov_create(const DevCSR &A, int row_cap, hipStream_t)
     const int n = A.n;
     k->n = n;
     k->cap = row_cap;
-    k->nbe = (n + kBlock - 1) / kBlock;
-    k->nblk = A.nblk;
     k->p = dev_alloc<double>(n);
     k->r = dev_alloc<double>(n);
     k->t = dev_alloc<double>(n);
     k->u_best = dev_alloc<double>(n);
-    k->P1 = dev_alloc<double>(A.nblk);
-    k->P2 = dev_alloc<double>(4 * (size_t)k->nbe);
-    k->P3 = dev_alloc<double>(A.nblk);
-    k->st = dev_alloc<CgState>(2);
-    k->cst = dev_alloc<CgConst>(1);
-    k->mb = dev_alloc<CgMailB>(1);
-    k->mc = dev_alloc<CgMailC>(1);
+    k->st = dev_alloc<CgState>(1);
     k->gp = dev_alloc<double>((size_t)(max_RESTART + 1) * n);
     k->gw = dev_alloc<double>(n);
     k->gx_best = dev_alloc<double>(n);
     k->hcol = dev_alloc<double>(max_RESTART + 2);
     k->rs_dev = dev_alloc<double>(max_RESTART + 2);
-    bool ok = k->p && k->r && k->t && k->u_best && k->P1 && k->P2 && k->P3 && k->st && k->cst && k->mb && k->mc &&
-              k->gp && k->gw && k->gx_best && k->hcol && k->rs_dev;
+    k->scal = dev_alloc<double>(2);
+    bool ok = k->p && k->r && k->t && k->u_best && k->st && k->gp && k->gw && k->gx_best && k->hcol && k->rs_dev &&
+              k->scal;
     ok = ok && hipHostMalloc((void **)&k->h_st, sizeof(CgState)) == hipSuccess;
-    ok = ok && hipHostMalloc((void **)&k->h_cst, sizeof(CgConst)) == hipSuccess;
     ok = ok && hipHostMalloc((void **)&k->h_buf, sizeof(double) * 64) == hipSuccess;
     if (!ok) {
         coarse_krylov_destroy(k);
@@ -454,25 +405,22 @@ CoarseKrylov *coarse_krylov_create(const DevCSR &A, int row_cap, hipStream_t)
 void coarse_krylov_destroy(CoarseKrylov *k)
 {
     if (!k) return;
-    for (void *p : {(void *)k->p, (void *)k->r, (void *)k->t, (void *)k->u_best, (void *)k->P1, (void *)k->P2,
-                    (void *)k->P3, (void *)k->st, (void *)k->cst, (void *)k->mb, (void *)k->mc, (void *)k->gp,
-                    (void *)k->gw, (void *)k->gx_best, (void *)k->hcol, (void *)k->rs_dev})
+    for (void *p : {(void *)k->p, (void *)k->r, (void *)k->t, (void *)k->u_best, (void *)k->st, (void *)k->gp,
+                    (void *)k->gw, (void *)k->gx_best, (void *)k->hcol, (void *)k->rs_dev, (void *)k->scal})
         dev_free(p);
     if (k->h_st) (void)hipHostFree(k->h_st);
-    if (k->h_cst) (void)hipHostFree(k->h_cst);
     if (k->h_buf) (void)hipHostFree(k->h_buf);
     delete k;
 }
 
-// sum of squares of r = b - A*u (rows < cap), read back to the host
+// r = b - A*u (rows < cap) and ||r|| (sequential order) read back to the host
 static int host_resid_norm(CoarseKrylov *k, const DevCSR &A, const double *u, const double *b, double *r,
                            double *out, hipStream_t s)
 {
-    hipLaunchKernelGGL(k_resid, dim3(A.nblk), dim3(kBlock), 0, s, A.blk, A.rp, A.ci, A.v, u, b, r, k->cap, k->P3,
-                       k->st, 0);
-    int rc = launch_final_sum(k->P3, A.nblk, k->rs_dev + max_RESTART + 1, true, s);
-    if (rc) return rc;
-    SSS_HIP(hipMemcpyAsync(k->h_buf, k->rs_dev + max_RESTART + 1, sizeof(double), hipMemcpyDeviceToHost, s));
+    hipLaunchKernelGGL(k_resid, dim3(A.nblk), dim3(kBlock), 0, s, A.blk, A.rp, A.ci, A.v, u, b, r, k->cap,
+                       (const CgState *)nullptr, 0);
+    hipLaunchKernelGGL(k_seq_norm, dim3(1), dim3(kSeqBlock), 0, s, k->n, r, k->scal);
+    SSS_HIP(hipMemcpyAsync(k->h_buf, k->scal, sizeof(double), hipMemcpyDeviceToHost, s));
     SSS_HIP(hipStreamSynchronize(s));
     *out = k->h_buf[0];
     return 0;
@@ -481,51 +429,51 @@ static int host_resid_norm(CoarseKrylov *k, const DevCSR &A, const double *u, co
 static int run_cg(CoarseKrylov *k, const DevCSR &A, const double *b, double *u, double tol, int maxit, hipStream_t s,
                   int *status)
 {
-    const int n = k->n, nbe = k->nbe, nblk = A.nblk;
+    const int n = k->n, nblk = A.nblk;
     SSS_HIP(hipMemsetAsync(k->t, 0, sizeof(double) * n, s));
     SSS_HIP(hipMemsetAsync(k->u_best, 0, sizeof(double) * n, s));
-    hipLaunchKernelGGL(k_resid, dim3(nblk), dim3(kBlock), 0, s, A.blk, A.rp, A.ci, A.v, u, b, k->r, k->cap, k->P3,
-                       k->st, 0);
-    hipLaunchKernelGGL(k_cg_init, dim3(1), dim3(1024), 0, s, n, nblk, k->P3, k->r, k->p, tol, maxit, k->st, k->cst);
-    int K = 0;
+    hipLaunchKernelGGL(k_resid, dim3(nblk), dim3(kBlock), 0, s, A.blk, A.rp, A.ci, A.v, u, b, k->r, k->cap,
+                       (const CgState *)nullptr, 0);
+    hipLaunchKernelGGL(k_cg_init, dim3(1), dim3(kSeqBlock), 0, s, n, k->r, k->p, tol, maxit, k->st);
     for (int it = 1; it <= maxit; ++it) {
-        CgState *sin = k->st + (it & 1), *sout = k->st + ((it + 1) & 1);
-        hipLaunchKernelGGL(k_cg_spmv, dim3(nblk), dim3(kBlock), 0, s, A.blk, A.rp, A.ci, A.v, k->p, k->t, k->cap,
-                           k->P1, sin);
-        hipLaunchKernelGGL(k_cg_update, dim3(nbe), dim3(kBlock), 0, s, n, nblk, k->P1, u, k->r, k->p, k->t, k->P2, sin,
-                           k->cst, k->mb);
-        hipLaunchKernelGGL(k_cg_check, dim3(nblk), dim3(kBlock), 0, s, nbe, A.blk, A.rp, A.ci, A.v, u, b, k->r,
-                           k->u_best, k->cap, k->P2, k->P3, sin, k->cst, k->mb, k->mc);
-        hipLaunchKernelGGL(k_cg_commit, dim3(nbe), dim3(kBlock), 0, s, n, nblk, it, k->r, k->p, k->P3, sin, sout,
-                           k->cst, k->mb, k->mc);
-        K = it;
+        hipLaunchKernelGGL(k_acc, dim3(nblk), dim3(kBlock), 0, s, A.blk, A.rp, A.ci, A.v, k->p, k->t, k->cap,
+                           (const CgState *)k->st);
+        hipLaunchKernelGGL(k_cg_step, dim3(1), dim3(kSeqBlock), 0, s, n, it, u, k->r, k->p, k->t, k->u_best, k->st);
+        hipLaunchKernelGGL(k_resid, dim3(nblk), dim3(kBlock), 0, s, A.blk, A.rp, A.ci, A.v, u, b, k->r, k->cap,
+                           (const CgState *)k->st, 1);
+        hipLaunchKernelGGL(k_cg_fix, dim3(1), dim3(kSeqBlock), 0, s, n, it, k->r, k->p, k->st);
         if (it % kPoll == 0 || it == maxit || it == 1) {
-            SSS_HIP(hipMemcpyAsync(k->h_st, sout, sizeof(CgState), hipMemcpyDeviceToHost, s));
+            SSS_HIP(hipMemcpyAsync(k->h_st, k->st, sizeof(CgState), hipMemcpyDeviceToHost, s));
             SSS_HIP(hipStreamSynchronize(s));
             if (k->h_st->mode != CG_RUN) break;
         }
     }
-    CgState *sfin = k->st + ((K + 1) & 1);
     hipLaunchKernelGGL(k_resid, dim3(nblk), dim3(kBlock), 0, s, A.blk, A.rp, A.ci, A.v, k->u_best, b, k->r, k->cap,
-                       k->P3, sfin, 1);
-    hipLaunchKernelGGL(k_cg_restore, dim3(nbe), dim3(kBlock), 0, s, n, nblk, u, k->u_best, k->P3, sfin, k->cst);
+                       (const CgState *)k->st, 2);
+    hipLaunchKernelGGL(k_cg_restore, dim3(1), dim3(kSeqBlock), 0, s, n, u, k->u_best, k->r, k->st);
     SSS_HIP(hipGetLastError());
-    SSS_HIP(hipMemcpyAsync(k->h_cst, k->cst, sizeof(CgConst), hipMemcpyDeviceToHost, s));
+    SSS_HIP(hipMemcpyAsync(k->h_st, k->st, sizeof(CgState), hipMemcpyDeviceToHost, s));
     SSS_HIP(hipStreamSynchronize(s));
-    *status = k->h_cst->status;
+    *status = k->h_st->status;
     return 0;
 }
 
 static int run_gmres(CoarseKrylov *k, const DevCSR &A, const double *b, double *x, double tol, int maxit,
                      hipStream_t s, int *status)
 {
-    const int n = k->n, restart = max_RESTART, nbe = k->nbe;
+    const int n = k->n, restart = max_RESTART, nbe = (n + kBlock - 1) / kBlock;
     const double maxdiff = tol * 1e-4;
     double hh[max_RESTART + 1][max_RESTART] = {}, c[max_RESTART] = {}, sn[max_RESTART] = {}, rs[max_RESTART + 1] = {};
     double r_norm, normr0, absres = BIGFLOAT, relres, absres_best = BIGFLOAT, t, gamma;
     int iter = 0, iter_best = 0, i = 0, rc;
     double *P = k->gp;
     auto pv = [&](int q) { return P + (size_t)q * n; };
+    auto upload_rs = [&]() -> int {
+        SSS_HIP(hipStreamSynchronize(s));   // h_buf and rs_dev may still be in use
+        std::memcpy(k->h_buf, rs, sizeof(double) * (max_RESTART + 1));
+        SSS_HIP(hipMemcpyAsync(k->rs_dev, k->h_buf, sizeof(double) * (max_RESTART + 1), hipMemcpyHostToDevice, s));
+        return 0;
+    };
 
     SSS_HIP(hipMemsetAsync(P, 0, sizeof(double) * (size_t)(restart + 1) * n, s));
     SSS_HIP(hipMemsetAsync(k->gx_best, 0, sizeof(double) * n, s));
@@ -538,13 +486,15 @@ static int run_gmres(CoarseKrylov *k, const DevCSR &A, const double *b, double *
     }
     while (iter < maxit) {
         rs[0] = r_norm;
-        hipLaunchKernelGGL(k_scal, dim3(nbe), dim3(kBlock), 0, s, n, 1.0 / r_norm, pv(0));
+        t = 1.0 / r_norm;
+        hipLaunchKernelGGL(k_scal, dim3(nbe), dim3(kBlock), 0, s, n, t, pv(0));
         i = 0;
         while (i < restart && iter < maxit) {
             i++;
             iter++;
-            hipLaunchKernelGGL(k_acc, dim3(A.nblk), dim3(kBlock), 0, s, A.blk, A.rp, A.ci, A.v, pv(i - 1), pv(i), k->cap);
-            hipLaunchKernelGGL(k_mgs, dim3(1), dim3(1024), 0, s, n, i, P, k->hcol);
+            hipLaunchKernelGGL(k_acc, dim3(A.nblk), dim3(kBlock), 0, s, A.blk, A.rp, A.ci, A.v, pv(i - 1), pv(i), k->cap,
+                               (const CgState *)nullptr);
+            hipLaunchKernelGGL(k_mgs, dim3(1), dim3(kSeqBlock), 0, s, n, i, P, k->hcol);
             SSS_HIP(hipMemcpyAsync(k->h_buf, k->hcol, sizeof(double) * (i + 1), hipMemcpyDeviceToHost, s));
             SSS_HIP(hipStreamSynchronize(s));
             for (int j = 0; j <= i; ++j) hh[j][i - 1] = k->h_buf[j];
@@ -578,8 +528,7 @@ static int run_gmres(CoarseKrylov *k, const DevCSR &A, const double *b, double *
             absres_best = absres;
             iter_best = iter;
         }
-        std::memcpy(k->h_buf, rs, sizeof(double) * (max_RESTART + 1));
-        SSS_HIP(hipMemcpyAsync(k->rs_dev, k->h_buf, sizeof(double) * (max_RESTART + 1), hipMemcpyHostToDevice, s));
+        if ((rc = upload_rs())) return rc;
         hipLaunchKernelGGL(k_gm_update, dim3(nbe), dim3(kBlock), 0, s, n, i, P, k->rs_dev, x, k->gx_best, copy_best);
         if (relres <= tol) {
             if ((rc = host_resid_norm(k, A, x, b, k->gw, &r_norm, s))) return rc;
@@ -594,17 +543,14 @@ static int run_gmres(CoarseKrylov *k, const DevCSR &A, const double *b, double *
             rs[j] = c[j - 1] * rs[j];
         }
         if (i) {
-            SSS_HIP(hipStreamSynchronize(s));   // rs_dev may still be read by k_gm_update
-            std::memcpy(k->h_buf, rs, sizeof(double) * (max_RESTART + 1));
-            SSS_HIP(hipMemcpyAsync(k->rs_dev, k->h_buf, sizeof(double) * (max_RESTART + 1), hipMemcpyHostToDevice, s));
+            if ((rc = upload_rs())) return rc;
             hipLaunchKernelGGL(k_gm_recombine, dim3(nbe), dim3(kBlock), 0, s, n, i, P, k->rs_dev);
         }
     }
     if (iter != iter_best) {
         double best;
         if ((rc = host_resid_norm(k, A, k->gx_best, b, k->gw, &best, s))) return rc;
-        if (absres > best + maxdiff)
-            hipLaunchKernelGGL(k_copy, dim3(nbe), dim3(kBlock), 0, s, n, k->gx_best, x);
+        if (absres > best + maxdiff) hipLaunchKernelGGL(k_copy, dim3(nbe), dim3(kBlock), 0, s, n, k->gx_best, x);
     }
     SSS_HIP(hipGetLastError());
     SSS_HIP(hipStreamSynchronize(s));
@@ -615,7 +561,7 @@ static int run_gmres(CoarseKrylov *k, const DevCSR &A, const double *b, double *
 int coarse_krylov_solve(CoarseKrylov *k, const DevCSR &A, const double *b, double *x, double ctol, hipStream_t s)
 {
     const int n = A.n;
-    const int nn = (int)(int)((long long)n * n);
+    const int nn = (int)(long long)((long long)n * n);   // n*n in int, as the reference
     const int maxit = std::max(250, std::min(nn, 1000));
     int status = 0, rc;
     if ((rc = run_cg(k, A, b, x, ctol, maxit, s, &status))) return rc;

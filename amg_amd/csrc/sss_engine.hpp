@@ -47,6 +47,8 @@ struct DevCSR {
     double *v = nullptr;
     int nblk = 0;          // SpMV row blocks
     int *blk = nullptr;    // block -> first row (nblk + 1 entries)
+    bool wave_rows = false;  // long rows: wave-per-row kernels (avg nnz/row >= kWaveRowMin)
+    int ngrid = 0;           // workgroups of one SpMV launch (size of a per-block partial array)
 };
 int devcsr_upload(DevCSR &d, const SSS_MAT &h);
 void devcsr_free(DevCSR &d);
@@ -64,6 +66,12 @@ struct PassSchedule {          // rows of one class (F or C), grouped by DAG dep
     int *rows = nullptr;       // device
     int nrows = 0;
     int max_width = 0;
+    // Row-compacted CSR of this class (rows ascending) with CSR-adaptive blocking: used when
+    // the pass has no intra-class couplings (depth 1) or for C/F-Jacobi.
+    bool compact = false;
+    DevCSR sub;
+    int *map = nullptr;        // local row -> global row
+    double *y = nullptr;       // Jacobi: new values of this class, scattered after the pass
 };
 struct SmootherPlan {
     int kind = SSS_HIP_SMOOTH_EXACT;
@@ -72,7 +80,6 @@ struct SmootherPlan {
     double *d_later = nullptr; // ... for later sweeps (aliases d_first when all rows have a diagonal)
     int *cls = nullptr;        // per row: 1 if mark == 1 else 0
     bool long_rows = false;    // wave-per-row kernels
-    double *x_tmp = nullptr;   // Jacobi ping-pong buffer
 };
 int smoother_build(SmootherPlan &sp, const SSS_MAT &A, const int *mark, int kind);
 void smoother_free(SmootherPlan &sp);

@@ -14,6 +14,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <string>
+#include <vector>
 
 using namespace sss;
 
@@ -34,7 +35,11 @@ struct sss_hip_hier {
     double *d_norm = nullptr;
     double *h_norm = nullptr;    // pinned
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
-    int owns_device = 0;
+    // hipGraph replay of the cycle: segments between host-steered coarse solves (a null exec
+    // marks "run the Krylov coarse solve here"); the residual-norm tail has its own graph.
+    std::vector<hipGraphExec_t> cycle_steps;
+    bool cycle_graph_ready = false;
+    hipGraphExec_t resid_exec = nullptr;
 };
 
 static int env_int(const char *name, int dflt)
@@ -50,7 +55,7 @@ extern "C" void sss_hip_opts_default(sss_hip_opts *o)
     o->smoother = SSS_HIP_SMOOTH_EXACT;
     o->coarse = SSS_HIP_COARSE_KRYLOV;
     o->row_cap = env_int("SSS_HIP_ROWCAP", 0);
-    o->use_graph = env_int("SSS_HIP_GRAPH", 0);
+    o->use_graph = env_int("SSS_HIP_GRAPH", 1);
     o->verbose = env_int("SSS_HIP_VERBOSE", 0);
     if (const char *s = getenv("SSS_HIP_SMOOTHER")) {
         std::string v(s);
@@ -91,6 +96,9 @@ static void hier_release(sss_hip_hier *h)
         dev_free(L.wp);
         smoother_free(L.sm);
     }
+    for (auto g : h->cycle_steps)
+        if (g) (void)hipGraphExecDestroy(g);
+    if (h->resid_exec) (void)hipGraphExecDestroy(h->resid_exec);
     coarse_direct_free(h->direct);
     coarse_krylov_destroy(h->krylov);
     dev_free(h->partial);
@@ -139,7 +147,7 @@ extern "C" sss_hip_hier *sss_hip_hier_create(const SSS_AMG *mg, const sss_hip_op
             hipMemset(L.wp, 0, sizeof(double) * n) != hipSuccess)
             return fail("memset");
     }
-    h->partial = dev_alloc<double>((size_t)h->L[0].A.nblk);
+    h->partial = dev_alloc<double>((size_t)h->L[0].A.ngrid);
     h->d_norm = dev_alloc<double>(1);
     if (!h->partial || !h->d_norm || hipHostMalloc((void **)&h->h_norm, sizeof(double)) != hipSuccess)
         return fail("norm buffers");
@@ -154,6 +162,17 @@ extern "C" sss_hip_hier *sss_hip_hier_create(const SSS_AMG *mg, const sss_hip_op
         if (!h->krylov) return fail("coarse Krylov workspace");
     }
     if (hipStreamSynchronize(h->stream) != hipSuccess) return fail("sync");
+    // Graph replay only pays for, and is only robust with, a modest node count: the exact
+    // smoother on deep coarse levels issues one launch per DAG depth (~10^5 per cycle).
+    long long launches = 0;
+    for (int l = 0; l + 1 < h->nl; ++l) {
+        const auto &sm = h->L[l].sm;
+        long long per_sweep = 0;
+        for (const auto &ps : sm.pass)
+            per_sweep += ps.nrows == 0 ? 0 : ps.compact ? (sm.kind == SSS_HIP_SMOOTH_JACOBI ? 2 : 1) : ps.depth;
+        launches += per_sweep * (h->pars.pre_iter + h->pars.post_iter) + 4;
+    }
+    if (launches > 4096) h->opts.use_graph = 0;
     if (h->opts.verbose) {
         for (int l = 0; l < h->nl; ++l)
             fprintf(stderr, "[sss_hip] level %d: n=%d nnz=%d blocks=%d dagF=%d dagC=%d kind=%d\n", l, h->L[l].A.n,
@@ -213,10 +232,13 @@ extern "C" int sss_hip_smooth(sss_hip_hier *h, int level, int post)
     return smoother_run(L.sm, L.A, L.b, L.x, sweeps, h->stream);
 }
 
-extern "C" int sss_hip_cycle(sss_hip_hier *h)
+// Walks SSS_amg_cycle's static control flow, enqueueing kernels; `coarse(h)` is called where
+// the coarsest solve goes.
+template <class CoarseFn>
+static int walk_cycle(sss_hip_hier *h, CoarseFn coarse)
 {
     const int nl = h->nl;
-    int cycle_type = h->pars.cycle_type <= 0 ? 1 : h->pars.cycle_type;
+    const int cycle_type = h->pars.cycle_type <= 0 ? 1 : h->pars.cycle_type;
     int visits[kMaxLevels] = {0};
     int l = 0, rc;
     hipStream_t s = h->stream;
@@ -230,7 +252,7 @@ extern "C" int sss_hip_cycle(sss_hip_hier *h)
             l++;
             SSS_HIP(hipMemsetAsync(h->L[l].x, 0, sizeof(double) * (size_t)h->L[l].A.n, s));
         }
-        if ((rc = sss_hip_coarse_solve(h))) return rc;
+        if ((rc = coarse(h))) return rc;
         while (l > 0) {
             l--;
             auto &L = h->L[l];
@@ -244,18 +266,80 @@ extern "C" int sss_hip_cycle(sss_hip_hier *h)
     return 0;
 }
 
+static int end_capture(sss_hip_hier *h, hipGraphExec_t *exec)
+{
+    hipGraph_t g = nullptr;
+    SSS_HIP(hipStreamEndCapture(h->stream, &g));
+    hipError_t e = hipGraphInstantiate(exec, g, nullptr, nullptr, 0);
+    (void)hipGraphDestroy(g);
+    SSS_HIP(e);
+    return 0;
+}
+
+static int build_cycle_graph(sss_hip_hier *h)
+{
+    SSS_HIP(hipStreamBeginCapture(h->stream, hipStreamCaptureModeThreadLocal));
+    int rc = walk_cycle(h, [](sss_hip_hier *hh) -> int {
+        if (hh->coarse_mode == SSS_HIP_COARSE_DIRECT) return sss_hip_coarse_solve(hh);
+        hipGraphExec_t seg = nullptr;
+        int r = end_capture(hh, &seg);
+        if (r) return r;
+        hh->cycle_steps.push_back(seg);
+        hh->cycle_steps.push_back(nullptr);
+        SSS_HIP(hipStreamBeginCapture(hh->stream, hipStreamCaptureModeThreadLocal));
+        return 0;
+    });
+    hipGraphExec_t last = nullptr;
+    int rc2 = end_capture(h, &last);
+    if (rc) return rc;
+    if (rc2) return rc2;
+    h->cycle_steps.push_back(last);
+    h->cycle_graph_ready = true;
+    return 0;
+}
+
+extern "C" int sss_hip_cycle(sss_hip_hier *h)
+{
+    if (!h->opts.use_graph) return walk_cycle(h, [](sss_hip_hier *hh) { return sss_hip_coarse_solve(hh); });
+    if (!h->cycle_graph_ready) {
+        int rc = build_cycle_graph(h);
+        if (rc) return rc;
+    }
+    for (hipGraphExec_t g : h->cycle_steps) {
+        if (g) SSS_HIP(hipGraphLaunch(g, h->stream));
+        else {
+            int rc = sss_hip_coarse_solve(h);
+            if (rc) return rc;
+        }
+    }
+    return 0;
+}
+
 static int enqueue_residual_norm(sss_hip_hier *h)
 {
     auto &L = h->L[0];
     int rc = launch_spmv(L.A, SSS_HIP_SPMV_RESID, -1.0, L.x, L.b, L.wp, 0, h->partial, h->stream);
     if (rc) return rc;
-    return launch_final_sum(h->partial, L.A.nblk, h->d_norm, true, h->stream);
+    return launch_final_sum(h->partial, L.A.ngrid, h->d_norm, true, h->stream);
 }
 
 extern "C" int sss_hip_residual_norm(sss_hip_hier *h, double *absres)
 {
-    int rc = enqueue_residual_norm(h);
-    if (rc) return rc;
+    if (h->opts.use_graph) {
+        if (!h->resid_exec) {
+            SSS_HIP(hipStreamBeginCapture(h->stream, hipStreamCaptureModeThreadLocal));
+            int rc = enqueue_residual_norm(h);
+            hipGraphExec_t ex = nullptr;
+            int rc2 = end_capture(h, &ex);
+            if (rc) return rc;
+            if (rc2) return rc2;
+            h->resid_exec = ex;
+        }
+        SSS_HIP(hipGraphLaunch(h->resid_exec, h->stream));
+    } else {
+        int rc = enqueue_residual_norm(h);
+        if (rc) return rc;
+    }
     SSS_HIP(hipMemcpyAsync(h->h_norm, h->d_norm, sizeof(double), hipMemcpyDeviceToHost, h->stream));
     SSS_HIP(hipStreamSynchronize(h->stream));
     *absres = *h->h_norm;

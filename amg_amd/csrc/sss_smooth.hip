@@ -19,6 +19,7 @@
 // C/F-Jacobi (engine extension; SSS_SM_JACOBI): F pass then C pass, every row of a pass
 // reading the values from before the pass (ping-pong buffers), d = the row's last diagonal.
 #include "sss_engine.hpp"
+#include "sss_spmv_dev.hpp"
 
 #include <algorithm>
 #include <cmath>
@@ -72,7 +73,7 @@ int smoother_build(SmootherPlan &sp, const SSS_MAT &A, const int *mark, int kind
     }
     // level schedule per class
     long long nnz_total = rp[n];
-    sp.long_rows = n > 0 && nnz_total / n > 16;
+    sp.long_rows = n > 0 && nnz_total >= (long long)kWaveRowMin * n;
     for (int i = 0; i < n; ++i) {
         int dep = pushed[i];
         for (int k = rp[i]; k < rp[i + 1]; ++k) {
@@ -103,13 +104,38 @@ int smoother_build(SmootherPlan &sp, const SSS_MAT &A, const int *mark, int kind
         for (int i = 0; i < n; ++i)
             if (cls[i] == c) rows[fill[depth[i]]++] = i;
         if ((rc = upload_ints(&ps.rows, rows))) return rc;
+        ps.compact = kind == SSS_HIP_SMOOTH_JACOBI || ps.depth <= 1;
+        if (ps.compact && ps.nrows > 0) {
+            std::vector<int> crp(1, 0), cci, cmap;
+            std::vector<double> cv;
+            for (int i = 0; i < n; ++i) {
+                if (cls[i] != c) continue;
+                cmap.push_back(i);
+                for (int k = rp[i]; k < rp[i + 1]; ++k) {
+                    cci.push_back(ci[k] == i ? -1 : ci[k]);   // diagonal -> product +0.0 (identity)
+                    cv.push_back(v[k]);
+                }
+                crp.push_back((int)cci.size());
+            }
+            SSS_MAT sub;
+            sub.num_rows = (int)cmap.size();
+            sub.num_cols = A.num_cols;
+            sub.num_nnzs = (int)cci.size();
+            sub.row_ptr = crp.data();
+            sub.col_idx = cci.data();
+            sub.val = cv.data();
+            if ((rc = devcsr_upload(ps.sub, sub))) return rc;
+            if ((rc = upload_ints(&ps.map, cmap))) return rc;
+            if (kind == SSS_HIP_SMOOTH_JACOBI) {
+                ps.y = dev_alloc<double>(cmap.size());
+                if (!ps.y) return hip_fail(hipErrorOutOfMemory, "hipMalloc(y)", __FILE__, __LINE__);
+            }
+        }
     }
     if ((rc = upload_ints(&sp.cls, cls))) return rc;
     if (kind == SSS_HIP_SMOOTH_JACOBI) {
         if ((rc = upload_doubles(&sp.d_first, last_diag))) return rc;   // Jacobi: row's own diagonal
         sp.d_later = sp.d_first;
-        sp.x_tmp = dev_alloc<double>((size_t)n);
-        if (!sp.x_tmp) return hip_fail(hipErrorOutOfMemory, "hipMalloc(x_tmp)", __FILE__, __LINE__);
     } else {
         if ((rc = upload_doubles(&sp.d_first, d_first))) return rc;
         if (all_diag) sp.d_later = sp.d_first;
@@ -120,11 +146,15 @@ int smoother_build(SmootherPlan &sp, const SSS_MAT &A, const int *mark, int kind
 
 void smoother_free(SmootherPlan &sp)
 {
-    for (auto &ps : sp.pass) dev_free(ps.rows);
+    for (auto &ps : sp.pass) {
+        dev_free(ps.rows);
+        devcsr_free(ps.sub);
+        dev_free(ps.map);
+        dev_free(ps.y);
+    }
     if (sp.d_later != sp.d_first) dev_free(sp.d_later);
     dev_free(sp.d_first);
     dev_free(sp.cls);
-    dev_free(sp.x_tmp);
     sp = SmootherPlan();
 }
 
@@ -147,128 +177,109 @@ __global__ __launch_bounds__(kBlock) void gs_depth_thread(const int *__restrict_
     if (fabs(d) > SMALLFLOAT) x[i] = acc / d;
 }
 
-// exact GS, one wave per row: lanes form the products, lane 0 subtracts them in CSR order
-// (the diagonal contributes +0.0, an exact identity for subtraction)
-__global__ __launch_bounds__(64) void gs_depth_wave(const int *__restrict__ rows, const int *__restrict__ rp,
-                                                    const int *__restrict__ ci, const double *__restrict__ v,
-                                                    const double *__restrict__ b, double *x,
-                                                    const double *__restrict__ deff)
+// exact GS on long rows: four rows of the current depth per workgroup, one per wave; lanes
+// gather the products, lane 0 subtracts them in CSR order (sss_spmv_dev.hpp wave_row_chain).
+__global__ __launch_bounds__(kBlock) void gs_depth_wave(const int *__restrict__ rows, int cnt,
+                                                        const int *__restrict__ rp, const int *__restrict__ ci,
+                                                        const double *__restrict__ v, const double *__restrict__ b,
+                                                        double *x, const double *__restrict__ deff)
 {
-    __shared__ double prod[64];
-    const int i = rows[blockIdx.x];
-    const int lane = threadIdx.x;
-    const int k0 = rp[i], k1 = rp[i + 1];
-    double acc = b[i];
-    for (int base = k0; base < k1; base += 64) {
-        const int k = base + lane;
-        double p = 0.0;
-        if (k < k1) {
-            const int j = ci[k];
-            if (j != i) p = v[k] * x[j];
-        }
-        prod[lane] = p;
-        __syncthreads();
-        if (lane == 0) {
-            const int m = min(64, k1 - base);
-            for (int q = 0; q < m; ++q) acc -= prod[q];
-        }
-        __syncthreads();
-    }
-    if (lane == 0) {
+    __shared__ double strips[4][kWaveStage];
+    const int wave = threadIdx.x >> 6;
+    const int t = blockIdx.x * 4 + wave;
+    if (t >= cnt) return;
+    const int i = rows[t];
+    const double acc = wave_row_chain<true>(rp[i], rp[i + 1], ci, v, x, i, b[i], strips[wave]);
+    if ((threadIdx.x & 63) == 0) {
         const double d = deff[i];
         if (fabs(d) > SMALLFLOAT) x[i] = acc / d;
     }
 }
 
-// C/F-Jacobi pass over all rows: rows of class `c` are relaxed from x_in, others copied
-__global__ __launch_bounds__(kBlock) void jacobi_pass_thread(int n, int c, const int *__restrict__ cls,
-                                                             const int *__restrict__ rp, const int *__restrict__ ci,
-                                                             const double *__restrict__ v, const double *__restrict__ b,
-                                                             const double *__restrict__ x_in, double *__restrict__ x_out,
-                                                             const double *__restrict__ dg)
+// Independent-row pass over the class-compacted CSR: GS with depth 1 (in place) or the
+// relaxation half of a C/F-Jacobi pass (into y, scattered afterwards).
+template <bool INPLACE>
+__global__ __launch_bounds__(kBlock) void relax_compact(const int *__restrict__ blk, const int *__restrict__ rp,
+                                                        const int *__restrict__ ci, const double *__restrict__ v,
+                                                        const int *__restrict__ map, const double *__restrict__ b,
+                                                        double *x, double *__restrict__ y,
+                                                        const double *__restrict__ deff)
 {
-    const int i = blockIdx.x * kBlock + threadIdx.x;
-    if (i >= n) return;
-    double out = x_in[i];
-    if (c < 0 || cls[i] == c) {
-        double acc = b[i];
-        for (int k = rp[i]; k < rp[i + 1]; ++k) {
-            const int j = ci[k];
-            if (j != i) acc -= v[k] * x_in[j];
+    __shared__ SpmvSmem sm;
+    csr_block_relax(blk, rp, ci, v, map, b, x, sm, [&](int r, int i, double acc) {
+        const double d = deff[i];
+        if (INPLACE) {
+            if (fabs(d) > SMALLFLOAT) x[i] = acc / d;
+        } else {
+            y[r] = fabs(d) > SMALLFLOAT ? acc / d : x[i];
         }
-        const double d = dg[i];
-        if (fabs(d) > SMALLFLOAT) out = acc / d;
-    }
-    x_out[i] = out;
+    });
 }
 
-__global__ __launch_bounds__(64) void jacobi_pass_wave(int c, const int *__restrict__ cls, const int *__restrict__ rp,
-                                                       const int *__restrict__ ci, const double *__restrict__ v,
-                                                       const double *__restrict__ b, const double *__restrict__ x_in,
-                                                       double *__restrict__ x_out, const double *__restrict__ dg)
+template <bool INPLACE>
+__global__ __launch_bounds__(kBlock) void relax_wave(int m, const int *__restrict__ rp, const int *__restrict__ ci,
+                                                     const double *__restrict__ v, const int *__restrict__ map,
+                                                     const double *__restrict__ b, double *x, double *__restrict__ y,
+                                                     const double *__restrict__ deff)
 {
-    __shared__ double prod[64];
-    const int i = blockIdx.x;
-    const int lane = threadIdx.x;
-    if (!(c < 0 || cls[i] == c)) {
-        if (lane == 0) x_out[i] = x_in[i];
-        return;
-    }
-    const int k0 = rp[i], k1 = rp[i + 1];
-    double acc = b[i];
-    for (int base = k0; base < k1; base += 64) {
-        const int k = base + lane;
-        double p = 0.0;
-        if (k < k1) {
-            const int j = ci[k];
-            if (j != i) p = v[k] * x_in[j];
+    __shared__ double strips[4][kWaveStage];
+    const int wave = threadIdx.x >> 6;
+    const int r = blockIdx.x * 4 + wave;
+    if (r >= m) return;
+    const int i = map[r];
+    const double acc = wave_row_chain<true>(rp[r], rp[r + 1], ci, v, x, i, b[i], strips[wave]);
+    if ((threadIdx.x & 63) == 0) {
+        const double d = deff[i];
+        if (INPLACE) {
+            if (fabs(d) > SMALLFLOAT) x[i] = acc / d;
+        } else {
+            y[r] = fabs(d) > SMALLFLOAT ? acc / d : x[i];
         }
-        prod[lane] = p;
-        __syncthreads();
-        if (lane == 0) {
-            const int m = min(64, k1 - base);
-            for (int q = 0; q < m; ++q) acc -= prod[q];
-        }
-        __syncthreads();
     }
-    if (lane == 0) {
-        const double d = dg[i];
-        x_out[i] = fabs(d) > SMALLFLOAT ? acc / d : x_in[i];
-    }
+}
+
+__global__ __launch_bounds__(kBlock) void scatter_rows(int m, const int *__restrict__ map, const double *__restrict__ y,
+                                                       double *__restrict__ x)
+{
+    const int r = blockIdx.x * kBlock + threadIdx.x;
+    if (r < m) x[map[r]] = y[r];
 }
 
 int smoother_run(const SmootherPlan &sp, const DevCSR &A, const double *b, double *x, int sweeps, hipStream_t s)
 {
     const int n = A.n;
     if (n == 0) return 0;
-    if (sp.kind == SSS_HIP_SMOOTH_JACOBI) {
-        double *cur = x, *nxt = sp.x_tmp;
-        for (int sw = 0; sw < sweeps; ++sw) {
-            for (int c = 0; c < 2; ++c) {
-                if (sp.pass[c].nrows == 0) continue;
-                if (sp.long_rows)
-                    hipLaunchKernelGGL(jacobi_pass_wave, dim3(n), dim3(64), 0, s, c, sp.cls, A.rp, A.ci, A.v, b, cur,
-                                       nxt, sp.d_first);
-                else
-                    hipLaunchKernelGGL(jacobi_pass_thread, dim3((n + kBlock - 1) / kBlock), dim3(kBlock), 0, s, n, c,
-                                       sp.cls, A.rp, A.ci, A.v, b, cur, nxt, sp.d_first);
-                std::swap(cur, nxt);
-            }
-        }
-        if (cur != x) SSS_HIP(hipMemcpyAsync(x, cur, sizeof(double) * (size_t)n, hipMemcpyDeviceToDevice, s));
-        SSS_HIP(hipGetLastError());
-        return 0;
-    }
     for (int sw = 0; sw < sweeps; ++sw) {
         const double *deff = sw == 0 ? sp.d_first : sp.d_later;
         for (int c = 0; c < 2; ++c) {
             const PassSchedule &ps = sp.pass[c];
+            if (ps.nrows == 0) continue;
+            if (sp.kind == SSS_HIP_SMOOTH_JACOBI) {
+                if (ps.sub.wave_rows)
+                    hipLaunchKernelGGL(relax_wave<false>, dim3(ps.sub.ngrid), dim3(kBlock), 0, s, ps.nrows, ps.sub.rp,
+                                       ps.sub.ci, ps.sub.v, ps.map, b, x, ps.y, sp.d_first);
+                else
+                    hipLaunchKernelGGL(relax_compact<false>, dim3(ps.sub.nblk), dim3(kBlock), 0, s, ps.sub.blk,
+                                       ps.sub.rp, ps.sub.ci, ps.sub.v, ps.map, b, x, ps.y, sp.d_first);
+                hipLaunchKernelGGL(scatter_rows, dim3((ps.nrows + kBlock - 1) / kBlock), dim3(kBlock), 0, s, ps.nrows,
+                                   ps.map, ps.y, x);
+                continue;
+            }
+            if (ps.compact) {
+                if (ps.sub.wave_rows)
+                    hipLaunchKernelGGL(relax_wave<true>, dim3(ps.sub.ngrid), dim3(kBlock), 0, s, ps.nrows, ps.sub.rp,
+                                       ps.sub.ci, ps.sub.v, ps.map, b, x, (double *)nullptr, deff);
+                else
+                    hipLaunchKernelGGL(relax_compact<true>, dim3(ps.sub.nblk), dim3(kBlock), 0, s, ps.sub.blk,
+                                       ps.sub.rp, ps.sub.ci, ps.sub.v, ps.map, b, x, (double *)nullptr, deff);
+                continue;
+            }
             for (int l = 0; l < ps.depth; ++l) {
                 const int off = ps.h_off[l], cnt = ps.h_off[l + 1] - off;
                 if (cnt == 0) continue;
                 if (sp.long_rows)
-                    hipLaunchKernelGGL(gs_depth_wave, dim3(cnt), dim3(64), 0, s, ps.rows + off, A.rp, A.ci, A.v, b, x,
-                                       deff);
+                    hipLaunchKernelGGL(gs_depth_wave, dim3((cnt + 3) / 4), dim3(kBlock), 0, s, ps.rows + off, cnt, A.rp,
+                                       A.ci, A.v, b, x, deff);
                 else
                     hipLaunchKernelGGL(gs_depth_thread, dim3((cnt + kBlock - 1) / kBlock), dim3(kBlock), 0, s,
                                        ps.rows + off, cnt, A.rp, A.ci, A.v, b, x, deff);

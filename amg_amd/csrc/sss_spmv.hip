@@ -63,6 +63,8 @@ int devcsr_upload(DevCSR &d, const SSS_MAT &h)
     d.blk = dev_alloc<int>(blk.size());
     if (!d.blk) return hip_fail(hipErrorOutOfMemory, "hipMalloc(blk)", __FILE__, __LINE__);
     SSS_HIP(hipMemcpy(d.blk, blk.data(), sizeof(int) * blk.size(), hipMemcpyHostToDevice));
+    d.wave_rows = d.n > 0 && (long long)d.nnz >= (long long)kWaveRowMin * d.n;
+    d.ngrid = d.wave_rows ? (d.n + 3) / 4 : d.nblk;
     return 0;
 }
 
@@ -103,11 +105,48 @@ __global__ __launch_bounds__(kBlock) void spmv_adaptive(const int *__restrict__ 
 }
 
 template <int OP, bool NORM>
+__global__ __launch_bounds__(kBlock) void spmv_wave(int n, const int *__restrict__ rp, const int *__restrict__ ci,
+                                                    const double *__restrict__ v, const double *__restrict__ x,
+                                                    const double *__restrict__ b, double *__restrict__ y, double alpha,
+                                                    int cap, double *__restrict__ partial)
+{
+    __shared__ double strips[4][kWaveStage];
+    __shared__ double red[kBlock / 64];
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int r = blockIdx.x * 4 + wave;
+    double sq = 0.0;
+    if (r < n) {
+        const double s = wave_row_chain<false>(rp[r], rp[r + 1], ci, v, x, -1, 0.0, strips[wave]);
+        if (lane == 0) {
+            bool write = true;
+            double out;
+            if constexpr (OP == SSS_HIP_SPMV_MXY) out = s;
+            else if constexpr (OP == SSS_HIP_SPMV_AMXPY) out = y[r] + s * alpha;
+            else if constexpr (OP == SSS_HIP_SPMV_RESID) out = b[r] + s * alpha;
+            else {
+                write = !(cap > 0 && r >= cap);
+                out = write ? y[r] + s : 0.0;
+            }
+            if (write) y[r] = out;
+            if (NORM) sq = out * out;
+        }
+    }
+    if (NORM) {
+        const double t = block_sum(sq, red);
+        if (threadIdx.x == 0) partial[blockIdx.x] = t;
+    }
+}
+
+template <int OP, bool NORM>
 static void launch_op(const DevCSR &A, double alpha, const double *x, const double *b, double *y, int cap,
                       double *partial, hipStream_t s)
 {
-    hipLaunchKernelGGL((spmv_adaptive<OP, NORM>), dim3(A.nblk), dim3(kBlock), 0, s, A.blk, A.rp, A.ci, A.v, x, b,
-                       y, alpha, cap, partial);
+    if (A.wave_rows)
+        hipLaunchKernelGGL((spmv_wave<OP, NORM>), dim3(A.ngrid), dim3(kBlock), 0, s, A.n, A.rp, A.ci, A.v, x, b, y,
+                           alpha, cap, partial);
+    else
+        hipLaunchKernelGGL((spmv_adaptive<OP, NORM>), dim3(A.nblk), dim3(kBlock), 0, s, A.blk, A.rp, A.ci, A.v, x,
+                           b, y, alpha, cap, partial);
 }
 
 int launch_spmv(const DevCSR &A, int op, double alpha, const double *x, const double *b, double *y, int cap,
@@ -167,6 +206,8 @@ extern "C" sss_hip_spmv_plan *sss_hip_spmv_plan_create(int n, int nnz, const int
     p->csr.nnz = nnz;
     p->csr.rp = const_cast<int *>(d_rp);
     p->csr.nblk = sss::build_row_blocks(h_rp, n, blk);
+    p->csr.wave_rows = n > 0 && (long long)nnz >= (long long)sss::kWaveRowMin * n;
+    p->csr.ngrid = p->csr.wave_rows ? (n + 3) / 4 : p->csr.nblk;
     p->csr.blk = sss::dev_alloc<int>(blk.size());
     if (!p->csr.blk || hipMemcpy(p->csr.blk, blk.data(), sizeof(int) * blk.size(), hipMemcpyHostToDevice) != hipSuccess) {
         sss::dev_free(p->csr.blk);

@@ -11,10 +11,34 @@
 namespace sss {
 
 struct SpmvSmem {
-    double v[kTileEntries];
-    int c[kTileEntries];
+    double v[kTileEntries];    // products a_k * x_{c_k} of the tile
     double red[kBlock / 64];
 };
+
+// In-order chains over LDS products: 8 reads issued ahead of 8 dependent adds/subtractions,
+// the additions themselves in exactly the stored order.
+__device__ __forceinline__ double chain_add(double s, const double *p, int a, int e)
+{
+    int k = a;
+    for (; k + 8 <= e; k += 8) {
+        const double p0 = p[k], p1 = p[k + 1], p2 = p[k + 2], p3 = p[k + 3];
+        const double p4 = p[k + 4], p5 = p[k + 5], p6 = p[k + 6], p7 = p[k + 7];
+        s += p0; s += p1; s += p2; s += p3; s += p4; s += p5; s += p6; s += p7;
+    }
+    for (; k < e; ++k) s += p[k];
+    return s;
+}
+__device__ __forceinline__ double chain_sub(double s, const double *p, int a, int e)
+{
+    int k = a;
+    for (; k + 8 <= e; k += 8) {
+        const double p0 = p[k], p1 = p[k + 1], p2 = p[k + 2], p3 = p[k + 3];
+        const double p4 = p[k + 4], p5 = p[k + 5], p6 = p[k + 6], p7 = p[k + 7];
+        s -= p0; s -= p1; s -= p2; s -= p3; s -= p4; s -= p5; s -= p6; s -= p7;
+    }
+    for (; k < e; ++k) s -= p[k];
+    return s;
+}
 
 // Fixed-order block reduction (xor butterfly inside the wave, then waves in order).
 // Result valid in thread 0.  Must be reached by every thread of the block.
@@ -45,6 +69,10 @@ __device__ __forceinline__ double block_max(double v, double *red)
 }
 
 // Returns this thread's summed epilogue contribution (0 for idle threads).
+// Phase 1: every thread of the workgroup forms products of the tile (coalesced val/col loads,
+// independent x gathers, all in flight).  Phase 2: one thread per row adds its products from
+// LDS in stored order starting from 0.0 (SSS_utils.c:174).  Rows longer than the tile are
+// processed alone, tile by tile, with thread 0 carrying the chain.
 template <class Epi>
 __device__ __forceinline__ double csr_block_rows(const int *__restrict__ blk, const int *__restrict__ rp,
                                                  const int *__restrict__ ci, const double *__restrict__ v,
@@ -55,16 +83,11 @@ __device__ __forceinline__ double csr_block_rows(const int *__restrict__ blk, co
     const int cnt = k1 - k0;
     double contrib = 0.0;
     if (cnt <= kTileEntries) {
-        for (int k = threadIdx.x; k < cnt; k += kBlock) {
-            sm.v[k] = v[k0 + k];
-            sm.c[k] = ci[k0 + k];
-        }
+        for (int k = threadIdx.x; k < cnt; k += kBlock) sm.v[k] = v[k0 + k] * x[ci[k0 + k]];
         __syncthreads();
         const int r = r0 + (int)threadIdx.x;
         if (r < r1) {
-            const int a = rp[r] - k0, e = rp[r + 1] - k0;
-            double s = 0.0;
-            for (int k = a; k < e; ++k) s += sm.v[k] * x[sm.c[k]];
+            const double s = chain_add(0.0, sm.v, rp[r] - k0, rp[r + 1] - k0);
             contrib = epi(r, s);
         }
     } else {
@@ -73,22 +96,112 @@ __device__ __forceinline__ double csr_block_rows(const int *__restrict__ blk, co
             const int m = min(kTileEntries, k1 - base);
             for (int k = threadIdx.x; k < m; k += kBlock) sm.v[k] = v[base + k] * x[ci[base + k]];
             __syncthreads();
-            if (threadIdx.x == 0) {
-                int k = 0;
-                for (; k + 4 <= m; k += 4) {
-                    const double p0 = sm.v[k], p1 = sm.v[k + 1], p2 = sm.v[k + 2], p3 = sm.v[k + 3];
-                    s += p0;
-                    s += p1;
-                    s += p2;
-                    s += p3;
-                }
-                for (; k < m; ++k) s += sm.v[k];
-            }
+            if (threadIdx.x == 0) s = chain_add(s, sm.v, 0, m);
             __syncthreads();
         }
         if (threadIdx.x == 0) contrib = epi(r0, s);
     }
     return contrib;
+}
+
+}  // namespace sss
+
+namespace sss {
+
+// Relaxation rows over a row-compacted CSR (one smoother class): local row r is global row
+// map[r]; diagonal entries carry column -1 (set at upload) so their product is +0.0, an exact
+// identity for subtraction.  The chain is  acc = b_i;  acc -= a_k * x_{j_k}  for every
+// off-diagonal entry in stored order — exactly Solve/SSS_smooth.c:21-26 — then `epi(r, i, acc)`.
+template <class Epi>
+__device__ __forceinline__ void csr_block_relax(const int *__restrict__ blk, const int *__restrict__ rp,
+                                                const int *__restrict__ ci, const double *__restrict__ v,
+                                                const int *__restrict__ map, const double *__restrict__ b,
+                                                const double *x, SpmvSmem &sm, Epi epi)
+{
+    const int r0 = blk[blockIdx.x], r1 = blk[blockIdx.x + 1];
+    const int k0 = rp[r0], k1 = rp[r1];
+    const int cnt = k1 - k0;
+    if (cnt <= kTileEntries) {
+        for (int k = threadIdx.x; k < cnt; k += kBlock) {
+            const int j = ci[k0 + k];
+            sm.v[k] = j < 0 ? 0.0 : v[k0 + k] * x[j];
+        }
+        __syncthreads();
+        const int r = r0 + (int)threadIdx.x;
+        if (r < r1) {
+            const int i = map[r];
+            const double acc = chain_sub(b[i], sm.v, rp[r] - k0, rp[r + 1] - k0);
+            epi(r, i, acc);
+        }
+    } else {
+        const int i = map[r0];
+        double acc = b[i];
+        for (int base = k0; base < k1; base += kTileEntries) {
+            const int m = min(kTileEntries, k1 - base);
+            for (int k = threadIdx.x; k < m; k += kBlock) {
+                const int j = ci[base + k];
+                sm.v[k] = j < 0 ? 0.0 : v[base + k] * x[j];
+            }
+            __syncthreads();
+            if (threadIdx.x == 0) acc = chain_sub(acc, sm.v, 0, m);
+            __syncthreads();
+        }
+        if (threadIdx.x == 0) epi(r0, i, acc);
+    }
+}
+
+}  // namespace sss
+
+namespace sss {
+
+// ---- wave-per-row path for long rows (avg nnz/row >= kWaveRowMin) ----------------------------
+// Four rows per 256-thread workgroup, one per wave.  All 64 lanes gather a_k * x_{j_k} for a
+// strip of the row (every load in flight at once) into the wave's private LDS strip; lane 0 then
+// runs the reference's in-order chain over the strip.  LDS traffic of one wave is in order, so a
+// wave-level fence is the only synchronisation needed.
+constexpr int kWaveStage = 1024;   // doubles per wave strip (8 KiB; 32 KiB per workgroup)
+constexpr int kWaveRowMin = 1 << 30;   // wave path disabled: the tile path wins at every measured row length
+
+__device__ __forceinline__ void wave_sync()
+{
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// SUB = false: returns 0.0 + p_0 + p_1 + ... (SpMV order, SSS_utils.c:174).
+// SUB = true : returns init - p_0 - p_1 - ... skipping j == self (GS order, SSS_smooth.c:21-26).
+// Result valid in lane 0 of the wave.
+template <bool SUB>
+__device__ __forceinline__ double wave_row_chain(int k0, int k1, const int *__restrict__ ci,
+                                                 const double *__restrict__ v, const double *x, int self,
+                                                 double init, double *strip)
+{
+    const int lane = threadIdx.x & 63;
+    double acc = init;
+    for (int base = k0; base < k1; base += kWaveStage) {
+        const int m = min(kWaveStage, k1 - base);
+        for (int q = lane; q < m; q += 64) {
+            const int j = ci[base + q];
+            strip[q] = (j < 0 || (SUB && j == self)) ? 0.0 : v[base + q] * x[j];
+        }
+        wave_sync();
+        if (lane == 0) {
+            int q = 0;
+            for (; q + 8 <= m; q += 8) {
+                const double a0 = strip[q], a1 = strip[q + 1], a2 = strip[q + 2], a3 = strip[q + 3];
+                const double a4 = strip[q + 4], a5 = strip[q + 5], a6 = strip[q + 6], a7 = strip[q + 7];
+                if (SUB) { acc -= a0; acc -= a1; acc -= a2; acc -= a3; acc -= a4; acc -= a5; acc -= a6; acc -= a7; }
+                else { acc += a0; acc += a1; acc += a2; acc += a3; acc += a4; acc += a5; acc += a6; acc += a7; }
+            }
+            for (; q < m; ++q) {
+                if (SUB) acc -= strip[q];
+                else acc += strip[q];
+            }
+        }
+        wave_sync();
+    }
+    return acc;
 }
 
 }  // namespace sss

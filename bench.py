@@ -1,0 +1,248 @@
+"""bench.py — V-cycle iterations/s + fine-level SpMV HBM GB/s on the 7-pt Poisson problem.
+
+BASELINE.json metric: "V-cycle iters/sec + fine-level SpMV GB/s (%HBM peak), 64M-row 7pt Poisson".
+A step = one outer iteration of SSS_amg_solve (Solve/SSS_SOLVE.c:53-80): one V-cycle, r = b - A0 x,
+||r|| read back to the host.  Workload at N=1: 7-pt Poisson 400^3 (64,000,000 rows), FP64, b = x0 = 1
+(SSS_main.c:141-145), synthetic operator generated in memory (a 400^3 .mtx would be ~60 GB of text).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--n 400] [--mode throughput|parity]
+                    [--no-cpu-baseline]
+
+Modes:
+  throughput : exact GS-CF on level 0 (red-black -> fully parallel), C/F-Jacobi on coarser levels,
+               explicit-inverse coarse solve.  Converges to the same tolerance, a few more V-cycles.
+  parity     : exact GS-CF on every level + the reference CG(beta=1)+GMRES coarse solve; x is bitwise
+               identical to the reference after every V-cycle (tests/test_gpu_parity.py).
+
+N > 1 (launched by torch.distributed.run): each rank solves its own replica of the workload on its
+own GPU (weak scaling, no data-path collective yet); `value` = all ranks' V-cycles / max-over-ranks
+time.  The row-partitioned RCCL version is on the DESIGN.md roadmap.
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes as C
+import json
+import os
+import sys
+import threading
+import time
+from pathlib import Path
+
+import numpy as np
+
+ROOT = Path(__file__).resolve().parent
+sys.path.insert(0, str(ROOT))
+
+PEAK_HBM_GBS = 8000.0       # MI355X HBM3E spec (MI355X_MICROARCH.md:36)
+COPY_PEAK_GBS = 6290.0      # measured float4 copy peak (same source)
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=10)
+    p.add_argument("--warmup", type=int, default=3)
+    p.add_argument("--n", type=int, default=400, help="grid edge per rank (400 -> 64M rows)")
+    p.add_argument("--mode", default="throughput", choices=["throughput", "parity"])
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--cpu-n", type=int, default=0, help="grid edge of the CPU sample (default: same workload)")
+    p.add_argument("--mode-smoother", default=None, help="override: exact|hybrid|jacobi")
+    p.add_argument("--mode-coarse", default=None, help="override: krylov|direct")
+    p.add_argument("--converge-max", type=int, default=100, help="max V-cycles of the iterations-to-tol run (0: skip)")
+    return p.parse_args()
+
+
+class Dist:
+    """torch.distributed (gloo, host-side barrier / max only) when launched with WORLD_SIZE > 1."""
+
+    def __init__(self):
+        self.world = int(os.environ.get("WORLD_SIZE", "1"))
+        self.rank = int(os.environ.get("RANK", "0"))
+        self.local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+        self.pg = None
+        if self.world > 1:
+            import torch.distributed as dist
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            dist.init_process_group("gloo")
+            self.dist = dist
+
+    def barrier(self):
+        if self.world > 1:
+            self.dist.barrier()
+
+    def max(self, v: float) -> float:
+        if self.world == 1:
+            return v
+        import torch
+        t = torch.tensor([v], dtype=torch.float64)
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
+        return float(t.item())
+
+    def close(self):
+        if self.world > 1:
+            self.dist.destroy_process_group()
+
+
+def quiet_call(fn, *a, **kw):
+    """Run fn with the C library's stdout (setup tables) sent to stderr."""
+    sys.stdout.flush()
+    saved = os.dup(1)
+    os.dup2(2, 1)
+    try:
+        return fn(*a, **kw)
+    finally:
+        C.CDLL(None).fflush(None)
+        os.dup2(saved, 1)
+        os.close(saved)
+
+
+def cpu_baseline_worker(H, out: dict):
+    """One outer iteration of the CPU restatement (reference semantics, 1 thread)."""
+    import oracle
+    ora = oracle.load()
+    n = H.level(0).A.num_rows
+    b = np.ones(n)
+    x = np.ones(n)
+    from amg_amd._native import SSS_VEC, dptr
+    H.mg.cg[0].x = SSS_VEC(n, dptr(x))
+    H.mg.cg[0].b = SSS_VEC(n, dptr(b))
+    opts = oracle.opts()
+    ora.ora_reset_timers()
+    t0 = time.perf_counter()
+    ora.ora_cycle(C.byref(H.mg), C.byref(opts))
+    r = np.empty(n)
+    r[:] = b
+    ora.ora_mv_amxpy(-1.0, C.byref(H.level(0).A), dptr(x), dptr(r), 0)
+    float(np.sqrt(np.dot(r, r)))
+    dt = time.perf_counter() - t0
+    out.update(seconds=dt, coarse_seconds=ora.ora_coarse_seconds())
+
+
+def main():
+    args = parse()
+    D = Dist()
+    import amg_amd as A
+
+    if D.world > 1:
+        os.environ["SSS_HIP_DEVICE"] = str(D.local_rank)
+    n = args.n
+    smoother, coarse = ("hybrid", "direct") if args.mode == "throughput" else ("exact", "krylov")
+    smoother = args.mode_smoother or smoother
+    coarse = args.mode_coarse or coarse
+
+    t0 = time.perf_counter()
+    M = A.generate(7, n)
+    H = quiet_call(A.Hierarchy, M)
+    setup_s = time.perf_counter() - t0
+    A.lib().SSS_mat_destroy(C.byref(M))
+    N = H.level(0).A.num_rows
+    nnz = H.level(0).A.num_nnzs
+
+    t0 = time.perf_counter()
+    dev = D.local_rank if D.world > 1 else -1
+    DH = A.DeviceHierarchy(H, smoother=smoother, coarse=coarse, device=dev)
+    upload_s = time.perf_counter() - t0
+    ones = np.ones(N)
+    DH.upload(0, "b", ones)
+    DH.upload(0, "x", ones)
+
+    cpu = {}
+    cpu_thread = None
+    if D.rank == 0 and D.world == 1 and not args.no_cpu_baseline:
+        Hc = H
+        if args.cpu_n and args.cpu_n != n:
+            Mc = A.generate(7, args.cpu_n)
+            Hc = quiet_call(A.Hierarchy, Mc)
+        cpu_thread = threading.Thread(target=cpu_baseline_worker, args=(Hc, cpu), daemon=True)
+        cpu_thread.start()
+
+    for _ in range(args.warmup):
+        DH.cycle()
+        DH.residual_norm()
+    DH.sync()
+    D.barrier()
+    t0 = time.perf_counter()
+    absres = 0.0
+    for it in range(args.steps):
+        DH.cycle()
+        absres = DH.residual_norm()      # synchronises (8-byte D2H per iteration, as the reference)
+        if args.steps <= 4:
+            print(f"[bench] timed step {it + 1}", file=sys.stderr, flush=True)
+    DH.sync()
+    t1 = time.perf_counter()
+    D.barrier()
+    elapsed = D.max(t1 - t0)
+    ms_per_step = elapsed * 1e3 / args.steps
+    value = D.world * args.steps / elapsed
+
+    # roofline of the dominant streaming kernel: level-0 fused residual SpMV (wp = b - A0 x)
+    spmv_ms = DH.time_level0_spmv(20)
+    spmv_bytes = 12 * nnz + 4 * (N + 1) + 8 * N + 8 * N + 8 * N   # val+col, row_ptr, x, b, y
+    achieved = spmv_bytes / (spmv_ms * 1e-3) / 1e9
+
+    # iterations to tol from x0 = 1 (the CLI's problem), and time to solution
+    DH.upload(0, "x", ones)
+    sumb = float(np.sqrt(N))
+    its = 0
+    t0 = time.perf_counter()
+    relres = 1.0
+    while its < args.converge_max:
+        DH.cycle()
+        relres = DH.residual_norm() / sumb
+        its += 1
+        print(f"[bench] converge iteration {its}: relres {relres:.6e}", file=sys.stderr, flush=True)
+        if relres < H.pars.tol:
+            break
+    solve_s = time.perf_counter() - t0
+    levels = [(H.level(l).A.num_rows, H.level(l).A.num_nnzs) for l in range(H.num_levels)]
+
+    traffic = None
+    pmc = ROOT / "profiles" / "r01_level0_spmv_pmc.json"
+    if pmc.exists():
+        try:
+            rec = json.loads(pmc.read_text())
+            if rec.get("n") == n:
+                traffic = rec.get("hbm_bytes_per_launch")
+        except Exception:
+            traffic = None
+
+    cpu_baseline = None
+    if cpu_thread is not None:
+        cpu_thread.join()
+        if cpu.get("seconds"):
+            cpu_n = args.cpu_n or n
+            cpu_baseline = {
+                "value": 1.0 / cpu["seconds"], "unit": "V-cycle iter/s", "cores": 1, "kind": "port",
+                "sample": f"one outer iteration (V-cycle incl. reference CG(beta=1)+GMRES coarse solve, "
+                          f"residual, norm) of oracle/sss_oracle.c on the same 7-pt {cpu_n}^3 hierarchy, "
+                          f"1 host thread; coarse solve {cpu['coarse_seconds']:.1f} s of {cpu['seconds']:.1f} s",
+                "seconds": cpu["seconds"], "coarse_seconds": cpu["coarse_seconds"],
+            }
+
+    rec = {
+        "metric": "V-cycle iters/sec + fine-level SpMV GB/s (%HBM peak), 64M-row 7pt Poisson",
+        "value": value, "unit": "V-cycle iter/s", "n_gpus": D.world, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": ms_per_step, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+        "dtype": "f64", "data": "synthetic (7-pt Poisson generated in memory, b = x0 = 1)",
+        "config": {"workload": f"poisson7_{n}^3", "rows": N, "nnz": nnz, "levels": len(levels),
+                   "mode": args.mode, "smoother": smoother, "coarse": coarse,
+                   "iterations_to_tol": its, "final_relres": relres, "time_to_solution_s": solve_s,
+                   "setup_s": setup_s, "upload_s": upload_s,
+                   "parallelism": f"replicas{D.world}" if D.world > 1 else "single-gpu"},
+        "roofline": {"bound": "hbm", "kernel": "spmv_adaptive<RESID> level 0", "achieved": achieved,
+                     "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": achieved / PEAK_HBM_GBS,
+                     "frac_of_copy_peak": achieved / COPY_PEAK_GBS, "avg_launch_ms": spmv_ms,
+                     "bytes_per_launch": spmv_bytes, "traffic": traffic},
+        "cpu_baseline": cpu_baseline,
+    }
+    if cpu_baseline:
+        rec["speedup_vs_cpu"] = value / cpu_baseline["value"]
+    DH.close()
+    if D.rank == 0:
+        print(json.dumps(rec), flush=True)
+    D.close()
+
+
+if __name__ == "__main__":
+    main()

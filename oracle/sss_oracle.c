@@ -76,6 +76,7 @@ void ora_opts_default(ora_opts *o)
 {
     memset(o, 0, sizeof(*o));
     o->jacobi_from = 1;
+    o->omega = 1.0;
 }
 
 /* ---------------------------------------------------------------- BLAS-1, sequential order */
@@ -178,7 +179,8 @@ void ora_gs(double *u, int i1, int in, int step, const SSS_MAT *A, const double 
 /* C/F-Jacobi (engine extension): per sweep an F pass then a C pass; inside a pass
  * every row reads the values from before the pass.  d = last diagonal entry of the row; rows
  * with |d| <= 1e-20 (or none) are left unchanged.  mark == NULL: one pass over all rows. */
-void ora_cf_jacobi(double *u, const SSS_MAT *A, const double *b, int sweeps, const int *mark)
+void ora_cf_jacobi_w(double *u, const SSS_MAT *A, const double *b, int sweeps, const int *mark, double omega,
+                     int l1)
 {
     const int n = A->num_rows;
     double *old = (double *)malloc(sizeof(double) * (size_t)(n > 0 ? n : 1));
@@ -186,20 +188,33 @@ void ora_cf_jacobi(double *u, const SSS_MAT *A, const double *b, int sweeps, con
         for (int pass = 0; pass < (mark ? 2 : 1); ++pass) {
             copy(n, u, old);
             for (int i = 0; i < n; ++i) {
-                double t, d = 0.0;
+                double t, d = 0.0, off = 0.0;
                 if (mark && (mark[i] == 1) != pass) continue;
                 t = b[i];
                 for (int k = A->row_ptr[i]; k < A->row_ptr[i + 1]; ++k) {
                     int j = A->col_idx[k];
-                    if (j != i) t -= A->val[k] * old[j];
-                    else d = A->val[k];
+                    if (j != i) {
+                        t -= A->val[k] * old[j];
+                        if (l1 && (!mark || (mark[j] == 1) == pass)) off += SSS_ABS(A->val[k]);
+                    } else d = A->val[k];
                 }
-                if (SSS_ABS(d) > SMALLFLOAT) u[i] = t / d;
+                if (l1) d += off;
+                if (SSS_ABS(d) > SMALLFLOAT) {
+                    const double xn = t / d;
+                    u[i] = omega == 1.0 ? xn : old[i] + omega * (xn - old[i]);
+                }
             }
         }
     }
     free(old);
 }
+
+void ora_cf_jacobi(double *u, const SSS_MAT *A, const double *b, int sweeps, const int *mark)
+{
+    ora_cf_jacobi_w(u, A, b, sweeps, mark, 1.0, 0);
+}
+
+static const ora_opts *g_cur_opts = NULL;
 
 static void smoother_dispatch(SSS_SMTR *s, int post, const char *fname)
 {
@@ -211,7 +226,8 @@ static void smoother_dispatch(SSS_SMTR *s, int post, const char *fname)
         else ora_gs(s->x->d, s->iend, s->istart, s->istep, s->A, s->b->d, s->nsweeps);
         break;
     case SSS_SM_JACOBI:
-        ora_cf_jacobi(s->x->d, s->A, s->b->d, s->nsweeps, use_cf ? s->ordering : NULL);
+        ora_cf_jacobi_w(s->x->d, s->A, s->b->d, s->nsweeps, use_cf ? s->ordering : NULL,
+                        g_cur_opts ? g_cur_opts->omega : 1.0, g_cur_opts ? g_cur_opts->jacobi_l1 : 0);
         break;
     default:
         printf("### ERROR: Wrong smoother type %d!\n", s->smoother);
@@ -533,8 +549,10 @@ static void level_smoother(SSS_AMG *mg, int l, int post, const ora_opts *o)
     s.ndeg = mg->pars.poly_deg;
     s.cf_order = mg->pars.cf_order;
     s.ordering = mg->cg[l].cfmark.d;
+    g_cur_opts = o;
     if (post) ora_smoother_post(&s);
     else ora_smoother_pre(&s);
+    g_cur_opts = NULL;
 }
 
 void ora_cycle(SSS_AMG *mg, const ora_opts *o)

@@ -20,6 +20,8 @@ typedef struct {
     int smoother;     /* 0: exact smoother per pars (GS-CF); 1: C/F-Jacobi on levels >= jacobi_from */
     int jacobi_from;  /* first level that uses C/F-Jacobi when smoother == 1 */
     int verbose;      /* print the reference iteration table */
+    int jacobi_l1;    /* C/F-Jacobi divisor: 0 = a_ii, 1 = a_ii + sum_{j != i} |a_ij| over same-class j (l1) */
+    double omega;     /* C/F-Jacobi weight (1.0 = plain) */
 } ora_opts;
 
 void ora_opts_default(ora_opts *o);
@@ -33,6 +35,8 @@ void ora_mv_acc(const SSS_MAT *A, const double *x, double *y, int cap);
 void ora_gs_cf(double *u, const SSS_MAT *A, const double *b, int sweeps, const int *mark, int order);
 void ora_gs(double *u, int i1, int in, int step, const SSS_MAT *A, const double *b, int sweeps);
 void ora_cf_jacobi(double *u, const SSS_MAT *A, const double *b, int sweeps, const int *mark);
+void ora_cf_jacobi_w(double *u, const SSS_MAT *A, const double *b, int sweeps, const int *mark, double omega,
+                     int l1);
 void ora_smoother_pre(SSS_SMTR *s);
 void ora_smoother_post(SSS_SMTR *s);
 

@@ -1,0 +1,90 @@
+"""Shared test setup.
+
+Markers:  gpu — needs a HIP device (run on the MI355X box: `pytest -m gpu`); everything else
+runs on CPU here.  The product library and the oracle are built on first use if missing.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+import sys
+from pathlib import Path
+
+import numpy as np
+import pytest
+
+ROOT = Path(__file__).resolve().parent.parent
+sys.path.insert(0, str(ROOT))
+
+GOLDEN = ROOT / "tests" / "golden"
+REF_MTX = Path("/root/reference/amg/Matrix/1138_bus.mtx")
+BUS_MTX = GOLDEN / "1138_bus.mtx" if (GOLDEN / "1138_bus.mtx").exists() else REF_MTX
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs an AMD GPU (MI355X) with the HIP runtime")
+    config.addinivalue_line("markers", "slow: larger CPU cases")
+
+
+def _ensure_built():
+    lib = ROOT / "amg_amd" / "lib" / "libsss_amg.so"
+    ora = ROOT / "oracle" / "liboracle.so"
+    if not lib.exists():
+        subprocess.run(["make", "-j8"], cwd=ROOT, check=True, stdout=subprocess.DEVNULL)
+    if not ora.exists():
+        subprocess.run(["make", "oracle"], cwd=ROOT, check=True, stdout=subprocess.DEVNULL)
+
+
+_ensure_built()
+
+import amg_amd as A  # noqa: E402
+import oracle  # noqa: E402
+from amg_amd._native import dptr, iptr  # noqa: E402
+
+
+def vec(a: np.ndarray) -> A.SSS_VEC:
+    return A.SSS_VEC(len(a), dptr(a))
+
+
+def seq_sum(a: np.ndarray) -> float:
+    """Left-to-right sum (the reference's order), for 17-digit known-answer checks."""
+    return float(np.cumsum(a)[-1]) if len(a) else 0.0
+
+
+def oracle_solve(H, b: np.ndarray, x: np.ndarray, **kw):
+    """Run the CPU oracle's SSS_amg_solve; returns (rtn, relres history)."""
+    rel = np.zeros(128)
+    ab = np.zeros(128)
+    o = oracle.opts(**kw)
+    rtn = oracle.load().ora_solve(C.byref(H.mg), C.byref(vec(x)), C.byref(vec(b)), C.byref(o), dptr(rel),
+                                  dptr(ab), 128)
+    return rtn, rel[: rtn.nits].copy(), ab[: rtn.nits].copy()
+
+
+@pytest.fixture(scope="session")
+def bus_matrix():
+    return A.read_mtx(BUS_MTX)
+
+
+@pytest.fixture(scope="session")
+def quiet():
+    """Silence the C library's stdout chatter (setup prints) at the fd level."""
+    class Q:
+        def __enter__(self):
+            sys.stdout.flush()
+            self.saved = os.dup(1)
+            self.null = os.open(os.devnull, os.O_WRONLY)
+            os.dup2(self.null, 1)
+
+        def __exit__(self, *a):
+            C.CDLL(None).fflush(None)
+            os.dup2(self.saved, 1)
+            os.close(self.saved)
+            os.close(self.null)
+    return Q
+
+
+def build_hierarchy(M, quiet_cls):
+    with quiet_cls():
+        return A.Hierarchy(M)

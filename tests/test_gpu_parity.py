@@ -1,0 +1,300 @@
+"""GPU parity tests (run on the MI355X box: `pytest -m gpu`).
+
+Every comparison is HIP path (through the C ABI of libsss_amg.so) vs the CPU oracle on the same
+inputs.  Tolerance ladder:
+  * SpMV / residual / restriction / prolongation and the exact GS-CF smoother: BITWISE;
+  * coarse Krylov solve (sequential-order reductions on device): BITWISE;
+  * whole solve, parity mode: identical iteration count, BITWISE x, per-iteration relres
+    rel <= 1e-13 (the level-0 ||r|| is a fixed-order tree reduction);
+  * whole solve, direct coarse: identical iteration count on Poisson, relres rel <= 1e-6 per row,
+    final x rel <= 1e-6.
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+import pytest
+
+import amg_amd as A
+import oracle
+from amg_amd._native import SSS_SMTR, dptr, iptr
+from conftest import build_hierarchy, oracle_solve, vec
+
+pytestmark = pytest.mark.gpu
+
+
+def _lib():
+    return A.lib()
+
+
+@pytest.fixture(scope="module")
+def bus_h(bus_matrix, quiet):
+    return build_hierarchy(bus_matrix, quiet)
+
+
+@pytest.fixture(scope="module")
+def p32_h(quiet):
+    return build_hierarchy(A.generate(7, 32), quiet)
+
+
+@pytest.fixture(scope="module")
+def a27_h(quiet):
+    return build_hierarchy(A.generate(27, 16), quiet)
+
+
+def test_device_present():
+    assert A.device_count() >= 1
+
+
+# ---------------------------------------------------------------- SpMV family, bitwise
+@pytest.mark.parametrize("hname", ["bus_h", "p32_h", "a27_h"])
+@pytest.mark.parametrize("op", ["mxy", "amxpy", "resid", "acc"])
+def test_spmv_bitwise_all_levels(request, hname, op):
+    H = request.getfixturevalue(hname)
+    ora = oracle.load()
+    rng = np.random.default_rng(7)
+    for l in range(H.num_levels):
+        mats = [("A", H.level(l).A)]
+        if l < H.num_levels - 1:
+            mats += [("P", H.level(l).P), ("R", H.level(l).R)]
+        for name, M in mats:
+            x = rng.standard_normal(M.num_cols)
+            b = rng.standard_normal(M.num_rows)
+            y0 = rng.standard_normal(M.num_rows)
+            y_gpu, y_ref = y0.copy(), y0.copy()
+            alpha = -1.0 if op in ("resid", "amxpy") else 1.0
+            cap = 100 if op == "acc" else 0
+            rc = _lib().sss_hip_host_spmv(A.SPMV[op], alpha, C.byref(M), dptr(x), dptr(b), dptr(y_gpu), cap)
+            assert rc == 0
+            if op == "mxy":
+                ora.ora_mv_mxy(C.byref(M), dptr(x), dptr(y_ref))
+            elif op == "amxpy":
+                ora.ora_mv_amxpy(alpha, C.byref(M), dptr(x), dptr(y_ref), 0)
+            elif op == "resid":
+                y_ref[:] = b
+                ora.ora_mv_amxpy(-1.0, C.byref(M), dptr(x), dptr(y_ref), 0)
+            else:
+                ora.ora_mv_acc(C.byref(M), dptr(x), dptr(y_ref), cap)
+            assert np.array_equal(y_gpu.view(np.uint64), y_ref.view(np.uint64)), (hname, l, name, op)
+
+
+def test_spmv_long_rows_bitwise():
+    """Rows longer than the LDS tile (2048) take the wave-parallel product path."""
+    n = 300
+    rng = np.random.default_rng(3)
+    lens = np.where(np.arange(n) % 37 == 0, 5000, rng.integers(0, 40, n))
+    rp = np.concatenate([[0], np.cumsum(lens)]).astype(np.int32)
+    ci = rng.integers(0, n, rp[-1]).astype(np.int32)
+    v = rng.standard_normal(rp[-1])
+    M = A.NumpyCSR(rp, ci, v)
+    x = rng.standard_normal(n)
+    y_gpu, y_ref = np.zeros(n), np.zeros(n)
+    assert _lib().sss_hip_host_spmv(A.SPMV["mxy"], 1.0, C.byref(M.mat), dptr(x), None, dptr(y_gpu), 0) == 0
+    oracle.load().ora_mv_mxy(C.byref(M.mat), dptr(x), dptr(y_ref))
+    assert np.array_equal(y_gpu.view(np.uint64), y_ref.view(np.uint64))
+
+
+def test_spmv_empty_rows():
+    rp = np.array([0, 0, 2, 2, 3, 3], np.int32)
+    ci = np.array([0, 4, 1], np.int32)
+    v = np.array([1.5, -2.0, 3.0])
+    M = A.NumpyCSR(rp, ci, v)
+    x = np.arange(5, dtype=np.float64) + 1
+    y = np.full(5, 7.0)
+    assert _lib().sss_hip_host_spmv(A.SPMV["mxy"], 1.0, C.byref(M.mat), dptr(x), None, dptr(y), 0) == 0
+    assert np.array_equal(y, [0.0, 1.5 - 10.0, 0.0, 6.0, 0.0])
+
+
+# ---------------------------------------------------------------- smoother, bitwise
+def _smtr(M, b, x, mark, sweeps, post, smoother=2):
+    s = SSS_SMTR()
+    s.smoother = smoother
+    s.A = C.pointer(M)
+    s.b = C.pointer(vec(b))
+    s.x = C.pointer(vec(x))
+    s.nsweeps = sweeps
+    s.istart, s.iend, s.istep = 0, M.num_rows - 1, -1 if post else 1
+    s.cf_order = 1
+    s.ordering = mark
+    return s
+
+
+@pytest.mark.parametrize("hname", ["bus_h", "p32_h", "a27_h"])
+@pytest.mark.parametrize("post", [False, True])
+def test_gscf_bitwise_all_levels(request, hname, post):
+    H = request.getfixturevalue(hname)
+    ora = oracle.load()
+    rng = np.random.default_rng(11)
+    for l in range(H.num_levels - 1):
+        L = H.level(l)
+        n = L.A.num_rows
+        b = rng.standard_normal(n)
+        x0 = rng.standard_normal(n)
+        xg, xr = x0.copy(), x0.copy()
+        sg = _smtr(L.A, b, xg, L.cfmark.d, 2, post)
+        sr = _smtr(L.A, b, xr, L.cfmark.d, 2, post)
+        assert _lib().sss_hip_host_smooth(C.byref(sg), int(post)) == 0
+        (ora.ora_smoother_post if post else ora.ora_smoother_pre)(C.byref(sr))
+        assert np.array_equal(xg.view(np.uint64), xr.view(np.uint64)), (hname, l)
+
+
+def test_gscf_missing_diagonal_stale_d():
+    """Rows without a diagonal reuse the previous divisor (Solve/SSS_smooth.c:30,46)."""
+    rng = np.random.default_rng(5)
+    n = 40
+    rows = []
+    for i in range(n):
+        cols = sorted(set(rng.integers(0, n, 4).tolist()) | ({i} if i % 7 else set()))
+        rows.append(cols)
+    rp = np.concatenate([[0], np.cumsum([len(r) for r in rows])]).astype(np.int32)
+    ci = np.array([c for r in rows for c in r], np.int32)
+    v = np.array([4.0 + i if c == i else -0.3 for i, r in enumerate(rows) for c in r])
+    M = A.NumpyCSR(rp, ci, v)
+    mark = np.array([(i * 5) % 3 == 0 for i in range(n)], np.int32)
+    b = rng.standard_normal(n)
+    x0 = rng.standard_normal(n)
+    xg, xr = x0.copy(), x0.copy()
+    sg = _smtr(M.mat, b, xg, iptr(mark), 3, False)
+    sr = _smtr(M.mat, b, xr, iptr(mark), 3, False)
+    assert _lib().sss_hip_host_smooth(C.byref(sg), 0) == 0
+    oracle.load().ora_smoother_pre(C.byref(sr))
+    assert np.array_equal(xg.view(np.uint64), xr.view(np.uint64))
+
+
+@pytest.mark.parametrize("hname", ["bus_h", "p32_h"])
+def test_cf_jacobi_bitwise(request, hname):
+    H = request.getfixturevalue(hname)
+    ora = oracle.load()
+    rng = np.random.default_rng(2)
+    for l in range(H.num_levels - 1):
+        L = H.level(l)
+        n = L.A.num_rows
+        b = rng.standard_normal(n)
+        x0 = rng.standard_normal(n)
+        xg, xr = x0.copy(), x0.copy()
+        sg = _smtr(L.A, b, xg, L.cfmark.d, 2, False, smoother=1)
+        assert _lib().sss_hip_host_smooth(C.byref(sg), 0) == 0
+        ora.ora_cf_jacobi(dptr(xr), C.byref(L.A), dptr(b), 2, L.cfmark.d)
+        assert np.array_equal(xg.view(np.uint64), xr.view(np.uint64)), (hname, l)
+
+
+# ---------------------------------------------------------------- coarse solve
+@pytest.mark.parametrize("hname", ["bus_h", "p32_h", "a27_h"])
+def test_coarse_krylov_matches_oracle(request, hname):
+    H = request.getfixturevalue(hname)
+    Lc = H.level(H.num_levels - 1)
+    n = Lc.A.num_rows
+    rng = np.random.default_rng(9)
+    b = rng.standard_normal(n)
+    xg, xr = np.zeros(n), np.zeros(n)
+    assert _lib().sss_hip_host_coarse_solve(C.byref(Lc.A), C.byref(vec(b)), C.byref(vec(xg)), 1e-7, 0, 0) == 0
+    oracle.load().ora_coarest_solve(C.byref(Lc.A), C.byref(vec(b)), C.byref(vec(xr)), 1e-7,
+                                    C.byref(oracle.opts()))
+    assert np.array_equal(xg.view(np.uint64), xr.view(np.uint64))
+
+
+@pytest.mark.parametrize("cap", [0, 40])
+def test_coarse_krylov_row_cap(bus_h, cap):
+    """The as-shipped <<<64,64>>> row cap (rows >= cap untouched by the coarse SpMVs)."""
+    Lc = bus_h.level(bus_h.num_levels - 1)
+    n = Lc.A.num_rows
+    b = np.linspace(-1.0, 2.0, n)
+    xg, xr = np.zeros(n), np.zeros(n)
+    assert _lib().sss_hip_host_coarse_solve(C.byref(Lc.A), C.byref(vec(b)), C.byref(vec(xg)), 1e-7, 0, cap) == 0
+    oracle.load().ora_coarest_solve(C.byref(Lc.A), C.byref(vec(b)), C.byref(vec(xr)), 1e-7,
+                                    C.byref(oracle.opts(row_cap=cap)))
+    assert np.array_equal(xg.view(np.uint64), xr.view(np.uint64))
+
+
+def test_coarse_direct_solves(p32_h):
+    Lc = p32_h.level(p32_h.num_levels - 1)
+    n = Lc.A.num_rows
+    rng = np.random.default_rng(1)
+    b = rng.standard_normal(n)
+    x = np.zeros(n)
+    assert _lib().sss_hip_host_coarse_solve(C.byref(Lc.A), C.byref(vec(b)), C.byref(vec(x)), 1e-7, 1, 0) == 0
+    rp, ci, v = A.csr_arrays(Lc.A)
+    Ax = np.zeros(n)
+    for i in range(n):
+        Ax[i] = np.dot(v[rp[i]:rp[i + 1]], x[ci[rp[i]:rp[i + 1]]])
+    assert np.linalg.norm(Ax - b) <= 1e-10 * np.linalg.norm(b)
+
+
+# ---------------------------------------------------------------- whole solve
+def _gpu_history(H, smoother="exact", coarse="krylov", row_cap=0, max_it=100):
+    n = H.level(0).A.num_rows
+    D = A.DeviceHierarchy(H, smoother=smoother, coarse=coarse, row_cap=row_cap)
+    b = np.ones(n)
+    D.upload(0, "b", b)
+    D.upload(0, "x", np.ones(n))
+    sumb = np.sqrt(np.dot(b, b))
+    rel = []
+    for _ in range(max_it):
+        D.cycle()
+        rel.append(D.residual_norm() / sumb)
+        if rel[-1] < H.pars.tol:
+            break
+    x = D.download(0, "x")
+    D.close()
+    return np.array(rel), x
+
+
+def _oracle_history(H, **kw):
+    n = H.level(0).A.num_rows
+    b, x = np.ones(n), np.ones(n)
+    rtn, rel, _ = oracle_solve(H, b, x, **kw)
+    return rel, x
+
+
+@pytest.mark.parametrize("hname", ["bus_h", "p32_h", "a27_h"])
+def test_solve_parity_mode(request, hname):
+    H = request.getfixturevalue(hname)
+    rel_r, x_r = _oracle_history(H)
+    rel_g, x_g = _gpu_history(H)
+    assert len(rel_g) == len(rel_r)
+    # x is bitwise identical; only the level-0 norm is reduced in tree order on the GPU
+    assert np.array_equal(x_g.view(np.uint64), x_r.view(np.uint64))
+    assert np.allclose(rel_g, rel_r, rtol=1e-13, atol=0)
+
+
+@pytest.mark.parametrize("hname", ["p32_h", "a27_h"])
+def test_solve_direct_coarse(request, hname):
+    H = request.getfixturevalue(hname)
+    rel_r, x_r = _oracle_history(H)
+    rel_g, x_g = _gpu_history(H, coarse="direct")
+    assert len(rel_g) == len(rel_r)
+    assert np.allclose(rel_g, rel_r, rtol=1e-6, atol=0)
+    assert np.linalg.norm(x_g - x_r) <= 1e-6 * np.linalg.norm(x_r)
+
+
+def test_solve_hybrid_jacobi_converges(p32_h):
+    rel_o, x_o = _oracle_history(p32_h, smoother=1, coarse_mode=1)
+    rel_g, x_g = _gpu_history(p32_h, smoother="hybrid", coarse="direct")
+    assert len(rel_g) == len(rel_o)
+    assert np.allclose(rel_g, rel_o, rtol=1e-6)
+    rel_ref, _ = _oracle_history(p32_h)
+    assert len(rel_g) <= len(rel_ref) + 2
+
+
+def test_solve_bus_known_answer(bus_h):
+    """GPU history equals the reference's printed table."""
+    expect = [2.907170e+00, 4.389125e-01, 1.321964e-01, 4.453643e-02, 1.213532e-02, 3.537244e-03, 1.358532e-03,
+              3.614966e-04, 1.381984e-04, 2.328166e-05, 9.120090e-06, 2.602226e-06, 8.230269e-07]
+    rel, _ = _gpu_history(bus_h)
+    assert ["%.6e" % r for r in rel] == ["%.6e" % r for r in expect]
+
+
+def test_drop_in_solver_amg(bus_matrix, capfd):
+    """SSS_solver_amg through the C ABI prints the reference's table and fills the caller's x."""
+    n = bus_matrix.num_rows
+    b, x = np.ones(n), np.ones(n)
+    pars = A.default_pars()
+    rtn = _lib().SSS_solver_amg(C.byref(bus_matrix), C.byref(vec(x)), C.byref(vec(b)), C.byref(pars))
+    C.CDLL(None).fflush(None)
+    out = capfd.readouterr().out
+    assert rtn.nits == 13
+    assert "    13 |  8.230269e-07   |  2.776420e-05  |     0.3163" in out
+    rel_r, x_r = _oracle_history(build_hierarchy(bus_matrix, type(
+        "Q", (), {"__enter__": lambda s: None, "__exit__": lambda s, *a: None})))
+    assert np.linalg.norm(x - x_r) <= 1e-10 * np.linalg.norm(x_r)
