@@ -298,3 +298,20 @@ def test_drop_in_solver_amg(bus_matrix, capfd):
     rel_r, x_r = _oracle_history(build_hierarchy(bus_matrix, type(
         "Q", (), {"__enter__": lambda s: None, "__exit__": lambda s, *a: None})))
     assert np.linalg.norm(x - x_r) <= 1e-10 * np.linalg.norm(x_r)
+
+
+def test_reference_main_dropin():
+    """The reference's unmodified SSS_main.c linked against libsss_amg.so."""
+    import subprocess
+    from pathlib import Path
+    from conftest import BUS_MTX, GOLDEN
+    exe = Path(oracle.__file__).resolve().parent / "_ref" / "amg_dropin"
+    if not exe.exists():
+        pytest.skip("built only where the reference tree was present")
+    r = subprocess.run([str(exe), str(BUS_MTX)], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr
+    import json
+    g = json.loads((GOLDEN / "golden.json").read_text())["survey"]["bus_history"]
+    rows = [l.split("|") for l in r.stdout.splitlines() if l[:6].strip().isdigit() and "|" in l]
+    assert ["%s" % c[1].strip() for c in rows] == g["relres"]
+    assert "AMG iterations: 13" in r.stdout
