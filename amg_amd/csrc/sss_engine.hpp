@@ -47,12 +47,15 @@ struct DevCSR {
     double *v = nullptr;
     int nblk = 0;          // SpMV row blocks
     int *blk = nullptr;    // block -> first row (nblk + 1 entries)
+    int split_row = -1;    // class split row the blocks were cut at (-1: none)
+    int split_blk = 0;     // index of the block starting at split_row
     bool wave_rows = false;  // long rows: wave-per-row kernels (avg nnz/row >= kWaveRowMin)
     int ngrid = 0;           // workgroups of one SpMV launch (size of a per-block partial array)
 };
-int devcsr_upload(DevCSR &d, const SSS_MAT &h);
+// split >= 0 forces a row-block boundary at that row (the F|C class boundary of a relabeled level)
+int devcsr_upload(DevCSR &d, const SSS_MAT &h, int split = -1);
 void devcsr_free(DevCSR &d);
-int build_row_blocks(const int *h_rp, int n, std::vector<int> &blk);
+int build_row_blocks(const int *h_rp, int n, std::vector<int> &blk, int split = -1);
 
 // y <- op(A x) on `stream` (see SSS_HIP_SPMV_*).  `partial` (optional, RESID only): one
 // sum-of-squares of the written y per row block, for a deterministic fused norm.
@@ -69,6 +72,10 @@ struct PassSchedule {          // rows of one class (F or C), grouped by DAG dep
     // Row-compacted CSR of this class (rows ascending) with CSR-adaptive blocking: used when
     // the pass has no intra-class couplings (depth 1) or for C/F-Jacobi.
     bool compact = false;
+    // Contiguous class (relabeled level, F rows first): the pass is rows [lo, hi) = blocks [blo, bhi)
+    // of the level matrix itself; no copy.
+    bool range = false;
+    int lo = 0, hi = 0, blo = 0, bhi = 0;
     DevCSR sub;
     int *map = nullptr;        // local row -> global row
     double *y = nullptr;       // Jacobi: new values of this class, scattered after the pass
@@ -80,8 +87,11 @@ struct SmootherPlan {
     double *d_later = nullptr; // ... for later sweeps (aliases d_first when all rows have a diagonal)
     int *cls = nullptr;        // per row: 1 if mark == 1 else 0
     bool long_rows = false;    // wave-per-row kernels
+    int *diag_pos = nullptr;   // range passes: CSR position of each row's diagonal (-1: none)
 };
-int smoother_build(SmootherPlan &sp, const SSS_MAT &A, const int *mark, int kind);
+// contiguous: mark is relabeled so class F occupies rows [0, nF) and class C rows [nF, n), and A was
+// uploaded with a block split at nF (its DevCSR is passed to allow range passes).
+int smoother_build(SmootherPlan &sp, const SSS_MAT &A, const int *mark, int kind, const DevCSR *dA = nullptr);
 void smoother_free(SmootherPlan &sp);
 int smoother_run(const SmootherPlan &sp, const DevCSR &A, const double *b, double *x, int sweeps,
                  hipStream_t stream);

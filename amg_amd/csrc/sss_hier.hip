@@ -11,9 +11,11 @@
 // norm is the only per-iteration device->host transfer.
 #include "sss_engine.hpp"
 
+#include <algorithm>
 #include <cstdlib>
 #include <cstring>
 #include <string>
+#include <thread>
 #include <vector>
 
 using namespace sss;
@@ -27,7 +29,11 @@ struct sss_hip_hier {
         DevCSR A, P, R;
         double *b = nullptr, *x = nullptr, *wp = nullptr;
         SmootherPlan sm;
+        // Relabeling (new -> old) of this level's unknowns: F points first, then C points, each in
+        // ascending original order; empty = identity (coarsest level, or relabeling off).
+        std::vector<int> perm;
     } L[kMaxLevels];
+    std::vector<double> stage;   // host staging for permuted vector transfers
     int coarse_mode = SSS_HIP_COARSE_DIRECT;
     CoarseDirect direct;
     CoarseKrylov *krylov = nullptr;
@@ -57,6 +63,7 @@ extern "C" void sss_hip_opts_default(sss_hip_opts *o)
     o->row_cap = env_int("SSS_HIP_ROWCAP", 0);
     o->use_graph = env_int("SSS_HIP_GRAPH", 1);
     o->verbose = env_int("SSS_HIP_VERBOSE", 0);
+    o->relabel = env_int("SSS_HIP_RELABEL", 1);
     if (const char *s = getenv("SSS_HIP_SMOOTHER")) {
         std::string v(s);
         if (v == "hybrid") o->smoother = SSS_HIP_SMOOTH_HYBRID;
@@ -110,6 +117,67 @@ static void hier_release(sss_hip_hier *h)
     delete h;
 }
 
+// ---- class-contiguous relabeling ------------------------------------------------------------
+// Each level's unknowns are renumbered F-first (mark != 1), C-second, keeping the original order
+// inside each class.  Every kernel computes a row from the same entries in the same CSR order, GS
+// sweeps visit each class in the same relative order, and the coarsest level (Krylov dot products)
+// keeps its labels, so the iterates are bitwise those of the unrelabeled hierarchy.  What changes
+// is the memory layout: every smoother pass is a contiguous row range of the level matrix, the
+// x values it gathers (the other class) are contiguous too, and it writes a dense half of x.
+template <class Fn>
+static void parallel_rows(int n, Fn fn)
+{
+    const int nt = (int)std::max(1u, std::min(32u, std::thread::hardware_concurrency()));
+    if (n < (1 << 16) || nt == 1) { fn(0, n); return; }
+    std::vector<std::thread> th;
+    const int chunk = (n + nt - 1) / nt;
+    for (int t = 0; t < nt; ++t) {
+        const int lo = t * chunk, hi = std::min(n, lo + chunk);
+        if (lo < hi) th.emplace_back(fn, lo, hi);
+    }
+    for (auto &t : th) t.join();
+}
+
+struct RelabeledCSR {   // owns the arrays an SSS_MAT view points into
+    std::vector<int> rp, ci;
+    std::vector<double> v;
+    SSS_MAT view(int nrows, int ncols)
+    {
+        SSS_MAT m;
+        m.num_rows = nrows;
+        m.num_cols = ncols;
+        m.num_nnzs = (int)ci.size();
+        m.row_ptr = rp.data();
+        m.col_idx = ci.data();
+        m.val = v.data();
+        return m;
+    }
+};
+
+// B = A with rows taken in order rperm (new -> old; empty = identity) and columns renamed by
+// cinv (old -> new; empty = identity); entry order inside a row is unchanged.
+static void relabel_csr(const SSS_MAT &A, const std::vector<int> &rperm, const std::vector<int> &cinv, RelabeledCSR &B)
+{
+    const int n = A.num_rows;
+    B.rp.assign((size_t)n + 1, 0);
+    for (int i = 0; i < n; ++i) {
+        const int o = rperm.empty() ? i : rperm[i];
+        B.rp[i + 1] = B.rp[i] + (A.row_ptr[o + 1] - A.row_ptr[o]);
+    }
+    B.ci.resize((size_t)B.rp[n]);
+    B.v.resize((size_t)B.rp[n]);
+    parallel_rows(n, [&](int lo, int hi) {
+        for (int i = lo; i < hi; ++i) {
+            const int o = rperm.empty() ? i : rperm[i];
+            int q = B.rp[i];
+            for (int k = A.row_ptr[o]; k < A.row_ptr[o + 1]; ++k, ++q) {
+                B.ci[q] = cinv.empty() ? A.col_idx[k] : cinv[A.col_idx[k]];
+                B.v[q] = A.val[k];
+            }
+        }
+    });
+}
+
 extern "C" sss_hip_hier *sss_hip_hier_create(const SSS_AMG *mg, const sss_hip_opts *o)
 {
     if (sss_hip_device_count() <= 0) {
@@ -130,14 +198,57 @@ extern "C" sss_hip_hier *sss_hip_hier_create(const SSS_AMG *mg, const sss_hip_op
     if (hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess) return fail("stream");
     if (hipEventCreate(&h->ev0) != hipSuccess || hipEventCreate(&h->ev1) != hipSuccess) return fail("events");
 
+    // F|C relabeling of every level but the coarsest (identity there)
+    std::vector<std::vector<int>> inv(h->nl);
+    std::vector<int> nF(h->nl, -1);
+    if (h->opts.relabel)
+        for (int l = 0; l + 1 < h->nl; ++l) {
+            const SSS_AMG_COMP &C = mg->cg[l];
+            const int n = C.A.num_rows;
+            if (!C.cfmark.d || C.cfmark.n < n) continue;
+            auto &perm = h->L[l].perm;
+            perm.reserve(n);
+            for (int i = 0; i < n; ++i)
+                if (C.cfmark.d[i] != 1) perm.push_back(i);
+            nF[l] = (int)perm.size();
+            for (int i = 0; i < n; ++i)
+                if (C.cfmark.d[i] == 1) perm.push_back(i);
+            inv[l].resize(n);
+            for (int i = 0; i < n; ++i) inv[l][perm[i]] = i;
+        }
+
     for (int l = 0; l < h->nl; ++l) {
         const SSS_AMG_COMP &C = mg->cg[l];
         auto &L = h->L[l];
         const int n = C.A.num_rows;
-        if (devcsr_upload(L.A, C.A)) return fail("upload A");
+        const bool rl = !L.perm.empty();
+        if (rl) {
+            RelabeledCSR B;
+            relabel_csr(C.A, L.perm, inv[l], B);
+            SSS_MAT Av = B.view(n, C.A.num_cols);
+            if (devcsr_upload(L.A, Av, nF[l])) return fail("upload A");
+            std::vector<int> mark(n);
+            for (int i = 0; i < n; ++i) mark[i] = C.cfmark.d[L.perm[i]];
+            if (smoother_build(L.sm, Av, mark.data(), level_smoother_kind(h->opts, l), &L.A))
+                return fail("smoother plan");
+        } else {
+            if (devcsr_upload(L.A, C.A)) return fail("upload A");
+            if (l < h->nl - 1 &&
+                smoother_build(L.sm, C.A, C.cfmark.d, level_smoother_kind(h->opts, l)))
+                return fail("smoother plan");
+        }
         if (l < h->nl - 1) {
-            if (devcsr_upload(L.P, C.P) || devcsr_upload(L.R, C.R)) return fail("upload P/R");
-            if (smoother_build(L.sm, C.A, C.cfmark.d, level_smoother_kind(h->opts, l))) return fail("smoother plan");
+            const auto &pc = h->L[l + 1].perm;   // (filled above for every relabeled level)
+            if (rl || !pc.empty()) {
+                RelabeledCSR P, R;
+                relabel_csr(C.P, L.perm, inv[l + 1], P);
+                relabel_csr(C.R, pc, inv[l], R);
+                if (devcsr_upload(L.P, P.view(C.P.num_rows, C.P.num_cols)) ||
+                    devcsr_upload(L.R, R.view(C.R.num_rows, C.R.num_cols)))
+                    return fail("upload P/R");
+            } else if (devcsr_upload(L.P, C.P) || devcsr_upload(L.R, C.R)) {
+                return fail("upload P/R");
+            }
         }
         L.b = dev_alloc<double>((size_t)n);
         L.x = dev_alloc<double>((size_t)n);
@@ -194,7 +305,17 @@ static double *level_vec(sss_hip_hier *h, int level, int which)
 extern "C" int sss_hip_upload_vec(sss_hip_hier *h, int level, int which, const double *src, int n)
 {
     double *d = level_vec(h, level, which);
-    if (!d || n > h->L[level].A.n) return ERROR_INPUT_PAR;
+    if (!d || n < 0 || n > h->L[level].A.n) return ERROR_INPUT_PAR;
+    const auto &perm = h->L[level].perm;
+    if (!perm.empty()) {
+        if (n != h->L[level].A.n) return ERROR_INPUT_PAR;   // relabeled levels move whole vectors
+        h->stage.resize((size_t)n);
+        double *st = h->stage.data();
+        parallel_rows(n, [&](int lo, int hi) {
+            for (int i = lo; i < hi; ++i) st[i] = src[perm[i]];
+        });
+        src = st;
+    }
     SSS_HIP(hipMemcpyAsync(d, src, sizeof(double) * (size_t)n, hipMemcpyHostToDevice, h->stream));
     SSS_HIP(hipStreamSynchronize(h->stream));
     return 0;
@@ -203,9 +324,21 @@ extern "C" int sss_hip_upload_vec(sss_hip_hier *h, int level, int which, const d
 extern "C" int sss_hip_download_vec(sss_hip_hier *h, int level, int which, double *dst, int n)
 {
     double *d = level_vec(h, level, which);
-    if (!d || n > h->L[level].A.n) return ERROR_INPUT_PAR;
-    SSS_HIP(hipMemcpyAsync(dst, d, sizeof(double) * (size_t)n, hipMemcpyDeviceToHost, h->stream));
+    if (!d || n < 0 || n > h->L[level].A.n) return ERROR_INPUT_PAR;
+    const auto &perm = h->L[level].perm;
+    if (perm.empty()) {
+        SSS_HIP(hipMemcpyAsync(dst, d, sizeof(double) * (size_t)n, hipMemcpyDeviceToHost, h->stream));
+        SSS_HIP(hipStreamSynchronize(h->stream));
+        return 0;
+    }
+    if (n != h->L[level].A.n) return ERROR_INPUT_PAR;
+    h->stage.resize((size_t)n);
+    double *st = h->stage.data();
+    SSS_HIP(hipMemcpyAsync(st, d, sizeof(double) * (size_t)n, hipMemcpyDeviceToHost, h->stream));
     SSS_HIP(hipStreamSynchronize(h->stream));
+    parallel_rows(n, [&](int lo, int hi) {
+        for (int i = lo; i < hi; ++i) dst[perm[i]] = st[i];
+    });
     return 0;
 }
 

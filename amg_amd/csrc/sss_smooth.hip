@@ -42,7 +42,7 @@ static int upload_doubles(double **dst, const std::vector<double> &src)
     return 0;
 }
 
-int smoother_build(SmootherPlan &sp, const SSS_MAT &A, const int *mark, int kind)
+int smoother_build(SmootherPlan &sp, const SSS_MAT &A, const int *mark, int kind, const DevCSR *dA)
 {
     const int n = A.num_rows;
     const int *rp = A.row_ptr, *ci = A.col_idx;
@@ -50,14 +50,20 @@ int smoother_build(SmootherPlan &sp, const SSS_MAT &A, const int *mark, int kind
     std::vector<int> cls(n), depth(n, 0), pushed(n, 0);
     std::vector<double> last_diag(n, 0.0), d_first(n, 0.0), d_later(n, 0.0);
     std::vector<char> has_diag(n, 0);
-    bool all_diag = true;
+    std::vector<int> diag_pos(n, -1);
+    bool all_diag = true, single_diag = true;
     int rc;
 
     sp.kind = kind;
     for (int i = 0; i < n; ++i) {
         cls[i] = mark ? (mark[i] == 1 ? 1 : 0) : 0;
         for (int k = rp[i]; k < rp[i + 1]; ++k)
-            if (ci[k] == i) { last_diag[i] = v[k]; has_diag[i] = 1; }
+            if (ci[k] == i) {
+                last_diag[i] = v[k];
+                if (has_diag[i]) single_diag = false;
+                has_diag[i] = 1;
+                diag_pos[i] = k;
+            }
         all_diag = all_diag && has_diag[i];
     }
     // stale-d resolution: simulate the divisor register over two sweeps of (F pass, C pass)
@@ -105,7 +111,30 @@ int smoother_build(SmootherPlan &sp, const SSS_MAT &A, const int *mark, int kind
             if (cls[i] == c) rows[fill[depth[i]]++] = i;
         if ((rc = upload_ints(&ps.rows, rows))) return rc;
         ps.compact = kind == SSS_HIP_SMOOTH_JACOBI || ps.depth <= 1;
-        if (ps.compact && ps.nrows > 0) {
+        if (ps.compact && ps.nrows > 0 && dA && single_diag) {
+            // contiguous class?  (relabeled level: F rows first, then C rows)
+            int lo = -1, hi = -1;
+            bool contiguous = true;
+            for (int i = 0; i < n && contiguous; ++i) {
+                if (cls[i] != c) continue;
+                if (lo < 0) lo = i;
+                else if (i != hi) contiguous = false;
+                hi = i + 1;
+            }
+            if (contiguous) {
+                // the pass must be a whole number of the level's row blocks
+                if (lo == 0 && hi == n) ps.range = true, ps.blo = 0, ps.bhi = dA->nblk;
+                else if (lo == 0 && hi == dA->split_row) ps.range = true, ps.blo = 0, ps.bhi = dA->split_blk;
+                else if (lo == dA->split_row && hi == n) ps.range = true, ps.blo = dA->split_blk, ps.bhi = dA->nblk;
+                ps.lo = lo;
+                ps.hi = hi;
+            }
+            if (ps.range && kind == SSS_HIP_SMOOTH_JACOBI) {
+                ps.y = dev_alloc<double>((size_t)(hi - lo));
+                if (!ps.y) return hip_fail(hipErrorOutOfMemory, "hipMalloc(y)", __FILE__, __LINE__);
+            }
+        }
+        if (ps.compact && ps.nrows > 0 && !ps.range) {
             std::vector<int> crp(1, 0), cci, cmap;
             std::vector<double> cv;
             for (int i = 0; i < n; ++i) {
@@ -133,6 +162,8 @@ int smoother_build(SmootherPlan &sp, const SSS_MAT &A, const int *mark, int kind
         }
     }
     if ((rc = upload_ints(&sp.cls, cls))) return rc;
+    if (sp.pass[0].range || sp.pass[1].range)
+        if ((rc = upload_ints(&sp.diag_pos, diag_pos))) return rc;
     if (kind == SSS_HIP_SMOOTH_JACOBI) {
         if ((rc = upload_doubles(&sp.d_first, last_diag))) return rc;   // Jacobi: row's own diagonal
         sp.d_later = sp.d_first;
@@ -155,6 +186,7 @@ void smoother_free(SmootherPlan &sp)
     if (sp.d_later != sp.d_first) dev_free(sp.d_later);
     dev_free(sp.d_first);
     dev_free(sp.cls);
+    dev_free(sp.diag_pos);
     sp = SmootherPlan();
 }
 
@@ -238,6 +270,63 @@ __global__ __launch_bounds__(kBlock) void relax_wave(int m, const int *__restric
     }
 }
 
+// Class pass over rows [lo, hi) of a relabeled level, blocks [blo, ...) of its own CSR: GS with
+// depth 1 (in place) or the relaxation half of C/F-Jacobi (into y[r - lo], copied back after).
+template <bool INPLACE>
+__global__ __launch_bounds__(kBlock) void relax_range(int blo, const int *__restrict__ blk, const int *__restrict__ rp,
+                                                      const int *__restrict__ ci, const double *__restrict__ v,
+                                                      const int *__restrict__ diag_pos, int lo,
+                                                      const double *__restrict__ b, double *x,
+                                                      double *__restrict__ y, const double *__restrict__ deff)
+{
+    __shared__ SpmvSmem sm;
+    const int bid = blo + blockIdx.x;
+    const int r0 = blk[bid], r1 = blk[bid + 1];
+    const int k0 = rp[r0], k1 = rp[r1];
+    const int cnt = k1 - k0;
+    if (cnt <= kTileEntries) {
+        for (int k = threadIdx.x; k < cnt; k += kBlock) sm.v[k] = v[k0 + k] * x[ci[k0 + k]];
+        __syncthreads();
+        const int r = r0 + (int)threadIdx.x;
+        if (r < r1) {
+            const int a = rp[r] - k0, e = rp[r + 1] - k0, dp = diag_pos[r];
+            double acc = b[r];
+            if (dp < 0) acc = chain_sub(acc, sm.v, a, e);
+            else {
+                acc = chain_sub(acc, sm.v, a, dp - k0);
+                acc = chain_sub(acc, sm.v, dp - k0 + 1, e);
+            }
+            const double d = deff[r];
+            if (INPLACE) {
+                if (fabs(d) > SMALLFLOAT) x[r] = acc / d;
+            } else {
+                y[r - lo] = fabs(d) > SMALLFLOAT ? acc / d : x[r];
+            }
+        }
+    } else {
+        const int r = r0;
+        double acc = b[r];
+        for (int base = k0; base < k1; base += kTileEntries) {
+            const int m = min(kTileEntries, k1 - base);
+            for (int k = threadIdx.x; k < m; k += kBlock) {
+                const int j = ci[base + k];
+                sm.v[k] = (j != r) ? v[base + k] * x[j] : 0.0;
+            }
+            __syncthreads();
+            if (threadIdx.x == 0) acc = chain_sub(acc, sm.v, 0, m);
+            __syncthreads();
+        }
+        if (threadIdx.x == 0) {
+            const double d = deff[r];
+            if (INPLACE) {
+                if (fabs(d) > SMALLFLOAT) x[r] = acc / d;
+            } else {
+                y[r - lo] = fabs(d) > SMALLFLOAT ? acc / d : x[r];
+            }
+        }
+    }
+}
+
 __global__ __launch_bounds__(kBlock) void scatter_rows(int m, const int *__restrict__ map, const double *__restrict__ y,
                                                        double *__restrict__ x)
 {
@@ -254,6 +343,19 @@ int smoother_run(const SmootherPlan &sp, const DevCSR &A, const double *b, doubl
         for (int c = 0; c < 2; ++c) {
             const PassSchedule &ps = sp.pass[c];
             if (ps.nrows == 0) continue;
+            if (ps.range) {
+                const int nb = ps.bhi - ps.blo;
+                if (sp.kind == SSS_HIP_SMOOTH_JACOBI) {
+                    hipLaunchKernelGGL(relax_range<false>, dim3(nb), dim3(kBlock), 0, s, ps.blo, A.blk, A.rp, A.ci,
+                                       A.v, sp.diag_pos, ps.lo, b, x, ps.y, deff);
+                    SSS_HIP(hipMemcpyAsync(x + ps.lo, ps.y, sizeof(double) * (size_t)(ps.hi - ps.lo),
+                                           hipMemcpyDeviceToDevice, s));
+                } else {
+                    hipLaunchKernelGGL(relax_range<true>, dim3(nb), dim3(kBlock), 0, s, ps.blo, A.blk, A.rp, A.ci, A.v,
+                                       sp.diag_pos, ps.lo, b, x, (double *)nullptr, deff);
+                }
+                continue;
+            }
             if (sp.kind == SSS_HIP_SMOOTH_JACOBI) {
                 if (ps.sub.wave_rows)
                     hipLaunchKernelGGL(relax_wave<false>, dim3(ps.sub.ngrid), dim3(kBlock), 0, s, ps.nrows, ps.sub.rp,

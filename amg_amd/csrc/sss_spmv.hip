@@ -27,16 +27,17 @@ int hip_fail(hipError_t e, const char *what, const char *file, int line)
     return ERROR_MISC;
 }
 
-int build_row_blocks(const int *h_rp, int n, std::vector<int> &blk)
+int build_row_blocks(const int *h_rp, int n, std::vector<int> &blk, int split)
 {
     blk.clear();
     int r = 0;
     while (r < n) {
         blk.push_back(r);
         const int base = h_rp[r];
+        const int lim = (split > r && split < n) ? split : n;   // never straddle the class split
         int e = r + 1;
         if (h_rp[e] - base <= kTileEntries) {
-            while (e < n && e - r < kBlock && h_rp[e + 1] - base <= kTileEntries) ++e;
+            while (e < lim && e - r < kBlock && h_rp[e + 1] - base <= kTileEntries) ++e;
         }
         r = e;
     }
@@ -44,7 +45,7 @@ int build_row_blocks(const int *h_rp, int n, std::vector<int> &blk)
     return (int)blk.size() - 1;
 }
 
-int devcsr_upload(DevCSR &d, const SSS_MAT &h)
+int devcsr_upload(DevCSR &d, const SSS_MAT &h, int split)
 {
     d.n = h.num_rows;
     d.ncols = h.num_cols;
@@ -59,7 +60,12 @@ int devcsr_upload(DevCSR &d, const SSS_MAT &h)
         SSS_HIP(hipMemcpy(d.v, h.val, sizeof(double) * (size_t)d.nnz, hipMemcpyHostToDevice));
     }
     std::vector<int> blk;
-    d.nblk = build_row_blocks(h.row_ptr, d.n, blk);
+    d.nblk = build_row_blocks(h.row_ptr, d.n, blk, split);
+    d.split_blk = d.nblk;
+    d.split_row = split;
+    if (split >= 0)
+        for (int q = 0; q <= d.nblk; ++q)
+            if (blk[q] >= split) { d.split_blk = q; break; }
     d.blk = dev_alloc<int>(blk.size());
     if (!d.blk) return hip_fail(hipErrorOutOfMemory, "hipMalloc(blk)", __FILE__, __LINE__);
     SSS_HIP(hipMemcpy(d.blk, blk.data(), sizeof(int) * blk.size(), hipMemcpyHostToDevice));

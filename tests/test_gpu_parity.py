@@ -222,9 +222,9 @@ def test_coarse_direct_solves(p32_h):
 
 
 # ---------------------------------------------------------------- whole solve
-def _gpu_history(H, smoother="exact", coarse="krylov", row_cap=0, max_it=100):
+def _gpu_history(H, smoother="exact", coarse="krylov", row_cap=0, max_it=100, relabel=None, graph=None):
     n = H.level(0).A.num_rows
-    D = A.DeviceHierarchy(H, smoother=smoother, coarse=coarse, row_cap=row_cap)
+    D = A.DeviceHierarchy(H, smoother=smoother, coarse=coarse, row_cap=row_cap, relabel=relabel, graph=graph)
     b = np.ones(n)
     D.upload(0, "b", b)
     D.upload(0, "x", np.ones(n))
@@ -275,6 +275,52 @@ def test_solve_hybrid_jacobi_converges(p32_h):
     assert np.allclose(rel_g, rel_o, rtol=1e-6)
     rel_ref, _ = _oracle_history(p32_h)
     assert len(rel_g) <= len(rel_ref) + 2
+
+
+@pytest.mark.parametrize("hname", ["bus_h", "p32_h", "a27_h"])
+@pytest.mark.parametrize("smoother,coarse", [("exact", "krylov"), ("hybrid", "direct"), ("jacobi", "direct")])
+def test_relabel_is_bitwise_neutral(request, hname, smoother, coarse):
+    """The device F|C renumbering (sss_hier.hip relabel_csr) changes only labels: the iterates with
+    it on/off (and with graph replay on/off) are bitwise identical."""
+    H = request.getfixturevalue(hname)
+    rel0, x0 = _gpu_history(H, smoother, coarse, max_it=12, relabel=0, graph=0)
+    rel1, x1 = _gpu_history(H, smoother, coarse, max_it=12, relabel=1, graph=1)
+    assert len(rel0) == len(rel1)
+    assert np.array_equal(x0.view(np.uint64), x1.view(np.uint64))
+    assert np.allclose(rel0, rel1, rtol=1e-13, atol=0)
+
+
+@pytest.mark.parametrize("hname", ["bus_h", "p32_h", "a27_h"])
+@pytest.mark.parametrize("smoother", ["exact", "jacobi"])
+def test_relabeled_level_smoothers_bitwise(request, hname, smoother):
+    """Per level, through the relabeled mirror: upload (b, x) in the caller's labels, run the device
+    pre/post smoother, download, compare bitwise with the oracle on the original labels."""
+    H = request.getfixturevalue(hname)
+    ora = oracle.load()
+    D = A.DeviceHierarchy(H, smoother=smoother, coarse="direct", relabel=1)
+    rng = np.random.default_rng(23)
+    try:
+        for l in range(H.num_levels - 1):
+            L = H.level(l)
+            n = L.A.num_rows
+            for post in (False, True):
+                b = rng.standard_normal(n)
+                x0 = rng.standard_normal(n)
+                D.upload(l, "b", b)
+                D.upload(l, "x", x0)
+                D.smooth(l, post)
+                xg = D.download(l, "x")
+                assert np.array_equal(D.download(l, "b").view(np.uint64), b.view(np.uint64))
+                xr = x0.copy()
+                sweeps = H.pars.post_iter if post else H.pars.pre_iter
+                if smoother == "jacobi":
+                    ora.ora_cf_jacobi(dptr(xr), C.byref(L.A), dptr(b), sweeps, L.cfmark.d)
+                else:
+                    sr = _smtr(L.A, b, xr, L.cfmark.d, sweeps, post)
+                    (ora.ora_smoother_post if post else ora.ora_smoother_pre)(C.byref(sr))
+                assert np.array_equal(xg.view(np.uint64), xr.view(np.uint64)), (hname, l, post)
+    finally:
+        D.close()
 
 
 def test_solve_bus_known_answer(bus_h):
