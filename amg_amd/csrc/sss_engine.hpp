@@ -76,6 +76,7 @@ struct PassSchedule {          // rows of one class (F or C), grouped by DAG dep
     // of the level matrix itself; no copy.
     bool range = false;
     int lo = 0, hi = 0, blo = 0, bhi = 0;
+    double *y2 = nullptr;      // second inner-iterate buffer (two-stage)
     DevCSR sub;
     int *map = nullptr;        // local row -> global row
     double *y = nullptr;       // Jacobi: new values of this class, scattered after the pass
@@ -88,10 +89,14 @@ struct SmootherPlan {
     int *cls = nullptr;        // per row: 1 if mark == 1 else 0
     bool long_rows = false;    // wave-per-row kernels
     int *diag_pos = nullptr;   // range passes: CSR position of each row's diagonal (-1: none)
+    int inner = 0;             // two-stage GS-CF inner steps (kind == JACOBI, range passes only)
+    int *cts = nullptr;        // two-stage: the level's columns with same-class strictly-lower entries
+                               // stored as ~j (decoded by every two-stage kernel)
 };
 // contiguous: mark is relabeled so class F occupies rows [0, nF) and class C rows [nF, n), and A was
 // uploaded with a block split at nF (its DevCSR is passed to allow range passes).
-int smoother_build(SmootherPlan &sp, const SSS_MAT &A, const int *mark, int kind, const DevCSR *dA = nullptr);
+int smoother_build(SmootherPlan &sp, const SSS_MAT &A, const int *mark, int kind, const DevCSR *dA = nullptr,
+                   int inner = 0);
 void smoother_free(SmootherPlan &sp);
 int smoother_run(const SmootherPlan &sp, const DevCSR &A, const double *b, double *x, int sweeps,
                  hipStream_t stream);

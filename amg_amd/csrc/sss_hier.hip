@@ -64,6 +64,7 @@ extern "C" void sss_hip_opts_default(sss_hip_opts *o)
     o->use_graph = env_int("SSS_HIP_GRAPH", 1);
     o->verbose = env_int("SSS_HIP_VERBOSE", 0);
     o->relabel = env_int("SSS_HIP_RELABEL", 1);
+    o->inner = env_int("SSS_HIP_INNER", 1);
     if (const char *s = getenv("SSS_HIP_SMOOTHER")) {
         std::string v(s);
         if (v == "hybrid") o->smoother = SSS_HIP_SMOOTH_HYBRID;
@@ -201,11 +202,13 @@ extern "C" sss_hip_hier *sss_hip_hier_create(const SSS_AMG *mg, const sss_hip_op
     // F|C relabeling of every level but the coarsest (identity there)
     std::vector<std::vector<int>> inv(h->nl);
     std::vector<int> nF(h->nl, -1);
-    if (h->opts.relabel)
-        for (int l = 0; l + 1 < h->nl; ++l) {
+    for (int l = 0; l + 1 < h->nl; ++l) {
             const SSS_AMG_COMP &C = mg->cg[l];
             const int n = C.A.num_rows;
             if (!C.cfmark.d || C.cfmark.n < n) continue;
+            // two-stage levels need contiguous classes; otherwise follow opts.relabel
+            const bool two_stage = level_smoother_kind(h->opts, l) == SSS_HIP_SMOOTH_JACOBI && h->opts.inner > 0;
+            if (!two_stage && !(h->opts.relabel == 1 || (h->opts.relabel == 2 && l > 0))) continue;
             auto &perm = h->L[l].perm;
             perm.reserve(n);
             for (int i = 0; i < n; ++i)
@@ -229,7 +232,7 @@ extern "C" sss_hip_hier *sss_hip_hier_create(const SSS_AMG *mg, const sss_hip_op
             if (devcsr_upload(L.A, Av, nF[l])) return fail("upload A");
             std::vector<int> mark(n);
             for (int i = 0; i < n; ++i) mark[i] = C.cfmark.d[L.perm[i]];
-            if (smoother_build(L.sm, Av, mark.data(), level_smoother_kind(h->opts, l), &L.A))
+            if (smoother_build(L.sm, Av, mark.data(), level_smoother_kind(h->opts, l), &L.A, h->opts.inner))
                 return fail("smoother plan");
         } else {
             if (devcsr_upload(L.A, C.A)) return fail("upload A");
@@ -280,7 +283,7 @@ extern "C" sss_hip_hier *sss_hip_hier_create(const SSS_AMG *mg, const sss_hip_op
         const auto &sm = h->L[l].sm;
         long long per_sweep = 0;
         for (const auto &ps : sm.pass)
-            per_sweep += ps.nrows == 0 ? 0 : ps.compact ? (sm.kind == SSS_HIP_SMOOTH_JACOBI ? 2 : 1) : ps.depth;
+            per_sweep += ps.nrows == 0 ? 0 : ps.compact ? (sm.kind == SSS_HIP_SMOOTH_JACOBI ? 2 + sm.inner : 1) : ps.depth;
         launches += per_sweep * (h->pars.pre_iter + h->pars.post_iter) + 4;
     }
     if (launches > 4096) h->opts.use_graph = 0;

@@ -42,7 +42,7 @@ static int upload_doubles(double **dst, const std::vector<double> &src)
     return 0;
 }
 
-int smoother_build(SmootherPlan &sp, const SSS_MAT &A, const int *mark, int kind, const DevCSR *dA)
+int smoother_build(SmootherPlan &sp, const SSS_MAT &A, const int *mark, int kind, const DevCSR *dA, int inner)
 {
     const int n = A.num_rows;
     const int *rp = A.row_ptr, *ci = A.col_idx;
@@ -132,6 +132,10 @@ int smoother_build(SmootherPlan &sp, const SSS_MAT &A, const int *mark, int kind
             if (ps.range && kind == SSS_HIP_SMOOTH_JACOBI) {
                 ps.y = dev_alloc<double>((size_t)(hi - lo));
                 if (!ps.y) return hip_fail(hipErrorOutOfMemory, "hipMalloc(y)", __FILE__, __LINE__);
+                if (inner > 0) {
+                    ps.y2 = dev_alloc<double>((size_t)(hi - lo));
+                    if (!ps.y2) return hip_fail(hipErrorOutOfMemory, "hipMalloc(y2)", __FILE__, __LINE__);
+                }
             }
         }
         if (ps.compact && ps.nrows > 0 && !ps.range) {
@@ -162,6 +166,16 @@ int smoother_build(SmootherPlan &sp, const SSS_MAT &A, const int *mark, int kind
         }
     }
     if ((rc = upload_ints(&sp.cls, cls))) return rc;
+    if (kind == SSS_HIP_SMOOTH_JACOBI && inner > 0 && sp.pass[0].range == (sp.pass[0].nrows > 0) &&
+        sp.pass[1].range == (sp.pass[1].nrows > 0)) {
+        // two-stage: mark same-class strictly-lower entries (j < i) as ~j in a private column copy
+        sp.inner = inner;
+        std::vector<int> cts(ci, ci + rp[n]);
+        for (int i = 0; i < n; ++i)
+            for (int k = rp[i]; k < rp[i + 1]; ++k)
+                if (ci[k] < i && cls[ci[k]] == cls[i]) cts[k] = ~ci[k];
+        if ((rc = upload_ints(&sp.cts, cts))) return rc;
+    }
     if (sp.pass[0].range || sp.pass[1].range)
         if ((rc = upload_ints(&sp.diag_pos, diag_pos))) return rc;
     if (kind == SSS_HIP_SMOOTH_JACOBI) {
@@ -182,11 +196,13 @@ void smoother_free(SmootherPlan &sp)
         devcsr_free(ps.sub);
         dev_free(ps.map);
         dev_free(ps.y);
+        dev_free(ps.y2);
     }
     if (sp.d_later != sp.d_first) dev_free(sp.d_later);
     dev_free(sp.d_first);
     dev_free(sp.cls);
     dev_free(sp.diag_pos);
+    dev_free(sp.cts);
     sp = SmootherPlan();
 }
 
@@ -270,60 +286,71 @@ __global__ __launch_bounds__(kBlock) void relax_wave(int m, const int *__restric
     }
 }
 
-// Class pass over rows [lo, hi) of a relabeled level, blocks [blo, ...) of its own CSR: GS with
-// depth 1 (in place) or the relaxation half of C/F-Jacobi (into y[r - lo], copied back after).
-template <bool INPLACE>
+// Class pass over rows [lo, hi) of a relabeled level, blocks [blo, ...) of its own CSR.
+//   MODE 0: GS-CF pass of depth 1, in place (x[r] = t / d).
+//   MODE 1: C/F-Jacobi pass / two-stage stage 0: y[r - lo] = t / d, every x from before the pass.
+//   MODE 2: two-stage inner step: same-class strictly-lower entries (encoded ~j in `ci`) read the
+//           previous inner iterate yp[j - lo], every other entry x[j] (from before the pass).
+// t = b_r - sum over off-diagonal entries in stored order (diag_pos skips the diagonal); rows with
+// |d| <= 1e-20 keep their value.  Columns may carry the two-stage encoding in every mode.
+template <int MODE>
 __global__ __launch_bounds__(kBlock) void relax_range(int blo, const int *__restrict__ blk, const int *__restrict__ rp,
                                                       const int *__restrict__ ci, const double *__restrict__ v,
                                                       const int *__restrict__ diag_pos, int lo,
                                                       const double *__restrict__ b, double *x,
-                                                      double *__restrict__ y, const double *__restrict__ deff)
+                                                      const double *__restrict__ yp, double *__restrict__ y,
+                                                      const double *__restrict__ deff)
 {
     __shared__ SpmvSmem sm;
     const int bid = blo + blockIdx.x;
     const int r0 = blk[bid], r1 = blk[bid + 1];
     const int k0 = rp[r0], k1 = rp[r1];
-    const int cnt = k1 - k0;
-    if (cnt <= kTileEntries) {
-        for (int k = threadIdx.x; k < cnt; k += kBlock) sm.v[k] = v[k0 + k] * x[ci[k0 + k]];
-        __syncthreads();
+    auto fetch = [&](int c) -> double {
+        if (MODE == 2) return c < 0 ? yp[~c - lo] : x[c];
+        return x[c < 0 ? ~c : c];
+    };
+    auto finish = [&](int r, double acc) {
+        const double d = deff[r];
+        if (MODE == 0) {
+            if (fabs(d) > SMALLFLOAT) x[r] = acc / d;
+        } else {
+            const double keep = MODE == 2 ? yp[r - lo] : x[r];
+            y[r - lo] = fabs(d) > SMALLFLOAT ? acc / d : keep;
+        }
+    };
+    if (k1 - k0 <= kTileEntries) {
         const int r = r0 + (int)threadIdx.x;
+        int a = 0, e = 0, dp = -1;
+        double acc = 0.0;
+        if (r < r1) a = rp[r] - k0, e = rp[r + 1] - k0, dp = diag_pos[r], acc = b[r];   // ahead of the tile
+        stage_products_f(sm.v, k0, k1, ci, v, fetch);
+        __syncthreads();
         if (r < r1) {
-            const int a = rp[r] - k0, e = rp[r + 1] - k0, dp = diag_pos[r];
-            double acc = b[r];
             if (dp < 0) acc = chain_sub(acc, sm.v, a, e);
             else {
                 acc = chain_sub(acc, sm.v, a, dp - k0);
                 acc = chain_sub(acc, sm.v, dp - k0 + 1, e);
             }
-            const double d = deff[r];
-            if (INPLACE) {
-                if (fabs(d) > SMALLFLOAT) x[r] = acc / d;
-            } else {
-                y[r - lo] = fabs(d) > SMALLFLOAT ? acc / d : x[r];
-            }
+            finish(r, acc);
         }
     } else {
-        const int r = r0;
+        const int r = r0, dp = diag_pos[r];
         double acc = b[r];
         for (int base = k0; base < k1; base += kTileEntries) {
             const int m = min(kTileEntries, k1 - base);
-            for (int k = threadIdx.x; k < m; k += kBlock) {
-                const int j = ci[base + k];
-                sm.v[k] = (j != r) ? v[base + k] * x[j] : 0.0;
+            stage_products_f(sm.v, base, base + m, ci, v, fetch);
+            __syncthreads();
+            if (threadIdx.x == 0) {
+                if (dp >= base && dp < base + m) {
+                    acc = chain_sub(acc, sm.v, 0, dp - base);
+                    acc = chain_sub(acc, sm.v, dp - base + 1, m);
+                } else {
+                    acc = chain_sub(acc, sm.v, 0, m);
+                }
             }
             __syncthreads();
-            if (threadIdx.x == 0) acc = chain_sub(acc, sm.v, 0, m);
-            __syncthreads();
         }
-        if (threadIdx.x == 0) {
-            const double d = deff[r];
-            if (INPLACE) {
-                if (fabs(d) > SMALLFLOAT) x[r] = acc / d;
-            } else {
-                y[r - lo] = fabs(d) > SMALLFLOAT ? acc / d : x[r];
-            }
-        }
+        if (threadIdx.x == 0) finish(r, acc);
     }
 }
 
@@ -344,15 +371,21 @@ int smoother_run(const SmootherPlan &sp, const DevCSR &A, const double *b, doubl
             const PassSchedule &ps = sp.pass[c];
             if (ps.nrows == 0) continue;
             if (ps.range) {
-                const int nb = ps.bhi - ps.blo;
+                const int nb = ps.bhi - ps.blo, m = ps.hi - ps.lo;
                 if (sp.kind == SSS_HIP_SMOOTH_JACOBI) {
-                    hipLaunchKernelGGL(relax_range<false>, dim3(nb), dim3(kBlock), 0, s, ps.blo, A.blk, A.rp, A.ci,
-                                       A.v, sp.diag_pos, ps.lo, b, x, ps.y, deff);
-                    SSS_HIP(hipMemcpyAsync(x + ps.lo, ps.y, sizeof(double) * (size_t)(ps.hi - ps.lo),
-                                           hipMemcpyDeviceToDevice, s));
+                    const int *cols = sp.cts ? sp.cts : A.ci;
+                    hipLaunchKernelGGL(relax_range<1>, dim3(nb), dim3(kBlock), 0, s, ps.blo, A.blk, A.rp, cols, A.v,
+                                       sp.diag_pos, ps.lo, b, x, (const double *)nullptr, ps.y, deff);
+                    double *cur = ps.y, *nxt = ps.y2;
+                    for (int st = 0; st < sp.inner; ++st) {
+                        hipLaunchKernelGGL(relax_range<2>, dim3(nb), dim3(kBlock), 0, s, ps.blo, A.blk, A.rp, cols,
+                                           A.v, sp.diag_pos, ps.lo, b, x, (const double *)cur, nxt, deff);
+                        std::swap(cur, nxt);
+                    }
+                    SSS_HIP(hipMemcpyAsync(x + ps.lo, cur, sizeof(double) * (size_t)m, hipMemcpyDeviceToDevice, s));
                 } else {
-                    hipLaunchKernelGGL(relax_range<true>, dim3(nb), dim3(kBlock), 0, s, ps.blo, A.blk, A.rp, A.ci, A.v,
-                                       sp.diag_pos, ps.lo, b, x, (double *)nullptr, deff);
+                    hipLaunchKernelGGL(relax_range<0>, dim3(nb), dim3(kBlock), 0, s, ps.blo, A.blk, A.rp, A.ci, A.v,
+                                       sp.diag_pos, ps.lo, b, x, (const double *)nullptr, (double *)nullptr, deff);
                 }
                 continue;
             }

@@ -9,8 +9,9 @@ A step = one outer iteration of SSS_amg_solve (Solve/SSS_SOLVE.c:53-80): one V-c
                     [--no-cpu-baseline]
 
 Modes:
-  throughput : exact GS-CF on level 0 (red-black -> fully parallel), C/F-Jacobi on coarser levels,
-               explicit-inverse coarse solve.  Converges to the same tolerance, a few more V-cycles.
+  throughput : exact GS-CF on level 0 (red-black -> fully parallel), two-stage GS-CF on coarser
+               levels (a Jacobi step + `--inner` Jacobi-Richardson steps on each pass's lower
+               triangle), explicit-inverse coarse solve.  Converges to the same tolerance.
   parity     : exact GS-CF on every level + the reference CG(beta=1)+GMRES coarse solve; x is bitwise
                identical to the reference after every V-cycle (tests/test_gpu_parity.py).
 
@@ -49,6 +50,8 @@ def parse():
     p.add_argument("--cpu-n", type=int, default=0, help="grid edge of the CPU sample (default: same workload)")
     p.add_argument("--mode-smoother", default=None, help="override: exact|hybrid|jacobi")
     p.add_argument("--mode-coarse", default=None, help="override: krylov|direct")
+    p.add_argument("--inner", type=int, default=None,
+                   help="two-stage inner steps on C/F-Jacobi levels (default: SSS_HIP_INNER or 1; 0 = plain C/F-Jacobi)")
     p.add_argument("--converge-max", type=int, default=100, help="max V-cycles of the iterations-to-tol run (0: skip)")
     return p.parse_args()
 
@@ -141,7 +144,8 @@ def main():
 
     t0 = time.perf_counter()
     dev = D.local_rank if D.world > 1 else -1
-    DH = A.DeviceHierarchy(H, smoother=smoother, coarse=coarse, device=dev)
+    DH = A.DeviceHierarchy(H, smoother=smoother, coarse=coarse, device=dev, inner=args.inner)
+    inner = args.inner if args.inner is not None else int(os.environ.get("SSS_HIP_INNER", "1"))
     upload_s = time.perf_counter() - t0
     ones = np.ones(N)
     DH.upload(0, "b", ones)
@@ -227,6 +231,7 @@ def main():
         "dtype": "f64", "data": "synthetic (7-pt Poisson generated in memory, b = x0 = 1)",
         "config": {"workload": f"poisson7_{n}^3", "rows": N, "nnz": nnz, "levels": len(levels),
                    "mode": args.mode, "smoother": smoother, "coarse": coarse,
+                   "inner": inner if smoother != "exact" else None,
                    "iterations_to_tol": its, "final_relres": relres, "time_to_solution_s": solve_s,
                    "setup_s": setup_s, "upload_s": upload_s,
                    "parallelism": f"replicas{D.world}" if D.world > 1 else "single-gpu"},

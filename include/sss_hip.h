@@ -43,12 +43,15 @@ typedef struct sss_hip_opts {
     int row_cap;       /* 0 = uncapped coarse SpMV; 4096 reproduces <<<64,64>>> (as shipped) */
     int use_graph;     /* capture the V-cycle into a hipGraph once and replay it */
     int verbose;       /* engine diagnostics on stderr */
-    int relabel;       /* renumber each level F-first/C-second on the device (bitwise-neutral) */
+    int inner;         /* C/F-Jacobi levels: 0 = plain C/F-Jacobi; k > 0 = two-stage GS-CF with k
+                          Jacobi-Richardson steps on each pass's same-class lower triangle */
+    int relabel;       /* renumber levels F-first/C-second on the device (bitwise-neutral):
+                          0 off, 1 every level but the coarsest, 2 as 1 but level 0 kept */
 } sss_hip_opts;
 
 /* Defaults, overridable by environment: SSS_HIP_SMOOTHER=exact|hybrid|jacobi,
  * SSS_HIP_COARSE=krylov|direct, SSS_HIP_ROWCAP=<n>, SSS_HIP_GRAPH=0|1, SSS_HIP_DEVICE=<n>,
- * SSS_HIP_VERBOSE=0|1, SSS_HIP_RELABEL=0|1 (default 1). */
+ * SSS_HIP_VERBOSE=0|1, SSS_HIP_RELABEL=0|1|2 (default 1), SSS_HIP_INNER=<k> (default 1). */
 void sss_hip_opts_default(sss_hip_opts *o);
 
 /* Number of usable HIP devices (0 when none; never exits). */

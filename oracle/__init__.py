@@ -23,7 +23,7 @@ REF_PATH = HERE / "_ref" / "libsss_ref.so"
 class ORA_OPTS(C.Structure):
     _fields_ = [("row_cap", C.c_int), ("coarse_mode", C.c_int), ("smoother", C.c_int), ("jacobi_from", C.c_int),
                 ("verbose", C.c_int),
-                ("jacobi_l1", C.c_int), ("omega", C.c_double)]
+                ("jacobi_l1", C.c_int), ("omega", C.c_double), ("inner", C.c_int)]
 
 
 _ora = None
@@ -47,6 +47,7 @@ def load():
             "ora_gs": (None, [dp, C.c_int, C.c_int, C.c_int, P(SSS_MAT), dp, C.c_int]),
             "ora_cf_jacobi": (None, [dp, P(SSS_MAT), dp, C.c_int, ip]),
             "ora_cf_jacobi_w": (None, [dp, P(SSS_MAT), dp, C.c_int, ip, C.c_double, C.c_int]),
+            "ora_cf_twostage": (None, [dp, P(SSS_MAT), dp, C.c_int, ip, C.c_int]),
             "ora_smoother_pre": (None, [P(SSS_SMTR)]),
             "ora_smoother_post": (None, [P(SSS_SMTR)]),
             "ora_cg": (C.c_int, [P(SSS_KRYLOV), C.c_int]),

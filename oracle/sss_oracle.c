@@ -214,6 +214,50 @@ void ora_cf_jacobi(double *u, const SSS_MAT *A, const double *b, int sweeps, con
     ora_cf_jacobi_w(u, A, b, sweeps, mark, 1.0, 0);
 }
 
+/* Two-stage GS-CF (engine extension): each class pass solves the pass's triangular
+ * system  (D + L_cc) x_c = b_c - U_cc x_c_old - A_c,other x_other  approximately: a Jacobi step
+ * y0 (every row reads the values from before the pass), then `inner` Jacobi-Richardson steps in
+ * which row i reads y_{k-1}[j] for same-class j < i and the pre-pass value for every other j.
+ * inner >= DAG depth of the pass reproduces ora_gs_cf's values; per row the subtraction order is
+ * the stored CSR order; d and the |d| > 1e-20 guard as in C/F-Jacobi. */
+void ora_cf_twostage(double *u, const SSS_MAT *A, const double *b, int sweeps, const int *mark, int inner)
+{
+    const int n = A->num_rows;
+    const size_t sz = sizeof(double) * (size_t)(n > 0 ? n : 1);
+    double *old = (double *)malloc(sz), *cur = (double *)malloc(sz), *nxt = (double *)malloc(sz);
+    while (sweeps--) {
+        for (int pass = 0; pass < (mark ? 2 : 1); ++pass) {
+            copy(n, u, old);
+            copy(n, u, cur);
+            for (int stage = 0; stage <= inner; ++stage) {
+                copy(n, cur, nxt);
+                for (int i = 0; i < n; ++i) {
+                    double t, d = 0.0;
+                    if (mark && (mark[i] == 1) != pass) continue;
+                    t = b[i];
+                    for (int k = A->row_ptr[i]; k < A->row_ptr[i + 1]; ++k) {
+                        const int j = A->col_idx[k];
+                        if (j == i) {
+                            d = A->val[k];
+                            continue;
+                        }
+                        const int lower = stage > 0 && j < i && (!mark || (mark[j] == 1) == pass);
+                        t -= A->val[k] * (lower ? cur[j] : old[j]);
+                    }
+                    if (SSS_ABS(d) > SMALLFLOAT) nxt[i] = t / d;
+                }
+                double *sw = cur;
+                cur = nxt;
+                nxt = sw;
+            }
+            copy(n, cur, u);
+        }
+    }
+    free(old);
+    free(cur);
+    free(nxt);
+}
+
 static const ora_opts *g_cur_opts = NULL;
 
 static void smoother_dispatch(SSS_SMTR *s, int post, const char *fname)
@@ -226,6 +270,10 @@ static void smoother_dispatch(SSS_SMTR *s, int post, const char *fname)
         else ora_gs(s->x->d, s->iend, s->istart, s->istep, s->A, s->b->d, s->nsweeps);
         break;
     case SSS_SM_JACOBI:
+        if (g_cur_opts && g_cur_opts->inner > 0) {
+            ora_cf_twostage(s->x->d, s->A, s->b->d, s->nsweeps, use_cf ? s->ordering : NULL, g_cur_opts->inner);
+            break;
+        }
         ora_cf_jacobi_w(s->x->d, s->A, s->b->d, s->nsweeps, use_cf ? s->ordering : NULL,
                         g_cur_opts ? g_cur_opts->omega : 1.0, g_cur_opts ? g_cur_opts->jacobi_l1 : 0);
         break;

@@ -22,6 +22,8 @@ typedef struct {
     int verbose;      /* print the reference iteration table */
     int jacobi_l1;    /* C/F-Jacobi divisor: 0 = a_ii, 1 = a_ii + sum_{j != i} |a_ij| over same-class j (l1) */
     double omega;     /* C/F-Jacobi weight (1.0 = plain) */
+    int inner;        /* > 0: two-stage GS-CF instead of C/F-Jacobi, with `inner` Jacobi-Richardson
+                         steps on the same-class lower triangle (ora_cf_twostage) */
 } ora_opts;
 
 void ora_opts_default(ora_opts *o);
@@ -37,6 +39,7 @@ void ora_gs(double *u, int i1, int in, int step, const SSS_MAT *A, const double 
 void ora_cf_jacobi(double *u, const SSS_MAT *A, const double *b, int sweeps, const int *mark);
 void ora_cf_jacobi_w(double *u, const SSS_MAT *A, const double *b, int sweeps, const int *mark, double omega,
                      int l1);
+void ora_cf_twostage(double *u, const SSS_MAT *A, const double *b, int sweeps, const int *mark, int inner);
 void ora_smoother_pre(SSS_SMTR *s);
 void ora_smoother_post(SSS_SMTR *s);
 

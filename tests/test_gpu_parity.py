@@ -222,9 +222,10 @@ def test_coarse_direct_solves(p32_h):
 
 
 # ---------------------------------------------------------------- whole solve
-def _gpu_history(H, smoother="exact", coarse="krylov", row_cap=0, max_it=100, relabel=None, graph=None):
+def _gpu_history(H, smoother="exact", coarse="krylov", row_cap=0, max_it=100, relabel=None, graph=None, inner=None):
     n = H.level(0).A.num_rows
-    D = A.DeviceHierarchy(H, smoother=smoother, coarse=coarse, row_cap=row_cap, relabel=relabel, graph=graph)
+    D = A.DeviceHierarchy(H, smoother=smoother, coarse=coarse, row_cap=row_cap, relabel=relabel, graph=graph,
+                          inner=inner)
     b = np.ones(n)
     D.upload(0, "b", b)
     D.upload(0, "x", np.ones(n))
@@ -268,9 +269,10 @@ def test_solve_direct_coarse(request, hname):
     assert np.linalg.norm(x_g - x_r) <= 1e-6 * np.linalg.norm(x_r)
 
 
-def test_solve_hybrid_jacobi_converges(p32_h):
-    rel_o, x_o = _oracle_history(p32_h, smoother=1, coarse_mode=1)
-    rel_g, x_g = _gpu_history(p32_h, smoother="hybrid", coarse="direct")
+@pytest.mark.parametrize("inner", [0, 1])
+def test_solve_hybrid_jacobi_converges(p32_h, inner):
+    rel_o, x_o = _oracle_history(p32_h, smoother=1, coarse_mode=1, inner=inner)
+    rel_g, x_g = _gpu_history(p32_h, smoother="hybrid", coarse="direct", inner=inner)
     assert len(rel_g) == len(rel_o)
     assert np.allclose(rel_g, rel_o, rtol=1e-6)
     rel_ref, _ = _oracle_history(p32_h)
@@ -291,13 +293,14 @@ def test_relabel_is_bitwise_neutral(request, hname, smoother, coarse):
 
 
 @pytest.mark.parametrize("hname", ["bus_h", "p32_h", "a27_h"])
-@pytest.mark.parametrize("smoother", ["exact", "jacobi"])
-def test_relabeled_level_smoothers_bitwise(request, hname, smoother):
+@pytest.mark.parametrize("smoother,inner", [("exact", 0), ("jacobi", 0), ("jacobi", 1), ("jacobi", 2)])
+def test_relabeled_level_smoothers_bitwise(request, hname, smoother, inner):
     """Per level, through the relabeled mirror: upload (b, x) in the caller's labels, run the device
-    pre/post smoother, download, compare bitwise with the oracle on the original labels."""
+    pre/post smoother (GS-CF, C/F-Jacobi or two-stage GS-CF), download, compare bitwise with the
+    oracle on the original labels."""
     H = request.getfixturevalue(hname)
     ora = oracle.load()
-    D = A.DeviceHierarchy(H, smoother=smoother, coarse="direct", relabel=1)
+    D = A.DeviceHierarchy(H, smoother=smoother, coarse="direct", relabel=1, inner=inner)
     rng = np.random.default_rng(23)
     try:
         for l in range(H.num_levels - 1):
@@ -313,7 +316,9 @@ def test_relabeled_level_smoothers_bitwise(request, hname, smoother):
                 assert np.array_equal(D.download(l, "b").view(np.uint64), b.view(np.uint64))
                 xr = x0.copy()
                 sweeps = H.pars.post_iter if post else H.pars.pre_iter
-                if smoother == "jacobi":
+                if smoother == "jacobi" and inner > 0:
+                    ora.ora_cf_twostage(dptr(xr), C.byref(L.A), dptr(b), sweeps, L.cfmark.d, inner)
+                elif smoother == "jacobi":
                     ora.ora_cf_jacobi(dptr(xr), C.byref(L.A), dptr(b), sweeps, L.cfmark.d)
                 else:
                     sr = _smtr(L.A, b, xr, L.cfmark.d, sweeps, post)
@@ -321,6 +326,18 @@ def test_relabeled_level_smoothers_bitwise(request, hname, smoother):
                 assert np.array_equal(xg.view(np.uint64), xr.view(np.uint64)), (hname, l, post)
     finally:
         D.close()
+
+
+@pytest.mark.parametrize("hname", ["bus_h", "p32_h", "a27_h"])
+@pytest.mark.parametrize("inner", [0, 1])
+def test_solve_hybrid_krylov_bitwise(request, hname, inner):
+    """Throughput smoothers with the reference coarse solver: x bitwise equal to the oracle's."""
+    H = request.getfixturevalue(hname)
+    rel_r, x_r = _oracle_history(H, smoother=1, inner=inner)
+    rel_g, x_g = _gpu_history(H, smoother="hybrid", coarse="krylov", inner=inner)
+    assert len(rel_g) == len(rel_r)
+    assert np.array_equal(x_g.view(np.uint64), x_r.view(np.uint64))
+    assert np.allclose(rel_g, rel_r, rtol=1e-13, atol=0)
 
 
 def test_solve_bus_known_answer(bus_h):
