@@ -56,6 +56,7 @@ struct DevCSR {
 int devcsr_upload(DevCSR &d, const SSS_MAT &h, int split = -1);
 void devcsr_free(DevCSR &d);
 int build_row_blocks(const int *h_rp, int n, std::vector<int> &blk, int split = -1);
+int wave_row_min();
 
 // y <- op(A x) on `stream` (see SSS_HIP_SPMV_*).  `partial` (optional, RESID only): one
 // sum-of-squares of the written y per row block, for a deterministic fused norm.

@@ -22,6 +22,7 @@
 #include "sss_spmv_dev.hpp"
 
 #include <algorithm>
+#include <type_traits>
 #include <cmath>
 
 namespace sss {
@@ -79,7 +80,8 @@ int smoother_build(SmootherPlan &sp, const SSS_MAT &A, const int *mark, int kind
     }
     // level schedule per class
     long long nnz_total = rp[n];
-    sp.long_rows = n > 0 && nnz_total >= (long long)kWaveRowMin * n;
+    // exact GS depth launches hold few rows each: a wave per row pays from short lengths on
+    sp.long_rows = n > 0 && nnz_total >= (long long)std::min(32, wave_row_min()) * n;
     for (int i = 0; i < n; ++i) {
         int dep = pushed[i];
         for (int k = rp[i]; k < rp[i + 1]; ++k) {
@@ -237,7 +239,8 @@ __global__ __launch_bounds__(kBlock) void gs_depth_wave(const int *__restrict__ 
     const int t = blockIdx.x * 4 + wave;
     if (t >= cnt) return;
     const int i = rows[t];
-    const double acc = wave_row_chain<true>(rp[i], rp[i + 1], ci, v, x, i, b[i], strips[wave]);
+    const double acc = wave_row_chain<true>(
+        rp[i], rp[i + 1], ci, v, [&](int c, double a) { return c == i ? 0.0 : a * x[c]; }, b[i], strips[wave]);
     if ((threadIdx.x & 63) == 0) {
         const double d = deff[i];
         if (fabs(d) > SMALLFLOAT) x[i] = acc / d;
@@ -275,7 +278,9 @@ __global__ __launch_bounds__(kBlock) void relax_wave(int m, const int *__restric
     const int r = blockIdx.x * 4 + wave;
     if (r >= m) return;
     const int i = map[r];
-    const double acc = wave_row_chain<true>(rp[r], rp[r + 1], ci, v, x, i, b[i], strips[wave]);
+    const double acc = wave_row_chain<true>(
+        rp[r], rp[r + 1], ci, v, [&](int c, double a) { return (c < 0 || c == i) ? 0.0 : a * x[c]; }, b[i],
+        strips[wave]);
     if ((threadIdx.x & 63) == 0) {
         const double d = deff[i];
         if (INPLACE) {
@@ -354,6 +359,38 @@ __global__ __launch_bounds__(kBlock) void relax_range(int blo, const int *__rest
     }
 }
 
+// relax_range for long-row levels: one wave per row (rows lo + 4 * blockIdx.x + wave).  The
+// diagonal (single per row on range levels) contributes an exact 0.0 to the chain.
+template <int MODE>
+__global__ __launch_bounds__(kBlock) void relax_range_wave(int lo, int hi, const int *__restrict__ rp,
+                                                           const int *__restrict__ ci, const double *__restrict__ v,
+                                                           const double *__restrict__ b, double *x,
+                                                           const double *__restrict__ yp, double *__restrict__ y,
+                                                           const double *__restrict__ deff)
+{
+    __shared__ double strips[4][kWaveStage];
+    const int wave = threadIdx.x >> 6;
+    const int r = lo + blockIdx.x * 4 + wave;
+    if (r >= hi) return;
+    const double acc = wave_row_chain<true>(
+        rp[r], rp[r + 1], ci, v,
+        [&](int c, double a) -> double {
+            if (c == r) return 0.0;
+            if (MODE == 2) return a * (c < 0 ? yp[~c - lo] : x[c]);
+            return a * x[c < 0 ? ~c : c];
+        },
+        b[r], strips[wave]);
+    if ((threadIdx.x & 63) == 0) {
+        const double d = deff[r];
+        if (MODE == 0) {
+            if (fabs(d) > SMALLFLOAT) x[r] = acc / d;
+        } else {
+            const double keep = MODE == 2 ? yp[r - lo] : x[r];
+            y[r - lo] = fabs(d) > SMALLFLOAT ? acc / d : keep;
+        }
+    }
+}
+
 __global__ __launch_bounds__(kBlock) void scatter_rows(int m, const int *__restrict__ map, const double *__restrict__ y,
                                                        double *__restrict__ x)
 {
@@ -371,21 +408,28 @@ int smoother_run(const SmootherPlan &sp, const DevCSR &A, const double *b, doubl
             const PassSchedule &ps = sp.pass[c];
             if (ps.nrows == 0) continue;
             if (ps.range) {
-                const int nb = ps.bhi - ps.blo, m = ps.hi - ps.lo;
+                const int nb = ps.bhi - ps.blo, m = ps.hi - ps.lo, nw = (m + 3) / 4;
+                const bool wave = A.wave_rows;
+                auto relax = [&](auto mode, const int *cols, const double *yp, double *y) {
+                    constexpr int M = decltype(mode)::value;
+                    if (wave)
+                        hipLaunchKernelGGL(relax_range_wave<M>, dim3(nw), dim3(kBlock), 0, s, ps.lo, ps.hi, A.rp, cols,
+                                           A.v, b, x, yp, y, deff);
+                    else
+                        hipLaunchKernelGGL(relax_range<M>, dim3(nb), dim3(kBlock), 0, s, ps.blo, A.blk, A.rp, cols,
+                                           A.v, sp.diag_pos, ps.lo, b, x, yp, y, deff);
+                };
                 if (sp.kind == SSS_HIP_SMOOTH_JACOBI) {
                     const int *cols = sp.cts ? sp.cts : A.ci;
-                    hipLaunchKernelGGL(relax_range<1>, dim3(nb), dim3(kBlock), 0, s, ps.blo, A.blk, A.rp, cols, A.v,
-                                       sp.diag_pos, ps.lo, b, x, (const double *)nullptr, ps.y, deff);
+                    relax(std::integral_constant<int, 1>(), cols, (const double *)nullptr, ps.y);
                     double *cur = ps.y, *nxt = ps.y2;
                     for (int st = 0; st < sp.inner; ++st) {
-                        hipLaunchKernelGGL(relax_range<2>, dim3(nb), dim3(kBlock), 0, s, ps.blo, A.blk, A.rp, cols,
-                                           A.v, sp.diag_pos, ps.lo, b, x, (const double *)cur, nxt, deff);
+                        relax(std::integral_constant<int, 2>(), cols, (const double *)cur, nxt);
                         std::swap(cur, nxt);
                     }
                     SSS_HIP(hipMemcpyAsync(x + ps.lo, cur, sizeof(double) * (size_t)m, hipMemcpyDeviceToDevice, s));
                 } else {
-                    hipLaunchKernelGGL(relax_range<0>, dim3(nb), dim3(kBlock), 0, s, ps.blo, A.blk, A.rp, A.ci, A.v,
-                                       sp.diag_pos, ps.lo, b, x, (const double *)nullptr, (double *)nullptr, deff);
+                    relax(std::integral_constant<int, 0>(), A.ci, (const double *)nullptr, (double *)nullptr);
                 }
                 continue;
             }

@@ -15,6 +15,8 @@
 // Roofline: HBM-bound, 12 B/nnz (fp64 value + int32 column) + 4 B/row (row_ptr) + 8 B/row
 // per vector stream (x compulsory, y, b); no MFMA (≈0.13 flop/byte).
 #include "sss_engine.hpp"
+
+#include <cstdlib>
 #include "sss_spmv_dev.hpp"
 
 #include <algorithm>
@@ -25,6 +27,14 @@ int hip_fail(hipError_t e, const char *what, const char *file, int line)
 {
     fprintf(stderr, "### ERROR: HIP call %s failed at %s:%d: %s\n", what, file, line, hipGetErrorString(e));
     return ERROR_MISC;
+}
+
+// Average entries per row from which a matrix takes the wave-per-row kernels (kWaveRowMin;
+// SSS_HIP_WAVE_MIN overrides it at upload time, which the tests use to cover both paths).
+int wave_row_min()
+{
+    const char *e = getenv("SSS_HIP_WAVE_MIN");
+    return (e && *e) ? atoi(e) : kWaveRowMin;
 }
 
 int build_row_blocks(const int *h_rp, int n, std::vector<int> &blk, int split)
@@ -69,7 +79,7 @@ int devcsr_upload(DevCSR &d, const SSS_MAT &h, int split)
     d.blk = dev_alloc<int>(blk.size());
     if (!d.blk) return hip_fail(hipErrorOutOfMemory, "hipMalloc(blk)", __FILE__, __LINE__);
     SSS_HIP(hipMemcpy(d.blk, blk.data(), sizeof(int) * blk.size(), hipMemcpyHostToDevice));
-    d.wave_rows = d.n > 0 && (long long)d.nnz >= (long long)kWaveRowMin * d.n;
+    d.wave_rows = d.n > 0 && (long long)d.nnz >= (long long)wave_row_min() * d.n;
     d.ngrid = d.wave_rows ? (d.n + 3) / 4 : d.nblk;
     return 0;
 }
@@ -122,7 +132,8 @@ __global__ __launch_bounds__(kBlock) void spmv_wave(int n, const int *__restrict
     const int r = blockIdx.x * 4 + wave;
     double sq = 0.0;
     if (r < n) {
-        const double s = wave_row_chain<false>(rp[r], rp[r + 1], ci, v, x, -1, 0.0, strips[wave]);
+        const double s = wave_row_chain<false>(rp[r], rp[r + 1], ci, v,
+                                               [&](int c, double a) { return a * x[c]; }, 0.0, strips[wave]);
         if (lane == 0) {
             bool write = true;
             double out;
@@ -212,7 +223,7 @@ extern "C" sss_hip_spmv_plan *sss_hip_spmv_plan_create(int n, int nnz, const int
     p->csr.nnz = nnz;
     p->csr.rp = const_cast<int *>(d_rp);
     p->csr.nblk = sss::build_row_blocks(h_rp, n, blk);
-    p->csr.wave_rows = n > 0 && (long long)nnz >= (long long)sss::kWaveRowMin * n;
+    p->csr.wave_rows = n > 0 && (long long)nnz >= (long long)sss::wave_row_min() * n;
     p->csr.ngrid = p->csr.wave_rows ? (n + 3) / 4 : p->csr.nblk;
     p->csr.blk = sss::dev_alloc<int>(blk.size());
     if (!p->csr.blk || hipMemcpy(p->csr.blk, blk.data(), sizeof(int) * blk.size(), hipMemcpyHostToDevice) != hipSuccess) {

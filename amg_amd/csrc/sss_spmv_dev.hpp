@@ -205,12 +205,13 @@ __device__ __forceinline__ void csr_block_relax(const int *__restrict__ blk, con
 namespace sss {
 
 // ---- wave-per-row path for long rows (avg nnz/row >= kWaveRowMin) ----------------------------
-// Four rows per 256-thread workgroup, one per wave.  All 64 lanes gather a_k * x_{j_k} for a
-// strip of the row (every load in flight at once) into the wave's private LDS strip; lane 0 then
-// runs the reference's in-order chain over the strip.  LDS traffic of one wave is in order, so a
-// wave-level fence is the only synchronisation needed.
-constexpr int kWaveStage = 1024;   // doubles per wave strip (8 KiB; 32 KiB per workgroup)
-constexpr int kWaveRowMin = 1 << 30;   // wave path disabled: the tile path wins at every measured row length
+// Four rows per 256-thread workgroup, one per wave.  All 64 lanes gather a strip of the row's
+// products (kWaveStage / 64 independent loads per lane) into the wave's private LDS strip; lane 0
+// then runs the in-order chain over the strip.  LDS traffic of one wave is in order, so a
+// wave-level fence is the only synchronisation needed.  Measured on the 7-pt 256^3 hierarchy
+// (tools/lab_rows.py): the tile path wins up to ~400 entries per row, this path from ~700.
+constexpr int kWaveStage = 256;    // doubles per wave strip (2 KiB; 8 KiB per workgroup)
+constexpr int kWaveRowMin = 600;   // average entries per row from which a matrix uses this path
 
 __device__ __forceinline__ void wave_sync()
 {
@@ -219,36 +220,33 @@ __device__ __forceinline__ void wave_sync()
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-// SUB = false: returns 0.0 + p_0 + p_1 + ... (SpMV order, SSS_utils.c:174).
-// SUB = true : returns init - p_0 - p_1 - ... skipping j == self (GS order, SSS_smooth.c:21-26).
-// Result valid in lane 0 of the wave.
-template <bool SUB>
+// SUB = false: returns init + p_0 + p_1 + ...;  SUB = true: init - p_0 - p_1 - ...  (stored order)
+// with p_k = prod(col_k, val_k).  Result valid in lane 0 of the wave.
+template <bool SUB, class Prod>
 __device__ __forceinline__ double wave_row_chain(int k0, int k1, const int *__restrict__ ci,
-                                                 const double *__restrict__ v, const double *x, int self,
-                                                 double init, double *strip)
+                                                 const double *__restrict__ v, Prod prod, double init,
+                                                 double *strip)
 {
+    constexpr int U = kWaveStage / 64;
     const int lane = threadIdx.x & 63;
     double acc = init;
     for (int base = k0; base < k1; base += kWaveStage) {
         const int m = min(kWaveStage, k1 - base);
-        for (int q = lane; q < m; q += 64) {
-            const int j = ci[base + q];
-            strip[q] = (j < 0 || (SUB && j == self)) ? 0.0 : v[base + q] * x[j];
+        int c[U];
+        double a[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int q = lane + 64 * u;
+            c[u] = q < m ? ci[base + q] : 0;
+            a[u] = q < m ? v[base + q] : 0.0;
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int q = lane + 64 * u;
+            if (q < m) strip[q] = prod(c[u], a[u]);
         }
         wave_sync();
-        if (lane == 0) {
-            int q = 0;
-            for (; q + 8 <= m; q += 8) {
-                const double a0 = strip[q], a1 = strip[q + 1], a2 = strip[q + 2], a3 = strip[q + 3];
-                const double a4 = strip[q + 4], a5 = strip[q + 5], a6 = strip[q + 6], a7 = strip[q + 7];
-                if (SUB) { acc -= a0; acc -= a1; acc -= a2; acc -= a3; acc -= a4; acc -= a5; acc -= a6; acc -= a7; }
-                else { acc += a0; acc += a1; acc += a2; acc += a3; acc += a4; acc += a5; acc += a6; acc += a7; }
-            }
-            for (; q < m; ++q) {
-                if (SUB) acc -= strip[q];
-                else acc += strip[q];
-            }
-        }
+        if (lane == 0) acc = SUB ? chain_sub(acc, strip, 0, m) : chain_add(acc, strip, 0, m);
         wave_sync();
     }
     return acc;

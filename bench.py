@@ -230,6 +230,7 @@ def main():
         "ms_per_step": ms_per_step, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
         "dtype": "f64", "data": "synthetic (7-pt Poisson generated in memory, b = x0 = 1)",
         "config": {"workload": f"poisson7_{n}^3", "rows": N, "nnz": nnz, "levels": len(levels),
+                   "hierarchy": [list(t) for t in levels],
                    "mode": args.mode, "smoother": smoother, "coarse": coarse,
                    "inner": inner if smoother != "exact" else None,
                    "iterations_to_tol": its, "final_relres": relres, "time_to_solution_s": solve_s,

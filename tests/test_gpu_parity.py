@@ -48,9 +48,18 @@ def test_device_present():
 
 
 # ---------------------------------------------------------------- SpMV family, bitwise
+@pytest.fixture(params=["tile", "wave"])
+def row_path(request, monkeypatch):
+    """Run a test with the default kernel choice, then with every matrix forced onto the
+    wave-per-row kernels (SSS_HIP_WAVE_MIN=1), so both row paths are checked bitwise."""
+    if request.param == "wave":
+        monkeypatch.setenv("SSS_HIP_WAVE_MIN", "1")
+    return request.param
+
+
 @pytest.mark.parametrize("hname", ["bus_h", "p32_h", "a27_h"])
 @pytest.mark.parametrize("op", ["mxy", "amxpy", "resid", "acc"])
-def test_spmv_bitwise_all_levels(request, hname, op):
+def test_spmv_bitwise_all_levels(request, hname, op, row_path):
     H = request.getfixturevalue(hname)
     ora = oracle.load()
     rng = np.random.default_rng(7)
@@ -122,7 +131,7 @@ def _smtr(M, b, x, mark, sweeps, post, smoother=2):
 
 @pytest.mark.parametrize("hname", ["bus_h", "p32_h", "a27_h"])
 @pytest.mark.parametrize("post", [False, True])
-def test_gscf_bitwise_all_levels(request, hname, post):
+def test_gscf_bitwise_all_levels(request, hname, post, row_path):
     H = request.getfixturevalue(hname)
     ora = oracle.load()
     rng = np.random.default_rng(11)
@@ -163,7 +172,7 @@ def test_gscf_missing_diagonal_stale_d():
 
 
 @pytest.mark.parametrize("hname", ["bus_h", "p32_h"])
-def test_cf_jacobi_bitwise(request, hname):
+def test_cf_jacobi_bitwise(request, hname, row_path):
     H = request.getfixturevalue(hname)
     ora = oracle.load()
     rng = np.random.default_rng(2)
@@ -249,7 +258,7 @@ def _oracle_history(H, **kw):
 
 
 @pytest.mark.parametrize("hname", ["bus_h", "p32_h", "a27_h"])
-def test_solve_parity_mode(request, hname):
+def test_solve_parity_mode(request, hname, row_path):
     H = request.getfixturevalue(hname)
     rel_r, x_r = _oracle_history(H)
     rel_g, x_g = _gpu_history(H)
@@ -294,7 +303,7 @@ def test_relabel_is_bitwise_neutral(request, hname, smoother, coarse):
 
 @pytest.mark.parametrize("hname", ["bus_h", "p32_h", "a27_h"])
 @pytest.mark.parametrize("smoother,inner", [("exact", 0), ("jacobi", 0), ("jacobi", 1), ("jacobi", 2)])
-def test_relabeled_level_smoothers_bitwise(request, hname, smoother, inner):
+def test_relabeled_level_smoothers_bitwise(request, hname, smoother, inner, row_path):
     """Per level, through the relabeled mirror: upload (b, x) in the caller's labels, run the device
     pre/post smoother (GS-CF, C/F-Jacobi or two-stage GS-CF), download, compare bitwise with the
     oracle on the original labels."""
@@ -330,7 +339,7 @@ def test_relabeled_level_smoothers_bitwise(request, hname, smoother, inner):
 
 @pytest.mark.parametrize("hname", ["bus_h", "p32_h", "a27_h"])
 @pytest.mark.parametrize("inner", [0, 1])
-def test_solve_hybrid_krylov_bitwise(request, hname, inner):
+def test_solve_hybrid_krylov_bitwise(request, hname, inner, row_path):
     """Throughput smoothers with the reference coarse solver: x bitwise equal to the oracle's."""
     H = request.getfixturevalue(hname)
     rel_r, x_r = _oracle_history(H, smoother=1, inner=inner)

@@ -1,0 +1,27 @@
+"""Run only the level-0 residual SpMV of the bench workload (for rocprofv3 --pmc passes).
+
+    rocprofv3 --pmc FETCH_SIZE --output-format csv -d OUT -o run -- python3 tools/pmc_level0.py 400
+"""
+import os
+import sys
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent.parent
+sys.path.insert(0, str(ROOT))
+import numpy as np  # noqa: E402
+
+import amg_amd as A  # noqa: E402
+
+n = int(sys.argv[1]) if len(sys.argv) > 1 else 400
+reps = int(sys.argv[2]) if len(sys.argv) > 2 else 5
+fd = os.dup(1)
+nul = os.open(os.devnull, os.O_WRONLY)
+os.dup2(nul, 1)
+H = A.Hierarchy(A.generate(7, n))
+os.dup2(fd, 1)
+D = A.DeviceHierarchy(H, smoother="hybrid", coarse="direct")
+N = H.level(0).A.num_rows
+D.upload(0, "b", np.ones(N))
+D.upload(0, "x", np.ones(N))
+ms = D.time_level0_spmv(reps)
+print(f"level0 n={N} nnz={H.level(0).A.num_nnzs} avg_ms={ms:.4f}", flush=True)
