@@ -78,6 +78,12 @@ struct PassSchedule {          // rows of one class (F or C), grouped by DAG dep
     bool range = false;
     int lo = 0, hi = 0, blo = 0, bhi = 0;
     double *y2 = nullptr;      // second inner-iterate buffer (two-stage)
+    // Two-stage GS-CF (sss_smooth.hip): the pass's rows with their off-diagonal entries reordered
+    // to [N_i | L_i] (L_i: same class, j < i; both in stored order), the split positions, the
+    // L-only rows, and P_i = b_i - sum_{N_i} a_ij x_j of the current pass.
+    DevCSR ts_nl, ts_lo;
+    int *ts_split = nullptr;
+    double *ts_P = nullptr;
     DevCSR sub;
     int *map = nullptr;        // local row -> global row
     double *y = nullptr;       // Jacobi: new values of this class, scattered after the pass
@@ -91,8 +97,6 @@ struct SmootherPlan {
     bool long_rows = false;    // wave-per-row kernels
     int *diag_pos = nullptr;   // range passes: CSR position of each row's diagonal (-1: none)
     int inner = 0;             // two-stage GS-CF inner steps (kind == JACOBI, range passes only)
-    int *cts = nullptr;        // two-stage: the level's columns with same-class strictly-lower entries
-                               // stored as ~j (decoded by every two-stage kernel)
 };
 // contiguous: mark is relabeled so class F occupies rows [0, nF) and class C rows [nF, n), and A was
 // uploaded with a block split at nF (its DevCSR is passed to allow range passes).

@@ -170,13 +170,44 @@ int smoother_build(SmootherPlan &sp, const SSS_MAT &A, const int *mark, int kind
     if ((rc = upload_ints(&sp.cls, cls))) return rc;
     if (kind == SSS_HIP_SMOOTH_JACOBI && inner > 0 && sp.pass[0].range == (sp.pass[0].nrows > 0) &&
         sp.pass[1].range == (sp.pass[1].nrows > 0)) {
-        // two-stage: mark same-class strictly-lower entries (j < i) as ~j in a private column copy
         sp.inner = inner;
-        std::vector<int> cts(ci, ci + rp[n]);
-        for (int i = 0; i < n; ++i)
-            for (int k = rp[i]; k < rp[i + 1]; ++k)
-                if (ci[k] < i && cls[ci[k]] == cls[i]) cts[k] = ~ci[k];
-        if ((rc = upload_ints(&sp.cts, cts))) return rc;
+        for (auto &ps : sp.pass) {
+            if (ps.nrows == 0) continue;
+            const int m = ps.hi - ps.lo;
+            std::vector<int> nrp(1, 0), nci, lrp(1, 0), lci, split(m);
+            std::vector<double> nv, lv;
+            for (int i = ps.lo; i < ps.hi; ++i) {
+                for (int k = rp[i]; k < rp[i + 1]; ++k) {   // N_i: off-diagonal, not same-class lower
+                    const int j = ci[k];
+                    if (j != i && !(j >= ps.lo && j < i)) nci.push_back(j), nv.push_back(v[k]);
+                }
+                split[i - ps.lo] = (int)nci.size();
+                for (int k = rp[i]; k < rp[i + 1]; ++k) {   // L_i
+                    const int j = ci[k];
+                    if (j >= ps.lo && j < i) {
+                        nci.push_back(j), nv.push_back(v[k]);
+                        lci.push_back(j), lv.push_back(v[k]);
+                    }
+                }
+                nrp.push_back((int)nci.size());
+                lrp.push_back((int)lci.size());
+            }
+            auto mk = [&](std::vector<int> &r, std::vector<int> &c, std::vector<double> &w) {
+                SSS_MAT M;
+                M.num_rows = m;
+                M.num_cols = n;
+                M.num_nnzs = (int)c.size();
+                M.row_ptr = r.data();
+                M.col_idx = c.data();
+                M.val = w.data();
+                return M;
+            };
+            SSS_MAT Mn = mk(nrp, nci, nv), Ml = mk(lrp, lci, lv);
+            if ((rc = devcsr_upload(ps.ts_nl, Mn)) || (rc = devcsr_upload(ps.ts_lo, Ml))) return rc;
+            if ((rc = upload_ints(&ps.ts_split, split))) return rc;
+            ps.ts_P = dev_alloc<double>((size_t)m);
+            if (!ps.ts_P) return hip_fail(hipErrorOutOfMemory, "hipMalloc(P)", __FILE__, __LINE__);
+        }
     }
     if (sp.pass[0].range || sp.pass[1].range)
         if ((rc = upload_ints(&sp.diag_pos, diag_pos))) return rc;
@@ -199,12 +230,15 @@ void smoother_free(SmootherPlan &sp)
         dev_free(ps.map);
         dev_free(ps.y);
         dev_free(ps.y2);
+        devcsr_free(ps.ts_nl);
+        devcsr_free(ps.ts_lo);
+        dev_free(ps.ts_split);
+        dev_free(ps.ts_P);
     }
     if (sp.d_later != sp.d_first) dev_free(sp.d_later);
     dev_free(sp.d_first);
     dev_free(sp.cls);
     dev_free(sp.diag_pos);
-    dev_free(sp.cts);
     sp = SmootherPlan();
 }
 
@@ -294,10 +328,8 @@ __global__ __launch_bounds__(kBlock) void relax_wave(int m, const int *__restric
 // Class pass over rows [lo, hi) of a relabeled level, blocks [blo, ...) of its own CSR.
 //   MODE 0: GS-CF pass of depth 1, in place (x[r] = t / d).
 //   MODE 1: C/F-Jacobi pass / two-stage stage 0: y[r - lo] = t / d, every x from before the pass.
-//   MODE 2: two-stage inner step: same-class strictly-lower entries (encoded ~j in `ci`) read the
-//           previous inner iterate yp[j - lo], every other entry x[j] (from before the pass).
 // t = b_r - sum over off-diagonal entries in stored order (diag_pos skips the diagonal); rows with
-// |d| <= 1e-20 keep their value.  Columns may carry the two-stage encoding in every mode.
+// |d| <= 1e-20 keep their value.
 template <int MODE>
 __global__ __launch_bounds__(kBlock) void relax_range(int blo, const int *__restrict__ blk, const int *__restrict__ rp,
                                                       const int *__restrict__ ci, const double *__restrict__ v,
@@ -310,17 +342,13 @@ __global__ __launch_bounds__(kBlock) void relax_range(int blo, const int *__rest
     const int bid = blo + blockIdx.x;
     const int r0 = blk[bid], r1 = blk[bid + 1];
     const int k0 = rp[r0], k1 = rp[r1];
-    auto fetch = [&](int c) -> double {
-        if (MODE == 2) return c < 0 ? yp[~c - lo] : x[c];
-        return x[c < 0 ? ~c : c];
-    };
+    auto fetch = [&](int c) -> double { return x[c]; };
     auto finish = [&](int r, double acc) {
         const double d = deff[r];
         if (MODE == 0) {
             if (fabs(d) > SMALLFLOAT) x[r] = acc / d;
         } else {
-            const double keep = MODE == 2 ? yp[r - lo] : x[r];
-            y[r - lo] = fabs(d) > SMALLFLOAT ? acc / d : keep;
+            y[r - lo] = fabs(d) > SMALLFLOAT ? acc / d : x[r];
         }
     };
     if (k1 - k0 <= kTileEntries) {
@@ -374,20 +402,128 @@ __global__ __launch_bounds__(kBlock) void relax_range_wave(int lo, int hi, const
     if (r >= hi) return;
     const double acc = wave_row_chain<true>(
         rp[r], rp[r + 1], ci, v,
-        [&](int c, double a) -> double {
-            if (c == r) return 0.0;
-            if (MODE == 2) return a * (c < 0 ? yp[~c - lo] : x[c]);
-            return a * x[c < 0 ? ~c : c];
-        },
+        [&](int c, double a) -> double { return c == r ? 0.0 : a * x[c]; },
         b[r], strips[wave]);
     if ((threadIdx.x & 63) == 0) {
         const double d = deff[r];
         if (MODE == 0) {
             if (fabs(d) > SMALLFLOAT) x[r] = acc / d;
         } else {
-            const double keep = MODE == 2 ? yp[r - lo] : x[r];
-            y[r - lo] = fabs(d) > SMALLFLOAT ? acc / d : keep;
+            y[r - lo] = fabs(d) > SMALLFLOAT ? acc / d : x[r];
         }
+    }
+}
+
+// ---- two-stage GS-CF (oracle: ora_cf_twostage) ----------------------------------------------
+// Stage 0 over the reordered pass rows [N_i | L_i] (local row q = global lo + q):
+//   P_q = b - sum_{N_i} a x;  y_q = (P_q - sum_{L_i} a x) / d   (x from before the pass)
+template <bool WAVE>
+__global__ __launch_bounds__(kBlock) void ts_stage0(int lo, DevCSR M, const int *__restrict__ split,
+                                                    const double *__restrict__ b, const double *__restrict__ x,
+                                                    const double *__restrict__ deff, double *__restrict__ P,
+                                                    double *__restrict__ y)
+{
+    auto finish = [&](int q, double acc) {
+        const int r = lo + q;
+        const double d = deff[r];
+        y[q] = fabs(d) > SMALLFLOAT ? acc / d : x[r];
+    };
+    if (WAVE) {
+        __shared__ double strips[4][kWaveStage];
+        const int wave = threadIdx.x >> 6, q = blockIdx.x * 4 + wave;
+        if (q >= M.n) return;
+        auto prod = [&](int c, double a) { return a * x[c]; };
+        const int a = M.rp[q], sp = split[q], e = M.rp[q + 1];
+        double acc = wave_row_chain<true>(a, sp, M.ci, M.v, prod, b[lo + q], strips[wave]);
+        acc = __shfl(acc, 0, 64);
+        if ((threadIdx.x & 63) == 0) P[q] = acc;
+        acc = wave_row_chain<true>(sp, e, M.ci, M.v, prod, acc, strips[wave]);
+        if ((threadIdx.x & 63) == 0) finish(q, acc);
+        return;
+    }
+    __shared__ SpmvSmem sm;
+    const int q0 = M.blk[blockIdx.x], q1 = M.blk[blockIdx.x + 1];
+    const int k0 = M.rp[q0], k1 = M.rp[q1];
+    if (k1 - k0 <= kTileEntries) {
+        const int q = q0 + (int)threadIdx.x;
+        int a = 0, sp = 0, e = 0;
+        double acc = 0.0;
+        if (q < q1) a = M.rp[q] - k0, sp = split[q] - k0, e = M.rp[q + 1] - k0, acc = b[lo + q];
+        stage_products(sm.v, k0, k1, M.ci, M.v, x);
+        __syncthreads();
+        if (q < q1) {
+            acc = chain_sub(acc, sm.v, a, sp);
+            P[q] = acc;
+            acc = chain_sub(acc, sm.v, sp, e);
+            finish(q, acc);
+        }
+    } else {   // one long row, chunk by chunk, thread 0 carries the chain
+        const int q = q0, sp = split[q];
+        double acc = b[lo + q];
+        for (int base = k0; base < k1; base += kTileEntries) {
+            const int m = min(kTileEntries, k1 - base);
+            stage_products(sm.v, base, base + m, M.ci, M.v, x);
+            __syncthreads();
+            if (threadIdx.x == 0) {
+                if (sp >= base && sp < base + m) {
+                    acc = chain_sub(acc, sm.v, 0, sp - base);
+                    P[q] = acc;
+                    acc = chain_sub(acc, sm.v, sp - base, m);
+                } else {
+                    acc = chain_sub(acc, sm.v, 0, m);
+                }
+            }
+            __syncthreads();
+        }
+        if (threadIdx.x == 0) {
+            if (sp == k1) P[q] = acc;   // no L entries
+            finish(q, acc);
+        }
+    }
+}
+
+// Inner step over the L-only rows:  y_q = (P_q - sum_{L_i} a yp[j - lo]) / d  (keeps yp_q if |d| small)
+template <bool WAVE>
+__global__ __launch_bounds__(kBlock) void ts_inner(int lo, DevCSR M, const double *__restrict__ deff,
+                                                   const double *__restrict__ P, const double *__restrict__ yp,
+                                                   double *__restrict__ y)
+{
+    auto fetch = [&](int c) -> double { return yp[c - lo]; };
+    auto finish = [&](int q, double acc) {
+        const double d = deff[lo + q];
+        y[q] = fabs(d) > SMALLFLOAT ? acc / d : yp[q];
+    };
+    if (WAVE) {
+        __shared__ double strips[4][kWaveStage];
+        const int wave = threadIdx.x >> 6, q = blockIdx.x * 4 + wave;
+        if (q >= M.n) return;
+        const double acc = wave_row_chain<true>(
+            M.rp[q], M.rp[q + 1], M.ci, M.v, [&](int c, double a) { return a * fetch(c); }, P[q], strips[wave]);
+        if ((threadIdx.x & 63) == 0) finish(q, acc);
+        return;
+    }
+    __shared__ SpmvSmem sm;
+    const int q0 = M.blk[blockIdx.x], q1 = M.blk[blockIdx.x + 1];
+    const int k0 = M.rp[q0], k1 = M.rp[q1];
+    if (k1 - k0 <= kTileEntries) {
+        const int q = q0 + (int)threadIdx.x;
+        int a = 0, e = 0;
+        double acc = 0.0;
+        if (q < q1) a = M.rp[q] - k0, e = M.rp[q + 1] - k0, acc = P[q];
+        stage_products_f(sm.v, k0, k1, M.ci, M.v, fetch);
+        __syncthreads();
+        if (q < q1) finish(q, chain_sub(acc, sm.v, a, e));
+    } else {
+        const int q = q0;
+        double acc = P[q];
+        for (int base = k0; base < k1; base += kTileEntries) {
+            const int m = min(kTileEntries, k1 - base);
+            stage_products_f(sm.v, base, base + m, M.ci, M.v, fetch);
+            __syncthreads();
+            if (threadIdx.x == 0) acc = chain_sub(acc, sm.v, 0, m);
+            __syncthreads();
+        }
+        if (threadIdx.x == 0) finish(q, acc);
     }
 }
 
@@ -419,15 +555,28 @@ int smoother_run(const SmootherPlan &sp, const DevCSR &A, const double *b, doubl
                         hipLaunchKernelGGL(relax_range<M>, dim3(nb), dim3(kBlock), 0, s, ps.blo, A.blk, A.rp, cols,
                                            A.v, sp.diag_pos, ps.lo, b, x, yp, y, deff);
                 };
-                if (sp.kind == SSS_HIP_SMOOTH_JACOBI) {
-                    const int *cols = sp.cts ? sp.cts : A.ci;
-                    relax(std::integral_constant<int, 1>(), cols, (const double *)nullptr, ps.y);
+                if (sp.kind == SSS_HIP_SMOOTH_JACOBI && sp.inner > 0) {
+                    const DevCSR &Mn = ps.ts_nl, &Ml = ps.ts_lo;
+                    if (Mn.wave_rows)
+                        hipLaunchKernelGGL(ts_stage0<true>, dim3(Mn.ngrid), dim3(kBlock), 0, s, ps.lo, Mn, ps.ts_split,
+                                           b, (const double *)x, deff, ps.ts_P, ps.y);
+                    else
+                        hipLaunchKernelGGL(ts_stage0<false>, dim3(Mn.nblk), dim3(kBlock), 0, s, ps.lo, Mn,
+                                           ps.ts_split, b, (const double *)x, deff, ps.ts_P, ps.y);
                     double *cur = ps.y, *nxt = ps.y2;
                     for (int st = 0; st < sp.inner; ++st) {
-                        relax(std::integral_constant<int, 2>(), cols, (const double *)cur, nxt);
+                        if (Ml.wave_rows)
+                            hipLaunchKernelGGL(ts_inner<true>, dim3(Ml.ngrid), dim3(kBlock), 0, s, ps.lo, Ml, deff,
+                                               (const double *)ps.ts_P, (const double *)cur, nxt);
+                        else
+                            hipLaunchKernelGGL(ts_inner<false>, dim3(Ml.nblk), dim3(kBlock), 0, s, ps.lo, Ml, deff,
+                                               (const double *)ps.ts_P, (const double *)cur, nxt);
                         std::swap(cur, nxt);
                     }
                     SSS_HIP(hipMemcpyAsync(x + ps.lo, cur, sizeof(double) * (size_t)m, hipMemcpyDeviceToDevice, s));
+                } else if (sp.kind == SSS_HIP_SMOOTH_JACOBI) {
+                    relax(std::integral_constant<int, 1>(), A.ci, (const double *)nullptr, ps.y);
+                    SSS_HIP(hipMemcpyAsync(x + ps.lo, ps.y, sizeof(double) * (size_t)m, hipMemcpyDeviceToDevice, s));
                 } else {
                     relax(std::integral_constant<int, 0>(), A.ci, (const double *)nullptr, (double *)nullptr);
                 }

@@ -214,51 +214,72 @@ void ora_cf_jacobi(double *u, const SSS_MAT *A, const double *b, int sweeps, con
     ora_cf_jacobi_w(u, A, b, sweeps, mark, 1.0, 0);
 }
 
-/* Two-stage GS-CF (engine extension, DESIGN.md): each class pass solves the pass's triangular
- * system  (D + L_cc) x_c = b_c - U_cc x_c_old - A_c,other x_other  approximately: a Jacobi step
- * y0 (every row reads the values from before the pass), then `inner` Jacobi-Richardson steps in
- * which row i reads y_{k-1}[j] for same-class j < i and the pre-pass value for every other j.
- * inner >= DAG depth of the pass reproduces ora_gs_cf's values; per row the subtraction order is
- * the stored CSR order; d and the |d| > 1e-20 guard as in C/F-Jacobi. */
+/* Two-stage GS-CF (engine extension, DESIGN.md §4): each class pass solves the pass's triangular
+ * system  (D + L_cc) x_c = b_c - U_cc x_c_old - A_c,other x_other  approximately.  Per row i of the
+ * pass, its off-diagonal entries split into L_i (same class, j < i) and N_i (the rest):
+ *   P_i  = b_i - sum_{N_i} a_ij x_old_j                    (stored order)
+ *   y0_i = (P_i - sum_{L_i} a_ij x_old_j) / d_i            (= the C/F-Jacobi value, other order)
+ *   y_s,i = (P_i - sum_{L_i} a_ij y_{s-1},j) / d_i,  s = 1..inner
+ * then x_c = y_inner.  P is formed once per pass, so each inner step reads only the L entries.
+ * inner >= the pass's DAG depth reproduces ora_gs_cf's values up to that summation order.  d is
+ * the row's last diagonal entry; rows with |d| <= 1e-20 keep their value. */
 void ora_cf_twostage(double *u, const SSS_MAT *A, const double *b, int sweeps, const int *mark, int inner)
 {
     const int n = A->num_rows;
     const size_t sz = sizeof(double) * (size_t)(n > 0 ? n : 1);
     double *old = (double *)malloc(sz), *cur = (double *)malloc(sz), *nxt = (double *)malloc(sz);
+    double *P = (double *)malloc(sz), *dg = (double *)malloc(sz);
     while (sweeps--) {
         for (int pass = 0; pass < (mark ? 2 : 1); ++pass) {
+#define IN_PASS(r) (!mark || (mark[r] == 1) == pass)
             copy(n, u, old);
             copy(n, u, cur);
-            for (int stage = 0; stage <= inner; ++stage) {
+            for (int i = 0; i < n; ++i) {   /* P and stage 0 */
+                double t, d = 0.0;
+                if (!IN_PASS(i)) continue;
+                t = b[i];
+                for (int k = A->row_ptr[i]; k < A->row_ptr[i + 1]; ++k) {
+                    const int j = A->col_idx[k];
+                    if (j == i) d = A->val[k];
+                    else if (!(j < i && IN_PASS(j))) t -= A->val[k] * old[j];
+                }
+                P[i] = t;
+                dg[i] = d;
+                for (int k = A->row_ptr[i]; k < A->row_ptr[i + 1]; ++k) {
+                    const int j = A->col_idx[k];
+                    if (j != i && j < i && IN_PASS(j)) t -= A->val[k] * old[j];
+                }
+                if (SSS_ABS(d) > SMALLFLOAT) cur[i] = t / d;
+            }
+            for (int stage = 1; stage <= inner; ++stage) {
                 copy(n, cur, nxt);
                 for (int i = 0; i < n; ++i) {
-                    double t, d = 0.0;
-                    if (mark && (mark[i] == 1) != pass) continue;
-                    t = b[i];
+                    double t;
+                    if (!IN_PASS(i)) continue;
+                    t = P[i];
                     for (int k = A->row_ptr[i]; k < A->row_ptr[i + 1]; ++k) {
                         const int j = A->col_idx[k];
-                        if (j == i) {
-                            d = A->val[k];
-                            continue;
-                        }
-                        const int lower = stage > 0 && j < i && (!mark || (mark[j] == 1) == pass);
-                        t -= A->val[k] * (lower ? cur[j] : old[j]);
+                        if (j != i && j < i && IN_PASS(j)) t -= A->val[k] * cur[j];
                     }
-                    if (SSS_ABS(d) > SMALLFLOAT) nxt[i] = t / d;
+                    if (SSS_ABS(dg[i]) > SMALLFLOAT) nxt[i] = t / dg[i];
                 }
                 double *sw = cur;
                 cur = nxt;
                 nxt = sw;
             }
             copy(n, cur, u);
+#undef IN_PASS
         }
     }
     free(old);
     free(cur);
     free(nxt);
+    free(P);
+    free(dg);
 }
 
 static const ora_opts *g_cur_opts = NULL;
+static int g_cur_level = 0;
 
 static void smoother_dispatch(SSS_SMTR *s, int post, const char *fname)
 {
@@ -270,7 +291,8 @@ static void smoother_dispatch(SSS_SMTR *s, int post, const char *fname)
         else ora_gs(s->x->d, s->iend, s->istart, s->istep, s->A, s->b->d, s->nsweeps);
         break;
     case SSS_SM_JACOBI:
-        if (g_cur_opts && g_cur_opts->inner > 0) {
+        if (g_cur_opts && g_cur_opts->inner > 0 &&
+            (!g_cur_opts->inner_mask || (g_cur_opts->inner_mask >> g_cur_level & 1))) {
             ora_cf_twostage(s->x->d, s->A, s->b->d, s->nsweeps, use_cf ? s->ordering : NULL, g_cur_opts->inner);
             break;
         }
@@ -598,6 +620,7 @@ static void level_smoother(SSS_AMG *mg, int l, int post, const ora_opts *o)
     s.cf_order = mg->pars.cf_order;
     s.ordering = mg->cg[l].cfmark.d;
     g_cur_opts = o;
+    g_cur_level = l;
     if (post) ora_smoother_post(&s);
     else ora_smoother_pre(&s);
     g_cur_opts = NULL;

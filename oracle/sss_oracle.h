@@ -24,6 +24,7 @@ typedef struct {
     double omega;     /* C/F-Jacobi weight (1.0 = plain) */
     int inner;        /* > 0: two-stage GS-CF instead of C/F-Jacobi, with `inner` Jacobi-Richardson
                          steps on the same-class lower triangle (ora_cf_twostage) */
+    int inner_mask;   /* experiments: bit l set = level l uses two-stage (0 = every C/F-Jacobi level) */
 } ora_opts;
 
 void ora_opts_default(ora_opts *o);
