@@ -75,7 +75,7 @@ class SSS_KRYLOV(C.Structure):
 class SSS_HIP_OPTS(C.Structure):
     _fields_ = [("device", C.c_int), ("smoother", C.c_int), ("coarse", C.c_int), ("row_cap", C.c_int),
                 ("use_graph", C.c_int), ("verbose", C.c_int),
-                ("inner", C.c_int), ("relabel", C.c_int)]
+                ("inner", C.c_int), ("inner_from", C.c_int), ("relabel", C.c_int)]
 
 
 class SSS_HIP_LEVEL_INFO(C.Structure):
@@ -255,7 +255,7 @@ class DeviceHierarchy:
 
     def __init__(self, H: Hierarchy, smoother: str = "exact", coarse: str = "krylov", row_cap: int = 0,
                  device: int = -1, verbose: int = 0, relabel: int | None = None, graph: int | None = None,
-                 inner: int | None = None):
+                 inner: int | None = None, inner_from: int | None = None):
         o = SSS_HIP_OPTS()
         lib().sss_hip_opts_default(C.byref(o))
         o.smoother, o.coarse, o.row_cap, o.device, o.verbose = SMOOTH[smoother], COARSE[coarse], row_cap, device, verbose
@@ -265,6 +265,8 @@ class DeviceHierarchy:
             o.use_graph = graph
         if inner is not None:
             o.inner = inner
+        if inner_from is not None:
+            o.inner_from = inner_from
         self.H = H
         self.h = lib().sss_hip_hier_create(C.byref(H.mg), C.byref(o))
         if not self.h:

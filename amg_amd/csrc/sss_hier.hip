@@ -65,6 +65,7 @@ extern "C" void sss_hip_opts_default(sss_hip_opts *o)
     o->verbose = env_int("SSS_HIP_VERBOSE", 0);
     o->relabel = env_int("SSS_HIP_RELABEL", 1);
     o->inner = env_int("SSS_HIP_INNER", 1);
+    o->inner_from = env_int("SSS_HIP_INNER_FROM", 2);
     if (const char *s = getenv("SSS_HIP_SMOOTHER")) {
         std::string v(s);
         if (v == "hybrid") o->smoother = SSS_HIP_SMOOTH_HYBRID;
@@ -88,6 +89,12 @@ static int level_smoother_kind(const sss_hip_opts &o, int l)
     if (o.smoother == SSS_HIP_SMOOTH_JACOBI) return SSS_HIP_SMOOTH_JACOBI;
     if (o.smoother == SSS_HIP_SMOOTH_HYBRID && l > 0) return SSS_HIP_SMOOTH_JACOBI;
     return SSS_HIP_SMOOTH_EXACT;
+}
+
+// two-stage inner steps of level l (0 = plain C/F-Jacobi there, or not a C/F-Jacobi level)
+static int level_inner(const sss_hip_opts &o, int l)
+{
+    return level_smoother_kind(o, l) == SSS_HIP_SMOOTH_JACOBI && l >= o.inner_from ? o.inner : 0;
 }
 
 static void hier_release(sss_hip_hier *h)
@@ -207,7 +214,7 @@ extern "C" sss_hip_hier *sss_hip_hier_create(const SSS_AMG *mg, const sss_hip_op
             const int n = C.A.num_rows;
             if (!C.cfmark.d || C.cfmark.n < n) continue;
             // two-stage levels need contiguous classes; otherwise follow opts.relabel
-            const bool two_stage = level_smoother_kind(h->opts, l) == SSS_HIP_SMOOTH_JACOBI && h->opts.inner > 0;
+            const bool two_stage = level_inner(h->opts, l) > 0;
             if (!two_stage && !(h->opts.relabel == 1 || (h->opts.relabel == 2 && l > 0))) continue;
             auto &perm = h->L[l].perm;
             perm.reserve(n);
@@ -232,7 +239,7 @@ extern "C" sss_hip_hier *sss_hip_hier_create(const SSS_AMG *mg, const sss_hip_op
             if (devcsr_upload(L.A, Av, nF[l])) return fail("upload A");
             std::vector<int> mark(n);
             for (int i = 0; i < n; ++i) mark[i] = C.cfmark.d[L.perm[i]];
-            if (smoother_build(L.sm, Av, mark.data(), level_smoother_kind(h->opts, l), &L.A, h->opts.inner))
+            if (smoother_build(L.sm, Av, mark.data(), level_smoother_kind(h->opts, l), &L.A, level_inner(h->opts, l)))
                 return fail("smoother plan");
         } else {
             if (devcsr_upload(L.A, C.A)) return fail("upload A");

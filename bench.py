@@ -52,6 +52,8 @@ def parse():
     p.add_argument("--mode-coarse", default=None, help="override: krylov|direct")
     p.add_argument("--inner", type=int, default=None,
                    help="two-stage inner steps on C/F-Jacobi levels (default: SSS_HIP_INNER or 1; 0 = plain C/F-Jacobi)")
+    p.add_argument("--inner-from", type=int, default=None,
+                   help="first level with the two-stage form (default: SSS_HIP_INNER_FROM or 2)")
     p.add_argument("--converge-max", type=int, default=100, help="max V-cycles of the iterations-to-tol run (0: skip)")
     return p.parse_args()
 
@@ -144,8 +146,10 @@ def main():
 
     t0 = time.perf_counter()
     dev = D.local_rank if D.world > 1 else -1
-    DH = A.DeviceHierarchy(H, smoother=smoother, coarse=coarse, device=dev, inner=args.inner)
+    DH = A.DeviceHierarchy(H, smoother=smoother, coarse=coarse, device=dev, inner=args.inner,
+                           inner_from=args.inner_from)
     inner = args.inner if args.inner is not None else int(os.environ.get("SSS_HIP_INNER", "1"))
+    inner_from = args.inner_from if args.inner_from is not None else int(os.environ.get("SSS_HIP_INNER_FROM", "2"))
     upload_s = time.perf_counter() - t0
     ones = np.ones(N)
     DH.upload(0, "b", ones)
@@ -233,6 +237,7 @@ def main():
                    "hierarchy": [list(t) for t in levels],
                    "mode": args.mode, "smoother": smoother, "coarse": coarse,
                    "inner": inner if smoother != "exact" else None,
+                   "inner_from": inner_from if smoother != "exact" else None,
                    "iterations_to_tol": its, "final_relres": relres, "time_to_solution_s": solve_s,
                    "setup_s": setup_s, "upload_s": upload_s,
                    "parallelism": f"replicas{D.world}" if D.world > 1 else "single-gpu"},

@@ -45,13 +45,15 @@ typedef struct sss_hip_opts {
     int verbose;       /* engine diagnostics on stderr */
     int inner;         /* C/F-Jacobi levels: 0 = plain C/F-Jacobi; k > 0 = two-stage GS-CF with k
                           Jacobi-Richardson steps on each pass's same-class lower triangle */
+    int inner_from;    /* first level that uses the two-stage form (plain C/F-Jacobi above it) */
     int relabel;       /* renumber levels F-first/C-second on the device (bitwise-neutral):
                           0 off, 1 every level but the coarsest, 2 as 1 but level 0 kept */
 } sss_hip_opts;
 
 /* Defaults, overridable by environment: SSS_HIP_SMOOTHER=exact|hybrid|jacobi,
  * SSS_HIP_COARSE=krylov|direct, SSS_HIP_ROWCAP=<n>, SSS_HIP_GRAPH=0|1, SSS_HIP_DEVICE=<n>,
- * SSS_HIP_VERBOSE=0|1, SSS_HIP_RELABEL=0|1|2 (default 1), SSS_HIP_INNER=<k> (default 1). */
+ * SSS_HIP_VERBOSE=0|1, SSS_HIP_RELABEL=0|1|2 (default 1), SSS_HIP_INNER=<k> (default 1),
+ * SSS_HIP_INNER_FROM=<level> (default 2). */
 void sss_hip_opts_default(sss_hip_opts *o);
 
 /* Number of usable HIP devices (0 when none; never exits). */

@@ -231,10 +231,11 @@ def test_coarse_direct_solves(p32_h):
 
 
 # ---------------------------------------------------------------- whole solve
-def _gpu_history(H, smoother="exact", coarse="krylov", row_cap=0, max_it=100, relabel=None, graph=None, inner=None):
+def _gpu_history(H, smoother="exact", coarse="krylov", row_cap=0, max_it=100, relabel=None, graph=None, inner=None,
+                 inner_from=None):
     n = H.level(0).A.num_rows
     D = A.DeviceHierarchy(H, smoother=smoother, coarse=coarse, row_cap=row_cap, relabel=relabel, graph=graph,
-                          inner=inner)
+                          inner=inner, inner_from=inner_from)
     b = np.ones(n)
     D.upload(0, "b", b)
     D.upload(0, "x", np.ones(n))
@@ -278,10 +279,15 @@ def test_solve_direct_coarse(request, hname):
     assert np.linalg.norm(x_g - x_r) <= 1e-6 * np.linalg.norm(x_r)
 
 
-@pytest.mark.parametrize("inner", [0, 1])
-def test_solve_hybrid_jacobi_converges(p32_h, inner):
-    rel_o, x_o = _oracle_history(p32_h, smoother=1, coarse_mode=1, inner=inner)
-    rel_g, x_g = _gpu_history(p32_h, smoother="hybrid", coarse="direct", inner=inner)
+def _mask(inner_from):
+    """oracle inner_mask for 'two-stage on levels >= inner_from'"""
+    return ~((1 << inner_from) - 1)
+
+
+@pytest.mark.parametrize("inner,inner_from", [(0, 2), (1, 1), (1, 2)])
+def test_solve_hybrid_jacobi_converges(p32_h, inner, inner_from):
+    rel_o, x_o = _oracle_history(p32_h, smoother=1, coarse_mode=1, inner=inner, inner_mask=_mask(inner_from))
+    rel_g, x_g = _gpu_history(p32_h, smoother="hybrid", coarse="direct", inner=inner, inner_from=inner_from)
     assert len(rel_g) == len(rel_o)
     assert np.allclose(rel_g, rel_o, rtol=1e-6)
     rel_ref, _ = _oracle_history(p32_h)
@@ -309,7 +315,7 @@ def test_relabeled_level_smoothers_bitwise(request, hname, smoother, inner, row_
     oracle on the original labels."""
     H = request.getfixturevalue(hname)
     ora = oracle.load()
-    D = A.DeviceHierarchy(H, smoother=smoother, coarse="direct", relabel=1, inner=inner)
+    D = A.DeviceHierarchy(H, smoother=smoother, coarse="direct", relabel=1, inner=inner, inner_from=0)
     rng = np.random.default_rng(23)
     try:
         for l in range(H.num_levels - 1):
@@ -338,12 +344,12 @@ def test_relabeled_level_smoothers_bitwise(request, hname, smoother, inner, row_
 
 
 @pytest.mark.parametrize("hname", ["bus_h", "p32_h", "a27_h"])
-@pytest.mark.parametrize("inner", [0, 1])
-def test_solve_hybrid_krylov_bitwise(request, hname, inner, row_path):
+@pytest.mark.parametrize("inner,inner_from", [(0, 2), (1, 1), (1, 2), (2, 2)])
+def test_solve_hybrid_krylov_bitwise(request, hname, inner, inner_from, row_path):
     """Throughput smoothers with the reference coarse solver: x bitwise equal to the oracle's."""
     H = request.getfixturevalue(hname)
-    rel_r, x_r = _oracle_history(H, smoother=1, inner=inner)
-    rel_g, x_g = _gpu_history(H, smoother="hybrid", coarse="krylov", inner=inner)
+    rel_r, x_r = _oracle_history(H, smoother=1, inner=inner, inner_mask=_mask(inner_from))
+    rel_g, x_g = _gpu_history(H, smoother="hybrid", coarse="krylov", inner=inner, inner_from=inner_from)
     assert len(rel_g) == len(rel_r)
     assert np.array_equal(x_g.view(np.uint64), x_r.view(np.uint64))
     assert np.allclose(rel_g, rel_r, rtol=1e-13, atol=0)
