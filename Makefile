@@ -45,7 +45,7 @@ $(BUILD)/hip/%.o: amg_amd/csrc/%.hip $(HEADERS)
 
 $(LIB): $(HOST_OBJ) $(HIP_OBJ)
 	@mkdir -p $(LIBDIR)
-	$(HIPCC) -shared -fPIC -o $@ $^ -Wl,-Bsymbolic-functions -lgomp -Wl,-rpath,$(ROCM)/lib
+	$(HIPCC) -shared -fPIC -o $@ $^ -Wl,-Bsymbolic-functions -lgomp -L$(ROCM)/lib -lrccl -Wl,-rpath,$(ROCM)/lib
 
 $(BIN): amg_amd/host/sss_main.c $(LIB) $(HEADERS)
 	@mkdir -p $(BINDIR)

@@ -4,7 +4,8 @@ The product is the C-ABI library ``amg_amd/lib/libsss_amg.so`` (host C + gfx950 
 and the ``amg_amd/bin/amg`` CLI; this package is the Python binding used by tests and bench.py.
 """
 from ._native import (  # noqa: F401
-    ABI_SYMBOLS, COARSE, SMOOTH, SPMV, DeviceHierarchy, Hierarchy, NumpyCSR, SSS_AMG, SSS_AMG_COMP,
+    ABI_SYMBOLS, COARSE, SMOOTH, SPMV, Comm, DeviceHierarchy, DistHierarchy, Hierarchy, NumpyCSR, PartPlan,
+    SSS_AMG, SSS_AMG_COMP,
     SSS_AMG_PARS, SSS_HIP_OPTS, SSS_MAT, SSS_RTN, SSS_SMTR, SSS_VEC, csr_arrays, default_pars, device_count,
     generate, lib, read_mtx,
 )

@@ -106,7 +106,22 @@ ABI_SYMBOLS = [
     "sss_hip_spmv_plan_create", "sss_hip_spmv_plan_destroy", "sss_hip_spmv", "sss_hip_host_spmv",
     "sss_hip_host_smooth", "sss_hip_host_coarse_solve", "sss_hip_time_level0_spmv", "sss_hip_time_iterations",
     "sss_gen_stencil",
+    "sss_hip_rccl_unique_id", "sss_hip_comm_rccl", "sss_hip_comm_host", "sss_hip_comm_destroy",
+    "sss_hip_dist_create", "sss_hip_dist_destroy", "sss_hip_dist_info", "sss_hip_dist_upload_vec",
+    "sss_hip_dist_download_vec", "sss_hip_dist_cycle", "sss_hip_dist_residual_norm", "sss_hip_dist_sync",
+    "sss_part_plan_create", "sss_part_plan_destroy", "sss_part_plan_nagg", "sss_part_plan_level",
+    "sss_part_plan_matrix", "sss_part_plan_ids", "sss_part_plan_halo",
 ]
+
+_ip, _dp = C.POINTER(C.c_int), C.POINTER(C.c_double)
+EXCHANGE_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_int, _ip, _ip, _dp, C.c_int, _ip, _ip, _dp)
+ALLREDUCE_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, _dp, C.c_int)
+ALLGATHERV_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, _dp, C.c_int, _dp, _ip, _ip)
+
+
+class SSS_HIP_HOST_TRANSPORT(C.Structure):
+    _fields_ = [("ctx", C.c_void_p), ("exchange", EXCHANGE_FN), ("allreduce_sum", ALLREDUCE_FN),
+                ("allgatherv", ALLGATHERV_FN)]
 
 _lib = None
 
@@ -152,6 +167,26 @@ def _declare(lib):
                                                 C.c_int]),
         "sss_hip_time_level0_spmv": (C.c_int, [C.c_void_p, C.c_int, _dbl_p]),
         "sss_hip_time_iterations": (C.c_int, [C.c_void_p, C.c_int, _dbl_p, _dbl_p]),
+        "sss_hip_rccl_unique_id": (C.c_int, [C.c_char_p]),
+        "sss_hip_comm_rccl": (C.c_void_p, [C.c_int, C.c_int, C.c_char_p, C.c_int]),
+        "sss_hip_comm_host": (C.c_void_p, [C.c_int, C.c_int, P(SSS_HIP_HOST_TRANSPORT)]),
+        "sss_hip_comm_destroy": (None, [C.c_void_p]),
+        "sss_hip_dist_create": (C.c_void_p, [P(SSS_AMG), P(SSS_HIP_OPTS), C.c_void_p, C.c_int]),
+        "sss_hip_dist_destroy": (None, [C.c_void_p]),
+        "sss_hip_dist_info": (C.c_int, [C.c_void_p, _int_p, _int_p, _int_p, _int_p]),
+        "sss_hip_dist_upload_vec": (C.c_int, [C.c_void_p, C.c_int, _dbl_p, C.c_int]),
+        "sss_hip_dist_download_vec": (C.c_int, [C.c_void_p, C.c_int, _dbl_p, C.c_int]),
+        "sss_hip_dist_cycle": (C.c_int, [C.c_void_p]),
+        "sss_hip_dist_residual_norm": (C.c_int, [C.c_void_p, _dbl_p]),
+        "sss_hip_dist_sync": (C.c_int, [C.c_void_p]),
+        "sss_part_plan_create": (C.c_void_p, [P(SSS_AMG), C.c_int, C.c_int, C.c_int]),
+        "sss_part_plan_destroy": (None, [C.c_void_p]),
+        "sss_part_plan_nagg": (C.c_int, [C.c_void_p]),
+        "sss_part_plan_level": (C.c_int, [C.c_void_p, C.c_int, _int_p, _int_p, _int_p, _int_p]),
+        "sss_part_plan_matrix": (C.c_int, [C.c_void_p, C.c_int, C.c_int, P(SSS_MAT)]),
+        "sss_part_plan_ids": (C.c_int, [C.c_void_p, C.c_int, P(_int_p), P(_int_p)]),
+        "sss_part_plan_halo": (C.c_int, [C.c_void_p, C.c_int, _int_p, P(_int_p), P(_int_p), P(_int_p), _int_p,
+                                         P(_int_p), P(_int_p)]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
@@ -332,3 +367,203 @@ class DeviceHierarchy:
 
 def device_count() -> int:
     return lib().sss_hip_device_count()
+
+
+# ---------------------------------------------------------------- row-partitioned multi-GPU
+class PartPlan:
+    """Host-only view of one rank's partition of a hierarchy (sss_part_plan_*)."""
+
+    def __init__(self, H: "Hierarchy", nranks: int, rank: int, agg_rows: int = 0):
+        self.H = H
+        self.p = lib().sss_part_plan_create(C.byref(H.mg), nranks, rank, agg_rows)
+        if not self.p:
+            raise RuntimeError("sss_part_plan_create failed")
+        self.nagg = lib().sss_part_plan_nagg(self.p)
+
+    def level(self, l: int):
+        lo, hi, m, g = C.c_int(), C.c_int(), C.c_int(), C.c_int()
+        assert lib().sss_part_plan_level(self.p, l, C.byref(lo), C.byref(hi), C.byref(m), C.byref(g)) == 0
+        return lo.value, hi.value, m.value, g.value
+
+    def matrix(self, l: int, which: str) -> SSS_MAT:
+        M = SSS_MAT()
+        assert lib().sss_part_plan_matrix(self.p, l, {"A": 0, "P": 1, "R": 2}[which], C.byref(M)) == 0
+        return M
+
+    def ids(self, l: int):
+        _, _, m, g = self.level(l)
+        pp, gp = _int_p(), _int_p()
+        assert lib().sss_part_plan_ids(self.p, l, C.byref(pp), C.byref(gp)) == 0
+        perm = np.ctypeslib.as_array(pp, shape=(m,)).copy() if m else np.zeros(0, np.int32)
+        ghosts = np.ctypeslib.as_array(gp, shape=(g,)).copy() if g else np.zeros(0, np.int32)
+        return perm, ghosts
+
+    def halo(self, l: int):
+        ns, nr = C.c_int(), C.c_int()
+        sd, sc, si, rs, rc = _int_p(), _int_p(), _int_p(), _int_p(), _int_p()
+        assert lib().sss_part_plan_halo(self.p, l, C.byref(ns), C.byref(sd), C.byref(sc), C.byref(si), C.byref(nr),
+                                        C.byref(rs), C.byref(rc)) == 0
+
+        def arr(ptr, n):
+            return np.ctypeslib.as_array(ptr, shape=(n,)).copy() if n else np.zeros(0, np.int32)
+
+        scount = arr(sc, ns.value)
+        return dict(sdst=arr(sd, ns.value), scount=scount, sidx=arr(si, int(scount.sum())),
+                    rsrc=arr(rs, nr.value), rcount=arr(rc, nr.value))
+
+    def close(self):
+        if self.p:
+            lib().sss_part_plan_destroy(self.p)
+            self.p = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class TorchHostTransport:
+    """sss_hip_host_transport over torch.distributed (gloo): the test transport of the
+    distributed engine (several ranks may then share one GPU, which RCCL refuses)."""
+
+    def __init__(self):
+        import torch
+        import torch.distributed as dist
+        self.torch, self.dist = torch, dist
+
+        def exchange(ctx, ns, sdst, scount, sbuf, nr, rsrc, rcount, rbuf):
+            try:
+                reqs, off = [], 0
+                sc = [scount[i] for i in range(ns)]
+                tot = sum(sc)
+                sb = np.ctypeslib.as_array(sbuf, shape=(max(tot, 1),))
+                for i in range(ns):
+                    t = torch.from_numpy(sb[off:off + sc[i]].copy())
+                    reqs.append(dist.isend(t, sdst[i]))
+                    off += sc[i]
+                rc = [rcount[i] for i in range(nr)]
+                outs = []
+                for i in range(nr):
+                    t = torch.empty(rc[i], dtype=torch.float64)
+                    reqs.append(dist.irecv(t, rsrc[i]))
+                    outs.append(t)
+                for r in reqs:
+                    r.wait()
+                if nr:
+                    rb = np.ctypeslib.as_array(rbuf, shape=(sum(rc),))
+                    off = 0
+                    for i in range(nr):
+                        rb[off:off + rc[i]] = outs[i].numpy()
+                        off += rc[i]
+                return 0
+            except Exception as e:  # pragma: no cover - reported through the C return code
+                print("transport exchange failed:", e, flush=True)
+                return 1
+
+        def allreduce(ctx, v, n):
+            a = np.ctypeslib.as_array(v, shape=(n,))
+            t = torch.from_numpy(a.copy())
+            dist.all_reduce(t)
+            a[:] = t.numpy()
+            return 0
+
+        def allgatherv(ctx, mine, count, out, counts, displs):
+            W = dist.get_world_size()
+            cnt = [counts[q] for q in range(W)]
+            mx = max(max(cnt), 1)
+            buf = torch.zeros(mx, dtype=torch.float64)
+            if count:
+                buf[:count] = torch.from_numpy(np.ctypeslib.as_array(mine, shape=(count,)).copy())
+            parts = [torch.zeros(mx, dtype=torch.float64) for _ in range(W)]
+            dist.all_gather(parts, buf)
+            o = np.ctypeslib.as_array(out, shape=(sum(cnt),))
+            for q in range(W):
+                o[displs[q]:displs[q] + cnt[q]] = parts[q][:cnt[q]].numpy()
+            return 0
+
+        self._fns = (EXCHANGE_FN(exchange), ALLREDUCE_FN(allreduce), ALLGATHERV_FN(allgatherv))
+        self.t = SSS_HIP_HOST_TRANSPORT(None, *self._fns)
+
+
+class Comm:
+    """sss_hip_comm: RCCL (one GPU per rank) or the host transport (tests)."""
+
+    def __init__(self, nranks: int, rank: int, kind: str = "rccl", device: int = -1):
+        self.kind = kind
+        if kind == "rccl":
+            import torch
+            import torch.distributed as dist
+            uid = C.create_string_buffer(128)
+            if rank == 0:
+                assert lib().sss_hip_rccl_unique_id(uid) == 0
+            t = torch.frombuffer(bytearray(uid.raw), dtype=torch.uint8).clone()
+            dist.broadcast(t, 0)
+            uid = C.create_string_buffer(bytes(t.numpy().tobytes()), 128)
+            self.c = lib().sss_hip_comm_rccl(nranks, rank, uid, device)
+        else:
+            self.transport = TorchHostTransport()
+            self.c = lib().sss_hip_comm_host(nranks, rank, C.byref(self.transport.t))
+        if not self.c:
+            raise RuntimeError(f"communicator ({kind}) creation failed")
+
+    def close(self):
+        if self.c:
+            lib().sss_hip_comm_destroy(self.c)
+            self.c = None
+
+
+class DistHierarchy:
+    """Row-partitioned device hierarchy (sss_hip_dist_*): this rank's rows of every level."""
+
+    def __init__(self, H: "Hierarchy", comm: Comm, smoother: str = "hybrid", coarse: str = "direct",
+                 device: int = -1, agg_rows: int = 0, inner: int | None = None, inner_from: int | None = None):
+        o = SSS_HIP_OPTS()
+        lib().sss_hip_opts_default(C.byref(o))
+        o.smoother, o.coarse, o.device = SMOOTH[smoother], COARSE[coarse], device
+        if inner is not None:
+            o.inner = inner
+        if inner_from is not None:
+            o.inner_from = inner_from
+        self.H, self.comm = H, comm
+        self.d = lib().sss_hip_dist_create(C.byref(H.mg), C.byref(o), comm.c, agg_rows)
+        if not self.d:
+            raise RuntimeError("sss_hip_dist_create failed")
+        lo, hi, nagg, g = C.c_int(), C.c_int(), C.c_int(), C.c_int()
+        lib().sss_hip_dist_info(self.d, C.byref(lo), C.byref(hi), C.byref(nagg), C.byref(g))
+        self.lo, self.hi, self.nagg, self.nghost0 = lo.value, hi.value, nagg.value, g.value
+
+    def _check(self, rc, what):
+        if rc != 0:
+            raise RuntimeError(f"{what} failed ({rc})")
+
+    def upload(self, which: str, own: np.ndarray):
+        own = np.ascontiguousarray(own, dtype=np.float64)
+        self._check(lib().sss_hip_dist_upload_vec(self.d, VEC[which], dptr(own), len(own)), "dist upload")
+
+    def download(self, which: str) -> np.ndarray:
+        out = np.empty(self.hi - self.lo, np.float64)
+        self._check(lib().sss_hip_dist_download_vec(self.d, VEC[which], dptr(out), len(out)), "dist download")
+        return out
+
+    def cycle(self):
+        self._check(lib().sss_hip_dist_cycle(self.d), "dist cycle")
+
+    def residual_norm(self) -> float:
+        r = C.c_double()
+        self._check(lib().sss_hip_dist_residual_norm(self.d, C.byref(r)), "dist residual")
+        return r.value
+
+    def sync(self):
+        self._check(lib().sss_hip_dist_sync(self.d), "dist sync")
+
+    def close(self):
+        if self.d:
+            lib().sss_hip_dist_destroy(self.d)
+            self.d = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

@@ -1,0 +1,482 @@
+// sss_dist.hip — row-partitioned multi-GPU solve phase: one process per GPU, halos and the
+// residual-norm reduction over RCCL (xGMI), or over a host transport for tests.
+//
+// Per partitioned level l < nagg, rank r holds its rows of A_l / P_l / R_l in local numbering
+// (sss_part.hpp) and length m + g vectors (own values, then ghosts).  The V-cycle of
+// SSS_amg_cycle (Solve/SSS_cycle.cu:848-967) then runs as on one GPU, with a halo exchange in
+// front of every kernel that reads off-rank values:
+//   smoother   : before every class pass (x), and after each two-stage stage (the stage's
+//                iterate, whose lower-rank ghost rows of the pass's class are "lower" entries);
+//   residual   : x;   restriction: wp;   prolongation: x_{l+1}.
+// Each rank computes every one of its rows exactly as the single-GPU engine does (same entries,
+// same order, same inputs), so the iterates are bitwise those of one GPU; only the outer norm is
+// summed in a different order.  Level 0 must be smoothed by depth-1 class passes (red-black,
+// e.g. 7-point Poisson) or a C/F-Jacobi form; exact GS-CF with intra-class chains is not
+// distributed.  Levels >= nagg run replicated on every rank (an ordinary single-GPU hierarchy
+// over mg->cg[nagg..]); the restriction into level nagg is all-gathered once per cycle.
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdlib>
+#include <cstring>
+#include <vector>
+
+#include "sss_engine.hpp"
+#include "sss_part.hpp"
+
+using namespace sss;
+
+struct sss_hip_comm {
+    int nranks = 1, rank = 0;
+    bool host = false;
+    ncclComm_t nccl = nullptr;
+    sss_hip_host_transport t{};
+};
+
+namespace {
+
+struct Halo {
+    std::vector<int> sdst, scount, soff, rsrc, rcount, roff;
+    int nsend = 0, nrecv = 0;
+    int *d_sidx = nullptr;
+    double *d_sbuf = nullptr;
+    std::vector<double> h_sbuf, h_rbuf;   // host transport staging
+};
+
+struct DLevel {
+    int lo = 0, hi = 0, m = 0, g = 0;
+    std::vector<int> perm;   // local -> global (own rows)
+    DevCSR A, P, R;
+    SmootherPlan sm;
+    double *b = nullptr, *x = nullptr, *wp = nullptr, *w0 = nullptr, *w1 = nullptr;
+    Halo halo;
+};
+
+__global__ void pack_kernel(int n, const int *__restrict__ idx, const double *__restrict__ v, double *__restrict__ out)
+{
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) out[i] = v[idx[i]];
+}
+
+__global__ void gather_kernel(int n, const int *__restrict__ idx, const double *__restrict__ v, double *__restrict__ out)
+{
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) out[i] = v[idx[i]];
+}
+
+int nccl_fail(ncclResult_t r, const char *what)
+{
+    fprintf(stderr, "### ERROR: RCCL %s: %s\n", what, ncclGetErrorString(r));
+    return ERROR_MISC;
+}
+#define SSS_NCCL(call)                                  \
+    do {                                                \
+        ncclResult_t r_ = (call);                       \
+        if (r_ != ncclSuccess) return nccl_fail(r_, #call); \
+    } while (0)
+
+}  // namespace
+
+struct sss_hip_dist {
+    sss_hip_comm *comm = nullptr;
+    SSS_AMG_PARS pars{};
+    sss_hip_opts opts{};
+    hipStream_t stream = nullptr;
+    int nagg = 0;
+    DLevel L[kMaxLevels];
+    sss_hip_hier *tail = nullptr;   // levels >= nagg, replicated
+    // restriction into the tail: own coarse rows (global order) -> all-gather -> tail order
+    int nc_own = 0, nc_all = 0;
+    std::vector<int> counts, displs;
+    double *d_cown = nullptr, *d_call = nullptr;
+    int *d_tail_perm = nullptr;     // tail level-0 new -> old (null: identity)
+    std::vector<double> h_cown, h_call;
+    double *partial = nullptr, *d_norm = nullptr, *h_norm = nullptr;
+    std::vector<double> stage;
+};
+
+namespace {
+
+int exchange(sss_hip_dist *d, int l, double *vec)
+{
+    DLevel &L = d->L[l];
+    Halo &H = L.halo;
+    sss_hip_comm *c = d->comm;
+    const hipStream_t s = d->stream;
+    if (H.nsend == 0 && H.nrecv == 0) return 0;
+    const int ns = H.soff.empty() ? 0 : H.soff.back();
+    if (ns > 0) hipLaunchKernelGGL(pack_kernel, dim3((ns + 255) / 256), dim3(256), 0, s, ns, H.d_sidx, vec, H.d_sbuf);
+    if (!c->host) {
+        SSS_NCCL(ncclGroupStart());
+        for (int i = 0; i < H.nsend; ++i)
+            SSS_NCCL(ncclSend(H.d_sbuf + H.soff[i], (size_t)H.scount[i], ncclDouble, H.sdst[i], c->nccl, s));
+        for (int i = 0; i < H.nrecv; ++i)
+            SSS_NCCL(ncclRecv(vec + L.m + H.roff[i], (size_t)H.rcount[i], ncclDouble, H.rsrc[i], c->nccl, s));
+        SSS_NCCL(ncclGroupEnd());
+        return 0;
+    }
+    H.h_sbuf.resize(std::max(ns, 1));
+    H.h_rbuf.resize(std::max(L.g, 1));
+    if (ns > 0) SSS_HIP(hipMemcpyAsync(H.h_sbuf.data(), H.d_sbuf, sizeof(double) * ns, hipMemcpyDeviceToHost, s));
+    SSS_HIP(hipStreamSynchronize(s));
+    if (c->t.exchange(c->t.ctx, H.nsend, H.sdst.data(), H.scount.data(), H.h_sbuf.data(), H.nrecv, H.rsrc.data(),
+                      H.rcount.data(), H.h_rbuf.data()))
+        return ERROR_MISC;
+    if (L.g > 0) SSS_HIP(hipMemcpyAsync(vec + L.m, H.h_rbuf.data(), sizeof(double) * L.g, hipMemcpyHostToDevice, s));
+    SSS_HIP(hipStreamSynchronize(s));   // the staging buffer is reused by the next exchange
+    return 0;
+}
+
+struct HookCtx {
+    sss_hip_dist *d;
+    int l;
+};
+int hook_exchange(void *ctx, double *vec)
+{
+    auto *h = static_cast<HookCtx *>(ctx);
+    return exchange(h->d, h->l, vec);
+}
+
+int smooth(sss_hip_dist *d, int l, int post)
+{
+    DLevel &L = d->L[l];
+    HookCtx hc{d, l};
+    PassHooks hk;
+    hk.ctx = &hc;
+    hk.exchange = hook_exchange;
+    hk.w0 = L.w0;
+    hk.w1 = L.w1;
+    const int sweeps = post ? d->pars.post_iter : d->pars.pre_iter;
+    return smoother_run(L.sm, L.A, L.b, L.x, sweeps, d->stream, &hk);
+}
+
+int allgather_coarse(sss_hip_dist *d)
+{
+    sss_hip_comm *c = d->comm;
+    const hipStream_t s = d->stream;
+    if (!c->host) {
+        SSS_NCCL(ncclGroupStart());
+        for (int q = 0; q < c->nranks; ++q) {
+            if (q == c->rank) continue;
+            if (d->nc_own > 0) SSS_NCCL(ncclSend(d->d_cown, (size_t)d->nc_own, ncclDouble, q, c->nccl, s));
+            if (d->counts[q] > 0)
+                SSS_NCCL(ncclRecv(d->d_call + d->displs[q], (size_t)d->counts[q], ncclDouble, q, c->nccl, s));
+        }
+        SSS_NCCL(ncclGroupEnd());
+        if (d->nc_own > 0)
+            SSS_HIP(hipMemcpyAsync(d->d_call + d->displs[c->rank], d->d_cown, sizeof(double) * d->nc_own,
+                                   hipMemcpyDeviceToDevice, s));
+        return 0;
+    }
+    d->h_cown.resize(std::max(d->nc_own, 1));
+    d->h_call.resize(std::max(d->nc_all, 1));
+    if (d->nc_own > 0)
+        SSS_HIP(hipMemcpyAsync(d->h_cown.data(), d->d_cown, sizeof(double) * d->nc_own, hipMemcpyDeviceToHost, s));
+    SSS_HIP(hipStreamSynchronize(s));
+    if (c->t.allgatherv(c->t.ctx, d->h_cown.data(), d->nc_own, d->h_call.data(), d->counts.data(), d->displs.data()))
+        return ERROR_MISC;
+    SSS_HIP(hipMemcpyAsync(d->d_call, d->h_call.data(), sizeof(double) * d->nc_all, hipMemcpyHostToDevice, s));
+    SSS_HIP(hipStreamSynchronize(s));
+    return 0;
+}
+
+int allreduce_norm(sss_hip_dist *d)   // d_norm (sum of squares) -> global sum, on the host
+{
+    sss_hip_comm *c = d->comm;
+    if (!c->host) SSS_NCCL(ncclAllReduce(d->d_norm, d->d_norm, 1, ncclDouble, ncclSum, c->nccl, d->stream));
+    SSS_HIP(hipMemcpyAsync(d->h_norm, d->d_norm, sizeof(double), hipMemcpyDeviceToHost, d->stream));
+    SSS_HIP(hipStreamSynchronize(d->stream));
+    if (c->host && c->t.allreduce_sum(c->t.ctx, d->h_norm, 1)) return ERROR_MISC;
+    return 0;
+}
+
+void release(sss_hip_dist *d)
+{
+    if (!d) return;
+    if (d->stream) (void)hipStreamSynchronize(d->stream);
+    for (int l = 0; l < d->nagg; ++l) {
+        DLevel &L = d->L[l];
+        devcsr_free(L.A);
+        devcsr_free(L.P);
+        devcsr_free(L.R);
+        smoother_free(L.sm);
+        dev_free(L.b);
+        dev_free(L.x);
+        dev_free(L.wp);
+        dev_free(L.w0);
+        dev_free(L.w1);
+        dev_free(L.halo.d_sidx);
+        dev_free(L.halo.d_sbuf);
+    }
+    if (d->tail) sss_hip_hier_destroy(d->tail);
+    dev_free(d->d_cown);
+    dev_free(d->d_call);
+    dev_free(d->d_tail_perm);
+    dev_free(d->partial);
+    dev_free(d->d_norm);
+    if (d->h_norm) (void)hipHostFree(d->h_norm);
+    if (d->stream) (void)hipStreamDestroy(d->stream);
+    delete d;
+}
+
+int upload_ints(int **dst, const std::vector<int> &src)
+{
+    *dst = dev_alloc<int>(src.size());
+    if (!*dst) return hip_fail(hipErrorOutOfMemory, "hipMalloc", __FILE__, __LINE__);
+    if (!src.empty()) SSS_HIP(hipMemcpy(*dst, src.data(), sizeof(int) * src.size(), hipMemcpyHostToDevice));
+    return 0;
+}
+
+}  // namespace
+
+extern "C" int sss_hip_rccl_unique_id(unsigned char *id)
+{
+    ncclUniqueId u;
+    SSS_NCCL(ncclGetUniqueId(&u));
+    std::memcpy(id, u.internal, SSS_HIP_RCCL_ID_BYTES);
+    return 0;
+}
+
+extern "C" sss_hip_comm *sss_hip_comm_rccl(int nranks, int rank, const unsigned char *id, int device)
+{
+    if (device >= 0 && hipSetDevice(device) != hipSuccess) return nullptr;
+    auto *c = new sss_hip_comm();
+    c->nranks = nranks;
+    c->rank = rank;
+    ncclUniqueId u;
+    std::memcpy(u.internal, id, SSS_HIP_RCCL_ID_BYTES);
+    ncclResult_t r = ncclCommInitRank(&c->nccl, nranks, u, rank);
+    if (r != ncclSuccess) {
+        nccl_fail(r, "ncclCommInitRank");
+        delete c;
+        return nullptr;
+    }
+    return c;
+}
+
+extern "C" sss_hip_comm *sss_hip_comm_host(int nranks, int rank, const sss_hip_host_transport *t)
+{
+    if (!t || !t->exchange || !t->allreduce_sum || !t->allgatherv) return nullptr;
+    auto *c = new sss_hip_comm();
+    c->nranks = nranks;
+    c->rank = rank;
+    c->host = true;
+    c->t = *t;
+    return c;
+}
+
+extern "C" void sss_hip_comm_destroy(sss_hip_comm *c)
+{
+    if (!c) return;
+    if (c->nccl) (void)ncclCommDestroy(c->nccl);
+    delete c;
+}
+
+extern "C" sss_hip_dist *sss_hip_dist_create(const SSS_AMG *mg, const sss_hip_opts *o, sss_hip_comm *c, int agg_rows)
+{
+    if (!mg || !c || sss_hip_device_count() <= 0) return nullptr;
+    auto *d = new sss_hip_dist();
+    d->comm = c;
+    d->pars = mg->pars;
+    if (o) d->opts = *o;
+    else sss_hip_opts_default(&d->opts);
+    auto fail = [&](const char *what) {
+        fprintf(stderr, "### ERROR: sss_hip_dist_create (rank %d): %s\n", c->rank, what);
+        release(d);
+        return (sss_hip_dist *)nullptr;
+    };
+    if (d->pars.cycle_type > 1) return fail("only V-cycles are distributed");
+    if (d->opts.device >= 0 && hipSetDevice(d->opts.device) != hipSuccess) return fail("hipSetDevice");
+    if (hipStreamCreateWithFlags(&d->stream, hipStreamNonBlocking) != hipSuccess) return fail("stream");
+    if (agg_rows <= 0) {
+        const char *e = getenv("SSS_HIP_AGG_ROWS");
+        agg_rows = (e && *e) ? atoi(e) : 20000;
+    }
+    PartPlan plan;
+    if (part_plan_build(plan, mg, c->nranks, c->rank, agg_rows)) return fail("partition");
+    d->nagg = plan.nagg;
+    if (d->nagg < 1) return fail("hierarchy too shallow to partition");
+
+    // replicated tail first: its level-0 relabeling fixes the column ids of P_{nagg-1}
+    SSS_AMG sub = *mg;
+    sub.cg = mg->cg + d->nagg;
+    sub.num_levels = mg->num_levels - d->nagg;
+    sss_hip_opts to = d->opts;
+    to.use_graph = 0;
+    d->tail = hier_create_impl(&sub, &to, d->nagg, d->stream);
+    if (!d->tail) return fail("replicated coarse levels");
+    const std::vector<int> &tperm = hier_perm(d->tail, 0);
+    const int nt = mg->cg[d->nagg].A.num_rows;
+    std::vector<int> tinv;
+    if (!tperm.empty()) {
+        tinv.resize(nt);
+        for (int i = 0; i < nt; ++i) tinv[tperm[i]] = i;
+        if (upload_ints(&d->d_tail_perm, tperm)) return fail("tail perm");
+    }
+
+    for (int l = 0; l < d->nagg; ++l) {
+        PartLevel &P = plan.L[l];
+        DLevel &L = d->L[l];
+        L.lo = P.lo;
+        L.hi = P.hi;
+        L.m = P.m;
+        L.g = P.g;
+        L.perm = P.perm;
+        const int kind = level_kind_of(d->opts, l), inner = level_inner_of(d->opts, l);
+        SSS_MAT Av = P.A.view();
+        if (devcsr_upload(L.A, Av, P.nF)) return fail("upload A");
+        if (smoother_build(L.sm, Av, P.mark.data(), kind, &L.A, inner, P.gcls.data())) return fail("smoother plan");
+        for (const auto &ps : L.sm.pass)
+            if (ps.nrows > 0 && !ps.range) return fail("level needs an exact GS-CF chain across ranks (not distributed)");
+        if (l + 1 == d->nagg && !tinv.empty())
+            for (int &j : P.P.ci) j = tinv[j];
+        SSS_MAT Pv = P.P.view(), Rv = P.R.view();
+        if (devcsr_upload(L.P, Pv) || devcsr_upload(L.R, Rv)) return fail("upload P/R");
+        const size_t nv = (size_t)(L.m + L.g);
+        L.b = dev_alloc<double>(nv);
+        L.x = dev_alloc<double>(nv);
+        L.wp = dev_alloc<double>(nv);
+        L.w0 = dev_alloc<double>(nv);
+        L.w1 = dev_alloc<double>(nv);
+        if (!L.b || !L.x || !L.wp || !L.w0 || !L.w1) return fail("vectors");
+        for (double *v : {L.b, L.x, L.wp, L.w0, L.w1})
+            if (hipMemset(v, 0, sizeof(double) * nv) != hipSuccess) return fail("memset");
+        Halo &H = L.halo;
+        H.sdst = P.sdst;
+        H.scount = P.scount;
+        H.rsrc = P.rsrc;
+        H.rcount = P.rcount;
+        H.nsend = (int)H.sdst.size();
+        H.nrecv = (int)H.rsrc.size();
+        H.soff.assign(1, 0);
+        for (int x : H.scount) H.soff.push_back(H.soff.back() + x);
+        H.roff.assign(1, 0);
+        for (int x : H.rcount) H.roff.push_back(H.roff.back() + x);
+        if (upload_ints(&H.d_sidx, P.sidx)) return fail("halo");
+        H.d_sbuf = dev_alloc<double>(P.sidx.size());
+        if (!H.d_sbuf) return fail("halo buffer");
+    }
+    // all-gather layout of level nagg
+    const auto &cut = plan.cut[d->nagg];
+    d->counts.resize(c->nranks);
+    d->displs.resize(c->nranks);
+    for (int q = 0; q < c->nranks; ++q) {
+        d->counts[q] = cut[q + 1] - cut[q];
+        d->displs[q] = cut[q];
+    }
+    d->nc_own = d->counts[c->rank];
+    d->nc_all = nt;
+    d->d_cown = dev_alloc<double>(d->nc_own);
+    d->d_call = dev_alloc<double>(nt);
+    d->partial = dev_alloc<double>((size_t)std::max(d->L[0].A.ngrid, 1));
+    d->d_norm = dev_alloc<double>(1);
+    if (!d->d_cown || !d->d_call || !d->partial || !d->d_norm ||
+        hipHostMalloc((void **)&d->h_norm, sizeof(double)) != hipSuccess)
+        return fail("buffers");
+    if (hipStreamSynchronize(d->stream) != hipSuccess) return fail("sync");
+    return d;
+}
+
+extern "C" void sss_hip_dist_destroy(sss_hip_dist *d) { release(d); }
+
+extern "C" int sss_hip_dist_info(sss_hip_dist *d, int *lo, int *hi, int *nagg, int *nghost0)
+{
+    if (!d) return ERROR_INPUT_PAR;
+    *lo = d->L[0].lo;
+    *hi = d->L[0].hi;
+    *nagg = d->nagg;
+    *nghost0 = d->L[0].g;
+    return 0;
+}
+
+static double *dist_vec(sss_hip_dist *d, int which)
+{
+    DLevel &L = d->L[0];
+    return which == SSS_HIP_VEC_B ? L.b : which == SSS_HIP_VEC_X ? L.x : which == SSS_HIP_VEC_WP ? L.wp : nullptr;
+}
+
+extern "C" int sss_hip_dist_upload_vec(sss_hip_dist *d, int which, const double *own, int n)
+{
+    double *v = dist_vec(d, which);
+    DLevel &L = d->L[0];
+    if (!v || n != L.m) return ERROR_INPUT_PAR;
+    d->stage.resize(std::max(n, 1));
+    for (int i = 0; i < n; ++i) d->stage[i] = own[L.perm[i] - L.lo];
+    SSS_HIP(hipMemcpyAsync(v, d->stage.data(), sizeof(double) * n, hipMemcpyHostToDevice, d->stream));
+    SSS_HIP(hipStreamSynchronize(d->stream));
+    return 0;
+}
+
+extern "C" int sss_hip_dist_download_vec(sss_hip_dist *d, int which, double *own, int n)
+{
+    double *v = dist_vec(d, which);
+    DLevel &L = d->L[0];
+    if (!v || n != L.m) return ERROR_INPUT_PAR;
+    d->stage.resize(std::max(n, 1));
+    SSS_HIP(hipMemcpyAsync(d->stage.data(), v, sizeof(double) * n, hipMemcpyDeviceToHost, d->stream));
+    SSS_HIP(hipStreamSynchronize(d->stream));
+    for (int i = 0; i < n; ++i) own[L.perm[i] - L.lo] = d->stage[i];
+    return 0;
+}
+
+extern "C" int sss_hip_dist_cycle(sss_hip_dist *d)
+{
+    const hipStream_t s = d->stream;
+    const int nagg = d->nagg;
+    int rc;
+    for (int l = 0; l < nagg; ++l) {   // descent
+        DLevel &L = d->L[l];
+        if ((rc = smooth(d, l, 0))) return rc;
+        if ((rc = exchange(d, l, L.x))) return rc;
+        if ((rc = launch_spmv(L.A, SSS_HIP_SPMV_RESID, -1.0, L.x, L.b, L.wp, 0, nullptr, s))) return rc;
+        if ((rc = exchange(d, l, L.wp))) return rc;
+        if (l + 1 < nagg) {
+            DLevel &C = d->L[l + 1];
+            if ((rc = launch_spmv(L.R, SSS_HIP_SPMV_MXY, 1.0, L.wp, nullptr, C.b, 0, nullptr, s))) return rc;
+            SSS_HIP(hipMemsetAsync(C.x, 0, sizeof(double) * (size_t)(C.m + C.g), s));
+        } else {
+            if ((rc = launch_spmv(L.R, SSS_HIP_SPMV_MXY, 1.0, L.wp, nullptr, d->d_cown, 0, nullptr, s))) return rc;
+            if ((rc = allgather_coarse(d))) return rc;
+            double *tb = hier_vec(d->tail, 0, SSS_HIP_VEC_B), *tx = hier_vec(d->tail, 0, SSS_HIP_VEC_X);
+            if (d->d_tail_perm)
+                hipLaunchKernelGGL(gather_kernel, dim3((d->nc_all + 255) / 256), dim3(256), 0, s, d->nc_all,
+                                   d->d_tail_perm, d->d_call, tb);
+            else
+                SSS_HIP(hipMemcpyAsync(tb, d->d_call, sizeof(double) * d->nc_all, hipMemcpyDeviceToDevice, s));
+            SSS_HIP(hipMemsetAsync(tx, 0, sizeof(double) * (size_t)d->nc_all, s));
+        }
+    }
+    if ((rc = sss_hip_cycle(d->tail))) return rc;   // replicated levels, same stream
+    for (int l = nagg - 1; l >= 0; --l) {           // ascent
+        DLevel &L = d->L[l];
+        const double *xc;
+        if (l + 1 < nagg) {
+            if ((rc = exchange(d, l + 1, d->L[l + 1].x))) return rc;
+            xc = d->L[l + 1].x;
+        } else {
+            xc = hier_vec(d->tail, 0, SSS_HIP_VEC_X);
+        }
+        if ((rc = launch_spmv(L.P, SSS_HIP_SPMV_AMXPY, 1.0, xc, nullptr, L.x, 0, nullptr, s))) return rc;
+        if ((rc = smooth(d, l, 1))) return rc;
+    }
+    return 0;
+}
+
+extern "C" int sss_hip_dist_residual_norm(sss_hip_dist *d, double *absres)
+{
+    DLevel &L = d->L[0];
+    int rc;
+    if ((rc = exchange(d, 0, L.x))) return rc;
+    if ((rc = launch_spmv(L.A, SSS_HIP_SPMV_RESID, -1.0, L.x, L.b, L.wp, 0, d->partial, d->stream))) return rc;
+    if ((rc = launch_final_sum(d->partial, L.A.ngrid, d->d_norm, false, d->stream))) return rc;
+    if ((rc = allreduce_norm(d))) return rc;
+    *absres = std::sqrt(*d->h_norm);
+    return 0;
+}
+
+extern "C" int sss_hip_dist_sync(sss_hip_dist *d)
+{
+    SSS_HIP(hipStreamSynchronize(d->stream));
+    return 0;
+}

@@ -58,6 +58,15 @@ void devcsr_free(DevCSR &d);
 int build_row_blocks(const int *h_rp, int n, std::vector<int> &blk, int split = -1);
 int wave_row_min();
 
+// ---- hierarchy internals shared with the distributed engine (sss_hier.hip) ------------------
+// A hierarchy over mg->cg[0 .. num_levels); its L[0] is global level `level_base` (smoother
+// kinds follow the global level); `stream` = nullptr creates a private stream.
+sss_hip_hier *hier_create_impl(const SSS_AMG *mg, const sss_hip_opts *o, int level_base, hipStream_t stream);
+double *hier_vec(sss_hip_hier *h, int level, int which);
+const std::vector<int> &hier_perm(sss_hip_hier *h, int level);   // new -> old (empty: identity)
+int level_kind_of(const sss_hip_opts &o, int global_level);
+int level_inner_of(const sss_hip_opts &o, int global_level);
+
 // y <- op(A x) on `stream` (see SSS_HIP_SPMV_*).  `partial` (optional, RESID only): one
 // sum-of-squares of the written y per row block, for a deterministic fused norm.
 int launch_spmv(const DevCSR &A, int op, double alpha, const double *x, const double *b, double *y,
@@ -100,11 +109,25 @@ struct SmootherPlan {
 };
 // contiguous: mark is relabeled so class F occupies rows [0, nF) and class C rows [nF, n), and A was
 // uploaded with a block split at nF (its DevCSR is passed to allow range passes).
+// gcls (distributed levels, A has ghost columns >= num_rows): per ghost, its class if it is owned by
+// a lower rank (a "lower" column for the two-stage form), else -1.
+// Distributed levels: called before every class pass with x (exchange its ghosts), and after each
+// two-stage stage with the stage's full-length work vector; w0/w1 are full-length (own + ghost) work
+// vectors the two-stage form then writes its iterates into.
+struct PassHooks {
+    void *ctx = nullptr;
+    int (*exchange)(void *ctx, double *vec) = nullptr;
+    double *w0 = nullptr, *w1 = nullptr;
+};
 int smoother_build(SmootherPlan &sp, const SSS_MAT &A, const int *mark, int kind, const DevCSR *dA = nullptr,
-                   int inner = 0);
+                   int inner = 0, const int *gcls = nullptr);
+void launch_ts_stage0(const DevCSR &M, int lo, const int *split, const double *b, const double *x, const double *deff,
+                      double *P, double *y, hipStream_t s);
+void launch_ts_inner(const DevCSR &M, int lo, const double *deff, const double *P, const double *ycols, int col_off,
+                     const double *ykeep, double *y, hipStream_t s);
 void smoother_free(SmootherPlan &sp);
 int smoother_run(const SmootherPlan &sp, const DevCSR &A, const double *b, double *x, int sweeps,
-                 hipStream_t stream);
+                 hipStream_t stream, const PassHooks *hooks = nullptr);
 
 // ---- reductions ----------------------------------------------------------------------------
 // Deterministic sum of `n` partials -> *out (device); optionally sqrt.

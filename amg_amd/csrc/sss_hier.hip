@@ -34,6 +34,8 @@ struct sss_hip_hier {
         std::vector<int> perm;
     } L[kMaxLevels];
     std::vector<double> stage;   // host staging for permuted vector transfers
+    int level_base = 0;          // global level index of L[0] (a tail of a distributed hierarchy)
+    bool own_stream = true;
     int coarse_mode = SSS_HIP_COARSE_DIRECT;
     CoarseDirect direct;
     CoarseKrylov *krylov = nullptr;
@@ -96,6 +98,8 @@ static int level_inner(const sss_hip_opts &o, int l)
 {
     return level_smoother_kind(o, l) == SSS_HIP_SMOOTH_JACOBI && l >= o.inner_from ? o.inner : 0;
 }
+int sss::level_kind_of(const sss_hip_opts &o, int l) { return level_smoother_kind(o, l); }
+int sss::level_inner_of(const sss_hip_opts &o, int l) { return level_inner(o, l); }
 
 static void hier_release(sss_hip_hier *h)
 {
@@ -121,7 +125,7 @@ static void hier_release(sss_hip_hier *h)
     if (h->h_norm) (void)hipHostFree(h->h_norm);
     if (h->ev0) (void)hipEventDestroy(h->ev0);
     if (h->ev1) (void)hipEventDestroy(h->ev1);
-    if (h->stream) (void)hipStreamDestroy(h->stream);
+    if (h->stream && h->own_stream) (void)hipStreamDestroy(h->stream);
     delete h;
 }
 
@@ -186,7 +190,7 @@ static void relabel_csr(const SSS_MAT &A, const std::vector<int> &rperm, const s
     });
 }
 
-extern "C" sss_hip_hier *sss_hip_hier_create(const SSS_AMG *mg, const sss_hip_opts *o)
+sss_hip_hier *sss::hier_create_impl(const SSS_AMG *mg, const sss_hip_opts *o, int level_base, hipStream_t stream)
 {
     if (sss_hip_device_count() <= 0) {
         fprintf(stderr, "### ERROR: no HIP device available for the AMG solve phase\n");
@@ -203,7 +207,13 @@ extern "C" sss_hip_hier *sss_hip_hier_create(const SSS_AMG *mg, const sss_hip_op
         hier_release(h);
         return (sss_hip_hier *)nullptr;
     };
-    if (hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess) return fail("stream");
+    h->level_base = level_base;
+    if (stream) {
+        h->stream = stream;
+        h->own_stream = false;
+    } else if (hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess) {
+        return fail("stream");
+    }
     if (hipEventCreate(&h->ev0) != hipSuccess || hipEventCreate(&h->ev1) != hipSuccess) return fail("events");
 
     // F|C relabeling of every level but the coarsest (identity there)
@@ -214,8 +224,9 @@ extern "C" sss_hip_hier *sss_hip_hier_create(const SSS_AMG *mg, const sss_hip_op
             const int n = C.A.num_rows;
             if (!C.cfmark.d || C.cfmark.n < n) continue;
             // two-stage levels need contiguous classes; otherwise follow opts.relabel
-            const bool two_stage = level_inner(h->opts, l) > 0;
-            if (!two_stage && !(h->opts.relabel == 1 || (h->opts.relabel == 2 && l > 0))) continue;
+            const int gl = h->level_base + l;
+            const bool two_stage = level_inner(h->opts, gl) > 0;
+            if (!two_stage && !(h->opts.relabel == 1 || (h->opts.relabel == 2 && gl > 0))) continue;
             auto &perm = h->L[l].perm;
             perm.reserve(n);
             for (int i = 0; i < n; ++i)
@@ -239,12 +250,13 @@ extern "C" sss_hip_hier *sss_hip_hier_create(const SSS_AMG *mg, const sss_hip_op
             if (devcsr_upload(L.A, Av, nF[l])) return fail("upload A");
             std::vector<int> mark(n);
             for (int i = 0; i < n; ++i) mark[i] = C.cfmark.d[L.perm[i]];
-            if (smoother_build(L.sm, Av, mark.data(), level_smoother_kind(h->opts, l), &L.A, level_inner(h->opts, l)))
+            if (smoother_build(L.sm, Av, mark.data(), level_smoother_kind(h->opts, h->level_base + l), &L.A,
+                               level_inner(h->opts, h->level_base + l)))
                 return fail("smoother plan");
         } else {
             if (devcsr_upload(L.A, C.A)) return fail("upload A");
             if (l < h->nl - 1 &&
-                smoother_build(L.sm, C.A, C.cfmark.d, level_smoother_kind(h->opts, l)))
+                smoother_build(L.sm, C.A, C.cfmark.d, level_smoother_kind(h->opts, h->level_base + l)))
                 return fail("smoother plan");
         }
         if (l < h->nl - 1) {
@@ -303,7 +315,21 @@ extern "C" sss_hip_hier *sss_hip_hier_create(const SSS_AMG *mg, const sss_hip_op
     return h;
 }
 
+extern "C" sss_hip_hier *sss_hip_hier_create(const SSS_AMG *mg, const sss_hip_opts *o)
+{
+    return sss::hier_create_impl(mg, o, 0, nullptr);
+}
+
 extern "C" void sss_hip_hier_destroy(sss_hip_hier *h) { hier_release(h); }
+
+double *sss::hier_vec(sss_hip_hier *h, int level, int which)
+{
+    if (!h || level < 0 || level >= h->nl) return nullptr;
+    auto &L = h->L[level];
+    return which == SSS_HIP_VEC_B ? L.b : which == SSS_HIP_VEC_X ? L.x : which == SSS_HIP_VEC_WP ? L.wp : nullptr;
+}
+
+const std::vector<int> &sss::hier_perm(sss_hip_hier *h, int level) { return h->L[level].perm; }
 
 static double *level_vec(sss_hip_hier *h, int level, int which)
 {

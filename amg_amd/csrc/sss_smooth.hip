@@ -43,7 +43,8 @@ static int upload_doubles(double **dst, const std::vector<double> &src)
     return 0;
 }
 
-int smoother_build(SmootherPlan &sp, const SSS_MAT &A, const int *mark, int kind, const DevCSR *dA, int inner)
+int smoother_build(SmootherPlan &sp, const SSS_MAT &A, const int *mark, int kind, const DevCSR *dA, int inner,
+                   const int *gcls)
 {
     const int n = A.num_rows;
     const int *rp = A.row_ptr, *ci = A.col_idx;
@@ -177,14 +178,18 @@ int smoother_build(SmootherPlan &sp, const SSS_MAT &A, const int *mark, int kind
             std::vector<int> nrp(1, 0), nci, lrp(1, 0), lci, split(m);
             std::vector<double> nv, lv;
             for (int i = ps.lo; i < ps.hi; ++i) {
+                // L_i: same class, j < i in the global order -- own rows of the pass below i, or
+                // (distributed levels) ghost columns of this class owned by lower ranks
+                const int c = (int)(&ps - sp.pass);
+                auto lower = [&](int j) { return j < n ? (j >= ps.lo && j < i) : (gcls && gcls[j - n] == c); };
                 for (int k = rp[i]; k < rp[i + 1]; ++k) {   // N_i: off-diagonal, not same-class lower
                     const int j = ci[k];
-                    if (j != i && !(j >= ps.lo && j < i)) nci.push_back(j), nv.push_back(v[k]);
+                    if (j != i && !lower(j)) nci.push_back(j), nv.push_back(v[k]);
                 }
                 split[i - ps.lo] = (int)nci.size();
                 for (int k = rp[i]; k < rp[i + 1]; ++k) {   // L_i
                     const int j = ci[k];
-                    if (j >= ps.lo && j < i) {
+                    if (lower(j)) {
                         nci.push_back(j), nv.push_back(v[k]);
                         lci.push_back(j), lv.push_back(v[k]);
                     }
@@ -195,7 +200,7 @@ int smoother_build(SmootherPlan &sp, const SSS_MAT &A, const int *mark, int kind
             auto mk = [&](std::vector<int> &r, std::vector<int> &c, std::vector<double> &w) {
                 SSS_MAT M;
                 M.num_rows = m;
-                M.num_cols = n;
+                M.num_cols = A.num_cols;
                 M.num_nnzs = (int)c.size();
                 M.row_ptr = r.data();
                 M.col_idx = c.data();
@@ -483,15 +488,16 @@ __global__ __launch_bounds__(kBlock) void ts_stage0(int lo, DevCSR M, const int 
 }
 
 // Inner step over the L-only rows:  y_q = (P_q - sum_{L_i} a yp[j - lo]) / d  (keeps yp_q if |d| small)
+// (column c reads ycols[c - col_off]; a row with |d| small keeps ykeep[q]; rows are lo + q)
 template <bool WAVE>
 __global__ __launch_bounds__(kBlock) void ts_inner(int lo, DevCSR M, const double *__restrict__ deff,
-                                                   const double *__restrict__ P, const double *__restrict__ yp,
-                                                   double *__restrict__ y)
+                                                   const double *__restrict__ P, const double *ycols, int col_off,
+                                                   const double *ykeep, double *__restrict__ y)
 {
-    auto fetch = [&](int c) -> double { return yp[c - lo]; };
+    auto fetch = [&](int c) -> double { return ycols[c - col_off]; };
     auto finish = [&](int q, double acc) {
         const double d = deff[lo + q];
-        y[q] = fabs(d) > SMALLFLOAT ? acc / d : yp[q];
+        y[q] = fabs(d) > SMALLFLOAT ? acc / d : ykeep[q];
     };
     if (WAVE) {
         __shared__ double strips[4][kWaveStage];
@@ -527,6 +533,28 @@ __global__ __launch_bounds__(kBlock) void ts_inner(int lo, DevCSR M, const doubl
     }
 }
 
+void launch_ts_stage0(const DevCSR &M, int lo, const int *split, const double *b, const double *x, const double *deff,
+                      double *P, double *y, hipStream_t s)
+{
+    if (M.n == 0) return;
+    if (M.wave_rows)
+        hipLaunchKernelGGL(ts_stage0<true>, dim3(M.ngrid), dim3(kBlock), 0, s, lo, M, split, b, x, deff, P, y);
+    else
+        hipLaunchKernelGGL(ts_stage0<false>, dim3(M.nblk), dim3(kBlock), 0, s, lo, M, split, b, x, deff, P, y);
+}
+
+void launch_ts_inner(const DevCSR &M, int lo, const double *deff, const double *P, const double *ycols, int col_off,
+                     const double *ykeep, double *y, hipStream_t s)
+{
+    if (M.n == 0) return;
+    if (M.wave_rows)
+        hipLaunchKernelGGL(ts_inner<true>, dim3(M.ngrid), dim3(kBlock), 0, s, lo, M, deff, P, ycols, col_off, ykeep,
+                           y);
+    else
+        hipLaunchKernelGGL(ts_inner<false>, dim3(M.nblk), dim3(kBlock), 0, s, lo, M, deff, P, ycols, col_off, ykeep,
+                           y);
+}
+
 __global__ __launch_bounds__(kBlock) void scatter_rows(int m, const int *__restrict__ map, const double *__restrict__ y,
                                                        double *__restrict__ x)
 {
@@ -534,15 +562,21 @@ __global__ __launch_bounds__(kBlock) void scatter_rows(int m, const int *__restr
     if (r < m) x[map[r]] = y[r];
 }
 
-int smoother_run(const SmootherPlan &sp, const DevCSR &A, const double *b, double *x, int sweeps, hipStream_t s)
+int smoother_run(const SmootherPlan &sp, const DevCSR &A, const double *b, double *x, int sweeps, hipStream_t s,
+                 const PassHooks *hk)
 {
     const int n = A.n;
     if (n == 0) return 0;
+    int rc;
     for (int sw = 0; sw < sweeps; ++sw) {
         const double *deff = sw == 0 ? sp.d_first : sp.d_later;
         for (int c = 0; c < 2; ++c) {
             const PassSchedule &ps = sp.pass[c];
             if (ps.nrows == 0) continue;
+            if (hk) {   // distributed level: refresh x's ghosts; only contiguous passes qualify
+                if (!ps.range) return ERROR_INPUT_PAR;
+                if ((rc = hk->exchange(hk->ctx, x))) return rc;
+            }
             if (ps.range) {
                 const int nb = ps.bhi - ps.blo, m = ps.hi - ps.lo, nw = (m + 3) / 4;
                 const bool wave = A.wave_rows;
@@ -555,22 +589,25 @@ int smoother_run(const SmootherPlan &sp, const DevCSR &A, const double *b, doubl
                         hipLaunchKernelGGL(relax_range<M>, dim3(nb), dim3(kBlock), 0, s, ps.blo, A.blk, A.rp, cols,
                                            A.v, sp.diag_pos, ps.lo, b, x, yp, y, deff);
                 };
-                if (sp.kind == SSS_HIP_SMOOTH_JACOBI && sp.inner > 0) {
+                if (sp.kind == SSS_HIP_SMOOTH_JACOBI && sp.inner > 0 && hk) {
+                    // iterates live in full-length work vectors whose ghosts (lower-rank rows of
+                    // this class) are refreshed after every stage
                     const DevCSR &Mn = ps.ts_nl, &Ml = ps.ts_lo;
-                    if (Mn.wave_rows)
-                        hipLaunchKernelGGL(ts_stage0<true>, dim3(Mn.ngrid), dim3(kBlock), 0, s, ps.lo, Mn, ps.ts_split,
-                                           b, (const double *)x, deff, ps.ts_P, ps.y);
-                    else
-                        hipLaunchKernelGGL(ts_stage0<false>, dim3(Mn.nblk), dim3(kBlock), 0, s, ps.lo, Mn,
-                                           ps.ts_split, b, (const double *)x, deff, ps.ts_P, ps.y);
+                    double *cur = hk->w0, *nxt = hk->w1;
+                    launch_ts_stage0(Mn, ps.lo, ps.ts_split, b, x, deff, ps.ts_P, cur + ps.lo, s);
+                    for (int st = 0; st < sp.inner; ++st) {
+                        if ((rc = hk->exchange(hk->ctx, cur))) return rc;
+                        launch_ts_inner(Ml, ps.lo, deff, ps.ts_P, cur, 0, cur + ps.lo, nxt + ps.lo, s);
+                        std::swap(cur, nxt);
+                    }
+                    SSS_HIP(hipMemcpyAsync(x + ps.lo, cur + ps.lo, sizeof(double) * (size_t)m, hipMemcpyDeviceToDevice,
+                                           s));
+                } else if (sp.kind == SSS_HIP_SMOOTH_JACOBI && sp.inner > 0) {
+                    const DevCSR &Mn = ps.ts_nl, &Ml = ps.ts_lo;
+                    launch_ts_stage0(Mn, ps.lo, ps.ts_split, b, x, deff, ps.ts_P, ps.y, s);
                     double *cur = ps.y, *nxt = ps.y2;
                     for (int st = 0; st < sp.inner; ++st) {
-                        if (Ml.wave_rows)
-                            hipLaunchKernelGGL(ts_inner<true>, dim3(Ml.ngrid), dim3(kBlock), 0, s, ps.lo, Ml, deff,
-                                               (const double *)ps.ts_P, (const double *)cur, nxt);
-                        else
-                            hipLaunchKernelGGL(ts_inner<false>, dim3(Ml.nblk), dim3(kBlock), 0, s, ps.lo, Ml, deff,
-                                               (const double *)ps.ts_P, (const double *)cur, nxt);
+                        launch_ts_inner(Ml, ps.lo, deff, ps.ts_P, cur, ps.lo, cur, nxt, s);
                         std::swap(cur, nxt);
                     }
                     SSS_HIP(hipMemcpyAsync(x + ps.lo, cur, sizeof(double) * (size_t)m, hipMemcpyDeviceToDevice, s));

@@ -117,6 +117,63 @@ int sss_hip_time_level0_spmv(sss_hip_hier *h, int reps, double *avg_ms);
  * stream, timed with HIP events; absres of the last iteration is returned. */
 int sss_hip_time_iterations(sss_hip_hier *h, int reps, double *avg_ms, double *absres);
 
+/* ---- row-partitioned multi-GPU solve (one process per GPU) ------------------------- */
+/* Every level l < nagg is split into contiguous row ranges: level 0 evenly, level l+1 by
+ * ownership of the C points of level l (coarse numbering is monotone in the fine index,
+ * SSS_coarsen's cmap).  Each rank keeps its rows (F|C relabeled) plus ghost columns; levels
+ * >= nagg (fewer than agg_rows rows, and always the coarsest) are replicated on every rank and
+ * cycled redundantly.  Halos move over RCCL (xGMI) or, for tests, over a host transport. */
+typedef struct sss_hip_comm sss_hip_comm;
+typedef struct sss_hip_dist sss_hip_dist;
+typedef struct sss_hip_host_transport {
+    void *ctx;
+    /* one point-to-point round: send scount[i] doubles (concatenated in sbuf) to rank sdst[i]
+     * and receive rcount[i] doubles (concatenated into rbuf) from rank rsrc[i]; 0 = success */
+    int (*exchange)(void *ctx, int nsend, const int *sdst, const int *scount, const double *sbuf, int nrecv,
+                    const int *rsrc, const int *rcount, double *rbuf);
+    int (*allreduce_sum)(void *ctx, double *v, int n);
+    /* all[displs[q] .. + counts[q]) <- rank q's `mine` */
+    int (*allgatherv)(void *ctx, const double *mine, int count, double *all, const int *counts, const int *displs);
+} sss_hip_host_transport;
+
+#define SSS_HIP_RCCL_ID_BYTES 128
+/* rank 0 creates the id; the caller broadcasts its bytes (e.g. over torch.distributed) */
+int sss_hip_rccl_unique_id(unsigned char *id);
+/* device >= 0: hipSetDevice(device) first (the communicator binds the current device) */
+sss_hip_comm *sss_hip_comm_rccl(int nranks, int rank, const unsigned char *id, int device);
+sss_hip_comm *sss_hip_comm_host(int nranks, int rank, const sss_hip_host_transport *t);
+void sss_hip_comm_destroy(sss_hip_comm *c);
+
+/* mg: the global hierarchy (every rank runs the same host setup).  V-cycles only.
+ * agg_rows <= 0: SSS_HIP_AGG_ROWS or 20000. */
+sss_hip_dist *sss_hip_dist_create(const SSS_AMG *mg, const sss_hip_opts *o, sss_hip_comm *c, int agg_rows);
+void sss_hip_dist_destroy(sss_hip_dist *d);
+/* own rows [lo, hi) of level 0 in the original numbering; nagg = number of partitioned levels */
+int sss_hip_dist_info(sss_hip_dist *d, int *lo, int *hi, int *nagg, int *nghost0);
+/* level-0 vectors, the rank's own rows in the original order (n = hi - lo) */
+int sss_hip_dist_upload_vec(sss_hip_dist *d, int which, const double *own, int n);
+int sss_hip_dist_download_vec(sss_hip_dist *d, int which, double *own, int n);
+int sss_hip_dist_cycle(sss_hip_dist *d);
+/* global ||b0 - A0 x0||_2 (one 8-byte allreduce), synchronises */
+int sss_hip_dist_residual_norm(sss_hip_dist *d, double *absres);
+int sss_hip_dist_sync(sss_hip_dist *d);
+
+/* Host-only view of the partition (no device needed; used by the CPU multi-process tests).
+ * which: 0 = A_l (m x (m+g)), 1 = P_l (m x next-level local), 2 = R_l (own coarse rows x (m+g)).
+ * Arrays stay owned by the plan. */
+typedef struct sss_part_plan sss_part_plan;
+sss_part_plan *sss_part_plan_create(const SSS_AMG *mg, int nranks, int rank, int agg_rows);
+void sss_part_plan_destroy(sss_part_plan *p);
+int sss_part_plan_nagg(const sss_part_plan *p);
+/* own range, own count, ghost count of level l (l <= nagg for the range; m/g for l < nagg) */
+int sss_part_plan_level(const sss_part_plan *p, int l, int *lo, int *hi, int *m, int *g);
+int sss_part_plan_matrix(const sss_part_plan *p, int l, int which, SSS_MAT *out);
+/* perm: local id -> global id (m); ghosts: ghost k -> global id (g) */
+int sss_part_plan_ids(const sss_part_plan *p, int l, const int **perm, const int **ghosts);
+/* halo of level l: nsend/nrecv peers; peer ranks, counts, send local ids (concatenated) */
+int sss_part_plan_halo(const sss_part_plan *p, int l, int *nsend, const int **sdst, const int **scount,
+                       const int **sidx, int *nrecv, const int **rsrc, const int **rcount);
+
 /* ---- generators (host) -------------------------------------------------------------- */
 /* kind 7 or 27; rows of z-planes [z0, z1) of an nx*ny*nz grid, global column indices. */
 int sss_gen_stencil(int kind, int nx, int ny, int nz, int z0, int z1, SSS_MAT *A);

@@ -67,22 +67,25 @@ def bus_matrix():
     return A.read_mtx(BUS_MTX)
 
 
+class quiet_ctx:
+    """Silence the C library's stdout chatter (setup prints) at the fd level."""
+
+    def __enter__(self):
+        sys.stdout.flush()
+        self.saved = os.dup(1)
+        self.null = os.open(os.devnull, os.O_WRONLY)
+        os.dup2(self.null, 1)
+
+    def __exit__(self, *a):
+        C.CDLL(None).fflush(None)
+        os.dup2(self.saved, 1)
+        os.close(self.saved)
+        os.close(self.null)
+
+
 @pytest.fixture(scope="session")
 def quiet():
-    """Silence the C library's stdout chatter (setup prints) at the fd level."""
-    class Q:
-        def __enter__(self):
-            sys.stdout.flush()
-            self.saved = os.dup(1)
-            self.null = os.open(os.devnull, os.O_WRONLY)
-            os.dup2(self.null, 1)
-
-        def __exit__(self, *a):
-            C.CDLL(None).fflush(None)
-            os.dup2(self.saved, 1)
-            os.close(self.saved)
-            os.close(self.null)
-    return Q
+    return quiet_ctx
 
 
 def build_hierarchy(M, quiet_cls):

@@ -1,0 +1,144 @@
+"""CPU, world_size 2 over gloo: the row partition of the distributed engine (sss_part_plan_*).
+
+Each rank builds the same global hierarchy, takes its partition, moves ghost values with the
+plan's halo lists over torch.distributed (gloo) point-to-point, and checks that its local A, R
+and P products equal the global products on its rows bitwise (same entries, same order): the
+host-side contract the multi-GPU engine (amg_amd/csrc/sss_dist.hip) runs on.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import socket
+import sys
+from pathlib import Path
+
+import numpy as np
+import pytest
+
+ROOT = Path(__file__).resolve().parent.parent
+sys.path.insert(0, str(ROOT))
+sys.path.insert(0, str(ROOT / "tests"))
+
+
+def _free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _halo_exchange(dist, torch, halo, local, m):
+    """local: own + ghost values (length m + g); fills the ghost part from the peers."""
+    reqs, off, outs = [], 0, []
+    for q, c in zip(halo["sdst"], halo["scount"]):
+        t = torch.from_numpy(local[halo["sidx"][off:off + c]].copy())
+        reqs.append(dist.isend(t, int(q)))
+        off += c
+    for q, c in zip(halo["rsrc"], halo["rcount"]):
+        t = torch.empty(int(c), dtype=torch.float64)
+        reqs.append(dist.irecv(t, int(q)))
+        outs.append(t)
+    for r in reqs:
+        r.wait()
+    off = m
+    for t in outs:
+        local[off:off + len(t)] = t.numpy()
+        off += len(t)
+
+
+def _worker(rank, world, port, kind, n, agg_rows, errq):
+    try:
+        os.environ["MASTER_ADDR"] = "127.0.0.1"
+        os.environ["MASTER_PORT"] = str(port)
+        import torch
+        import torch.distributed as dist
+
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        import amg_amd as A
+        import oracle
+        from amg_amd._native import dptr
+        from conftest import build_hierarchy, quiet_ctx
+
+        H = build_hierarchy(A.generate(kind, n), quiet_ctx)
+        plan = A.PartPlan(H, world, rank, agg_rows)
+        ora = oracle.load()
+        assert plan.nagg >= 2, plan.nagg
+        # ranges tile every partitioned level
+        for l in range(plan.nagg + 1):
+            lo, hi, _, _ = plan.level(l)
+            got = [None] * world
+            dist.all_gather_object(got, (lo, hi))
+            assert got[0][0] == 0 and got[-1][1] == H.level(l).A.num_rows
+            assert all(got[q][1] == got[q + 1][0] for q in range(world - 1))
+        rng = np.random.default_rng(3)
+        for l in range(plan.nagg):
+            lo, hi, m, g = plan.level(l)
+            perm, ghosts = plan.ids(l)
+            assert sorted(perm.tolist()) == list(range(lo, hi))
+            halo = plan.halo(l)
+            Ag, Rg, Pg = H.level(l).A, H.level(l).R, H.level(l).P
+            nl = Ag.num_rows
+            x = rng.standard_normal(nl)           # same on every rank (same seed sequence)
+            xc = rng.standard_normal(Pg.num_cols)
+            loc = np.zeros(m + g)
+            loc[:m] = x[perm]
+            _halo_exchange(dist, torch, halo, loc, m)
+            assert np.array_equal(loc[m:], x[ghosts]), ("halo", l)
+            # A rows
+            yg = np.zeros(nl)
+            ora.ora_mv_mxy(C.byref(Ag), dptr(x), dptr(yg))
+            Al = plan.matrix(l, "A")
+            yl = np.zeros(m)
+            ora.ora_mv_mxy(C.byref(Al), dptr(loc), dptr(yl))
+            assert np.array_equal(yl.view(np.uint64), yg[perm].view(np.uint64)), ("A", l)
+            # R rows (own coarse points, next level's local order or global order at nagg)
+            rg = np.zeros(Rg.num_rows)
+            ora.ora_mv_mxy(C.byref(Rg), dptr(x), dptr(rg))
+            Rl = plan.matrix(l, "R")
+            rl = np.zeros(Rl.num_rows)
+            ora.ora_mv_mxy(C.byref(Rl), dptr(loc), dptr(rl))
+            if l + 1 < plan.nagg:
+                crow = plan.ids(l + 1)[0]
+            else:
+                clo, chi, _, _ = plan.level(l + 1)
+                crow = np.arange(clo, chi)
+            assert np.array_equal(rl.view(np.uint64), rg[crow].view(np.uint64)), ("R", l)
+            # P rows: coarse vector in the next level's local numbering (with its halo)
+            pg = np.zeros(nl)
+            ora.ora_mv_mxy(C.byref(Pg), dptr(xc), dptr(pg))
+            Pl = plan.matrix(l, "P")
+            if l + 1 < plan.nagg:
+                _, _, mc, gc = plan.level(l + 1)
+                cperm, cghosts = plan.ids(l + 1)
+                cl = np.zeros(mc + gc)
+                cl[:mc] = xc[cperm]
+                _halo_exchange(dist, torch, plan.halo(l + 1), cl, mc)
+            else:
+                cl = xc.copy()
+            pl = np.zeros(m)
+            ora.ora_mv_mxy(C.byref(Pl), dptr(cl), dptr(pl))
+            assert np.array_equal(pl.view(np.uint64), pg[perm].view(np.uint64)), ("P", l)
+        dist.barrier()
+        dist.destroy_process_group()
+    except BaseException as e:  # noqa: BLE001
+        import traceback
+        errq.put(f"rank {rank}: {e!r}\n{traceback.format_exc()}")
+
+
+@pytest.mark.parametrize("kind,n,agg", [(7, 20, 60), (27, 12, 40)])
+def test_partition_products_world2(kind, n, agg):
+    import torch.multiprocessing as mp
+
+    ctx = mp.get_context("spawn")
+    errq = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, kind, n, agg, errq)) for r in range(2)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=300)
+    errs = []
+    while not errq.empty():
+        errs.append(errq.get())
+    assert not errs, "\n".join(errs)
+    assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]

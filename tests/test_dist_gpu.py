@@ -1,0 +1,101 @@
+"""GPU, world_size 2 on one device: the row-partitioned engine (sss_hip_dist_*) over the host
+transport (torch.distributed gloo; RCCL refuses two ranks on one GPU).  Each rank's rows are
+computed exactly as on one GPU, so after every V-cycle the gathered x equals the single-GPU
+engine's x bitwise; the residual norm is reduced in another order (rtol 1e-12)."""
+from __future__ import annotations
+
+import os
+import socket
+import sys
+from pathlib import Path
+
+import numpy as np
+import pytest
+
+ROOT = Path(__file__).resolve().parent.parent
+sys.path.insert(0, str(ROOT))
+sys.path.insert(0, str(ROOT / "tests"))
+
+pytestmark = pytest.mark.gpu
+
+
+def _free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _worker(rank, world, port, kind, n, smoother, inner_from, agg_rows, cycles, errq):
+    try:
+        os.environ["MASTER_ADDR"] = "127.0.0.1"
+        os.environ["MASTER_PORT"] = str(port)
+        import torch
+        import torch.distributed as dist
+
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        import amg_amd as A
+        from conftest import build_hierarchy, quiet_ctx
+
+        H = build_hierarchy(A.generate(kind, n), quiet_ctx)
+        N = H.level(0).A.num_rows
+        comm = A.Comm(world, rank, "host")
+        D = A.DistHierarchy(H, comm, smoother=smoother, coarse="direct", device=0, agg_rows=agg_rows,
+                            inner_from=inner_from)
+        assert D.nagg >= 2, D.nagg
+        own = D.hi - D.lo
+        D.upload("b", np.ones(own))
+        D.upload("x", np.ones(own))
+        rel = []
+        for _ in range(cycles):
+            D.cycle()
+            rel.append(D.residual_norm() / np.sqrt(N))
+        x_own = D.download("x")
+        parts = [None] * world
+        dist.all_gather_object(parts, (D.lo, x_own))
+        D.close()
+        comm.close()
+        if rank == 0:
+            x = np.zeros(N)
+            for lo, xo in parts:
+                x[lo:lo + len(xo)] = xo
+            R = A.DeviceHierarchy(H, smoother=smoother, coarse="direct", device=0, inner_from=inner_from)
+            R.upload(0, "b", np.ones(N))
+            R.upload(0, "x", np.ones(N))
+            rel_r = []
+            for _ in range(cycles):
+                R.cycle()
+                rel_r.append(R.residual_norm() / np.sqrt(N))
+            x_r = R.download(0, "x")
+            R.close()
+            assert np.array_equal(x.view(np.uint64), x_r.view(np.uint64)), \
+                f"max |dx| = {np.max(np.abs(x - x_r))}"
+            assert np.allclose(rel, rel_r, rtol=1e-12, atol=0), (rel, rel_r)
+        dist.barrier()
+        dist.destroy_process_group()
+    except BaseException as e:  # noqa: BLE001
+        import traceback
+        errq.put(f"rank {rank}: {e!r}\n{traceback.format_exc()}")
+
+
+@pytest.mark.parametrize("kind,n,smoother,inner_from,agg", [
+    (7, 24, "hybrid", 2, 100),     # level 0 exact red-black GS-CF, C/F-Jacobi, two-stage from level 2
+    (7, 24, "jacobi", 0, 100),     # two-stage everywhere: lower-rank ghost rows are "lower" entries
+    (27, 14, "jacobi", 2, 100),    # 27-point: not red-black, C/F-Jacobi forms only
+])
+def test_dist_equals_single_gpu(kind, n, smoother, inner_from, agg):
+    import torch.multiprocessing as mp
+
+    ctx = mp.get_context("spawn")
+    errq = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, kind, n, smoother, inner_from, agg, 4, errq))
+             for r in range(2)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=600)
+    errs = []
+    while not errq.empty():
+        errs.append(errq.get())
+    assert not errs, "\n".join(errs)
+    assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
