@@ -109,6 +109,7 @@ ABI_SYMBOLS = [
     "sss_hip_rccl_unique_id", "sss_hip_comm_rccl", "sss_hip_comm_host", "sss_hip_comm_destroy",
     "sss_hip_dist_create", "sss_hip_dist_destroy", "sss_hip_dist_info", "sss_hip_dist_upload_vec",
     "sss_hip_dist_download_vec", "sss_hip_dist_cycle", "sss_hip_dist_residual_norm", "sss_hip_dist_sync",
+    "sss_hip_dist_time_level0_spmv",
     "sss_part_plan_create", "sss_part_plan_destroy", "sss_part_plan_nagg", "sss_part_plan_level",
     "sss_part_plan_matrix", "sss_part_plan_ids", "sss_part_plan_halo",
 ]
@@ -179,6 +180,7 @@ def _declare(lib):
         "sss_hip_dist_cycle": (C.c_int, [C.c_void_p]),
         "sss_hip_dist_residual_norm": (C.c_int, [C.c_void_p, _dbl_p]),
         "sss_hip_dist_sync": (C.c_int, [C.c_void_p]),
+        "sss_hip_dist_time_level0_spmv": (C.c_int, [C.c_void_p, C.c_int, _dbl_p]),
         "sss_part_plan_create": (C.c_void_p, [P(SSS_AMG), C.c_int, C.c_int, C.c_int]),
         "sss_part_plan_destroy": (None, [C.c_void_p]),
         "sss_part_plan_nagg": (C.c_int, [C.c_void_p]),
@@ -556,6 +558,11 @@ class DistHierarchy:
 
     def sync(self):
         self._check(lib().sss_hip_dist_sync(self.d), "dist sync")
+
+    def time_level0_spmv(self, reps: int) -> float:
+        ms = C.c_double()
+        self._check(lib().sss_hip_dist_time_level0_spmv(self.d, reps, C.byref(ms)), "dist spmv timing")
+        return ms.value
 
     def close(self):
         if self.d:

@@ -475,6 +475,28 @@ extern "C" int sss_hip_dist_residual_norm(sss_hip_dist *d, double *absres)
     return 0;
 }
 
+extern "C" int sss_hip_dist_time_level0_spmv(sss_hip_dist *d, int reps, double *avg_ms)
+{
+    DLevel &L = d->L[0];
+    hipEvent_t e0, e1;
+    SSS_HIP(hipEventCreate(&e0));
+    SSS_HIP(hipEventCreate(&e1));
+    SSS_HIP(hipStreamSynchronize(d->stream));
+    SSS_HIP(hipEventRecord(e0, d->stream));
+    for (int r = 0; r < reps; ++r) {
+        int rc = launch_spmv(L.A, SSS_HIP_SPMV_RESID, -1.0, L.x, L.b, L.wp, 0, nullptr, d->stream);
+        if (rc) return rc;
+    }
+    SSS_HIP(hipEventRecord(e1, d->stream));
+    SSS_HIP(hipEventSynchronize(e1));
+    float ms = 0.f;
+    SSS_HIP(hipEventElapsedTime(&ms, e0, e1));
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+    *avg_ms = (double)ms / reps;
+    return 0;
+}
+
 extern "C" int sss_hip_dist_sync(sss_hip_dist *d)
 {
     SSS_HIP(hipStreamSynchronize(d->stream));

@@ -15,9 +15,9 @@ Modes:
   parity     : exact GS-CF on every level + the reference CG(beta=1)+GMRES coarse solve; x is bitwise
                identical to the reference after every V-cycle (tests/test_gpu_parity.py).
 
-N > 1 (launched by torch.distributed.run): each rank solves its own replica of the workload on its
-own GPU (weak scaling, no data-path collective yet); `value` = all ranks' V-cycles / max-over-ranks
-time.  The row-partitioned RCCL version is on the DESIGN.md roadmap.
+N > 1 (launched by torch.distributed.run): one global 400^3 problem, row-partitioned over the
+ranks (sss_hip_dist_*: halos and the norm over RCCL/xGMI, levels below SSS_HIP_AGG_ROWS rows
+replicated); strong scaling, `value` = global V-cycles / max-over-ranks time.
 """
 from __future__ import annotations
 
@@ -44,7 +44,7 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=10)
     p.add_argument("--warmup", type=int, default=3)
-    p.add_argument("--n", type=int, default=400, help="grid edge per rank (400 -> 64M rows)")
+    p.add_argument("--grid", "--n", dest="n", type=int, default=400, help="grid edge (400 -> 64M rows)")
     p.add_argument("--mode", default="throughput", choices=["throughput", "parity"])
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-n", type=int, default=0, help="grid edge of the CPU sample (default: same workload)")
@@ -82,6 +82,14 @@ class Dist:
         import torch
         t = torch.tensor([v], dtype=torch.float64)
         self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
+        return float(t.item())
+
+    def min(self, v: float) -> float:
+        if self.world == 1:
+            return v
+        import torch
+        t = torch.tensor([v], dtype=torch.float64)
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.MIN)
         return float(t.item())
 
     def close(self):
@@ -124,13 +132,58 @@ def cpu_baseline_worker(H, out: dict):
     out.update(seconds=dt, coarse_seconds=ora.ora_coarse_seconds())
 
 
+class Single:
+    """N = 1: the single-GPU engine (sss_hip_hier_*)."""
+
+    def __init__(self, DH, N):
+        self.DH, self.N = DH, N
+        self.rows, self.ghosts = N, 0
+
+    def set_ones(self):
+        self.DH.upload(0, "b", np.ones(self.N))
+        self.DH.upload(0, "x", np.ones(self.N))
+
+    def set_x_ones(self):
+        self.DH.upload(0, "x", np.ones(self.N))
+
+    def cycle(self):
+        self.DH.cycle()
+
+    def residual_norm(self):
+        return self.DH.residual_norm()
+
+    def sync(self):
+        self.DH.sync()
+
+    def time_level0_spmv(self, reps):
+        return self.DH.time_level0_spmv(reps)
+
+    def close(self):
+        self.DH.close()
+
+
+class Distributed(Single):
+    """N > 1: this rank's rows of the row-partitioned engine (sss_hip_dist_*)."""
+
+    def __init__(self, DD, H):
+        self.DH = DD
+        self.rows, self.ghosts = DD.hi - DD.lo, DD.nghost0
+        rp = np.ctypeslib.as_array(H.level(0).A.row_ptr, shape=(H.level(0).A.num_rows + 1,))
+        self.nnz = int(rp[DD.hi] - rp[DD.lo])
+
+    def set_ones(self):
+        self.DH.upload("b", np.ones(self.rows))
+        self.DH.upload("x", np.ones(self.rows))
+
+    def set_x_ones(self):
+        self.DH.upload("x", np.ones(self.rows))
+
+
 def main():
     args = parse()
     D = Dist()
     import amg_amd as A
 
-    if D.world > 1:
-        os.environ["SSS_HIP_DEVICE"] = str(D.local_rank)
     n = args.n
     smoother, coarse = ("hybrid", "direct") if args.mode == "throughput" else ("exact", "krylov")
     smoother = args.mode_smoother or smoother
@@ -145,15 +198,36 @@ def main():
     nnz = H.level(0).A.num_nnzs
 
     t0 = time.perf_counter()
-    dev = D.local_rank if D.world > 1 else -1
-    DH = A.DeviceHierarchy(H, smoother=smoother, coarse=coarse, device=dev, inner=args.inner,
-                           inner_from=args.inner_from)
     inner = args.inner if args.inner is not None else int(os.environ.get("SSS_HIP_INNER", "1"))
     inner_from = args.inner_from if args.inner_from is not None else int(os.environ.get("SSS_HIP_INNER_FROM", "2"))
+    transport = None
+    if D.world == 1:
+        DH = A.DeviceHierarchy(H, smoother=smoother, coarse=coarse, device=-1, inner=args.inner,
+                               inner_from=args.inner_from)
+        eng = Single(DH, N)
+    else:
+        # row-partitioned solve over RCCL (xGMI); every rank holds the same host hierarchy
+        dev = D.local_rank % max(A.device_count(), 1)
+        comm, ok = None, 1
+        try:
+            comm = A.Comm(D.world, D.rank, "rccl", device=dev)
+        except Exception as e:  # noqa: BLE001
+            print(f"[bench] rank {D.rank}: RCCL communicator failed ({e})", file=sys.stderr, flush=True)
+            ok = 0
+        if D.min(ok) < 1:   # every rank falls back together (e.g. two ranks sharing one GPU)
+            if comm is not None:
+                comm.close()
+            print(f"[bench] rank {D.rank}: using the host transport (gloo)", file=sys.stderr, flush=True)
+            comm = A.Comm(D.world, D.rank, "host")
+            transport = "host-gloo"
+        else:
+            transport = "rccl"
+        DD = A.DistHierarchy(H, comm, smoother=smoother, coarse=coarse, device=dev, inner=args.inner,
+                             inner_from=args.inner_from)
+        eng = Distributed(DD, H)
     upload_s = time.perf_counter() - t0
-    ones = np.ones(N)
-    DH.upload(0, "b", ones)
-    DH.upload(0, "x", ones)
+    eng.set_ones()
+    DH = eng
 
     cpu = {}
     cpu_thread = None
@@ -182,15 +256,20 @@ def main():
     D.barrier()
     elapsed = D.max(t1 - t0)
     ms_per_step = elapsed * 1e3 / args.steps
-    value = D.world * args.steps / elapsed
+    value = args.steps / elapsed   # global V-cycles per second (strong scaling at N > 1)
 
-    # roofline of the dominant streaming kernel: level-0 fused residual SpMV (wp = b - A0 x)
+    # roofline of the dominant streaming kernel: level-0 fused residual SpMV (wp = b - A0 x);
+    # N > 1: rank 0's share (its rows, x with ghosts), no exchange inside the timed launches
     spmv_ms = DH.time_level0_spmv(20)
-    spmv_bytes = 12 * nnz + 4 * (N + 1) + 8 * N + 8 * N + 8 * N   # val+col, row_ptr, x, b, y
+    if D.world == 1:
+        spmv_bytes = 12 * nnz + 4 * (N + 1) + 8 * N + 8 * N + 8 * N   # val+col, row_ptr, x, b, y
+    else:
+        m, g = DH.rows, DH.ghosts
+        spmv_bytes = 12 * DH.nnz + 4 * (m + 1) + 8 * (m + g) + 8 * m + 8 * m
     achieved = spmv_bytes / (spmv_ms * 1e-3) / 1e9
 
     # iterations to tol from x0 = 1 (the CLI's problem), and time to solution
-    DH.upload(0, "x", ones)
+    DH.set_x_ones()
     sumb = float(np.sqrt(N))
     its = 0
     t0 = time.perf_counter()
@@ -207,7 +286,7 @@ def main():
 
     traffic = None
     pmc = ROOT / "profiles" / "r01_level0_spmv_pmc.json"
-    if pmc.exists():
+    if pmc.exists() and D.world == 1:
         try:
             rec = json.loads(pmc.read_text())
             if rec.get("n") == n:
@@ -231,7 +310,8 @@ def main():
     rec = {
         "metric": "V-cycle iters/sec + fine-level SpMV GB/s (%HBM peak), 64M-row 7pt Poisson",
         "value": value, "unit": "V-cycle iter/s", "n_gpus": D.world, "steps": args.steps, "warmup": args.warmup,
-        "ms_per_step": ms_per_step, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+        "ms_per_step": ms_per_step, "higher_is_better": True,
+        "scaling": "strong" if D.world > 1 else "weak", "vs_baseline": None,
         "dtype": "f64", "data": "synthetic (7-pt Poisson generated in memory, b = x0 = 1)",
         "config": {"workload": f"poisson7_{n}^3", "rows": N, "nnz": nnz, "levels": len(levels),
                    "hierarchy": [list(t) for t in levels],
@@ -240,7 +320,8 @@ def main():
                    "inner_from": inner_from if smoother != "exact" else None,
                    "iterations_to_tol": its, "final_relres": relres, "time_to_solution_s": solve_s,
                    "setup_s": setup_s, "upload_s": upload_s,
-                   "parallelism": f"replicas{D.world}" if D.world > 1 else "single-gpu"},
+                   "parallelism": f"rowpart{D.world}" if D.world > 1 else "single-gpu",
+                   "transport": transport},
         "roofline": {"bound": "hbm", "kernel": "spmv_adaptive<RESID> level 0", "achieved": achieved,
                      "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": achieved / PEAK_HBM_GBS,
                      "frac_of_copy_peak": achieved / COPY_PEAK_GBS, "avg_launch_ms": spmv_ms,

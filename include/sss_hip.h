@@ -157,6 +157,8 @@ int sss_hip_dist_cycle(sss_hip_dist *d);
 /* global ||b0 - A0 x0||_2 (one 8-byte allreduce), synchronises */
 int sss_hip_dist_residual_norm(sss_hip_dist *d, double *absres);
 int sss_hip_dist_sync(sss_hip_dist *d);
+/* average ms of `reps` local level-0 residual SpMVs (no exchange): the per-rank roofline */
+int sss_hip_dist_time_level0_spmv(sss_hip_dist *d, int reps, double *avg_ms);
 
 /* Host-only view of the partition (no device needed; used by the CPU multi-process tests).
  * which: 0 = A_l (m x (m+g)), 1 = P_l (m x next-level local), 2 = R_l (own coarse rows x (m+g)).
