@@ -75,7 +75,8 @@ class SSS_KRYLOV(C.Structure):
 class SSS_HIP_OPTS(C.Structure):
     _fields_ = [("device", C.c_int), ("smoother", C.c_int), ("coarse", C.c_int), ("row_cap", C.c_int),
                 ("use_graph", C.c_int), ("verbose", C.c_int),
-                ("inner", C.c_int), ("inner_from", C.c_int), ("relabel", C.c_int)]
+                ("inner", C.c_int), ("inner_from", C.c_int), ("relabel", C.c_int),
+                ("sorted_tiles", C.c_int), ("sum_order", C.c_int)]
 
 
 class SSS_HIP_LEVEL_INFO(C.Structure):
@@ -292,10 +293,15 @@ class DeviceHierarchy:
 
     def __init__(self, H: Hierarchy, smoother: str = "exact", coarse: str = "krylov", row_cap: int = 0,
                  device: int = -1, verbose: int = 0, relabel: int | None = None, graph: int | None = None,
-                 inner: int | None = None, inner_from: int | None = None):
+                 inner: int | None = None, inner_from: int | None = None, sorted_tiles: int | None = None,
+                 sum_order: int | None = None):
         o = SSS_HIP_OPTS()
         lib().sss_hip_opts_default(C.byref(o))
         o.smoother, o.coarse, o.row_cap, o.device, o.verbose = SMOOTH[smoother], COARSE[coarse], row_cap, device, verbose
+        if sorted_tiles is not None:
+            o.sorted_tiles = sorted_tiles
+        if sum_order is not None:
+            o.sum_order = sum_order
         if relabel is not None:
             o.relabel = relabel
         if graph is not None:
@@ -519,10 +525,15 @@ class DistHierarchy:
     """Row-partitioned device hierarchy (sss_hip_dist_*): this rank's rows of every level."""
 
     def __init__(self, H: "Hierarchy", comm: Comm, smoother: str = "hybrid", coarse: str = "direct",
-                 device: int = -1, agg_rows: int = 0, inner: int | None = None, inner_from: int | None = None):
+                 device: int = -1, agg_rows: int = 0, inner: int | None = None, inner_from: int | None = None,
+                 sorted_tiles: int | None = None, sum_order: int | None = None):
         o = SSS_HIP_OPTS()
         lib().sss_hip_opts_default(C.byref(o))
         o.smoother, o.coarse, o.device = SMOOTH[smoother], COARSE[coarse], device
+        if sorted_tiles is not None:
+            o.sorted_tiles = sorted_tiles
+        if sum_order is not None:
+            o.sum_order = sum_order
         if inner is not None:
             o.inner = inner
         if inner_from is not None:

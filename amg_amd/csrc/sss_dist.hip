@@ -325,14 +325,16 @@ extern "C" sss_hip_dist *sss_hip_dist_create(const SSS_AMG *mg, const sss_hip_op
         L.perm = P.perm;
         const int kind = level_kind_of(d->opts, l), inner = level_inner_of(d->opts, l);
         SSS_MAT Av = P.A.view();
-        if (devcsr_upload(L.A, Av, P.nF)) return fail("upload A");
-        if (smoother_build(L.sm, Av, P.mark.data(), kind, &L.A, inner, P.gcls.data())) return fail("smoother plan");
+        const int enc = level_encoding(d->opts);
+        if (devcsr_upload(L.A, Av, P.nF, enc)) return fail("upload A");
+        if (smoother_build(L.sm, Av, P.mark.data(), kind, &L.A, inner, P.gcls.data(), enc))
+            return fail("smoother plan");
         for (const auto &ps : L.sm.pass)
             if (ps.nrows > 0 && !ps.range) return fail("level needs an exact GS-CF chain across ranks (not distributed)");
         if (l + 1 == d->nagg && !tinv.empty())
             for (int &j : P.P.ci) j = tinv[j];
         SSS_MAT Pv = P.P.view(), Rv = P.R.view();
-        if (devcsr_upload(L.P, Pv) || devcsr_upload(L.R, Rv)) return fail("upload P/R");
+        if (devcsr_upload(L.P, Pv, -1, enc) || devcsr_upload(L.R, Rv, -1, enc)) return fail("upload P/R");
         const size_t nv = (size_t)(L.m + L.g);
         L.b = dev_alloc<double>(nv);
         L.x = dev_alloc<double>(nv);

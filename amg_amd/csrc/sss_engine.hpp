@@ -51,9 +51,28 @@ struct DevCSR {
     int split_blk = 0;     // index of the block starting at split_row
     bool wave_rows = false;  // long rows: wave-per-row kernels (avg nnz/row >= kWaveRowMin)
     int ngrid = 0;           // workgroups of one SpMV launch (size of a per-block partial array)
+    // Column-sorted tile staging (kEncSortedTiles; bitwise-neutral): each staging segment of the
+    // blocking -- a block's entries, or a kTileEntries chunk of a longer row -- stored sorted by
+    // column as pk = (col << kTileShift) | (stored-order position in the segment), pv = values.
+    // Products land in LDS at their stored position, so every row chain keeps the reference's
+    // order; neighbouring rows' gathers of the same x lines coalesce (measured 1.4-1.7x on the
+    // coarse levels of 7-pt 400^3, tools/lab_rows.hip).  Needs ncols <= 2^(32 - kTileShift).
+    unsigned *pk = nullptr;
+    double *pv = nullptr;
+    // kEncFreeOrder on a wave_rows matrix: rows summed in a fixed tree order (64 strided lane
+    // sums, xor-shuffle reduction) over rows stored column-sorted (within [rp, seg) and
+    // [seg, rp+1) when a segment split is given).  Deterministic but NOT the reference order.
+    bool vec_rows = false;
 };
-// split >= 0 forces a row-block boundary at that row (the F|C class boundary of a relabeled level)
-int devcsr_upload(DevCSR &d, const SSS_MAT &h, int split = -1);
+constexpr int kTileShift = 11;           // log2(kTileEntries)
+static_assert((1 << kTileShift) == kTileEntries, "tile packing");
+enum { kEncSortedTiles = 1, kEncFreeOrder = 2 };
+// split >= 0 forces a row-block boundary at that row (the F|C class boundary of a relabeled level);
+// enc: kEnc* flags; seg (kEncFreeOrder only, optional): per row, the absolute CSR position that
+// splits the row into two independently summed segments (two-stage [N_i | L_i] rows).
+int devcsr_upload(DevCSR &d, const SSS_MAT &h, int split = -1, int enc = 0, const int *seg = nullptr);
+// encoding flags a hierarchy level uses for its matrices under the options o
+int level_encoding(const sss_hip_opts &o);
 void devcsr_free(DevCSR &d);
 int build_row_blocks(const int *h_rp, int n, std::vector<int> &blk, int split = -1);
 int wave_row_min();
@@ -120,7 +139,7 @@ struct PassHooks {
     double *w0 = nullptr, *w1 = nullptr;
 };
 int smoother_build(SmootherPlan &sp, const SSS_MAT &A, const int *mark, int kind, const DevCSR *dA = nullptr,
-                   int inner = 0, const int *gcls = nullptr);
+                   int inner = 0, const int *gcls = nullptr, int enc = 0);
 void launch_ts_stage0(const DevCSR &M, int lo, const int *split, const double *b, const double *x, const double *deff,
                       double *P, double *y, hipStream_t s);
 void launch_ts_inner(const DevCSR &M, int lo, const double *deff, const double *P, const double *ycols, int col_off,

@@ -68,6 +68,8 @@ extern "C" void sss_hip_opts_default(sss_hip_opts *o)
     o->relabel = env_int("SSS_HIP_RELABEL", 1);
     o->inner = env_int("SSS_HIP_INNER", 1);
     o->inner_from = env_int("SSS_HIP_INNER_FROM", 2);
+    o->sorted_tiles = env_int("SSS_HIP_SORTED_TILES", 1);
+    o->sum_order = env_int("SSS_HIP_SUM_ORDER", 0);
     if (const char *s = getenv("SSS_HIP_SMOOTHER")) {
         std::string v(s);
         if (v == "hybrid") o->smoother = SSS_HIP_SMOOTH_HYBRID;
@@ -99,6 +101,10 @@ static int level_inner(const sss_hip_opts &o, int l)
     return level_smoother_kind(o, l) == SSS_HIP_SMOOTH_JACOBI && l >= o.inner_from ? o.inner : 0;
 }
 int sss::level_kind_of(const sss_hip_opts &o, int l) { return level_smoother_kind(o, l); }
+int sss::level_encoding(const sss_hip_opts &o)
+{
+    return (o.sorted_tiles ? kEncSortedTiles : 0) | (o.sum_order == 1 ? kEncFreeOrder : 0);
+}
 int sss::level_inner_of(const sss_hip_opts &o, int l) { return level_inner(o, l); }
 
 static void hier_release(sss_hip_hier *h)
@@ -243,20 +249,22 @@ sss_hip_hier *sss::hier_create_impl(const SSS_AMG *mg, const sss_hip_opts *o, in
         auto &L = h->L[l];
         const int n = C.A.num_rows;
         const bool rl = !L.perm.empty();
+        // the coarsest operator only feeds the coarse solver: stored order there
+        const int enc = l + 1 < h->nl ? level_encoding(h->opts) : (level_encoding(h->opts) & kEncSortedTiles);
         if (rl) {
             RelabeledCSR B;
             relabel_csr(C.A, L.perm, inv[l], B);
             SSS_MAT Av = B.view(n, C.A.num_cols);
-            if (devcsr_upload(L.A, Av, nF[l])) return fail("upload A");
+            if (devcsr_upload(L.A, Av, nF[l], enc)) return fail("upload A");
             std::vector<int> mark(n);
             for (int i = 0; i < n; ++i) mark[i] = C.cfmark.d[L.perm[i]];
             if (smoother_build(L.sm, Av, mark.data(), level_smoother_kind(h->opts, h->level_base + l), &L.A,
-                               level_inner(h->opts, h->level_base + l)))
+                               level_inner(h->opts, h->level_base + l), nullptr, enc))
                 return fail("smoother plan");
         } else {
-            if (devcsr_upload(L.A, C.A)) return fail("upload A");
-            if (l < h->nl - 1 &&
-                smoother_build(L.sm, C.A, C.cfmark.d, level_smoother_kind(h->opts, h->level_base + l)))
+            if (devcsr_upload(L.A, C.A, -1, enc)) return fail("upload A");
+            if (l < h->nl - 1 && smoother_build(L.sm, C.A, C.cfmark.d, level_smoother_kind(h->opts, h->level_base + l),
+                                                nullptr, 0, nullptr, enc))
                 return fail("smoother plan");
         }
         if (l < h->nl - 1) {
@@ -265,10 +273,10 @@ sss_hip_hier *sss::hier_create_impl(const SSS_AMG *mg, const sss_hip_opts *o, in
                 RelabeledCSR P, R;
                 relabel_csr(C.P, L.perm, inv[l + 1], P);
                 relabel_csr(C.R, pc, inv[l], R);
-                if (devcsr_upload(L.P, P.view(C.P.num_rows, C.P.num_cols)) ||
-                    devcsr_upload(L.R, R.view(C.R.num_rows, C.R.num_cols)))
+                if (devcsr_upload(L.P, P.view(C.P.num_rows, C.P.num_cols), -1, enc) ||
+                    devcsr_upload(L.R, R.view(C.R.num_rows, C.R.num_cols), -1, enc))
                     return fail("upload P/R");
-            } else if (devcsr_upload(L.P, C.P) || devcsr_upload(L.R, C.R)) {
+            } else if (devcsr_upload(L.P, C.P, -1, enc) || devcsr_upload(L.R, C.R, -1, enc)) {
                 return fail("upload P/R");
             }
         }
@@ -583,7 +591,9 @@ extern "C" int sss_hip_host_spmv(int op, double alpha, const SSS_MAT *A, const d
 {
     if (sss_hip_device_count() <= 0) return ERROR_MISC;
     HostCSR M;
-    if (devcsr_upload(M.d, *A)) return ERROR_MISC;
+    sss_hip_opts o;
+    sss_hip_opts_default(&o);   // SSS_HIP_SORTED_TILES; always the reference's summation order here
+    if (devcsr_upload(M.d, *A, -1, level_encoding(o) & kEncSortedTiles)) return ERROR_MISC;
     const size_t ny = (size_t)A->num_rows, nx = (size_t)A->num_cols;
     double *dx = dev_alloc<double>(nx), *dy = dev_alloc<double>(ny), *db = dev_alloc<double>(ny);
     int rc = 0;

@@ -44,7 +44,7 @@ static int upload_doubles(double **dst, const std::vector<double> &src)
 }
 
 int smoother_build(SmootherPlan &sp, const SSS_MAT &A, const int *mark, int kind, const DevCSR *dA, int inner,
-                   const int *gcls)
+                   const int *gcls, int enc)
 {
     const int n = A.num_rows;
     const int *rp = A.row_ptr, *ci = A.col_idx;
@@ -208,7 +208,9 @@ int smoother_build(SmootherPlan &sp, const SSS_MAT &A, const int *mark, int kind
                 return M;
             };
             SSS_MAT Mn = mk(nrp, nci, nv), Ml = mk(lrp, lci, lv);
-            if ((rc = devcsr_upload(ps.ts_nl, Mn)) || (rc = devcsr_upload(ps.ts_lo, Ml))) return rc;
+            std::vector<int> seg(split);   // absolute [N_i | L_i] cut of each row of Mn
+            if ((rc = devcsr_upload(ps.ts_nl, Mn, -1, enc, seg.data())) || (rc = devcsr_upload(ps.ts_lo, Ml, -1, enc)))
+                return rc;
             if ((rc = upload_ints(&ps.ts_split, split))) return rc;
             ps.ts_P = dev_alloc<double>((size_t)m);
             if (!ps.ts_P) return hip_fail(hipErrorOutOfMemory, "hipMalloc(P)", __FILE__, __LINE__);
@@ -341,7 +343,8 @@ __global__ __launch_bounds__(kBlock) void relax_range(int blo, const int *__rest
                                                       const int *__restrict__ diag_pos, int lo,
                                                       const double *__restrict__ b, double *x,
                                                       const double *__restrict__ yp, double *__restrict__ y,
-                                                      const double *__restrict__ deff)
+                                                      const double *__restrict__ deff, const unsigned *__restrict__ pk,
+                                                      const double *__restrict__ pv)
 {
     __shared__ SpmvSmem sm;
     const int bid = blo + blockIdx.x;
@@ -361,7 +364,7 @@ __global__ __launch_bounds__(kBlock) void relax_range(int blo, const int *__rest
         int a = 0, e = 0, dp = -1;
         double acc = 0.0;
         if (r < r1) a = rp[r] - k0, e = rp[r + 1] - k0, dp = diag_pos[r], acc = b[r];   // ahead of the tile
-        stage_products_f(sm.v, k0, k1, ci, v, fetch);
+        stage_any(sm.v, k0, k1, ci, v, pk, pv, fetch);
         __syncthreads();
         if (r < r1) {
             if (dp < 0) acc = chain_sub(acc, sm.v, a, e);
@@ -376,7 +379,7 @@ __global__ __launch_bounds__(kBlock) void relax_range(int blo, const int *__rest
         double acc = b[r];
         for (int base = k0; base < k1; base += kTileEntries) {
             const int m = min(kTileEntries, k1 - base);
-            stage_products_f(sm.v, base, base + m, ci, v, fetch);
+            stage_any(sm.v, base, base + m, ci, v, pk, pv, fetch);
             __syncthreads();
             if (threadIdx.x == 0) {
                 if (dp >= base && dp < base + m) {
@@ -394,21 +397,21 @@ __global__ __launch_bounds__(kBlock) void relax_range(int blo, const int *__rest
 
 // relax_range for long-row levels: one wave per row (rows lo + 4 * blockIdx.x + wave).  The
 // diagonal (single per row on range levels) contributes an exact 0.0 to the chain.
-template <int MODE>
+// TREE: free sum order (DevCSR::vec_rows), t = b_r - (tree sum of the off-diagonal products).
+template <int MODE, bool TREE>
 __global__ __launch_bounds__(kBlock) void relax_range_wave(int lo, int hi, const int *__restrict__ rp,
                                                            const int *__restrict__ ci, const double *__restrict__ v,
                                                            const double *__restrict__ b, double *x,
                                                            const double *__restrict__ yp, double *__restrict__ y,
                                                            const double *__restrict__ deff)
 {
-    __shared__ double strips[4][kWaveStage];
+    __shared__ double strips[TREE ? 1 : 4][TREE ? 1 : kWaveStage];
     const int wave = threadIdx.x >> 6;
     const int r = lo + blockIdx.x * 4 + wave;
     if (r >= hi) return;
-    const double acc = wave_row_chain<true>(
-        rp[r], rp[r + 1], ci, v,
-        [&](int c, double a) -> double { return c == r ? 0.0 : a * x[c]; },
-        b[r], strips[wave]);
+    auto prod = [&](int c, double a) -> double { return c == r ? 0.0 : a * x[c]; };
+    const double acc = TREE ? b[r] - wave_row_sum(rp[r], rp[r + 1], ci, v, prod)
+                            : wave_row_chain<true>(rp[r], rp[r + 1], ci, v, prod, b[r], strips[TREE ? 0 : wave]);
     if ((threadIdx.x & 63) == 0) {
         const double d = deff[r];
         if (MODE == 0) {
@@ -422,7 +425,7 @@ __global__ __launch_bounds__(kBlock) void relax_range_wave(int lo, int hi, const
 // ---- two-stage GS-CF (oracle: ora_cf_twostage) ----------------------------------------------
 // Stage 0 over the reordered pass rows [N_i | L_i] (local row q = global lo + q):
 //   P_q = b - sum_{N_i} a x;  y_q = (P_q - sum_{L_i} a x) / d   (x from before the pass)
-template <bool WAVE>
+template <int PATH>   // 0 tile, 1 wave chain, 2 wave tree (free order)
 __global__ __launch_bounds__(kBlock) void ts_stage0(int lo, DevCSR M, const int *__restrict__ split,
                                                     const double *__restrict__ b, const double *__restrict__ x,
                                                     const double *__restrict__ deff, double *__restrict__ P,
@@ -433,7 +436,19 @@ __global__ __launch_bounds__(kBlock) void ts_stage0(int lo, DevCSR M, const int 
         const double d = deff[r];
         y[q] = fabs(d) > SMALLFLOAT ? acc / d : x[r];
     };
-    if (WAVE) {
+    if constexpr (PATH == 2) {
+        const int q = blockIdx.x * 4 + (threadIdx.x >> 6);
+        if (q >= M.n) return;
+        auto prod = [&](int c, double a) { return a * x[c]; };
+        const int a = M.rp[q], sp = split[q], e = M.rp[q + 1];
+        const double Pq = b[lo + q] - wave_row_sum(a, sp, M.ci, M.v, prod);
+        const double acc = Pq - wave_row_sum(sp, e, M.ci, M.v, prod);
+        if ((threadIdx.x & 63) == 0) {
+            P[q] = Pq;
+            finish(q, acc);
+        }
+        return;
+    } else if constexpr (PATH == 1) {
         __shared__ double strips[4][kWaveStage];
         const int wave = threadIdx.x >> 6, q = blockIdx.x * 4 + wave;
         if (q >= M.n) return;
@@ -445,51 +460,52 @@ __global__ __launch_bounds__(kBlock) void ts_stage0(int lo, DevCSR M, const int 
         acc = wave_row_chain<true>(sp, e, M.ci, M.v, prod, acc, strips[wave]);
         if ((threadIdx.x & 63) == 0) finish(q, acc);
         return;
-    }
-    __shared__ SpmvSmem sm;
-    const int q0 = M.blk[blockIdx.x], q1 = M.blk[blockIdx.x + 1];
-    const int k0 = M.rp[q0], k1 = M.rp[q1];
-    if (k1 - k0 <= kTileEntries) {
-        const int q = q0 + (int)threadIdx.x;
-        int a = 0, sp = 0, e = 0;
-        double acc = 0.0;
-        if (q < q1) a = M.rp[q] - k0, sp = split[q] - k0, e = M.rp[q + 1] - k0, acc = b[lo + q];
-        stage_products(sm.v, k0, k1, M.ci, M.v, x);
-        __syncthreads();
-        if (q < q1) {
-            acc = chain_sub(acc, sm.v, a, sp);
-            P[q] = acc;
-            acc = chain_sub(acc, sm.v, sp, e);
-            finish(q, acc);
-        }
-    } else {   // one long row, chunk by chunk, thread 0 carries the chain
-        const int q = q0, sp = split[q];
-        double acc = b[lo + q];
-        for (int base = k0; base < k1; base += kTileEntries) {
-            const int m = min(kTileEntries, k1 - base);
-            stage_products(sm.v, base, base + m, M.ci, M.v, x);
+    } else {
+        __shared__ SpmvSmem sm;
+        const int q0 = M.blk[blockIdx.x], q1 = M.blk[blockIdx.x + 1];
+        const int k0 = M.rp[q0], k1 = M.rp[q1];
+        if (k1 - k0 <= kTileEntries) {
+            const int q = q0 + (int)threadIdx.x;
+            int a = 0, sp = 0, e = 0;
+            double acc = 0.0;
+            if (q < q1) a = M.rp[q] - k0, sp = split[q] - k0, e = M.rp[q + 1] - k0, acc = b[lo + q];
+            stage_any(sm.v, k0, k1, M.ci, M.v, M.pk, M.pv, [&](int c) -> double { return x[c]; });
             __syncthreads();
-            if (threadIdx.x == 0) {
-                if (sp >= base && sp < base + m) {
-                    acc = chain_sub(acc, sm.v, 0, sp - base);
-                    P[q] = acc;
-                    acc = chain_sub(acc, sm.v, sp - base, m);
-                } else {
-                    acc = chain_sub(acc, sm.v, 0, m);
-                }
+            if (q < q1) {
+                acc = chain_sub(acc, sm.v, a, sp);
+                P[q] = acc;
+                acc = chain_sub(acc, sm.v, sp, e);
+                finish(q, acc);
             }
-            __syncthreads();
-        }
-        if (threadIdx.x == 0) {
-            if (sp == k1) P[q] = acc;   // no L entries
-            finish(q, acc);
+        } else {   // one long row, chunk by chunk, thread 0 carries the chain
+            const int q = q0, sp = split[q];
+            double acc = b[lo + q];
+            for (int base = k0; base < k1; base += kTileEntries) {
+                const int m = min(kTileEntries, k1 - base);
+                stage_any(sm.v, base, base + m, M.ci, M.v, M.pk, M.pv, [&](int c) -> double { return x[c]; });
+                __syncthreads();
+                if (threadIdx.x == 0) {
+                    if (sp >= base && sp < base + m) {
+                        acc = chain_sub(acc, sm.v, 0, sp - base);
+                        P[q] = acc;
+                        acc = chain_sub(acc, sm.v, sp - base, m);
+                    } else {
+                        acc = chain_sub(acc, sm.v, 0, m);
+                    }
+                }
+                __syncthreads();
+            }
+            if (threadIdx.x == 0) {
+                if (sp == k1) P[q] = acc;   // no L entries
+                finish(q, acc);
+            }
         }
     }
 }
 
 // Inner step over the L-only rows:  y_q = (P_q - sum_{L_i} a yp[j - lo]) / d  (keeps yp_q if |d| small)
 // (column c reads ycols[c - col_off]; a row with |d| small keeps ykeep[q]; rows are lo + q)
-template <bool WAVE>
+template <int PATH>   // 0 tile, 1 wave chain, 2 wave tree (free order)
 __global__ __launch_bounds__(kBlock) void ts_inner(int lo, DevCSR M, const double *__restrict__ deff,
                                                    const double *__restrict__ P, const double *ycols, int col_off,
                                                    const double *ykeep, double *__restrict__ y)
@@ -499,7 +515,14 @@ __global__ __launch_bounds__(kBlock) void ts_inner(int lo, DevCSR M, const doubl
         const double d = deff[lo + q];
         y[q] = fabs(d) > SMALLFLOAT ? acc / d : ykeep[q];
     };
-    if (WAVE) {
+    if constexpr (PATH == 2) {
+        const int q = blockIdx.x * 4 + (threadIdx.x >> 6);
+        if (q >= M.n) return;
+        const double acc =
+            P[q] - wave_row_sum(M.rp[q], M.rp[q + 1], M.ci, M.v, [&](int c, double a) { return a * fetch(c); });
+        if ((threadIdx.x & 63) == 0) finish(q, acc);
+        return;
+    } else if constexpr (PATH == 1) {
         __shared__ double strips[4][kWaveStage];
         const int wave = threadIdx.x >> 6, q = blockIdx.x * 4 + wave;
         if (q >= M.n) return;
@@ -507,29 +530,30 @@ __global__ __launch_bounds__(kBlock) void ts_inner(int lo, DevCSR M, const doubl
             M.rp[q], M.rp[q + 1], M.ci, M.v, [&](int c, double a) { return a * fetch(c); }, P[q], strips[wave]);
         if ((threadIdx.x & 63) == 0) finish(q, acc);
         return;
-    }
-    __shared__ SpmvSmem sm;
-    const int q0 = M.blk[blockIdx.x], q1 = M.blk[blockIdx.x + 1];
-    const int k0 = M.rp[q0], k1 = M.rp[q1];
-    if (k1 - k0 <= kTileEntries) {
-        const int q = q0 + (int)threadIdx.x;
-        int a = 0, e = 0;
-        double acc = 0.0;
-        if (q < q1) a = M.rp[q] - k0, e = M.rp[q + 1] - k0, acc = P[q];
-        stage_products_f(sm.v, k0, k1, M.ci, M.v, fetch);
-        __syncthreads();
-        if (q < q1) finish(q, chain_sub(acc, sm.v, a, e));
     } else {
-        const int q = q0;
-        double acc = P[q];
-        for (int base = k0; base < k1; base += kTileEntries) {
-            const int m = min(kTileEntries, k1 - base);
-            stage_products_f(sm.v, base, base + m, M.ci, M.v, fetch);
+        __shared__ SpmvSmem sm;
+        const int q0 = M.blk[blockIdx.x], q1 = M.blk[blockIdx.x + 1];
+        const int k0 = M.rp[q0], k1 = M.rp[q1];
+        if (k1 - k0 <= kTileEntries) {
+            const int q = q0 + (int)threadIdx.x;
+            int a = 0, e = 0;
+            double acc = 0.0;
+            if (q < q1) a = M.rp[q] - k0, e = M.rp[q + 1] - k0, acc = P[q];
+            stage_any(sm.v, k0, k1, M.ci, M.v, M.pk, M.pv, fetch);
             __syncthreads();
-            if (threadIdx.x == 0) acc = chain_sub(acc, sm.v, 0, m);
-            __syncthreads();
+            if (q < q1) finish(q, chain_sub(acc, sm.v, a, e));
+        } else {
+            const int q = q0;
+            double acc = P[q];
+            for (int base = k0; base < k1; base += kTileEntries) {
+                const int m = min(kTileEntries, k1 - base);
+                stage_any(sm.v, base, base + m, M.ci, M.v, M.pk, M.pv, fetch);
+                __syncthreads();
+                if (threadIdx.x == 0) acc = chain_sub(acc, sm.v, 0, m);
+                __syncthreads();
+            }
+            if (threadIdx.x == 0) finish(q, acc);
         }
-        if (threadIdx.x == 0) finish(q, acc);
     }
 }
 
@@ -537,22 +561,24 @@ void launch_ts_stage0(const DevCSR &M, int lo, const int *split, const double *b
                       double *P, double *y, hipStream_t s)
 {
     if (M.n == 0) return;
-    if (M.wave_rows)
-        hipLaunchKernelGGL(ts_stage0<true>, dim3(M.ngrid), dim3(kBlock), 0, s, lo, M, split, b, x, deff, P, y);
+    if (M.vec_rows)
+        hipLaunchKernelGGL(ts_stage0<2>, dim3(M.ngrid), dim3(kBlock), 0, s, lo, M, split, b, x, deff, P, y);
+    else if (M.wave_rows)
+        hipLaunchKernelGGL(ts_stage0<1>, dim3(M.ngrid), dim3(kBlock), 0, s, lo, M, split, b, x, deff, P, y);
     else
-        hipLaunchKernelGGL(ts_stage0<false>, dim3(M.nblk), dim3(kBlock), 0, s, lo, M, split, b, x, deff, P, y);
+        hipLaunchKernelGGL(ts_stage0<0>, dim3(M.nblk), dim3(kBlock), 0, s, lo, M, split, b, x, deff, P, y);
 }
 
 void launch_ts_inner(const DevCSR &M, int lo, const double *deff, const double *P, const double *ycols, int col_off,
                      const double *ykeep, double *y, hipStream_t s)
 {
     if (M.n == 0) return;
-    if (M.wave_rows)
-        hipLaunchKernelGGL(ts_inner<true>, dim3(M.ngrid), dim3(kBlock), 0, s, lo, M, deff, P, ycols, col_off, ykeep,
-                           y);
+    if (M.vec_rows)
+        hipLaunchKernelGGL(ts_inner<2>, dim3(M.ngrid), dim3(kBlock), 0, s, lo, M, deff, P, ycols, col_off, ykeep, y);
+    else if (M.wave_rows)
+        hipLaunchKernelGGL(ts_inner<1>, dim3(M.ngrid), dim3(kBlock), 0, s, lo, M, deff, P, ycols, col_off, ykeep, y);
     else
-        hipLaunchKernelGGL(ts_inner<false>, dim3(M.nblk), dim3(kBlock), 0, s, lo, M, deff, P, ycols, col_off, ykeep,
-                           y);
+        hipLaunchKernelGGL(ts_inner<0>, dim3(M.nblk), dim3(kBlock), 0, s, lo, M, deff, P, ycols, col_off, ykeep, y);
 }
 
 __global__ __launch_bounds__(kBlock) void scatter_rows(int m, const int *__restrict__ map, const double *__restrict__ y,
@@ -582,12 +608,15 @@ int smoother_run(const SmootherPlan &sp, const DevCSR &A, const double *b, doubl
                 const bool wave = A.wave_rows;
                 auto relax = [&](auto mode, const int *cols, const double *yp, double *y) {
                     constexpr int M = decltype(mode)::value;
-                    if (wave)
-                        hipLaunchKernelGGL(relax_range_wave<M>, dim3(nw), dim3(kBlock), 0, s, ps.lo, ps.hi, A.rp, cols,
-                                           A.v, b, x, yp, y, deff);
+                    if (wave && A.vec_rows)
+                        hipLaunchKernelGGL((relax_range_wave<M, true>), dim3(nw), dim3(kBlock), 0, s, ps.lo, ps.hi,
+                                           A.rp, cols, A.v, b, x, yp, y, deff);
+                    else if (wave)
+                        hipLaunchKernelGGL((relax_range_wave<M, false>), dim3(nw), dim3(kBlock), 0, s, ps.lo, ps.hi,
+                                           A.rp, cols, A.v, b, x, yp, y, deff);
                     else
                         hipLaunchKernelGGL(relax_range<M>, dim3(nb), dim3(kBlock), 0, s, ps.blo, A.blk, A.rp, cols,
-                                           A.v, sp.diag_pos, ps.lo, b, x, yp, y, deff);
+                                           A.v, sp.diag_pos, ps.lo, b, x, yp, y, deff, A.pk, A.pv);
                 };
                 if (sp.kind == SSS_HIP_SMOOTH_JACOBI && sp.inner > 0 && hk) {
                     // iterates live in full-length work vectors whose ghosts (lower-rank rows of

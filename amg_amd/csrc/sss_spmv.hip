@@ -55,19 +55,82 @@ int build_row_blocks(const int *h_rp, int n, std::vector<int> &blk, int split)
     return (int)blk.size() - 1;
 }
 
-int devcsr_upload(DevCSR &d, const SSS_MAT &h, int split)
+// Sorted tile segments of a blocking: a block's entries, or kTileEntries chunks of a long row
+// (exactly the segments the tile kernels stage, sss_spmv_dev.hpp csr_block_rows).
+static void build_sorted_tiles(const SSS_MAT &h, const std::vector<int> &blk, std::vector<unsigned> &pk,
+                               std::vector<double> &pv)
+{
+    const int *rp = h.row_ptr, *ci = h.col_idx;
+    const int nb = (int)blk.size() - 1;
+    pk.resize((size_t)h.num_nnzs);
+    pv.resize((size_t)h.num_nnzs);
+#pragma omp parallel
+    {
+        std::vector<int> idx;
+#pragma omp for schedule(dynamic, 256)
+        for (int q = 0; q < nb; ++q) {
+            const int a0 = rp[blk[q]], e0 = rp[blk[q + 1]];
+            for (int a = a0; a < e0; a += kTileEntries) {
+                const int e = std::min(e0, a + kTileEntries);
+                idx.resize((size_t)(e - a));
+                for (int t = 0; t < e - a; ++t) idx[t] = a + t;
+                std::stable_sort(idx.begin(), idx.end(), [&](int p, int r) { return ci[p] < ci[r]; });
+                for (int t = 0; t < e - a; ++t) {
+                    pk[(size_t)a + t] = ((unsigned)ci[idx[t]] << kTileShift) | (unsigned)(idx[t] - a);
+                    pv[(size_t)a + t] = h.val[idx[t]];
+                }
+            }
+        }
+    }
+}
+
+// Rows of a free-order (tree-summed) matrix, stored column-sorted within each segment.
+static void sort_row_segments(const SSS_MAT &h, const int *seg, std::vector<int> &ci, std::vector<double> &v)
+{
+    const int n = h.num_rows;
+    const int *rp = h.row_ptr;
+    ci.resize((size_t)h.num_nnzs);
+    v.resize((size_t)h.num_nnzs);
+#pragma omp parallel
+    {
+        std::vector<int> idx;
+#pragma omp for schedule(dynamic, 64)
+        for (int r = 0; r < n; ++r) {
+            const int cut[3] = {rp[r], seg ? seg[r] : rp[r + 1], rp[r + 1]};
+            for (int part = 0; part < 2; ++part) {
+                const int a = cut[part], e = cut[part + 1];
+                idx.resize((size_t)std::max(0, e - a));
+                for (int t = 0; t < e - a; ++t) idx[t] = a + t;
+                std::stable_sort(idx.begin(), idx.end(), [&](int p, int q) { return h.col_idx[p] < h.col_idx[q]; });
+                for (int t = 0; t < e - a; ++t) ci[(size_t)a + t] = h.col_idx[idx[t]], v[(size_t)a + t] = h.val[idx[t]];
+            }
+        }
+    }
+}
+
+int devcsr_upload(DevCSR &d, const SSS_MAT &h, int split, int enc, const int *seg)
 {
     d.n = h.num_rows;
     d.ncols = h.num_cols;
     d.nnz = h.num_nnzs;
+    d.wave_rows = d.n > 0 && (long long)d.nnz >= (long long)wave_row_min() * d.n;
+    d.vec_rows = d.wave_rows && (enc & kEncFreeOrder);
     d.rp = dev_alloc<int>((size_t)d.n + 1);
     d.ci = dev_alloc<int>((size_t)d.nnz);
     d.v = dev_alloc<double>((size_t)d.nnz);
     if (!d.rp || !d.ci || !d.v) return hip_fail(hipErrorOutOfMemory, "hipMalloc(CSR)", __FILE__, __LINE__);
     SSS_HIP(hipMemcpy(d.rp, h.row_ptr, sizeof(int) * ((size_t)d.n + 1), hipMemcpyHostToDevice));
     if (d.nnz > 0) {
-        SSS_HIP(hipMemcpy(d.ci, h.col_idx, sizeof(int) * (size_t)d.nnz, hipMemcpyHostToDevice));
-        SSS_HIP(hipMemcpy(d.v, h.val, sizeof(double) * (size_t)d.nnz, hipMemcpyHostToDevice));
+        if (d.vec_rows) {
+            std::vector<int> sci;
+            std::vector<double> sv;
+            sort_row_segments(h, seg, sci, sv);
+            SSS_HIP(hipMemcpy(d.ci, sci.data(), sizeof(int) * (size_t)d.nnz, hipMemcpyHostToDevice));
+            SSS_HIP(hipMemcpy(d.v, sv.data(), sizeof(double) * (size_t)d.nnz, hipMemcpyHostToDevice));
+        } else {
+            SSS_HIP(hipMemcpy(d.ci, h.col_idx, sizeof(int) * (size_t)d.nnz, hipMemcpyHostToDevice));
+            SSS_HIP(hipMemcpy(d.v, h.val, sizeof(double) * (size_t)d.nnz, hipMemcpyHostToDevice));
+        }
     }
     std::vector<int> blk;
     d.nblk = build_row_blocks(h.row_ptr, d.n, blk, split);
@@ -79,8 +142,19 @@ int devcsr_upload(DevCSR &d, const SSS_MAT &h, int split)
     d.blk = dev_alloc<int>(blk.size());
     if (!d.blk) return hip_fail(hipErrorOutOfMemory, "hipMalloc(blk)", __FILE__, __LINE__);
     SSS_HIP(hipMemcpy(d.blk, blk.data(), sizeof(int) * blk.size(), hipMemcpyHostToDevice));
-    d.wave_rows = d.n > 0 && (long long)d.nnz >= (long long)wave_row_min() * d.n;
     d.ngrid = d.wave_rows ? (d.n + 3) / 4 : d.nblk;
+    // the tile kernels of a wave_rows matrix never run on the hierarchy; no sorted copy for them
+    if ((enc & kEncSortedTiles) && !d.wave_rows && d.nnz > 0 &&
+        (unsigned long long)std::max(d.ncols, 1) <= (1ull << (32 - kTileShift))) {
+        std::vector<unsigned> pk;
+        std::vector<double> pv;
+        build_sorted_tiles(h, blk, pk, pv);
+        d.pk = dev_alloc<unsigned>((size_t)d.nnz);
+        d.pv = dev_alloc<double>((size_t)d.nnz);
+        if (!d.pk || !d.pv) return hip_fail(hipErrorOutOfMemory, "hipMalloc(sorted tiles)", __FILE__, __LINE__);
+        SSS_HIP(hipMemcpy(d.pk, pk.data(), sizeof(unsigned) * (size_t)d.nnz, hipMemcpyHostToDevice));
+        SSS_HIP(hipMemcpy(d.pv, pv.data(), sizeof(double) * (size_t)d.nnz, hipMemcpyHostToDevice));
+    }
     return 0;
 }
 
@@ -90,6 +164,8 @@ void devcsr_free(DevCSR &d)
     dev_free(d.ci);
     dev_free(d.v);
     dev_free(d.blk);
+    dev_free(d.pk);
+    dev_free(d.pv);
     d = DevCSR();
 }
 
@@ -99,7 +175,8 @@ __global__ __launch_bounds__(kBlock) void spmv_adaptive(const int *__restrict__ 
                                                         const int *__restrict__ ci, const double *__restrict__ v,
                                                         const double *__restrict__ x, const double *__restrict__ b,
                                                         double *__restrict__ y, double alpha, int cap,
-                                                        double *__restrict__ partial)
+                                                        double *__restrict__ partial, const unsigned *__restrict__ pk,
+                                                        const double *__restrict__ pv)
 {
     __shared__ SpmvSmem sm;
     const double sq = csr_block_rows(blk, rp, ci, v, x, sm, [&](int r, double s) -> double {
@@ -113,27 +190,30 @@ __global__ __launch_bounds__(kBlock) void spmv_adaptive(const int *__restrict__ 
         }
         y[r] = out;
         return NORM ? out * out : 0.0;
-    });
+    }, pk, pv);
     if (NORM) {
         const double t = block_sum(sq, sm.red);
         if (threadIdx.x == 0) partial[blockIdx.x] = t;
     }
 }
 
-template <int OP, bool NORM>
+// Long rows: one wave per row.  TREE = false: lane 0 chains the products in stored order
+// (bitwise); TREE = true: free-order tree sum (DevCSR::vec_rows).
+template <int OP, bool NORM, bool TREE>
 __global__ __launch_bounds__(kBlock) void spmv_wave(int n, const int *__restrict__ rp, const int *__restrict__ ci,
                                                     const double *__restrict__ v, const double *__restrict__ x,
                                                     const double *__restrict__ b, double *__restrict__ y, double alpha,
                                                     int cap, double *__restrict__ partial)
 {
-    __shared__ double strips[4][kWaveStage];
+    __shared__ double strips[TREE ? 1 : 4][TREE ? 1 : kWaveStage];
     __shared__ double red[kBlock / 64];
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int r = blockIdx.x * 4 + wave;
     double sq = 0.0;
     if (r < n) {
-        const double s = wave_row_chain<false>(rp[r], rp[r + 1], ci, v,
-                                               [&](int c, double a) { return a * x[c]; }, 0.0, strips[wave]);
+        auto prod = [&](int c, double a) { return a * x[c]; };
+        const double s = TREE ? wave_row_sum(rp[r], rp[r + 1], ci, v, prod)
+                              : wave_row_chain<false>(rp[r], rp[r + 1], ci, v, prod, 0.0, strips[TREE ? 0 : wave]);
         if (lane == 0) {
             bool write = true;
             double out;
@@ -158,12 +238,15 @@ template <int OP, bool NORM>
 static void launch_op(const DevCSR &A, double alpha, const double *x, const double *b, double *y, int cap,
                       double *partial, hipStream_t s)
 {
-    if (A.wave_rows)
-        hipLaunchKernelGGL((spmv_wave<OP, NORM>), dim3(A.ngrid), dim3(kBlock), 0, s, A.n, A.rp, A.ci, A.v, x, b, y,
-                           alpha, cap, partial);
+    if (A.vec_rows)
+        hipLaunchKernelGGL((spmv_wave<OP, NORM, true>), dim3(A.ngrid), dim3(kBlock), 0, s, A.n, A.rp, A.ci, A.v, x,
+                           b, y, alpha, cap, partial);
+    else if (A.wave_rows)
+        hipLaunchKernelGGL((spmv_wave<OP, NORM, false>), dim3(A.ngrid), dim3(kBlock), 0, s, A.n, A.rp, A.ci, A.v, x,
+                           b, y, alpha, cap, partial);
     else
         hipLaunchKernelGGL((spmv_adaptive<OP, NORM>), dim3(A.nblk), dim3(kBlock), 0, s, A.blk, A.rp, A.ci, A.v, x,
-                           b, y, alpha, cap, partial);
+                           b, y, alpha, cap, partial, A.pk, A.pv);
 }
 
 int launch_spmv(const DevCSR &A, int op, double alpha, const double *x, const double *b, double *y, int cap,

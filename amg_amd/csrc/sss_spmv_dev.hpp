@@ -121,6 +121,42 @@ __device__ __forceinline__ void stage_products_f(double *__restrict__ sm, int k0
     }
 }
 
+// Column-sorted staging (DevCSR::pk/pv): slot k of the segment [k0, k1) holds the entry packed as
+// (col << kTileShift) | pos, pos = its stored-order position in the segment; the product goes to
+// sm[pos], so the LDS image is exactly stage_products_f's and every chain over it is unchanged.
+template <class Fetch>
+__device__ __forceinline__ void stage_sorted(double *__restrict__ sm, int k0, int k1, const unsigned *__restrict__ pk,
+                                             const double *__restrict__ pv, Fetch fetch)
+{
+    constexpr int U = 8;
+    constexpr unsigned kMask = kTileEntries - 1;
+    for (int kb = k0 + (int)threadIdx.x; kb < k1; kb += U * kBlock) {
+        unsigned q[U];
+        double a[U], xv[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int k = kb + u * kBlock;
+            q[u] = k < k1 ? pk[k] : 0u;
+            a[u] = k < k1 ? pv[k] : 0.0;
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) xv[u] = kb + u * kBlock < k1 ? fetch((int)(q[u] >> kTileShift)) : 0.0;
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            if (kb + u * kBlock < k1) sm[q[u] & kMask] = a[u] * xv[u];
+    }
+}
+
+// Stage the products of segment [k0, k1): from the sorted copy when the matrix has one.
+template <class Fetch>
+__device__ __forceinline__ void stage_any(double *__restrict__ sm, int k0, int k1, const int *__restrict__ ci,
+                                          const double *__restrict__ v, const unsigned *__restrict__ pk,
+                                          const double *__restrict__ pv, Fetch fetch)
+{
+    if (pk) stage_sorted(sm, k0, k1, pk, pv, fetch);
+    else stage_products_f(sm, k0, k1, ci, v, fetch);
+}
+
 // Returns this thread's summed epilogue contribution (0 for idle threads).
 // Phase 1: every thread of the workgroup forms products of the tile (coalesced val/col loads,
 // independent x gathers, all in flight).  Phase 2: one thread per row adds its products from
@@ -129,8 +165,11 @@ __device__ __forceinline__ void stage_products_f(double *__restrict__ sm, int k0
 template <class Epi>
 __device__ __forceinline__ double csr_block_rows(const int *__restrict__ blk, const int *__restrict__ rp,
                                                  const int *__restrict__ ci, const double *__restrict__ v,
-                                                 const double *__restrict__ x, SpmvSmem &sm, Epi epi)
+                                                 const double *__restrict__ x, SpmvSmem &sm, Epi epi,
+                                                 const unsigned *__restrict__ pk = nullptr,
+                                                 const double *__restrict__ pv = nullptr)
 {
+    auto fetch = [&](int c) -> double { return x[c]; };
     const int r0 = blk[blockIdx.x], r1 = blk[blockIdx.x + 1];
     const int k0 = rp[r0], k1 = rp[r1];
     const int cnt = k1 - k0;
@@ -139,7 +178,8 @@ __device__ __forceinline__ double csr_block_rows(const int *__restrict__ blk, co
         const int r = r0 + (int)threadIdx.x;
         int ra = 0, re = 0;
         if (r < r1) ra = rp[r], re = rp[r + 1];   // issued ahead of the tile
-        stage_products(sm.v, k0, k1, ci, v, x);
+        if (pk) stage_sorted(sm.v, k0, k1, pk, pv, fetch);
+        else stage_products(sm.v, k0, k1, ci, v, x);
         __syncthreads();
         if (r < r1) {
             const double s = chain_add(0.0, sm.v, ra - k0, re - k0);
@@ -149,7 +189,8 @@ __device__ __forceinline__ double csr_block_rows(const int *__restrict__ blk, co
         double s = 0.0;
         for (int base = k0; base < k1; base += kTileEntries) {
             const int m = min(kTileEntries, k1 - base);
-            stage_products(sm.v, base, base + m, ci, v, x);
+            if (pk) stage_sorted(sm.v, base, base + m, pk, pv, fetch);
+            else stage_products(sm.v, base, base + m, ci, v, x);
             __syncthreads();
             if (threadIdx.x == 0) s = chain_add(s, sm.v, 0, m);
             __syncthreads();
@@ -250,6 +291,38 @@ __device__ __forceinline__ double wave_row_chain(int k0, int k1, const int *__re
         wave_sync();
     }
     return acc;
+}
+
+// Free sum order (DevCSR::vec_rows): sum_k prod(col_k, val_k) over [k0, k1) by the whole wave --
+// lane l takes entries k0 + l + 64 t (two interleaved accumulators, four loads in flight), then an
+// xor-butterfly.  Fixed order, so deterministic; valid in every lane.
+template <class Prod>
+__device__ __forceinline__ double wave_row_sum(int k0, int k1, const int *__restrict__ ci,
+                                               const double *__restrict__ v, Prod prod)
+{
+    constexpr int U = 4;
+    const int lane = threadIdx.x & 63;
+    double s0 = 0.0, s1 = 0.0;
+    for (int k = k0 + lane; k < k1; k += 64 * U) {
+        int c[U];
+        double a[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int kk = k + 64 * u;
+            c[u] = kk < k1 ? ci[kk] : -1;
+            a[u] = kk < k1 ? v[kk] : 0.0;
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const double p = c[u] >= 0 ? prod(c[u], a[u]) : 0.0;
+            if (u & 1) s1 += p;
+            else s0 += p;
+        }
+    }
+    double s = s0 + s1;
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off, 64);
+    return s;
 }
 
 }  // namespace sss

@@ -55,6 +55,10 @@ def parse():
     p.add_argument("--inner-from", type=int, default=None,
                    help="first level with the two-stage form (default: SSS_HIP_INNER_FROM or 2)")
     p.add_argument("--converge-max", type=int, default=100, help="max V-cycles of the iterations-to-tol run (0: skip)")
+    p.add_argument("--sum-order", type=int, default=None,
+                   help="0: stored CSR order everywhere (bitwise kernels); 1: tree-summed long rows "
+                        "(default: 1 in throughput mode, 0 in parity mode)")
+    p.add_argument("--sorted-tiles", type=int, default=None, help="column-sorted tile staging (default 1)")
     return p.parse_args()
 
 
@@ -188,6 +192,8 @@ def main():
     smoother, coarse = ("hybrid", "direct") if args.mode == "throughput" else ("exact", "krylov")
     smoother = args.mode_smoother or smoother
     coarse = args.mode_coarse or coarse
+    sum_order = args.sum_order if args.sum_order is not None else (1 if args.mode == "throughput" else 0)
+    sorted_tiles = args.sorted_tiles if args.sorted_tiles is not None else int(os.environ.get("SSS_HIP_SORTED_TILES", "1"))
 
     t0 = time.perf_counter()
     M = A.generate(7, n)
@@ -203,7 +209,7 @@ def main():
     transport = None
     if D.world == 1:
         DH = A.DeviceHierarchy(H, smoother=smoother, coarse=coarse, device=-1, inner=args.inner,
-                               inner_from=args.inner_from)
+                               inner_from=args.inner_from, sum_order=sum_order, sorted_tiles=sorted_tiles)
         eng = Single(DH, N)
     else:
         # row-partitioned solve over RCCL (xGMI); every rank holds the same host hierarchy
@@ -223,7 +229,7 @@ def main():
         else:
             transport = "rccl"
         DD = A.DistHierarchy(H, comm, smoother=smoother, coarse=coarse, device=dev, inner=args.inner,
-                             inner_from=args.inner_from)
+                             inner_from=args.inner_from, sum_order=sum_order, sorted_tiles=sorted_tiles)
         eng = Distributed(DD, H)
     upload_s = time.perf_counter() - t0
     eng.set_ones()
@@ -318,6 +324,8 @@ def main():
                    "mode": args.mode, "smoother": smoother, "coarse": coarse,
                    "inner": inner if smoother != "exact" else None,
                    "inner_from": inner_from if smoother != "exact" else None,
+                   "sum_order": "tree (long rows)" if sum_order == 1 else "stored CSR order",
+                   "sorted_tiles": bool(sorted_tiles),
                    "iterations_to_tol": its, "final_relres": relres, "time_to_solution_s": solve_s,
                    "setup_s": setup_s, "upload_s": upload_s,
                    "parallelism": f"rowpart{D.world}" if D.world > 1 else "single-gpu",

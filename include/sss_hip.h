@@ -48,11 +48,19 @@ typedef struct sss_hip_opts {
     int inner_from;    /* first level that uses the two-stage form (plain C/F-Jacobi above it) */
     int relabel;       /* renumber levels F-first/C-second on the device (bitwise-neutral):
                           0 off, 1 every level but the coarsest, 2 as 1 but level 0 kept */
+    int sorted_tiles;  /* store each SpMV/relaxation staging tile column-sorted with its stored
+                          positions (x gathers coalesce across rows; sums unchanged, bitwise) */
+    int sum_order;     /* 0: every row sum in the reference's stored CSR order (bitwise);
+                          1: rows of long-row levels (>= SSS_HIP_WAVE_MIN entries on average)
+                          summed by a wave in a fixed tree order over column-sorted rows --
+                          deterministic, within the reordered-summation bound of the reference,
+                          not bitwise (throughput mode) */
 } sss_hip_opts;
 
 /* Defaults, overridable by environment: SSS_HIP_SMOOTHER=exact|hybrid|jacobi,
  * SSS_HIP_COARSE=krylov|direct, SSS_HIP_ROWCAP=<n>, SSS_HIP_GRAPH=0|1, SSS_HIP_DEVICE=<n>,
  * SSS_HIP_VERBOSE=0|1, SSS_HIP_RELABEL=0|1|2 (default 1), SSS_HIP_INNER=<k> (default 1),
+ * SSS_HIP_SORTED_TILES=0|1 (default 1), SSS_HIP_SUM_ORDER=0|1 (default 0),
  * SSS_HIP_INNER_FROM=<level> (default 2). */
 void sss_hip_opts_default(sss_hip_opts *o);
 

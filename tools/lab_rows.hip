@@ -5,6 +5,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
+#include <algorithm>
 #include <vector>
 
 namespace {
@@ -23,6 +24,33 @@ __device__ __forceinline__ double chain_sub(double s, const double *p, int a, in
 }
 
 // tile: <= 256 rows / <= 2048 entries per block, products staged by all threads, one thread per row
+// chain with the next 8 LDS reads in flight while the current 8 are subtracted
+__device__ __forceinline__ double chain_sub_pipe(double s, const double *p, int a, int e)
+{
+    int k = a;
+    if (e - a >= 16) {
+        double c0 = p[k], c1 = p[k + 1], c2 = p[k + 2], c3 = p[k + 3];
+        double c4 = p[k + 4], c5 = p[k + 5], c6 = p[k + 6], c7 = p[k + 7];
+        for (; k + 16 <= e; k += 8) {
+            const double n0 = p[k + 8], n1 = p[k + 9], n2 = p[k + 10], n3 = p[k + 11];
+            const double n4 = p[k + 12], n5 = p[k + 13], n6 = p[k + 14], n7 = p[k + 15];
+            s -= c0; s -= c1; s -= c2; s -= c3; s -= c4; s -= c5; s -= c6; s -= c7;
+            c0 = n0, c1 = n1, c2 = n2, c3 = n3, c4 = n4, c5 = n5, c6 = n6, c7 = n7;
+        }
+        s -= c0; s -= c1; s -= c2; s -= c3; s -= c4; s -= c5; s -= c6; s -= c7;
+        k += 8;
+    }
+    for (; k < e; ++k) s -= p[k];
+    return s;
+}
+
+template <bool PIPE>
+__device__ __forceinline__ double chain_x(double s, const double *p, int a, int e)
+{
+    return PIPE ? chain_sub_pipe(s, p, a, e) : chain_sub(s, p, a, e);
+}
+
+template <bool PIPE = false>
 __global__ __launch_bounds__(kB) void k_tile(const int *blk, const int *rp, const int *ci, const double *v,
                                              const double *x, const double *b, double *y)
 {
@@ -47,14 +75,14 @@ __global__ __launch_bounds__(kB) void k_tile(const int *blk, const int *rp, cons
         }
         __syncthreads();
         const int r = r0 + threadIdx.x;
-        if (r < r1) y[r] = chain_sub(b[r], sm, rp[r] - k0, rp[r + 1] - k0);
+        if (r < r1) y[r] = chain_x<PIPE>(b[r], sm, rp[r] - k0, rp[r + 1] - k0);
     } else {
         double acc = b[r0];
         for (int base = k0; base < k1; base += 2048) {
             const int m = min(2048, k1 - base);
             for (int k = threadIdx.x; k < m; k += kB) sm[k] = v[base + k] * x[ci[base + k]];
             __syncthreads();
-            if (threadIdx.x == 0) acc = chain_sub(acc, sm, 0, m);
+            if (threadIdx.x == 0) acc = chain_x<PIPE>(acc, sm, 0, m);
             __syncthreads();
         }
         if (threadIdx.x == 0) y[r0] = acc;
@@ -104,7 +132,7 @@ __global__ __launch_bounds__(kB) void k_wave(int n, const int *rp, const int *ci
 }
 
 // wave per row with the next strip's loads issued before the current strip's chain
-template <int S>
+template <int S, bool PIPE = false>
 __global__ __launch_bounds__(kB) void k_wave_db(int n, const int *rp, const int *ci, const double *v, const double *x,
                                                 const double *b, double *y)
 {
@@ -138,7 +166,7 @@ __global__ __launch_bounds__(kB) void k_wave_db(int n, const int *rp, const int 
             if (lane + 64 * u < m) st[lane + 64 * u] = p[u];
         wsync();
         if (base + S < k1) load(base + S);   // in flight during the chain
-        if (lane == 0) acc = chain_sub(acc, st, 0, m);
+        if (lane == 0) acc = chain_x<PIPE>(acc, st, 0, m);
         wsync();
     }
     if (lane == 0) y[r] = acc;
@@ -183,9 +211,258 @@ __global__ __launch_bounds__(kB) void k_mrow(int n, const int *rp, const int *ci
     if (sub == 0 && r < n) y[r] = acc;
 }
 
+
+// lane per row, K entries of every row per chunk: the wave's 4*16 lanes... each of the 64 lanes
+// owns one row.  Loads are coalesced across rows (K consecutive entries of a row per K lanes),
+// products land in LDS at [row][k] (stride K+1: conflict-free column reads), then every lane
+// chains its own row's K products.  PF: the next chunk's products are formed in registers
+// before the current chunk is chained.
+template <int K, bool PF>
+__global__ __launch_bounds__(kB) void k_lanerow(int n, const int *rp, const int *ci, const double *v,
+                                                const double *x, const double *b, double *y)
+{
+    constexpr int U = K;                 // entries per lane per chunk (64 rows * K / 64 lanes)
+    constexpr int RPI = 64 / K;          // rows covered by one load instruction
+    __shared__ double st[4][64 * (K + 1)];
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int rbase = (blockIdx.x * 4 + w) * 64;
+    const int r = rbase + lane;
+    int k0 = 0, k1 = 0;
+    double acc = 0.0;
+    if (r < n) k0 = rp[r], k1 = rp[r + 1], acc = b[r];
+    const int len = k1 - k0;
+    int mx = len;
+    for (int off = 32; off > 0; off >>= 1) mx = max(mx, __shfl_xor(mx, off, 64));
+    // load mapping: instruction u covers rows u*RPI + lane/K, entry lane%K of the chunk
+    const int sub = lane % K;
+    int ls[U], ll[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const int rr = u * RPI + lane / K;
+        ls[u] = __shfl(k0, rr, 64);
+        ll[u] = __shfl(len, rr, 64);
+    }
+    double *sw = st[w];
+    double p[U];
+    auto load = [&](int c) {
+        int j[U];
+        double a[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int q = c + sub;
+            j[u] = q < ll[u] ? ci[ls[u] + q] : -1;
+            a[u] = q < ll[u] ? v[ls[u] + q] : 0.0;
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) p[u] = j[u] >= 0 ? a[u] * x[j[u]] : 0.0;
+    };
+    if (PF && mx > 0) load(0);
+    for (int c = 0; c < mx; c += K) {
+        if (!PF) load(c);
+#pragma unroll
+        for (int u = 0; u < U; ++u) sw[(u * RPI + lane / K) * (K + 1) + sub] = p[u];
+        wsync();
+        if (PF && c + K < mx) load(c + K);
+        const int e = min(K, len - c);
+        const double *row = sw + lane * (K + 1);
+        for (int k = 0; k < e; ++k) acc -= row[k];
+        wsync();
+    }
+    if (r < n) y[r] = acc;
+}
+
+// tile with column-sorted staging: within each staged segment (the block's tile, or a 2048 chunk
+// of a long row) entries are stored sorted by column, packed (col << 11) | pos, pos = stored-order
+// position in the segment; products land at their stored position, the chain is unchanged
+template <bool PIPE = false>
+__global__ __launch_bounds__(kB) void k_tile_sorted(const int *blk, const int *rp, const int *pk, const double *v,
+                                                    const double *x, const double *b, double *y)
+{
+    __shared__ double sm[2048];
+    const int r0 = blk[blockIdx.x], r1 = blk[blockIdx.x + 1];
+    const int k0 = rp[r0], k1 = rp[r1];
+    if (k1 - k0 <= 2048) {
+        const int r = r0 + threadIdx.x;
+        int ra = 0, re = 0;
+        double br = 0.0;
+        if (r < r1) ra = rp[r], re = rp[r + 1], br = b[r];
+        for (int kb = k0 + threadIdx.x; kb < k1; kb += 8 * kB) {
+            int j[8];
+            double a[8], xv[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                const int k = kb + u * kB;
+                j[u] = k < k1 ? pk[k] : 0;
+                a[u] = k < k1 ? v[k] : 0.0;
+            }
+#pragma unroll
+            for (int u = 0; u < 8; ++u) xv[u] = x[j[u] >> 11];
+#pragma unroll
+            for (int u = 0; u < 8; ++u)
+                if (kb + u * kB < k1) sm[j[u] & 2047] = a[u] * xv[u];
+        }
+        __syncthreads();
+        if (r < r1) y[r] = chain_x<PIPE>(br, sm, ra - k0, re - k0);
+    } else {
+        double acc = b[r0];
+        for (int base = k0; base < k1; base += 2048) {
+            const int m = min(2048, k1 - base);
+            for (int k = threadIdx.x; k < m; k += kB) {
+                const int q = pk[base + k];
+                sm[q & 2047] = v[base + k] * x[q >> 11];
+            }
+            __syncthreads();
+            if (threadIdx.x == 0) acc = chain_x<PIPE>(acc, sm, 0, m);
+            __syncthreads();
+        }
+        if (threadIdx.x == 0) y[r0] = acc;
+    }
+}
+
+// wave per row (as k_wave_db<256>) with each 256-entry strip column-sorted, packed (col << 8) | pos
+__global__ __launch_bounds__(kB) void k_wave_sorted(int n, const int *rp, const int *pk, const double *v,
+                                                    const double *x, const double *b, double *y)
+{
+    constexpr int S = 256, U = 4;
+    __shared__ double strips[4][S];
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int r = blockIdx.x * 4 + w;
+    if (r >= n) return;
+    double *st = strips[w];
+    const int k0 = rp[r], k1 = rp[r + 1];
+    double acc = b[r];
+    double p[U];
+    int pos[U];
+    auto load = [&](int base) {
+        const int m = min(S, k1 - base);
+        int j[U];
+        double a[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int q = lane + 64 * u;
+            j[u] = q < m ? pk[base + q] : -1;
+            a[u] = q < m ? v[base + q] : 0.0;
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            p[u] = j[u] >= 0 ? a[u] * x[j[u] >> 8] : 0.0;
+            pos[u] = j[u] >= 0 ? (j[u] & 255) : -1;
+        }
+    };
+    if (k0 < k1) load(k0);
+    for (int base = k0; base < k1; base += S) {
+        const int m = min(S, k1 - base);
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            if (pos[u] >= 0) st[pos[u]] = p[u];
+        wsync();
+        if (base + S < k1) load(base + S);
+        if (lane == 0) acc = chain_sub(acc, st, 0, m);
+        wsync();
+    }
+    if (lane == 0) y[r] = acc;
+}
+
+// generalised sorted tile: T entries per tile, NT threads, rows per block <= NT, packed
+// (col << log2 T) | pos; NOLOAD: products are synthetic (chain cost alone)
+template <int T, int NT, bool NOLOAD = false>
+__global__ __launch_bounds__(NT) void k_tsort(const int *blk, const int *rp, const unsigned *pk, const double *v,
+                                              const double *x, const double *b, double *y)
+{
+    constexpr int SH = __builtin_ctz(T);
+    constexpr unsigned MASK = T - 1;
+    __shared__ double sm[T];
+    const int r0 = blk[blockIdx.x], r1 = blk[blockIdx.x + 1];
+    const int k0 = rp[r0], k1 = rp[r1];
+    if (k1 - k0 <= T) {
+        const int r = r0 + threadIdx.x;
+        int ra = 0, re = 0;
+        double br = 0.0;
+        if (r < r1) ra = rp[r], re = rp[r + 1], br = b[r];
+        if (NOLOAD) {
+            for (int k = threadIdx.x; k < k1 - k0; k += NT) sm[k] = 1e-3 * k;
+        } else {
+            for (int kb = k0 + threadIdx.x; kb < k1; kb += 8 * NT) {
+                unsigned j[8];
+                double a[8], xv[8];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) {
+                    const int k = kb + u * NT;
+                    j[u] = k < k1 ? pk[k] : 0u;
+                    a[u] = k < k1 ? v[k] : 0.0;
+                }
+#pragma unroll
+                for (int u = 0; u < 8; ++u) xv[u] = x[j[u] >> SH];
+#pragma unroll
+                for (int u = 0; u < 8; ++u)
+                    if (kb + u * NT < k1) sm[j[u] & MASK] = a[u] * xv[u];
+            }
+        }
+        __syncthreads();
+        if (r < r1) y[r] = chain_sub(br, sm, ra - k0, re - k0);
+    } else {
+        double acc = b[r0];
+        for (int base = k0; base < k1; base += T) {
+            const int m = min(T, k1 - base);
+            for (int k = threadIdx.x; k < m; k += NT) {
+                const unsigned q = pk[base + k];
+                sm[q & MASK] = NOLOAD ? 1e-3 * k : v[base + k] * x[q >> SH];
+            }
+            __syncthreads();
+            if (threadIdx.x == 0) acc = chain_sub(acc, sm, 0, m);
+            __syncthreads();
+        }
+        if (threadIdx.x == 0) y[r0] = acc;
+    }
+}
+
+struct SortedCfg {
+    int T = 0, NT = 0, nblk = 0;
+    int *blk = nullptr;
+    unsigned *pk = nullptr;
+    double *v = nullptr;
+};
+
+// CSR-vector (throughput mode: NOT the reference's summation order): G lanes per row, lane g
+// accumulates entries g, g+G, ... (U loads in flight), xor-shuffle reduction inside the group.
+template <int G, int U>
+__global__ __launch_bounds__(kB) void k_vec(int n, const int *rp, const int *ci, const double *v, const double *x,
+                                            const double *b, double *y)
+{
+    const int r = blockIdx.x * (kB / G) + (int)threadIdx.x / G, g = threadIdx.x % G;
+    int k0 = 0, k1 = 0;
+    if (r < n) k0 = rp[r], k1 = rp[r + 1];
+    double s0 = 0.0, s1 = 0.0;
+    for (int k = k0 + g; k < k1; k += G * U) {
+        int j[U];
+        double a[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int kk = k + u * G;
+            j[u] = kk < k1 ? ci[kk] : -1;
+            a[u] = kk < k1 ? v[kk] : 0.0;
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const double xv = j[u] >= 0 ? x[j[u]] : 0.0;
+            if (u & 1) s1 += a[u] * xv; else s0 += a[u] * xv;
+        }
+    }
+    double s = s0 + s1;
+#pragma unroll
+    for (int off = G / 2; off > 0; off >>= 1) s += __shfl_xor(s, off, 64);
+    if (r < n && g == 0) y[r] = b[r] - s;
+}
+
 struct Dev {
     int n = 0, nnz = 0, nblk = 0;
-    int *rp = nullptr, *ci = nullptr, *blk = nullptr;
+    int *rp = nullptr, *ci = nullptr, *blk = nullptr, *pk11 = nullptr, *pk8 = nullptr;
+    double *v11 = nullptr, *v8 = nullptr;
+    std::vector<int> hrp, hci;
+    std::vector<double> hv;
+    SortedCfg cfg[4];   // T = 2048, 4096, 8192, 16384
+    int *rci = nullptr;        // row-sorted copies
+    double *rv = nullptr;
     double *v = nullptr, *x = nullptr, *b = nullptr, *y = nullptr;
 } D;
 }  // namespace
@@ -194,6 +471,7 @@ extern "C" int lab_load(int n, const int *rp, const int *ci, const double *v)
 {
     D.n = n;
     D.nnz = rp[n];
+    D.hrp.assign(rp, rp + n + 1), D.hci.assign(ci, ci + D.nnz), D.hv.assign(v, v + D.nnz);
     std::vector<int> blk;
     for (int r = 0; r < n;) {
         blk.push_back(r);
@@ -204,6 +482,38 @@ extern "C" int lab_load(int n, const int *rp, const int *ci, const double *v)
     }
     blk.push_back(n);
     D.nblk = (int)blk.size() - 1;
+    // column-sorted segments (tile: 2048-entry segments of blocks; wave: 256-entry strips of rows)
+    auto sorted = [&](int shift, auto segs, std::vector<int> &pk, std::vector<double> &vs) {
+        pk.assign(D.nnz, 0), vs.assign(D.nnz, 0.0);
+        std::vector<int> idx;
+        segs([&](int a, int e) {
+            idx.resize(e - a);
+            for (int t = 0; t < e - a; ++t) idx[t] = a + t;
+            std::stable_sort(idx.begin(), idx.end(), [&](int p, int q) { return ci[p] < ci[q]; });
+            for (int t = 0; t < e - a; ++t) pk[a + t] = (ci[idx[t]] << shift) | (idx[t] - a), vs[a + t] = v[idx[t]];
+        });
+    };
+    std::vector<int> pk11, pk8;
+    std::vector<double> v11, v8;
+    const bool ok11 = n < (1 << 20), ok8 = n < (1 << 23);
+    if (ok11)
+        sorted(11, [&](auto f) {
+            for (int bI = 0; bI < D.nblk; ++bI) {
+                const int a = rp[blk[bI]], e = rp[blk[bI + 1]];
+                for (int s = a; s < e; s += 2048) f(s, std::min(e, s + 2048));
+            }
+        }, pk11, v11);
+    if (ok8)
+        sorted(8, [&](auto f) {
+            for (int r = 0; r < n; ++r)
+                for (int s = rp[r]; s < rp[r + 1]; s += 256) f(s, std::min(rp[r + 1], s + 256));
+        }, pk8, v8);
+    auto up = [](auto *&d, const auto &h) {
+        if (h.empty()) return;
+        hipMalloc(&d, sizeof(h[0]) * h.size());
+        hipMemcpy(d, h.data(), sizeof(h[0]) * h.size(), hipMemcpyHostToDevice);
+    };
+    up(D.pk11, pk11), up(D.v11, v11), up(D.pk8, pk8), up(D.v8, v8);
     std::vector<double> hx(n), hb(n);
     for (int i = 0; i < n; ++i) hx[i] = 1.0 + 1e-3 * (i % 977), hb[i] = 0.5 + 1e-4 * (i % 131);
     if (hipMalloc(&D.rp, sizeof(int) * (n + 1)) || hipMalloc(&D.ci, sizeof(int) * (D.nnz + 8)) ||
@@ -221,15 +531,92 @@ extern "C" int lab_load(int n, const int *rp, const int *ci, const double *v)
 
 extern "C" void lab_free()
 {
+    for (auto &c : D.cfg) hipFree(c.blk), hipFree(c.pk), hipFree(c.v);
+    hipFree(D.rci), hipFree(D.rv);
+    hipFree(D.pk11), hipFree(D.pk8), hipFree(D.v11), hipFree(D.v8);
     hipFree(D.rp), hipFree(D.ci), hipFree(D.v), hipFree(D.blk), hipFree(D.x), hipFree(D.b), hipFree(D.y);
     D = Dev();
+}
+
+static void row_sorted()
+{
+    if (D.rci) return;
+    std::vector<int> c(D.nnz), idx;
+    std::vector<double> w(D.nnz);
+    for (int r = 0; r < D.n; ++r) {
+        const int a = D.hrp[r], e = D.hrp[r + 1];
+        idx.resize(e - a);
+        for (int t = 0; t < e - a; ++t) idx[t] = a + t;
+        std::stable_sort(idx.begin(), idx.end(), [&](int p, int q) { return D.hci[p] < D.hci[q]; });
+        for (int t = 0; t < e - a; ++t) c[a + t] = D.hci[idx[t]], w[a + t] = D.hv[idx[t]];
+    }
+    hipMalloc(&D.rci, sizeof(int) * (D.nnz + 8));
+    hipMalloc(&D.rv, sizeof(double) * (D.nnz + 8));
+    hipMemcpy(D.rci, c.data(), sizeof(int) * D.nnz, hipMemcpyHostToDevice);
+    hipMemcpy(D.rv, w.data(), sizeof(double) * D.nnz, hipMemcpyHostToDevice);
+}
+
+template <int G, int U>
+static void launch_vec(bool sorted)
+{
+    if (sorted) row_sorted();
+    hipLaunchKernelGGL((k_vec<G, U>), dim3((D.n + kB / G - 1) / (kB / G)), dim3(kB), 0, 0, D.n, D.rp,
+                       sorted ? D.rci : D.ci, sorted ? D.rv : D.v, D.x, D.b, D.y);
+}
+
+static SortedCfg *sorted_cfg(int T, int NT)
+{
+    const int slot = __builtin_ctz(T) - 11;
+    SortedCfg &c = D.cfg[slot];
+    if (c.T) return c.T == T && c.NT == NT ? &c : nullptr;
+    const int n = D.n, sh = __builtin_ctz(T);
+    if ((long long)n << sh > 0xffffffffLL) return nullptr;
+    const int *rp = D.hrp.data(), *ci = D.hci.data();
+    std::vector<int> blk;
+    for (int r = 0; r < n;) {
+        blk.push_back(r);
+        int e = r + 1;
+        if (rp[e] - rp[r] <= T)
+            while (e < n && e - r < NT && rp[e + 1] - rp[r] <= T) ++e;
+        r = e;
+    }
+    blk.push_back(n);
+    std::vector<unsigned> pk(D.nnz);
+    std::vector<double> vs(D.nnz);
+    std::vector<int> idx;
+    for (size_t bI = 0; bI + 1 < blk.size(); ++bI) {
+        const int a0 = rp[blk[bI]], e0 = rp[blk[bI + 1]];
+        for (int a = a0; a < e0; a += T) {
+            const int e = std::min(e0, a + T);
+            idx.resize(e - a);
+            for (int t = 0; t < e - a; ++t) idx[t] = a + t;
+            std::stable_sort(idx.begin(), idx.end(), [&](int p, int q) { return ci[p] < ci[q]; });
+            for (int t = 0; t < e - a; ++t) pk[a + t] = ((unsigned)ci[idx[t]] << sh) | (unsigned)(idx[t] - a), vs[a + t] = D.hv[idx[t]];
+        }
+    }
+    c.T = T, c.NT = NT, c.nblk = (int)blk.size() - 1;
+    hipMalloc(&c.blk, sizeof(int) * blk.size());
+    hipMemcpy(c.blk, blk.data(), sizeof(int) * blk.size(), hipMemcpyHostToDevice);
+    hipMalloc(&c.pk, sizeof(unsigned) * pk.size());
+    hipMemcpy(c.pk, pk.data(), sizeof(unsigned) * pk.size(), hipMemcpyHostToDevice);
+    hipMalloc(&c.v, sizeof(double) * vs.size());
+    hipMemcpy(c.v, vs.data(), sizeof(double) * vs.size(), hipMemcpyHostToDevice);
+    return &c;
+}
+
+template <int T, int NT, bool NOLOAD = false>
+static void launch_ts()
+{
+    SortedCfg *c = sorted_cfg(T, NT);
+    if (!c) return;
+    hipLaunchKernelGGL((k_tsort<T, NT, NOLOAD>), dim3(c->nblk), dim3(NT), 0, 0, c->blk, D.rp, c->pk, c->v, D.x, D.b, D.y);
 }
 
 static void launch(int variant)
 {
     const int nw = (D.n + 3) / 4;
     switch (variant) {
-    case 0: hipLaunchKernelGGL(k_tile, dim3(D.nblk), dim3(kB), 0, 0, D.blk, D.rp, D.ci, D.v, D.x, D.b, D.y); break;
+    case 0: hipLaunchKernelGGL(k_tile<false>, dim3(D.nblk), dim3(kB), 0, 0, D.blk, D.rp, D.ci, D.v, D.x, D.b, D.y); break;
     case 1: hipLaunchKernelGGL(k_wave<256>, dim3(nw), dim3(kB), 0, 0, D.n, D.rp, D.ci, D.v, D.x, D.b, D.y); break;
     case 2: hipLaunchKernelGGL(k_wave<512>, dim3(nw), dim3(kB), 0, 0, D.n, D.rp, D.ci, D.v, D.x, D.b, D.y); break;
     case 3: hipLaunchKernelGGL(k_wave<1024>, dim3(nw), dim3(kB), 0, 0, D.n, D.rp, D.ci, D.v, D.x, D.b, D.y); break;
@@ -239,6 +626,30 @@ static void launch(int variant)
     case 7: hipLaunchKernelGGL(k_mrow<8>, dim3((D.n + 31) / 32), dim3(kB), 0, 0, D.n, D.rp, D.ci, D.v, D.x, D.b, D.y); break;
     case 8: hipLaunchKernelGGL(k_mrow<16>, dim3((D.n + 63) / 64), dim3(kB), 0, 0, D.n, D.rp, D.ci, D.v, D.x, D.b, D.y); break;
     case 9: hipLaunchKernelGGL(k_mrow<32>, dim3((D.n + 127) / 128), dim3(kB), 0, 0, D.n, D.rp, D.ci, D.v, D.x, D.b, D.y); break;
+    case 10: hipLaunchKernelGGL((k_lanerow<16, false>), dim3((D.n + 255) / 256), dim3(kB), 0, 0, D.n, D.rp, D.ci, D.v, D.x, D.b, D.y); break;
+    case 11: hipLaunchKernelGGL((k_lanerow<16, true>), dim3((D.n + 255) / 256), dim3(kB), 0, 0, D.n, D.rp, D.ci, D.v, D.x, D.b, D.y); break;
+    case 12: hipLaunchKernelGGL((k_lanerow<8, true>), dim3((D.n + 255) / 256), dim3(kB), 0, 0, D.n, D.rp, D.ci, D.v, D.x, D.b, D.y); break;
+    case 13: hipLaunchKernelGGL((k_lanerow<32, true>), dim3((D.n + 255) / 256), dim3(kB), 0, 0, D.n, D.rp, D.ci, D.v, D.x, D.b, D.y); break;
+    case 14: hipLaunchKernelGGL(k_tile<true>, dim3(D.nblk), dim3(kB), 0, 0, D.blk, D.rp, D.ci, D.v, D.x, D.b, D.y); break;
+    case 15: hipLaunchKernelGGL((k_wave_db<256, true>), dim3(nw), dim3(kB), 0, 0, D.n, D.rp, D.ci, D.v, D.x, D.b, D.y); break;
+    case 16: hipLaunchKernelGGL((k_wave_db<512, true>), dim3(nw), dim3(kB), 0, 0, D.n, D.rp, D.ci, D.v, D.x, D.b, D.y); break;
+    case 17: hipLaunchKernelGGL((k_wave_db<1024, true>), dim3(nw), dim3(kB), 0, 0, D.n, D.rp, D.ci, D.v, D.x, D.b, D.y); break;
+    case 18: if (D.pk11) hipLaunchKernelGGL(k_tile_sorted<false>, dim3(D.nblk), dim3(kB), 0, 0, D.blk, D.rp, D.pk11, D.v11, D.x, D.b, D.y); break;
+    case 19: if (D.pk8) hipLaunchKernelGGL(k_wave_sorted, dim3(nw), dim3(kB), 0, 0, D.n, D.rp, D.pk8, D.v8, D.x, D.b, D.y); break;
+    case 20: launch_ts<2048, 256>(); break;
+    case 21: launch_ts<4096, 256>(); break;
+    case 22: launch_ts<8192, 512>(); break;
+    case 23: launch_ts<8192, 1024>(); break;
+    case 24: launch_ts<16384, 1024>(); break;
+    case 25: launch_ts<2048, 256, true>(); break;
+    case 26: launch_vec<8, 4>(false); break;
+    case 27: launch_vec<8, 4>(true); break;
+    case 28: launch_vec<16, 4>(true); break;
+    case 29: launch_vec<32, 4>(true); break;
+    case 30: launch_vec<64, 4>(true); break;
+    case 31: launch_vec<64, 4>(false); break;
+    case 32: launch_vec<4, 4>(true); break;
+    case 33: launch_vec<64, 8>(true); break;
     default: break;
     }
 }

@@ -21,9 +21,9 @@ os.dup2(nul, 1)
 H = A.Hierarchy(A.generate(7, N))
 os.dup2(fd, 1)
 print(f"setup {time.time() - t:.1f}s levels={H.num_levels}", flush=True)
-names = ["tile", "wave256", "wave512", "wave1024", "wavedb256", "wavedb512", "mrow4", "mrow8", "mrow16", "mrow32"]
-sel = [int(a) for a in os.environ.get("LAB_VARIANTS", "0,1,6,7,8,9").split(",")]
-for l in range(H.num_levels):
+names = ["tile", "wave256", "wave512", "wave1024", "wavedb256", "wavedb512", "mrow4", "mrow8", "mrow16", "mrow32", "lane16", "lane16pf", "lane8pf", "lane32pf", "tilepipe", "wdb256p", "wdb512p", "wdb1024p", "tilesort", "wavesort", "ts2k", "ts4k", "ts8k512", "ts8k1024", "ts16k", "chain2k", "v8u", "v8s", "v16s", "v32s", "v64s", "v64u", "v4s", "v64s8"]
+sel = [int(a) for a in os.environ.get("LAB_VARIANTS", "0,20,4,26,27,28,29,30,31,32,33").split(",")]
+for l in range(int(os.environ.get('LAB_FROM', '0')), H.num_levels):
     M = H.level(l).A
     rp, ci, v = A.csr_arrays(M)
     n, nnz = M.num_rows, M.num_nnzs
@@ -39,7 +39,8 @@ for l in range(H.num_levels):
         if ref is None:
             ref = y.copy()
         elif not np.array_equal(ref.view(np.uint64), y.view(np.uint64)):
-            ok = "!MISMATCH"
+            d = float(np.max(np.abs(ref - y) / np.maximum(np.abs(ref), 1e-300)))
+            ok = "!MISMATCH" if d > 1e-11 else f"(rel {d:.0e})"
         line.append(f"{nm}={ms * 1e3:.0f}us/{by / ms / 1e6:.0f}GB/s{ok}")
     print("  ".join(line), flush=True)
     lab.lab_free()
