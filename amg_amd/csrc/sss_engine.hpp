@@ -9,7 +9,10 @@
 
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+#include <atomic>
 #include <cstdio>
+#include <thread>
 #include <vector>
 
 #include "../../include/sss_hip.h"
@@ -40,6 +43,30 @@ inline void dev_free(void *p)
     if (p) (void)hipFree(p);
 }
 
+// Host-side data preparation at upload: fn(lo, hi) over [0, n) in chunks of `grain` items taken
+// from a shared counter by up to 32 threads (the .hip units are compiled without OpenMP).
+template <class Fn>
+void parallel_chunks(int n, int grain, Fn fn)
+{
+    const int nt = (int)std::max(1u, std::min(32u, std::thread::hardware_concurrency()));
+    if (n <= grain || nt == 1) {
+        if (n > 0) fn(0, n);
+        return;
+    }
+    std::atomic<int> next{0};
+    auto work = [&]() {
+        for (;;) {
+            const int lo = next.fetch_add(grain);
+            if (lo >= n) return;
+            fn(lo, std::min(n, lo + grain));
+        }
+    };
+    std::vector<std::thread> th;
+    for (int t = 1; t < nt; ++t) th.emplace_back(work);
+    work();
+    for (auto &t : th) t.join();
+}
+
 // CSR matrix resident in HBM, plus its CSR-adaptive row blocking for SpMV.
 struct DevCSR {
     int n = 0, ncols = 0, nnz = 0;
@@ -53,19 +80,25 @@ struct DevCSR {
     int ngrid = 0;           // workgroups of one SpMV launch (size of a per-block partial array)
     // Column-sorted tile staging (kEncSortedTiles; bitwise-neutral): each staging segment of the
     // blocking -- a block's entries, or a kTileEntries chunk of a longer row -- stored sorted by
-    // column as pk = (col << kTileShift) | (stored-order position in the segment), pv = values.
+    // column as pk = cluster << 31 | (col - base[cluster]) << kTileShift | (stored-order position
+    // in the segment), pv = values; pb[block] = {base0, base1}.  A block's columns form at most two
+    // clusters (cut at their widest gap: the F and C halves of a relabeled level, own rows and
+    // ghosts), each spanning < 2^kTileColBits columns, or the matrix keeps stored order (pk null).
     // Products land in LDS at their stored position, so every row chain keeps the reference's
     // order; neighbouring rows' gathers of the same x lines coalesce (measured 1.4-1.7x on the
-    // coarse levels of 7-pt 400^3, tools/lab_rows.hip).  Needs ncols <= 2^(32 - kTileShift).
+    // coarse levels of 7-pt 400^3, tools/lab_rows.hip).
     unsigned *pk = nullptr;
     double *pv = nullptr;
+    int2 *pb = nullptr;
     // kEncFreeOrder on a wave_rows matrix: rows summed in a fixed tree order (64 strided lane
     // sums, xor-shuffle reduction) over rows stored column-sorted (within [rp, seg) and
     // [seg, rp+1) when a segment split is given).  Deterministic but NOT the reference order.
     bool vec_rows = false;
 };
 constexpr int kTileShift = 11;           // log2(kTileEntries)
+constexpr int kTileColBits = 20;         // column offset bits of a packed sorted-tile entry
 static_assert((1 << kTileShift) == kTileEntries, "tile packing");
+static_assert(1 + kTileColBits + kTileShift == 32, "tile packing");
 enum { kEncSortedTiles = 1, kEncFreeOrder = 2 };
 // split >= 0 forces a row-block boundary at that row (the F|C class boundary of a relabeled level);
 // enc: kEnc* flags; seg (kEncFreeOrder only, optional): per row, the absolute CSR position that

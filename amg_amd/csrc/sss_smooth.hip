@@ -316,7 +316,7 @@ __global__ __launch_bounds__(kBlock) void relax_wave(int m, const int *__restric
 {
     __shared__ double strips[4][kWaveStage];
     const int wave = threadIdx.x >> 6;
-    const int r = blockIdx.x * 4 + wave;
+    const int r = xcd_bid() * 4 + wave;
     if (r >= m) return;
     const int i = map[r];
     const double acc = wave_row_chain<true>(
@@ -344,10 +344,10 @@ __global__ __launch_bounds__(kBlock) void relax_range(int blo, const int *__rest
                                                       const double *__restrict__ b, double *x,
                                                       const double *__restrict__ yp, double *__restrict__ y,
                                                       const double *__restrict__ deff, const unsigned *__restrict__ pk,
-                                                      const double *__restrict__ pv)
+                                                      const double *__restrict__ pv, const int2 *__restrict__ pb)
 {
     __shared__ SpmvSmem sm;
-    const int bid = blo + blockIdx.x;
+    const int bid = blo + xcd_bid();
     const int r0 = blk[bid], r1 = blk[bid + 1];
     const int k0 = rp[r0], k1 = rp[r1];
     auto fetch = [&](int c) -> double { return x[c]; };
@@ -364,7 +364,7 @@ __global__ __launch_bounds__(kBlock) void relax_range(int blo, const int *__rest
         int a = 0, e = 0, dp = -1;
         double acc = 0.0;
         if (r < r1) a = rp[r] - k0, e = rp[r + 1] - k0, dp = diag_pos[r], acc = b[r];   // ahead of the tile
-        stage_any(sm.v, k0, k1, ci, v, pk, pv, fetch);
+        stage_any(sm.v, k0, k1, ci, v, pk, pv, pb, bid, fetch);
         __syncthreads();
         if (r < r1) {
             if (dp < 0) acc = chain_sub(acc, sm.v, a, e);
@@ -379,7 +379,7 @@ __global__ __launch_bounds__(kBlock) void relax_range(int blo, const int *__rest
         double acc = b[r];
         for (int base = k0; base < k1; base += kTileEntries) {
             const int m = min(kTileEntries, k1 - base);
-            stage_any(sm.v, base, base + m, ci, v, pk, pv, fetch);
+            stage_any(sm.v, base, base + m, ci, v, pk, pv, pb, bid, fetch);
             __syncthreads();
             if (threadIdx.x == 0) {
                 if (dp >= base && dp < base + m) {
@@ -407,7 +407,7 @@ __global__ __launch_bounds__(kBlock) void relax_range_wave(int lo, int hi, const
 {
     __shared__ double strips[TREE ? 1 : 4][TREE ? 1 : kWaveStage];
     const int wave = threadIdx.x >> 6;
-    const int r = lo + blockIdx.x * 4 + wave;
+    const int r = lo + xcd_bid() * 4 + wave;
     if (r >= hi) return;
     auto prod = [&](int c, double a) -> double { return c == r ? 0.0 : a * x[c]; };
     const double acc = TREE ? b[r] - wave_row_sum(rp[r], rp[r + 1], ci, v, prod)
@@ -437,7 +437,7 @@ __global__ __launch_bounds__(kBlock) void ts_stage0(int lo, DevCSR M, const int 
         y[q] = fabs(d) > SMALLFLOAT ? acc / d : x[r];
     };
     if constexpr (PATH == 2) {
-        const int q = blockIdx.x * 4 + (threadIdx.x >> 6);
+        const int q = xcd_bid() * 4 + (threadIdx.x >> 6);
         if (q >= M.n) return;
         auto prod = [&](int c, double a) { return a * x[c]; };
         const int a = M.rp[q], sp = split[q], e = M.rp[q + 1];
@@ -450,7 +450,7 @@ __global__ __launch_bounds__(kBlock) void ts_stage0(int lo, DevCSR M, const int 
         return;
     } else if constexpr (PATH == 1) {
         __shared__ double strips[4][kWaveStage];
-        const int wave = threadIdx.x >> 6, q = blockIdx.x * 4 + wave;
+        const int wave = threadIdx.x >> 6, q = xcd_bid() * 4 + wave;
         if (q >= M.n) return;
         auto prod = [&](int c, double a) { return a * x[c]; };
         const int a = M.rp[q], sp = split[q], e = M.rp[q + 1];
@@ -462,14 +462,14 @@ __global__ __launch_bounds__(kBlock) void ts_stage0(int lo, DevCSR M, const int 
         return;
     } else {
         __shared__ SpmvSmem sm;
-        const int q0 = M.blk[blockIdx.x], q1 = M.blk[blockIdx.x + 1];
+        const int bq = xcd_bid(), q0 = M.blk[bq], q1 = M.blk[bq + 1];
         const int k0 = M.rp[q0], k1 = M.rp[q1];
         if (k1 - k0 <= kTileEntries) {
             const int q = q0 + (int)threadIdx.x;
             int a = 0, sp = 0, e = 0;
             double acc = 0.0;
             if (q < q1) a = M.rp[q] - k0, sp = split[q] - k0, e = M.rp[q + 1] - k0, acc = b[lo + q];
-            stage_any(sm.v, k0, k1, M.ci, M.v, M.pk, M.pv, [&](int c) -> double { return x[c]; });
+            stage_any(sm.v, k0, k1, M.ci, M.v, M.pk, M.pv, M.pb, bq, [&](int c) -> double { return x[c]; });
             __syncthreads();
             if (q < q1) {
                 acc = chain_sub(acc, sm.v, a, sp);
@@ -482,7 +482,7 @@ __global__ __launch_bounds__(kBlock) void ts_stage0(int lo, DevCSR M, const int 
             double acc = b[lo + q];
             for (int base = k0; base < k1; base += kTileEntries) {
                 const int m = min(kTileEntries, k1 - base);
-                stage_any(sm.v, base, base + m, M.ci, M.v, M.pk, M.pv, [&](int c) -> double { return x[c]; });
+                stage_any(sm.v, base, base + m, M.ci, M.v, M.pk, M.pv, M.pb, bq, [&](int c) -> double { return x[c]; });
                 __syncthreads();
                 if (threadIdx.x == 0) {
                     if (sp >= base && sp < base + m) {
@@ -516,7 +516,7 @@ __global__ __launch_bounds__(kBlock) void ts_inner(int lo, DevCSR M, const doubl
         y[q] = fabs(d) > SMALLFLOAT ? acc / d : ykeep[q];
     };
     if constexpr (PATH == 2) {
-        const int q = blockIdx.x * 4 + (threadIdx.x >> 6);
+        const int q = xcd_bid() * 4 + (threadIdx.x >> 6);
         if (q >= M.n) return;
         const double acc =
             P[q] - wave_row_sum(M.rp[q], M.rp[q + 1], M.ci, M.v, [&](int c, double a) { return a * fetch(c); });
@@ -524,7 +524,7 @@ __global__ __launch_bounds__(kBlock) void ts_inner(int lo, DevCSR M, const doubl
         return;
     } else if constexpr (PATH == 1) {
         __shared__ double strips[4][kWaveStage];
-        const int wave = threadIdx.x >> 6, q = blockIdx.x * 4 + wave;
+        const int wave = threadIdx.x >> 6, q = xcd_bid() * 4 + wave;
         if (q >= M.n) return;
         const double acc = wave_row_chain<true>(
             M.rp[q], M.rp[q + 1], M.ci, M.v, [&](int c, double a) { return a * fetch(c); }, P[q], strips[wave]);
@@ -532,14 +532,14 @@ __global__ __launch_bounds__(kBlock) void ts_inner(int lo, DevCSR M, const doubl
         return;
     } else {
         __shared__ SpmvSmem sm;
-        const int q0 = M.blk[blockIdx.x], q1 = M.blk[blockIdx.x + 1];
+        const int bq = xcd_bid(), q0 = M.blk[bq], q1 = M.blk[bq + 1];
         const int k0 = M.rp[q0], k1 = M.rp[q1];
         if (k1 - k0 <= kTileEntries) {
             const int q = q0 + (int)threadIdx.x;
             int a = 0, e = 0;
             double acc = 0.0;
             if (q < q1) a = M.rp[q] - k0, e = M.rp[q + 1] - k0, acc = P[q];
-            stage_any(sm.v, k0, k1, M.ci, M.v, M.pk, M.pv, fetch);
+            stage_any(sm.v, k0, k1, M.ci, M.v, M.pk, M.pv, M.pb, bq, fetch);
             __syncthreads();
             if (q < q1) finish(q, chain_sub(acc, sm.v, a, e));
         } else {
@@ -547,7 +547,7 @@ __global__ __launch_bounds__(kBlock) void ts_inner(int lo, DevCSR M, const doubl
             double acc = P[q];
             for (int base = k0; base < k1; base += kTileEntries) {
                 const int m = min(kTileEntries, k1 - base);
-                stage_any(sm.v, base, base + m, M.ci, M.v, M.pk, M.pv, fetch);
+                stage_any(sm.v, base, base + m, M.ci, M.v, M.pk, M.pv, M.pb, bq, fetch);
                 __syncthreads();
                 if (threadIdx.x == 0) acc = chain_sub(acc, sm.v, 0, m);
                 __syncthreads();
@@ -616,7 +616,7 @@ int smoother_run(const SmootherPlan &sp, const DevCSR &A, const double *b, doubl
                                            A.rp, cols, A.v, b, x, yp, y, deff);
                     else
                         hipLaunchKernelGGL(relax_range<M>, dim3(nb), dim3(kBlock), 0, s, ps.blo, A.blk, A.rp, cols,
-                                           A.v, sp.diag_pos, ps.lo, b, x, yp, y, deff, A.pk, A.pv);
+                                           A.v, sp.diag_pos, ps.lo, b, x, yp, y, deff, A.pk, A.pv, A.pb);
                 };
                 if (sp.kind == SSS_HIP_SMOOTH_JACOBI && sp.inner > 0 && hk) {
                     // iterates live in full-length work vectors whose ghosts (lower-rank rows of

@@ -56,32 +56,55 @@ int build_row_blocks(const int *h_rp, int n, std::vector<int> &blk, int split)
 }
 
 // Sorted tile segments of a blocking: a block's entries, or kTileEntries chunks of a long row
-// (exactly the segments the tile kernels stage, sss_spmv_dev.hpp csr_block_rows).
-static void build_sorted_tiles(const SSS_MAT &h, const std::vector<int> &blk, std::vector<unsigned> &pk,
-                               std::vector<double> &pv)
+// (exactly the segments the tile kernels stage, sss_spmv_dev.hpp csr_block_rows).  Per block the
+// columns are cut into two clusters at their widest gap; returns false when a cluster spans
+// 2^kTileColBits columns or more (the matrix then keeps stored-order staging).
+static bool build_sorted_tiles(const SSS_MAT &h, const std::vector<int> &blk, std::vector<unsigned> &pk,
+                               std::vector<double> &pv, std::vector<int2> &pb)
 {
     const int *rp = h.row_ptr, *ci = h.col_idx;
     const int nb = (int)blk.size() - 1;
+    constexpr long long kSpan = 1ll << kTileColBits;
     pk.resize((size_t)h.num_nnzs);
     pv.resize((size_t)h.num_nnzs);
-#pragma omp parallel
-    {
-        std::vector<int> idx;
-#pragma omp for schedule(dynamic, 256)
-        for (int q = 0; q < nb; ++q) {
+    pb.resize((size_t)std::max(nb, 1));
+    std::atomic<int> ok{1};
+    parallel_chunks(nb, 512, [&](int qlo, int qhi) {
+        std::vector<int> idx, cols;
+        for (int q = qlo; q < qhi; ++q) {
             const int a0 = rp[blk[q]], e0 = rp[blk[q + 1]];
+            if (a0 == e0) {
+                pb[q] = make_int2(0, 0);
+                continue;
+            }
+            cols.assign(ci + a0, ci + e0);
+            std::sort(cols.begin(), cols.end());
+            size_t gap = 0;   // cut after cols[gap]
+            for (size_t t = 1; t < cols.size(); ++t)
+                if (cols[t] - cols[t - 1] > cols[gap + 1] - cols[gap]) gap = t - 1;
+            const int b0 = cols.front(), b1 = cols.size() > 1 ? cols[gap + 1] : cols.front();
+            const int cut = b1;   // columns >= cut go to cluster 1
+            if (cols.size() > 1 && ((long long)cols[gap] - b0 >= kSpan || (long long)cols.back() - b1 >= kSpan)) {
+                ok = 0;
+                return;
+            }
+            pb[q] = make_int2(b0, b1);
             for (int a = a0; a < e0; a += kTileEntries) {
                 const int e = std::min(e0, a + kTileEntries);
                 idx.resize((size_t)(e - a));
                 for (int t = 0; t < e - a; ++t) idx[t] = a + t;
                 std::stable_sort(idx.begin(), idx.end(), [&](int p, int r) { return ci[p] < ci[r]; });
                 for (int t = 0; t < e - a; ++t) {
-                    pk[(size_t)a + t] = ((unsigned)ci[idx[t]] << kTileShift) | (unsigned)(idx[t] - a);
+                    const int c = ci[idx[t]];
+                    const unsigned cl = (cols.size() > 1 && c >= cut) ? 1u : 0u;
+                    const unsigned off = (unsigned)(c - (cl ? b1 : b0));
+                    pk[(size_t)a + t] = (cl << 31) | (off << kTileShift) | (unsigned)(idx[t] - a);
                     pv[(size_t)a + t] = h.val[idx[t]];
                 }
             }
         }
-    }
+    });
+    return ok != 0;
 }
 
 // Rows of a free-order (tree-summed) matrix, stored column-sorted within each segment.
@@ -91,11 +114,9 @@ static void sort_row_segments(const SSS_MAT &h, const int *seg, std::vector<int>
     const int *rp = h.row_ptr;
     ci.resize((size_t)h.num_nnzs);
     v.resize((size_t)h.num_nnzs);
-#pragma omp parallel
-    {
+    parallel_chunks(n, 2048, [&](int rlo, int rhi) {
         std::vector<int> idx;
-#pragma omp for schedule(dynamic, 64)
-        for (int r = 0; r < n; ++r) {
+        for (int r = rlo; r < rhi; ++r) {
             const int cut[3] = {rp[r], seg ? seg[r] : rp[r + 1], rp[r + 1]};
             for (int part = 0; part < 2; ++part) {
                 const int a = cut[part], e = cut[part + 1];
@@ -105,7 +126,7 @@ static void sort_row_segments(const SSS_MAT &h, const int *seg, std::vector<int>
                 for (int t = 0; t < e - a; ++t) ci[(size_t)a + t] = h.col_idx[idx[t]], v[(size_t)a + t] = h.val[idx[t]];
             }
         }
-    }
+    });
 }
 
 int devcsr_upload(DevCSR &d, const SSS_MAT &h, int split, int enc, const int *seg)
@@ -144,16 +165,17 @@ int devcsr_upload(DevCSR &d, const SSS_MAT &h, int split, int enc, const int *se
     SSS_HIP(hipMemcpy(d.blk, blk.data(), sizeof(int) * blk.size(), hipMemcpyHostToDevice));
     d.ngrid = d.wave_rows ? (d.n + 3) / 4 : d.nblk;
     // the tile kernels of a wave_rows matrix never run on the hierarchy; no sorted copy for them
-    if ((enc & kEncSortedTiles) && !d.wave_rows && d.nnz > 0 &&
-        (unsigned long long)std::max(d.ncols, 1) <= (1ull << (32 - kTileShift))) {
-        std::vector<unsigned> pk;
-        std::vector<double> pv;
-        build_sorted_tiles(h, blk, pk, pv);
+    std::vector<unsigned> pk;
+    std::vector<double> pv;
+    std::vector<int2> pb;
+    if ((enc & kEncSortedTiles) && !d.wave_rows && d.nnz > 0 && build_sorted_tiles(h, blk, pk, pv, pb)) {
         d.pk = dev_alloc<unsigned>((size_t)d.nnz);
         d.pv = dev_alloc<double>((size_t)d.nnz);
-        if (!d.pk || !d.pv) return hip_fail(hipErrorOutOfMemory, "hipMalloc(sorted tiles)", __FILE__, __LINE__);
+        d.pb = dev_alloc<int2>(pb.size());
+        if (!d.pk || !d.pv || !d.pb) return hip_fail(hipErrorOutOfMemory, "hipMalloc(sorted tiles)", __FILE__, __LINE__);
         SSS_HIP(hipMemcpy(d.pk, pk.data(), sizeof(unsigned) * (size_t)d.nnz, hipMemcpyHostToDevice));
         SSS_HIP(hipMemcpy(d.pv, pv.data(), sizeof(double) * (size_t)d.nnz, hipMemcpyHostToDevice));
+        SSS_HIP(hipMemcpy(d.pb, pb.data(), sizeof(int2) * pb.size(), hipMemcpyHostToDevice));
     }
     return 0;
 }
@@ -166,6 +188,7 @@ void devcsr_free(DevCSR &d)
     dev_free(d.blk);
     dev_free(d.pk);
     dev_free(d.pv);
+    dev_free(d.pb);
     d = DevCSR();
 }
 
@@ -176,7 +199,7 @@ __global__ __launch_bounds__(kBlock) void spmv_adaptive(const int *__restrict__ 
                                                         const double *__restrict__ x, const double *__restrict__ b,
                                                         double *__restrict__ y, double alpha, int cap,
                                                         double *__restrict__ partial, const unsigned *__restrict__ pk,
-                                                        const double *__restrict__ pv)
+                                                        const double *__restrict__ pv, const int2 *__restrict__ pb)
 {
     __shared__ SpmvSmem sm;
     const double sq = csr_block_rows(blk, rp, ci, v, x, sm, [&](int r, double s) -> double {
@@ -190,10 +213,10 @@ __global__ __launch_bounds__(kBlock) void spmv_adaptive(const int *__restrict__ 
         }
         y[r] = out;
         return NORM ? out * out : 0.0;
-    }, pk, pv);
+    }, pk, pv, pb);
     if (NORM) {
         const double t = block_sum(sq, sm.red);
-        if (threadIdx.x == 0) partial[blockIdx.x] = t;
+        if (threadIdx.x == 0) partial[xcd_bid()] = t;
     }
 }
 
@@ -208,7 +231,7 @@ __global__ __launch_bounds__(kBlock) void spmv_wave(int n, const int *__restrict
     __shared__ double strips[TREE ? 1 : 4][TREE ? 1 : kWaveStage];
     __shared__ double red[kBlock / 64];
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int r = blockIdx.x * 4 + wave;
+    const int r = xcd_bid() * 4 + wave;
     double sq = 0.0;
     if (r < n) {
         auto prod = [&](int c, double a) { return a * x[c]; };
@@ -230,7 +253,7 @@ __global__ __launch_bounds__(kBlock) void spmv_wave(int n, const int *__restrict
     }
     if (NORM) {
         const double t = block_sum(sq, red);
-        if (threadIdx.x == 0) partial[blockIdx.x] = t;
+        if (threadIdx.x == 0) partial[xcd_bid()] = t;
     }
 }
 
@@ -246,7 +269,7 @@ static void launch_op(const DevCSR &A, double alpha, const double *x, const doub
                            b, y, alpha, cap, partial);
     else
         hipLaunchKernelGGL((spmv_adaptive<OP, NORM>), dim3(A.nblk), dim3(kBlock), 0, s, A.blk, A.rp, A.ci, A.v, x,
-                           b, y, alpha, cap, partial, A.pk, A.pv);
+                           b, y, alpha, cap, partial, A.pk, A.pv, A.pb);
 }
 
 int launch_spmv(const DevCSR &A, int op, double alpha, const double *x, const double *b, double *y, int cap,

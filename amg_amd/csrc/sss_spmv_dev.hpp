@@ -10,6 +10,26 @@
 
 namespace sss {
 
+#ifndef SSS_XCD_REMAP
+#define SSS_XCD_REMAP 0
+#endif
+// Workgroups are dealt round-robin over the 8 XCDs (MI355X_MICROARCH.md, workgroup dispatch), so
+// consecutive row blocks -- which gather the same x lines -- land on 8 different L2s.  xcd_bid()
+// renumbers the grid so that the workgroups sharing an XCD (b, b + 8, ...) cover one contiguous run
+// of blocks instead.  A bijection on [0, gridDim.x); speed only (placement is not a contract).
+// Measured OFF by default: on the 7-pt 400^3 hierarchy the V-cycle took 39.8 ms with the remap
+// against 37.4 ms without (level-0 residual 1.32 vs 1.40 ms, but the restriction 1.09 vs 0.79 ms,
+// the level-1 residual 2.44 vs 1.97 ms and every coarse level slower): the x lines neighbouring
+// blocks share are served from the Infinity Cache either way, and eight XCDs streaming eight
+// distant regions lose more than the L2 reuse gains.
+__device__ __forceinline__ int xcd_bid()
+{
+    const int b = blockIdx.x;
+    if (!SSS_XCD_REMAP) return b;
+    const int nb = gridDim.x, per = nb >> 3, rem = nb & 7, xcd = b & 7, idx = b >> 3;
+    return xcd < rem ? xcd * (per + 1) + idx : rem * (per + 1) + (xcd - rem) * per + idx;
+}
+
 struct SpmvSmem {
     double v[kTileEntries];    // products a_k * x_{c_k} of the tile
     double red[kBlock / 64];
@@ -121,12 +141,18 @@ __device__ __forceinline__ void stage_products_f(double *__restrict__ sm, int k0
     }
 }
 
-// Column-sorted staging (DevCSR::pk/pv): slot k of the segment [k0, k1) holds the entry packed as
-// (col << kTileShift) | pos, pos = its stored-order position in the segment; the product goes to
-// sm[pos], so the LDS image is exactly stage_products_f's and every chain over it is unchanged.
+// Column-sorted staging (DevCSR::pk/pv/pb): slot k of the segment [k0, k1) holds the entry packed
+// as cluster << 31 | (col - base[cluster]) << kTileShift | pos, pos = its stored-order position in
+// the segment; the product goes to sm[pos], so the LDS image is exactly stage_products_f's and
+// every chain over it is unchanged.
+__device__ __forceinline__ int sorted_col(unsigned q, int2 base)
+{
+    return (int)((q >> kTileShift) & ((1u << kTileColBits) - 1)) + ((q >> 31) ? base.y : base.x);
+}
+
 template <class Fetch>
 __device__ __forceinline__ void stage_sorted(double *__restrict__ sm, int k0, int k1, const unsigned *__restrict__ pk,
-                                             const double *__restrict__ pv, Fetch fetch)
+                                             const double *__restrict__ pv, int2 base, Fetch fetch)
 {
     constexpr int U = 8;
     constexpr unsigned kMask = kTileEntries - 1;
@@ -140,20 +166,21 @@ __device__ __forceinline__ void stage_sorted(double *__restrict__ sm, int k0, in
             a[u] = k < k1 ? pv[k] : 0.0;
         }
 #pragma unroll
-        for (int u = 0; u < U; ++u) xv[u] = kb + u * kBlock < k1 ? fetch((int)(q[u] >> kTileShift)) : 0.0;
+        for (int u = 0; u < U; ++u) xv[u] = kb + u * kBlock < k1 ? fetch(sorted_col(q[u], base)) : 0.0;
 #pragma unroll
         for (int u = 0; u < U; ++u)
             if (kb + u * kBlock < k1) sm[q[u] & kMask] = a[u] * xv[u];
     }
 }
 
-// Stage the products of segment [k0, k1): from the sorted copy when the matrix has one.
+// Stage the products of segment [k0, k1) of block `bid`: from the sorted copy when the matrix has one.
 template <class Fetch>
 __device__ __forceinline__ void stage_any(double *__restrict__ sm, int k0, int k1, const int *__restrict__ ci,
                                           const double *__restrict__ v, const unsigned *__restrict__ pk,
-                                          const double *__restrict__ pv, Fetch fetch)
+                                          const double *__restrict__ pv, const int2 *__restrict__ pb, int bid,
+                                          Fetch fetch)
 {
-    if (pk) stage_sorted(sm, k0, k1, pk, pv, fetch);
+    if (pk) stage_sorted(sm, k0, k1, pk, pv, pb[bid], fetch);
     else stage_products_f(sm, k0, k1, ci, v, fetch);
 }
 
@@ -167,10 +194,12 @@ __device__ __forceinline__ double csr_block_rows(const int *__restrict__ blk, co
                                                  const int *__restrict__ ci, const double *__restrict__ v,
                                                  const double *__restrict__ x, SpmvSmem &sm, Epi epi,
                                                  const unsigned *__restrict__ pk = nullptr,
-                                                 const double *__restrict__ pv = nullptr)
+                                                 const double *__restrict__ pv = nullptr,
+                                                 const int2 *__restrict__ pb = nullptr)
 {
     auto fetch = [&](int c) -> double { return x[c]; };
-    const int r0 = blk[blockIdx.x], r1 = blk[blockIdx.x + 1];
+    const int bid = xcd_bid();
+    const int r0 = blk[bid], r1 = blk[bid + 1];
     const int k0 = rp[r0], k1 = rp[r1];
     const int cnt = k1 - k0;
     double contrib = 0.0;
@@ -178,7 +207,7 @@ __device__ __forceinline__ double csr_block_rows(const int *__restrict__ blk, co
         const int r = r0 + (int)threadIdx.x;
         int ra = 0, re = 0;
         if (r < r1) ra = rp[r], re = rp[r + 1];   // issued ahead of the tile
-        if (pk) stage_sorted(sm.v, k0, k1, pk, pv, fetch);
+        if (pk) stage_sorted(sm.v, k0, k1, pk, pv, pb[bid], fetch);
         else stage_products(sm.v, k0, k1, ci, v, x);
         __syncthreads();
         if (r < r1) {
@@ -189,7 +218,7 @@ __device__ __forceinline__ double csr_block_rows(const int *__restrict__ blk, co
         double s = 0.0;
         for (int base = k0; base < k1; base += kTileEntries) {
             const int m = min(kTileEntries, k1 - base);
-            if (pk) stage_sorted(sm.v, base, base + m, pk, pv, fetch);
+            if (pk) stage_sorted(sm.v, base, base + m, pk, pv, pb[bid], fetch);
             else stage_products(sm.v, base, base + m, ci, v, x);
             __syncthreads();
             if (threadIdx.x == 0) s = chain_add(s, sm.v, 0, m);
@@ -214,7 +243,8 @@ __device__ __forceinline__ void csr_block_relax(const int *__restrict__ blk, con
                                                 const int *__restrict__ map, const double *__restrict__ b,
                                                 const double *x, SpmvSmem &sm, Epi epi)
 {
-    const int r0 = blk[blockIdx.x], r1 = blk[blockIdx.x + 1];
+    const int bid = xcd_bid();
+    const int r0 = blk[bid], r1 = blk[bid + 1];
     const int k0 = rp[r0], k1 = rp[r1];
     const int cnt = k1 - k0;
     if (cnt <= kTileEntries) {

@@ -183,9 +183,17 @@ class Distributed(Single):
         self.DH.upload("x", np.ones(self.rows))
 
 
+def heartbeat(stop: threading.Event, t0: float):
+    """A progress line on stderr every 60 s through the long host phases (setup, upload)."""
+    while not stop.wait(60.0):
+        print(f"[bench] working ({time.perf_counter() - t0:.0f} s)", file=sys.stderr, flush=True)
+
+
 def main():
     args = parse()
     D = Dist()
+    hb_stop = threading.Event()
+    threading.Thread(target=heartbeat, args=(hb_stop, time.perf_counter()), daemon=True).start()
     import amg_amd as A
 
     n = args.n
@@ -232,6 +240,7 @@ def main():
                              inner_from=args.inner_from, sum_order=sum_order, sorted_tiles=sorted_tiles)
         eng = Distributed(DD, H)
     upload_s = time.perf_counter() - t0
+    print(f"[bench] setup {setup_s:.1f} s, upload {upload_s:.1f} s", file=sys.stderr, flush=True)
     eng.set_ones()
     DH = eng
 
@@ -339,6 +348,7 @@ def main():
     if cpu_baseline:
         rec["speedup_vs_cpu"] = value / cpu_baseline["value"]
     DH.close()
+    hb_stop.set()
     if D.rank == 0:
         print(json.dumps(rec), flush=True)
     D.close()

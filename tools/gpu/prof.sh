@@ -1,6 +1,9 @@
+# kernel-trace profile of a short bench run (N=1) + per-level breakdown of one V-cycle
 set -o pipefail
 cd $GRAFT_REPO_ROOT
-OUT=$GRAFT_REPO_ROOT/gpurun_out/prof_${TAG:-x}
 export TMPDIR=/tmp
-SSS_HIP_GRAPH=0 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $OUT -o run -- python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline --converge-max 0 ${BENCH_ARGS} > gpurun_out/prof_${TAG:-x}.log 2>&1 || exit 1
-echo prof-ok
+mkdir -p gpurun_out
+rm -rf gpurun_out/prof_cur
+timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_cur -o run --output-format rocpd csv -- python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline --converge-max 0 ${BENCH_ARGS} > gpurun_out/prof_cur.log 2>&1 || { echo prof failed; tail -30 gpurun_out/prof_cur.log; exit 1; }
+grep '^{' gpurun_out/prof_cur.log > gpurun_out/prof_bench.json
+python3 tools/level_breakdown.py $(find gpurun_out/prof_cur -name '*.db' | head -1) gpurun_out/prof_bench.json | tee gpurun_out/prof_levels.txt

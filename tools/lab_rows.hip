@@ -454,8 +454,84 @@ __global__ __launch_bounds__(kB) void k_vec(int n, const int *rp, const int *ci,
     if (r < n && g == 0) y[r] = b[r] - s;
 }
 
+// x staged in LDS, column-chunked (throughput mode: free order).  Columns are cut into chunks of K;
+// the matrix is stored chunk-major (for chunk c a CSR over all rows with 16-bit chunk-local
+// columns, rows column-sorted).  A persistent workgroup owns the rows [rs[b], rs[b+1]) (balanced
+// by nnz); for every chunk it stages x[cK, cK + K) in LDS, then each wave takes R consecutive rows
+// at a time, lane-strided over the row's chunk entries with R*Q loads in flight, one xor-reduction
+// per row and chunk, the running row sum kept in LDS by the owning wave.
+constexpr int kLxRows = 2048;   // max rows per workgroup
+template <int K, int NT, int R, int Q>
+__global__ __launch_bounds__(NT) void k_ldsx(int n, int nchunk, const int *rs, const int *crp,
+                                             const unsigned short *cci, const double *cv, const double *x,
+                                             const double *b, double *y)
+{
+    __shared__ double xs[K];
+    __shared__ double acc[kLxRows];
+    constexpr int NW = NT / 64;
+    const int r0 = rs[blockIdx.x], r1 = rs[blockIdx.x + 1];
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    for (int c = 0; c < nchunk; ++c) {
+        const int cbase = c * K, cn = min(K, n - cbase);
+        __syncthreads();
+        for (int i = threadIdx.x; i < cn; i += NT) xs[i] = x[cbase + i];
+        __syncthreads();
+        const int *rp = crp + (size_t)c * (n + 1);
+        for (int rb = r0 + wave * R; rb < r1; rb += NW * R) {
+            int k0[R], k1[R];
+            double s[R];
+            int len = 0;
+#pragma unroll
+            for (int u = 0; u < R; ++u) {
+                const int r = rb + u;
+                k0[u] = r < r1 ? rp[r] : 0;
+                k1[u] = r < r1 ? rp[r + 1] : 0;
+                len = max(len, k1[u] - k0[u]);
+                s[u] = 0.0;
+            }
+            for (int t = lane; t < len; t += 64 * Q) {
+                unsigned short cc[R][Q];
+                double aa[R][Q];
+#pragma unroll
+                for (int u = 0; u < R; ++u)
+#pragma unroll
+                    for (int q = 0; q < Q; ++q) {
+                        const int k = k0[u] + t + 64 * q;
+                        const bool ok = k < k1[u];
+                        cc[u][q] = ok ? cci[k] : (unsigned short)0;
+                        aa[u][q] = ok ? cv[k] : 0.0;
+                    }
+#pragma unroll
+                for (int u = 0; u < R; ++u)
+#pragma unroll
+                    for (int q = 0; q < Q; ++q) s[u] += aa[u][q] * xs[cc[u][q]];
+            }
+#pragma unroll
+            for (int u = 0; u < R; ++u) {
+                double v = s[u];
+#pragma unroll
+                for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+                const int r = rb + u;
+                if (lane == 0 && r < r1) {
+                    const double tot = c == 0 ? v : acc[r - r0] + v;
+                    if (c + 1 == nchunk) y[r] = b[r] - tot;
+                    else acc[r - r0] = tot;
+                }
+            }
+        }
+    }
+}
+
+struct Lx {
+    int K = 0, nchunk = 0, nb = 0;
+    int *rs = nullptr, *crp = nullptr;
+    unsigned short *cci = nullptr;
+    double *cv = nullptr;
+};
+
 struct Dev {
     int n = 0, nnz = 0, nblk = 0;
+    Lx lx[2];   // K = 8192, 16384
     int *rp = nullptr, *ci = nullptr, *blk = nullptr, *pk11 = nullptr, *pk8 = nullptr;
     double *v11 = nullptr, *v8 = nullptr;
     std::vector<int> hrp, hci;
@@ -532,6 +608,7 @@ extern "C" int lab_load(int n, const int *rp, const int *ci, const double *v)
 extern "C" void lab_free()
 {
     for (auto &c : D.cfg) hipFree(c.blk), hipFree(c.pk), hipFree(c.v);
+    for (auto &L : D.lx) hipFree(L.rs), hipFree(L.crp), hipFree(L.cci), hipFree(L.cv);
     hipFree(D.rci), hipFree(D.rv);
     hipFree(D.pk11), hipFree(D.pk8), hipFree(D.v11), hipFree(D.v8);
     hipFree(D.rp), hipFree(D.ci), hipFree(D.v), hipFree(D.blk), hipFree(D.x), hipFree(D.b), hipFree(D.y);
@@ -554,6 +631,81 @@ static void row_sorted()
     hipMalloc(&D.rv, sizeof(double) * (D.nnz + 8));
     hipMemcpy(D.rci, c.data(), sizeof(int) * D.nnz, hipMemcpyHostToDevice);
     hipMemcpy(D.rv, w.data(), sizeof(double) * D.nnz, hipMemcpyHostToDevice);
+}
+
+// chunk-major copy for k_ldsx: rows column-sorted, cut at multiples of K; nb row ranges of ~equal nnz
+static Lx *lx_get(int slot, int K, int nb)
+{
+    Lx &L = D.lx[slot];
+    if (L.K) return &L;
+    const int n = D.n;
+    if (n > 16 * 65536) return nullptr;
+    nb = std::max(nb, (n + kLxRows - 1) / kLxRows);
+    const int nc = (n + K - 1) / K;
+    std::vector<int> crp((size_t)nc * (n + 1), 0), cnt((size_t)nc * n, 0);
+    const int *rp = D.hrp.data(), *ci = D.hci.data();
+    for (int r = 0; r < n; ++r)
+        for (int k = rp[r]; k < rp[r + 1]; ++k) cnt[(size_t)(ci[k] / K) * n + r]++;
+    std::vector<long long> base(nc + 1, 0);
+    for (int c = 0; c < nc; ++c) {
+        long long s = 0;
+        for (int r = 0; r < n; ++r) s += cnt[(size_t)c * n + r];
+        base[c + 1] = base[c] + s;
+    }
+    // crp holds absolute positions into the concatenated chunk arrays
+    for (int c = 0; c < nc; ++c) {
+        long long p = base[c];
+        for (int r = 0; r < n; ++r) {
+            crp[(size_t)c * (n + 1) + r] = (int)p;
+            p += cnt[(size_t)c * n + r];
+        }
+        crp[(size_t)c * (n + 1) + n] = (int)p;
+    }
+    std::vector<unsigned short> cc(D.nnz);
+    std::vector<double> vv(D.nnz);
+    std::vector<int> fill(crp);
+    std::vector<int> idx;
+    for (int r = 0; r < n; ++r) {
+        idx.resize(rp[r + 1] - rp[r]);
+        for (int t = 0; t < (int)idx.size(); ++t) idx[t] = rp[r] + t;
+        std::stable_sort(idx.begin(), idx.end(), [&](int p, int q) { return ci[p] < ci[q]; });
+        for (int k : idx) {
+            const int c = ci[k] / K;
+            const int pos = fill[(size_t)c * (n + 1) + r]++;
+            cc[pos] = (unsigned short)(ci[k] - c * K);
+            vv[pos] = D.hv[k];
+        }
+    }
+    std::vector<int> rs(1, 0);
+    const double per = (double)D.nnz / nb;
+    for (int r = 0, b = 1; r < n && b < nb; ++r)
+        if ((double)rp[r + 1] >= per * b || r + 1 - rs.back() >= kLxRows) rs.push_back(r + 1), ++b;
+    while (rs.back() < n) {   // cap the last ranges at kLxRows rows
+        const int nx = std::min(n, rs.back() + kLxRows);
+        rs.push_back(nx);
+    }
+    L.K = K, L.nchunk = nc, L.nb = (int)rs.size() - 1;
+    hipMalloc(&L.rs, sizeof(int) * rs.size());
+    hipMemcpy(L.rs, rs.data(), sizeof(int) * rs.size(), hipMemcpyHostToDevice);
+    hipMalloc(&L.crp, sizeof(int) * crp.size());
+    hipMemcpy(L.crp, crp.data(), sizeof(int) * crp.size(), hipMemcpyHostToDevice);
+    hipMalloc(&L.cci, sizeof(unsigned short) * (cc.size() + 8));
+    hipMemcpy(L.cci, cc.data(), sizeof(unsigned short) * cc.size(), hipMemcpyHostToDevice);
+    hipMalloc(&L.cv, sizeof(double) * (vv.size() + 8));
+    hipMemcpy(L.cv, vv.data(), sizeof(double) * vv.size(), hipMemcpyHostToDevice);
+    return &L;
+}
+
+template <int K, int NT, int R, int Q>
+static void launch_lx(int slot, int nb)
+{
+    Lx *L = lx_get(slot, K, nb);
+    if (!L) {
+        fprintf(stderr, "lx_get(%d) failed\n", K);
+        return;
+    }
+    hipLaunchKernelGGL((k_ldsx<K, NT, R, Q>), dim3(L->nb), dim3(NT), 0, 0, D.n, L->nchunk, L->rs, L->crp, L->cci,
+                       L->cv, D.x, D.b, D.y);
 }
 
 template <int G, int U>
@@ -650,6 +802,12 @@ static void launch(int variant)
     case 31: launch_vec<64, 4>(false); break;
     case 32: launch_vec<4, 4>(true); break;
     case 33: launch_vec<64, 8>(true); break;
+    case 34: launch_lx<8192, 512, 4, 2>(0, 512); break;
+    case 35: launch_lx<8192, 1024, 4, 2>(0, 512); break;
+    case 36: launch_lx<16384, 1024, 4, 2>(1, 256); break;
+    case 37: launch_lx<16384, 1024, 2, 4>(1, 256); break;
+    case 38: launch_lx<16384, 1024, 8, 1>(1, 256); break;
+    case 39: launch_lx<16384, 512, 4, 2>(1, 256); break;
     default: break;
     }
 }
@@ -658,8 +816,11 @@ static void launch(int variant)
 extern "C" double lab_time(int variant, int reps, double *y_out)
 {
     hipMemset(D.y, 0, sizeof(double) * D.n);
+    (void)hipGetLastError();
     launch(variant);
-    hipDeviceSynchronize();
+    hipError_t le = hipGetLastError(), se = hipDeviceSynchronize();
+    if (le != hipSuccess || se != hipSuccess)
+        fprintf(stderr, "variant %d: launch %s, sync %s\n", variant, hipGetErrorString(le), hipGetErrorString(se));
     hipEvent_t e0, e1;
     hipEventCreate(&e0);
     hipEventCreate(&e1);
