@@ -123,6 +123,9 @@ int level_inner_of(const sss_hip_opts &o, int global_level);
 // sum-of-squares of the written y per row block, for a deterministic fused norm.
 int launch_spmv(const DevCSR &A, int op, double alpha, const double *x, const double *b, double *y,
                 int cap, double *partial, hipStream_t stream);
+// As launch_spmv, tile path only, over the row blocks [0, nblk) of A (nblk <= A.nblk).
+int launch_spmv_blocks(const DevCSR &A, int nblk, int op, double alpha, const double *x, const double *b, double *y,
+                       double *partial, hipStream_t stream);
 
 // ---- smoother schedules -------------------------------------------------------------------
 struct PassSchedule {          // rows of one class (F or C), grouped by DAG depth
@@ -158,6 +161,18 @@ struct SmootherPlan {
     bool long_rows = false;    // wave-per-row kernels
     int *diag_pos = nullptr;   // range passes: CSR position of each row's diagonal (-1: none)
     int inner = 0;             // two-stage GS-CF inner steps (kind == JACOBI, range passes only)
+    // The last class pass of a call (C, rows [split_row, n)) can also write the residual
+    // r = b - A x of its rows (ResidFuse): exact GS with depth-1 range passes (a red-black level),
+    // every row with exactly one diagonal, no long-row block among the C blocks.
+    bool fuse_resid = false;
+};
+// Residual fused into the smoother's last pass: r[i] = b[i] - sum_k a_ik x_k (stored order from
+// 0.0, x after the pass) for the C rows, and their per-block sums of squares into partial[block]
+// when partial is given; the caller then forms the F rows' residual (blocks [0, split_blk)).
+struct ResidFuse {
+    double *r = nullptr;
+    double *partial = nullptr;
+    bool done = false;         // set by smoother_run when it fused
 };
 // contiguous: mark is relabeled so class F occupies rows [0, nF) and class C rows [nF, n), and A was
 // uploaded with a block split at nF (its DevCSR is passed to allow range passes).
@@ -179,7 +194,7 @@ void launch_ts_inner(const DevCSR &M, int lo, const double *deff, const double *
                      const double *ykeep, double *y, hipStream_t s);
 void smoother_free(SmootherPlan &sp);
 int smoother_run(const SmootherPlan &sp, const DevCSR &A, const double *b, double *x, int sweeps,
-                 hipStream_t stream, const PassHooks *hooks = nullptr);
+                 hipStream_t stream, const PassHooks *hooks = nullptr, ResidFuse *rf = nullptr);
 
 // ---- reductions ----------------------------------------------------------------------------
 // Deterministic sum of `n` partials -> *out (device); optionally sqrt.

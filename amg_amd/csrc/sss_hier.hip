@@ -48,6 +48,11 @@ struct sss_hip_hier {
     std::vector<hipGraphExec_t> cycle_steps;
     bool cycle_graph_ready = false;
     hipGraphExec_t resid_exec = nullptr;
+    // ResidFuse on level 0 (SmootherPlan::fuse_resid): the cycle's last C pass leaves the C rows of
+    // r = b - A0 x in wp and their block partials in `partial`; the residual norm then only forms
+    // the F rows.  Valid from the end of a cycle until level-0 x or b is touched by anything else.
+    bool resid_c_ready = false;
+    hipGraphExec_t resid_f_exec = nullptr;
 };
 
 static int env_int(const char *name, int dflt)
@@ -124,6 +129,7 @@ static void hier_release(sss_hip_hier *h)
     for (auto g : h->cycle_steps)
         if (g) (void)hipGraphExecDestroy(g);
     if (h->resid_exec) (void)hipGraphExecDestroy(h->resid_exec);
+    if (h->resid_f_exec) (void)hipGraphExecDestroy(h->resid_f_exec);
     coarse_direct_free(h->direct);
     coarse_krylov_destroy(h->krylov);
     dev_free(h->partial);
@@ -350,6 +356,7 @@ extern "C" int sss_hip_upload_vec(sss_hip_hier *h, int level, int which, const d
 {
     double *d = level_vec(h, level, which);
     if (!d || n < 0 || n > h->L[level].A.n) return ERROR_INPUT_PAR;
+    h->resid_c_ready = false;
     const auto &perm = h->L[level].perm;
     if (!perm.empty()) {
         if (n != h->L[level].A.n) return ERROR_INPUT_PAR;   // relabeled levels move whole vectors
@@ -406,7 +413,24 @@ extern "C" int sss_hip_smooth(sss_hip_hier *h, int level, int post)
 {
     auto &L = h->L[level];
     const int sweeps = post ? h->pars.post_iter : h->pars.pre_iter;
+    h->resid_c_ready = false;
     return smoother_run(L.sm, L.A, L.b, L.x, sweeps, h->stream);
+}
+
+// Smoothing that leaves r = b - A x in wp: fused into the last C pass where the plan allows,
+// then the F rows by a residual SpMV over blocks [0, split_blk); otherwise a full residual SpMV.
+// `partial` (optional): per-block sums of squares of r, for the norm.
+static int smooth_then_residual(sss_hip_hier *h, int l, int post, double *partial)
+{
+    auto &L = h->L[l];
+    const int sweeps = post ? h->pars.post_iter : h->pars.pre_iter;
+    ResidFuse rf;
+    rf.r = L.wp;
+    rf.partial = partial;
+    int rc = smoother_run(L.sm, L.A, L.b, L.x, sweeps, h->stream, nullptr, &rf);
+    if (rc) return rc;
+    if (rf.done) return launch_spmv_blocks(L.A, L.A.split_blk, SSS_HIP_SPMV_RESID, -1.0, L.x, L.b, L.wp, partial, h->stream);
+    return launch_spmv(L.A, SSS_HIP_SPMV_RESID, -1.0, L.x, L.b, L.wp, 0, partial, h->stream);
 }
 
 // Walks SSS_amg_cycle's static control flow, enqueueing kernels; `coarse(h)` is called where
@@ -423,8 +447,7 @@ static int walk_cycle(sss_hip_hier *h, CoarseFn coarse)
         while (l < nl - 1) {
             auto &L = h->L[l];
             visits[l]++;
-            if ((rc = sss_hip_smooth(h, l, 0))) return rc;
-            if ((rc = launch_spmv(L.A, SSS_HIP_SPMV_RESID, -1.0, L.x, L.b, L.wp, 0, nullptr, s))) return rc;
+            if ((rc = smooth_then_residual(h, l, 0, nullptr))) return rc;
             if ((rc = launch_spmv(L.R, SSS_HIP_SPMV_MXY, 1.0, L.wp, nullptr, h->L[l + 1].b, 0, nullptr, s))) return rc;
             l++;
             SSS_HIP(hipMemsetAsync(h->L[l].x, 0, sizeof(double) * (size_t)h->L[l].A.n, s));
@@ -434,7 +457,14 @@ static int walk_cycle(sss_hip_hier *h, CoarseFn coarse)
             l--;
             auto &L = h->L[l];
             if ((rc = launch_spmv(L.P, SSS_HIP_SPMV_AMXPY, 1.0, h->L[l + 1].x, nullptr, L.x, 0, nullptr, s))) return rc;
-            if ((rc = sss_hip_smooth(h, l, 1))) return rc;
+            if (l == 0 && L.sm.fuse_resid) {   // the C rows of the outer residual come with the last pass
+                ResidFuse rf;
+                rf.r = L.wp;
+                rf.partial = h->partial;
+                if ((rc = smoother_run(L.sm, L.A, L.b, L.x, h->pars.post_iter, s, nullptr, &rf))) return rc;
+            } else if ((rc = sss_hip_smooth(h, l, 1))) {
+                return rc;
+            }
             if (visits[l] < cycle_type) break;
             visits[l] = 0;
         }
@@ -475,7 +505,17 @@ static int build_cycle_graph(sss_hip_hier *h)
     return 0;
 }
 
+static int cycle_impl(sss_hip_hier *h);
 extern "C" int sss_hip_cycle(sss_hip_hier *h)
+{
+    h->resid_c_ready = false;
+    int rc = cycle_impl(h);
+    if (rc) return rc;
+    h->resid_c_ready = h->nl > 1 && h->L[0].sm.fuse_resid && h->pars.post_iter > 0;
+    return 0;
+}
+
+static int cycle_impl(sss_hip_hier *h)
 {
     if (!h->opts.use_graph) return walk_cycle(h, [](sss_hip_hier *hh) { return sss_hip_coarse_solve(hh); });
     if (!h->cycle_graph_ready) {
@@ -492,29 +532,33 @@ extern "C" int sss_hip_cycle(sss_hip_hier *h)
     return 0;
 }
 
-static int enqueue_residual_norm(sss_hip_hier *h)
+// f_only: the C rows' residual and partials are already in place (resid_c_ready)
+static int enqueue_residual_norm(sss_hip_hier *h, bool f_only)
 {
     auto &L = h->L[0];
-    int rc = launch_spmv(L.A, SSS_HIP_SPMV_RESID, -1.0, L.x, L.b, L.wp, 0, h->partial, h->stream);
+    int rc = f_only ? launch_spmv_blocks(L.A, L.A.split_blk, SSS_HIP_SPMV_RESID, -1.0, L.x, L.b, L.wp, h->partial, h->stream)
+                    : launch_spmv(L.A, SSS_HIP_SPMV_RESID, -1.0, L.x, L.b, L.wp, 0, h->partial, h->stream);
     if (rc) return rc;
     return launch_final_sum(h->partial, L.A.ngrid, h->d_norm, true, h->stream);
 }
 
 extern "C" int sss_hip_residual_norm(sss_hip_hier *h, double *absres)
 {
+    const bool f_only = h->resid_c_ready;
     if (h->opts.use_graph) {
-        if (!h->resid_exec) {
+        hipGraphExec_t &exec = f_only ? h->resid_f_exec : h->resid_exec;
+        if (!exec) {
             SSS_HIP(hipStreamBeginCapture(h->stream, hipStreamCaptureModeThreadLocal));
-            int rc = enqueue_residual_norm(h);
+            int rc = enqueue_residual_norm(h, f_only);
             hipGraphExec_t ex = nullptr;
             int rc2 = end_capture(h, &ex);
             if (rc) return rc;
             if (rc2) return rc2;
-            h->resid_exec = ex;
+            exec = ex;
         }
-        SSS_HIP(hipGraphLaunch(h->resid_exec, h->stream));
+        SSS_HIP(hipGraphLaunch(exec, h->stream));
     } else {
-        int rc = enqueue_residual_norm(h);
+        int rc = enqueue_residual_norm(h, f_only);
         if (rc) return rc;
     }
     SSS_HIP(hipMemcpyAsync(h->h_norm, h->d_norm, sizeof(double), hipMemcpyDeviceToHost, h->stream));

@@ -22,6 +22,7 @@
 #include "sss_spmv_dev.hpp"
 
 #include <algorithm>
+#include <cstdlib>
 #include <type_traits>
 #include <cmath>
 
@@ -218,6 +219,18 @@ int smoother_build(SmootherPlan &sp, const SSS_MAT &A, const int *mark, int kind
     }
     if (sp.pass[0].range || sp.pass[1].range)
         if ((rc = upload_ints(&sp.diag_pos, diag_pos))) return rc;
+    const char *fz = getenv("SSS_HIP_FUSE_RESID");   // 0: never fuse (tests compare both paths)
+    if (!(fz && *fz == '0') && kind != SSS_HIP_SMOOTH_JACOBI && dA && !dA->wave_rows && all_diag && single_diag &&
+        dA->split_row > 0 &&
+        dA->split_row < n && sp.pass[0].range && sp.pass[1].range && sp.pass[0].lo == 0 &&
+        sp.pass[0].hi == dA->split_row && sp.pass[1].lo == dA->split_row && sp.pass[1].hi == n) {
+        std::vector<int> blk;
+        build_row_blocks(rp, n, blk, dA->split_row);
+        bool short_blocks = true;
+        for (int q = dA->split_blk; q < dA->nblk && short_blocks; ++q)
+            short_blocks = rp[blk[q + 1]] - rp[blk[q]] <= kTileEntries;
+        sp.fuse_resid = short_blocks;
+    }
     if (kind == SSS_HIP_SMOOTH_JACOBI) {
         if ((rc = upload_doubles(&sp.d_first, last_diag))) return rc;   // Jacobi: row's own diagonal
         sp.d_later = sp.d_first;
@@ -335,6 +348,10 @@ __global__ __launch_bounds__(kBlock) void relax_wave(int m, const int *__restric
 // Class pass over rows [lo, hi) of a relabeled level, blocks [blo, ...) of its own CSR.
 //   MODE 0: GS-CF pass of depth 1, in place (x[r] = t / d).
 //   MODE 1: C/F-Jacobi pass / two-stage stage 0: y[r - lo] = t / d, every x from before the pass.
+//   MODE 2: MODE 0, then the residual of the updated row (ResidFuse, sss_engine.hpp):
+//           rr[r] = b_r - (sum of a_k x_k in stored order from 0.0), the diagonal product formed
+//           with the new x_r -- exactly the residual SpMV's chain, since in a depth-1 pass no
+//           other product of the row changes; per-block sums of squares into partial[bid].
 // t = b_r - sum over off-diagonal entries in stored order (diag_pos skips the diagonal); rows with
 // |d| <= 1e-20 keep their value.
 template <int MODE>
@@ -344,7 +361,8 @@ __global__ __launch_bounds__(kBlock) void relax_range(int blo, const int *__rest
                                                       const double *__restrict__ b, double *x,
                                                       const double *__restrict__ yp, double *__restrict__ y,
                                                       const double *__restrict__ deff, const unsigned *__restrict__ pk,
-                                                      const double *__restrict__ pv, const int2 *__restrict__ pb)
+                                                      const double *__restrict__ pv, const int2 *__restrict__ pb,
+                                                      double *__restrict__ rr, double *__restrict__ partial)
 {
     __shared__ SpmvSmem sm;
     const int bid = blo + xcd_bid();
@@ -353,7 +371,7 @@ __global__ __launch_bounds__(kBlock) void relax_range(int blo, const int *__rest
     auto fetch = [&](int c) -> double { return x[c]; };
     auto finish = [&](int r, double acc) {
         const double d = deff[r];
-        if (MODE == 0) {
+        if (MODE != 1) {
             if (fabs(d) > SMALLFLOAT) x[r] = acc / d;
         } else {
             y[r - lo] = fabs(d) > SMALLFLOAT ? acc / d : x[r];
@@ -362,19 +380,39 @@ __global__ __launch_bounds__(kBlock) void relax_range(int blo, const int *__rest
     if (k1 - k0 <= kTileEntries) {
         const int r = r0 + (int)threadIdx.x;
         int a = 0, e = 0, dp = -1;
-        double acc = 0.0;
-        if (r < r1) a = rp[r] - k0, e = rp[r + 1] - k0, dp = diag_pos[r], acc = b[r];   // ahead of the tile
+        double acc = 0.0, br = 0.0;
+        if (r < r1) a = rp[r] - k0, e = rp[r + 1] - k0, dp = diag_pos[r], br = b[r];   // ahead of the tile
         stage_any(sm.v, k0, k1, ci, v, pk, pv, pb, bid, fetch);
         __syncthreads();
+        double sq = 0.0;
         if (r < r1) {
+            acc = br;
             if (dp < 0) acc = chain_sub(acc, sm.v, a, e);
             else {
                 acc = chain_sub(acc, sm.v, a, dp - k0);
                 acc = chain_sub(acc, sm.v, dp - k0 + 1, e);
             }
-            finish(r, acc);
+            if constexpr (MODE == 2) {   // plan guarantees one diagonal per row, deff = a_rr
+                const double d = deff[r];
+                const double xn = fabs(d) > SMALLFLOAT ? acc / d : x[r];
+                if (fabs(d) > SMALLFLOAT) x[r] = xn;
+                double s = chain_add(0.0, sm.v, a, dp - k0);
+                s += d * xn;
+                s = chain_add(s, sm.v, dp - k0 + 1, e);
+                const double out = br + s * -1.0;
+                rr[r] = out;
+                sq = out * out;
+            } else {
+                finish(r, acc);
+            }
         }
-    } else {
+        if constexpr (MODE == 2) {
+            if (partial) {
+                const double t = block_sum(sq, sm.red);
+                if (threadIdx.x == 0) partial[bid] = t;
+            }
+        }
+    } else if constexpr (MODE != 2) {   // MODE 2 plans have no long-row block
         const int r = r0, dp = diag_pos[r];
         double acc = b[r];
         for (int base = k0; base < k1; base += kTileEntries) {
@@ -589,8 +627,9 @@ __global__ __launch_bounds__(kBlock) void scatter_rows(int m, const int *__restr
 }
 
 int smoother_run(const SmootherPlan &sp, const DevCSR &A, const double *b, double *x, int sweeps, hipStream_t s,
-                 const PassHooks *hk)
+                 const PassHooks *hk, ResidFuse *rf)
 {
+    if (rf) rf->done = false;
     const int n = A.n;
     if (n == 0) return 0;
     int rc;
@@ -616,7 +655,8 @@ int smoother_run(const SmootherPlan &sp, const DevCSR &A, const double *b, doubl
                                            A.rp, cols, A.v, b, x, yp, y, deff);
                     else
                         hipLaunchKernelGGL(relax_range<M>, dim3(nb), dim3(kBlock), 0, s, ps.blo, A.blk, A.rp, cols,
-                                           A.v, sp.diag_pos, ps.lo, b, x, yp, y, deff, A.pk, A.pv, A.pb);
+                                           A.v, sp.diag_pos, ps.lo, b, x, yp, y, deff, A.pk, A.pv, A.pb,
+                                           (double *)nullptr, (double *)nullptr);
                 };
                 if (sp.kind == SSS_HIP_SMOOTH_JACOBI && sp.inner > 0 && hk) {
                     // iterates live in full-length work vectors whose ghosts (lower-rank rows of
@@ -643,6 +683,11 @@ int smoother_run(const SmootherPlan &sp, const DevCSR &A, const double *b, doubl
                 } else if (sp.kind == SSS_HIP_SMOOTH_JACOBI) {
                     relax(std::integral_constant<int, 1>(), A.ci, (const double *)nullptr, ps.y);
                     SSS_HIP(hipMemcpyAsync(x + ps.lo, ps.y, sizeof(double) * (size_t)m, hipMemcpyDeviceToDevice, s));
+                } else if (rf && sp.fuse_resid && c == 1 && sw + 1 == sweeps && !hk) {
+                    hipLaunchKernelGGL(relax_range<2>, dim3(nb), dim3(kBlock), 0, s, ps.blo, A.blk, A.rp, A.ci, A.v,
+                                       sp.diag_pos, ps.lo, b, x, (const double *)nullptr, (double *)nullptr, deff,
+                                       A.pk, A.pv, A.pb, rf->r, rf->partial);
+                    rf->done = true;
                 } else {
                     relax(std::integral_constant<int, 0>(), A.ci, (const double *)nullptr, (double *)nullptr);
                 }

@@ -290,6 +290,21 @@ int launch_spmv(const DevCSR &A, int op, double alpha, const double *x, const do
     return 0;
 }
 
+int launch_spmv_blocks(const DevCSR &A, int nblk, int op, double alpha, const double *x, const double *b, double *y,
+                       double *partial, hipStream_t s)
+{
+    if (A.wave_rows || nblk > A.nblk || op != SSS_HIP_SPMV_RESID) return ERROR_INPUT_PAR;
+    if (nblk <= 0) return 0;
+    if (partial)
+        hipLaunchKernelGGL((spmv_adaptive<SSS_HIP_SPMV_RESID, true>), dim3(nblk), dim3(kBlock), 0, s, A.blk, A.rp,
+                           A.ci, A.v, x, b, y, alpha, 0, partial, A.pk, A.pv, A.pb);
+    else
+        hipLaunchKernelGGL((spmv_adaptive<SSS_HIP_SPMV_RESID, false>), dim3(nblk), dim3(kBlock), 0, s, A.blk, A.rp,
+                           A.ci, A.v, x, b, y, alpha, 0, partial, A.pk, A.pv, A.pb);
+    SSS_HIP(hipGetLastError());
+    return 0;
+}
+
 // ---- deterministic final reduction ----------------------------------------------------------
 __global__ __launch_bounds__(1024) void final_sum_kernel(const double *__restrict__ partials, int n,
                                                          double *__restrict__ out, int take_sqrt)

@@ -358,6 +358,30 @@ def test_solve_hybrid_krylov_bitwise(request, hname, inner, inner_from, row_path
     assert np.allclose(rel_g, rel_r, rtol=1e-13, atol=0)
 
 
+@pytest.mark.parametrize("smoother,coarse", [("exact", "krylov"), ("hybrid", "direct")])
+def test_fused_residual_bitwise(p32_h, smoother, coarse, monkeypatch):
+    """Level 0 of 7-pt Poisson is red-black, so the last C pass of each smoother call also writes
+    the C rows of r = b - A x (ResidFuse).  With fusion on/off: x, the in-cycle residual wp and
+    the outer residual norm are bitwise identical over several cycles."""
+    n = p32_h.level(0).A.num_rows
+    out = []
+    for fuse in ("1", "0"):
+        monkeypatch.setenv("SSS_HIP_FUSE_RESID", fuse)
+        D = A.DeviceHierarchy(p32_h, smoother=smoother, coarse=coarse)
+        D.upload(0, "b", np.ones(n))
+        D.upload(0, "x", np.ones(n))
+        norms = []
+        for _ in range(4):
+            D.cycle()
+            norms.append(D.residual_norm())
+        out.append((np.array(norms), D.download(0, "x"), D.download(0, "wp")))
+        D.close()
+    (n1, x1, w1), (n0, x0, w0) = out
+    assert np.array_equal(n1.view(np.uint64), n0.view(np.uint64))
+    assert np.array_equal(x1.view(np.uint64), x0.view(np.uint64))
+    assert np.array_equal(w1.view(np.uint64), w0.view(np.uint64))
+
+
 def test_solve_bus_known_answer(bus_h):
     """GPU history equals the reference's printed table."""
     expect = [2.907170e+00, 4.389125e-01, 1.321964e-01, 4.453643e-02, 1.213532e-02, 3.537244e-03, 1.358532e-03,
