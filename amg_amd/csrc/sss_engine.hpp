@@ -161,6 +161,12 @@ struct SmootherPlan {
     bool long_rows = false;    // wave-per-row kernels
     int *diag_pos = nullptr;   // range passes: CSR position of each row's diagonal (-1: none)
     int inner = 0;             // two-stage GS-CF inner steps (kind == JACOBI, range passes only)
+    // No-copy C/F-Jacobi (kind == JACOBI, both passes range, class split at csplit): a pass writes
+    // its class's new values into the other of {x, x2} and later passes read each class from where
+    // its current values are; an even number of writes per class (the default 2 sweeps) leaves
+    // everything back in x.
+    double *x2 = nullptr;
+    int csplit = 0;
     // The last class pass of a call (C, rows [split_row, n)) can also write the residual
     // r = b - A x of its rows (ResidFuse): exact GS with depth-1 range passes (a red-black level),
     // every row with exactly one diagonal, no long-row block among the C blocks.
@@ -188,7 +194,15 @@ struct PassHooks {
 };
 int smoother_build(SmootherPlan &sp, const SSS_MAT &A, const int *mark, int kind, const DevCSR *dA = nullptr,
                    int inner = 0, const int *gcls = nullptr, int enc = 0);
-void launch_ts_stage0(const DevCSR &M, int lo, const int *split, const double *b, const double *x, const double *deff,
+// Where a pass reads its x values from: columns < split from f, the others from c.  The no-copy
+// C/F-Jacobi form keeps each class's current values in x or in the plan's second vector x2.
+struct XSrc {
+    const double *f, *c;
+    int split;
+    __device__ __forceinline__ double operator()(int j) const { return j < split ? f[j] : c[j]; }
+};
+inline XSrc xsrc_of(const double *x) { return XSrc{x, x, 0x7fffffff}; }
+void launch_ts_stage0(const DevCSR &M, int lo, const int *split, const double *b, XSrc x, const double *deff,
                       double *P, double *y, hipStream_t s);
 void launch_ts_inner(const DevCSR &M, int lo, const double *deff, const double *P, const double *ycols, int col_off,
                      const double *ykeep, double *y, hipStream_t s);

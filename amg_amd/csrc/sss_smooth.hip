@@ -219,6 +219,17 @@ int smoother_build(SmootherPlan &sp, const SSS_MAT &A, const int *mark, int kind
     }
     if (sp.pass[0].range || sp.pass[1].range)
         if ((rc = upload_ints(&sp.diag_pos, diag_pos))) return rc;
+    const char *nc = getenv("SSS_HIP_NOCOPY");   // 0: C/F-Jacobi through per-pass copies (tests)
+    if (!(nc && *nc == '0') && kind == SSS_HIP_SMOOTH_JACOBI && !gcls && A.num_cols == n) {
+        const PassSchedule &F = sp.pass[0], &Cp = sp.pass[1];
+        const bool f_ok = F.nrows == 0 || (F.range && F.lo == 0), c_ok = Cp.nrows == 0 || (Cp.range && Cp.hi == n);
+        const int cs = F.nrows > 0 ? F.hi : 0;
+        if (f_ok && c_ok && (Cp.nrows == 0 || Cp.lo == cs) && (F.nrows > 0 || Cp.nrows > 0)) {
+            sp.csplit = cs;
+            sp.x2 = dev_alloc<double>((size_t)n);
+            if (!sp.x2) return hip_fail(hipErrorOutOfMemory, "hipMalloc(x2)", __FILE__, __LINE__);
+        }
+    }
     const char *fz = getenv("SSS_HIP_FUSE_RESID");   // 0: never fuse (tests compare both paths)
     if (!(fz && *fz == '0') && kind != SSS_HIP_SMOOTH_JACOBI && dA && !dA->wave_rows && all_diag && single_diag &&
         dA->split_row > 0 &&
@@ -259,6 +270,7 @@ void smoother_free(SmootherPlan &sp)
     dev_free(sp.d_first);
     dev_free(sp.cls);
     dev_free(sp.diag_pos);
+    dev_free(sp.x2);
     sp = SmootherPlan();
 }
 
@@ -362,19 +374,19 @@ __global__ __launch_bounds__(kBlock) void relax_range(int blo, const int *__rest
                                                       const double *__restrict__ yp, double *__restrict__ y,
                                                       const double *__restrict__ deff, const unsigned *__restrict__ pk,
                                                       const double *__restrict__ pv, const int2 *__restrict__ pb,
-                                                      double *__restrict__ rr, double *__restrict__ partial)
+                                                      double *__restrict__ rr, double *__restrict__ partial, XSrc xs)
 {
     __shared__ SpmvSmem sm;
     const int bid = blo + xcd_bid();
     const int r0 = blk[bid], r1 = blk[bid + 1];
     const int k0 = rp[r0], k1 = rp[r1];
-    auto fetch = [&](int c) -> double { return x[c]; };
+    auto fetch = [&](int c) -> double { return MODE == 1 ? xs(c) : x[c]; };
     auto finish = [&](int r, double acc) {
         const double d = deff[r];
         if (MODE != 1) {
             if (fabs(d) > SMALLFLOAT) x[r] = acc / d;
         } else {
-            y[r - lo] = fabs(d) > SMALLFLOAT ? acc / d : x[r];
+            y[r - lo] = fabs(d) > SMALLFLOAT ? acc / d : xs(r);
         }
     };
     if (k1 - k0 <= kTileEntries) {
@@ -441,13 +453,13 @@ __global__ __launch_bounds__(kBlock) void relax_range_wave(int lo, int hi, const
                                                            const int *__restrict__ ci, const double *__restrict__ v,
                                                            const double *__restrict__ b, double *x,
                                                            const double *__restrict__ yp, double *__restrict__ y,
-                                                           const double *__restrict__ deff)
+                                                           const double *__restrict__ deff, XSrc xs)
 {
     __shared__ double strips[TREE ? 1 : 4][TREE ? 1 : kWaveStage];
     const int wave = threadIdx.x >> 6;
     const int r = lo + xcd_bid() * 4 + wave;
     if (r >= hi) return;
-    auto prod = [&](int c, double a) -> double { return c == r ? 0.0 : a * x[c]; };
+    auto prod = [&](int c, double a) -> double { return c == r ? 0.0 : a * (MODE == 1 ? xs(c) : x[c]); };
     const double acc = TREE ? b[r] - wave_row_sum(rp[r], rp[r + 1], ci, v, prod)
                             : wave_row_chain<true>(rp[r], rp[r + 1], ci, v, prod, b[r], strips[TREE ? 0 : wave]);
     if ((threadIdx.x & 63) == 0) {
@@ -455,7 +467,7 @@ __global__ __launch_bounds__(kBlock) void relax_range_wave(int lo, int hi, const
         if (MODE == 0) {
             if (fabs(d) > SMALLFLOAT) x[r] = acc / d;
         } else {
-            y[r - lo] = fabs(d) > SMALLFLOAT ? acc / d : x[r];
+            y[r - lo] = fabs(d) > SMALLFLOAT ? acc / d : xs(r);
         }
     }
 }
@@ -465,19 +477,19 @@ __global__ __launch_bounds__(kBlock) void relax_range_wave(int lo, int hi, const
 //   P_q = b - sum_{N_i} a x;  y_q = (P_q - sum_{L_i} a x) / d   (x from before the pass)
 template <int PATH>   // 0 tile, 1 wave chain, 2 wave tree (free order)
 __global__ __launch_bounds__(kBlock) void ts_stage0(int lo, DevCSR M, const int *__restrict__ split,
-                                                    const double *__restrict__ b, const double *__restrict__ x,
+                                                    const double *__restrict__ b, XSrc x,
                                                     const double *__restrict__ deff, double *__restrict__ P,
                                                     double *__restrict__ y)
 {
     auto finish = [&](int q, double acc) {
         const int r = lo + q;
         const double d = deff[r];
-        y[q] = fabs(d) > SMALLFLOAT ? acc / d : x[r];
+        y[q] = fabs(d) > SMALLFLOAT ? acc / d : x(r);
     };
     if constexpr (PATH == 2) {
         const int q = xcd_bid() * 4 + (threadIdx.x >> 6);
         if (q >= M.n) return;
-        auto prod = [&](int c, double a) { return a * x[c]; };
+        auto prod = [&](int c, double a) { return a * x(c); };
         const int a = M.rp[q], sp = split[q], e = M.rp[q + 1];
         const double Pq = b[lo + q] - wave_row_sum(a, sp, M.ci, M.v, prod);
         const double acc = Pq - wave_row_sum(sp, e, M.ci, M.v, prod);
@@ -490,7 +502,7 @@ __global__ __launch_bounds__(kBlock) void ts_stage0(int lo, DevCSR M, const int 
         __shared__ double strips[4][kWaveStage];
         const int wave = threadIdx.x >> 6, q = xcd_bid() * 4 + wave;
         if (q >= M.n) return;
-        auto prod = [&](int c, double a) { return a * x[c]; };
+        auto prod = [&](int c, double a) { return a * x(c); };
         const int a = M.rp[q], sp = split[q], e = M.rp[q + 1];
         double acc = wave_row_chain<true>(a, sp, M.ci, M.v, prod, b[lo + q], strips[wave]);
         acc = __shfl(acc, 0, 64);
@@ -507,7 +519,7 @@ __global__ __launch_bounds__(kBlock) void ts_stage0(int lo, DevCSR M, const int 
             int a = 0, sp = 0, e = 0;
             double acc = 0.0;
             if (q < q1) a = M.rp[q] - k0, sp = split[q] - k0, e = M.rp[q + 1] - k0, acc = b[lo + q];
-            stage_any(sm.v, k0, k1, M.ci, M.v, M.pk, M.pv, M.pb, bq, [&](int c) -> double { return x[c]; });
+            stage_any(sm.v, k0, k1, M.ci, M.v, M.pk, M.pv, M.pb, bq, [&](int c) -> double { return x(c); });
             __syncthreads();
             if (q < q1) {
                 acc = chain_sub(acc, sm.v, a, sp);
@@ -520,7 +532,7 @@ __global__ __launch_bounds__(kBlock) void ts_stage0(int lo, DevCSR M, const int 
             double acc = b[lo + q];
             for (int base = k0; base < k1; base += kTileEntries) {
                 const int m = min(kTileEntries, k1 - base);
-                stage_any(sm.v, base, base + m, M.ci, M.v, M.pk, M.pv, M.pb, bq, [&](int c) -> double { return x[c]; });
+                stage_any(sm.v, base, base + m, M.ci, M.v, M.pk, M.pv, M.pb, bq, [&](int c) -> double { return x(c); });
                 __syncthreads();
                 if (threadIdx.x == 0) {
                     if (sp >= base && sp < base + m) {
@@ -595,7 +607,7 @@ __global__ __launch_bounds__(kBlock) void ts_inner(int lo, DevCSR M, const doubl
     }
 }
 
-void launch_ts_stage0(const DevCSR &M, int lo, const int *split, const double *b, const double *x, const double *deff,
+void launch_ts_stage0(const DevCSR &M, int lo, const int *split, const double *b, XSrc x, const double *deff,
                       double *P, double *y, hipStream_t s)
 {
     if (M.n == 0) return;
@@ -633,6 +645,9 @@ int smoother_run(const SmootherPlan &sp, const DevCSR &A, const double *b, doubl
     const int n = A.n;
     if (n == 0) return 0;
     int rc;
+    // no-copy C/F-Jacobi: where each class's current values live (x or sp.x2)
+    const bool nocopy = sp.x2 && !hk;
+    double *cur[2] = {x, x};
     for (int sw = 0; sw < sweeps; ++sw) {
         const double *deff = sw == 0 ? sp.d_first : sp.d_later;
         for (int c = 0; c < 2; ++c) {
@@ -645,48 +660,62 @@ int smoother_run(const SmootherPlan &sp, const DevCSR &A, const double *b, doubl
             if (ps.range) {
                 const int nb = ps.bhi - ps.blo, m = ps.hi - ps.lo, nw = (m + 3) / 4;
                 const bool wave = A.wave_rows;
+                const XSrc xs = nocopy ? XSrc{cur[0], cur[1], sp.csplit} : xsrc_of(x);
                 auto relax = [&](auto mode, const int *cols, const double *yp, double *y) {
                     constexpr int M = decltype(mode)::value;
                     if (wave && A.vec_rows)
                         hipLaunchKernelGGL((relax_range_wave<M, true>), dim3(nw), dim3(kBlock), 0, s, ps.lo, ps.hi,
-                                           A.rp, cols, A.v, b, x, yp, y, deff);
+                                           A.rp, cols, A.v, b, x, yp, y, deff, xs);
                     else if (wave)
                         hipLaunchKernelGGL((relax_range_wave<M, false>), dim3(nw), dim3(kBlock), 0, s, ps.lo, ps.hi,
-                                           A.rp, cols, A.v, b, x, yp, y, deff);
+                                           A.rp, cols, A.v, b, x, yp, y, deff, xs);
                     else
                         hipLaunchKernelGGL(relax_range<M>, dim3(nb), dim3(kBlock), 0, s, ps.blo, A.blk, A.rp, cols,
                                            A.v, sp.diag_pos, ps.lo, b, x, yp, y, deff, A.pk, A.pv, A.pb,
-                                           (double *)nullptr, (double *)nullptr);
+                                           (double *)nullptr, (double *)nullptr, xs);
                 };
                 if (sp.kind == SSS_HIP_SMOOTH_JACOBI && sp.inner > 0 && hk) {
                     // iterates live in full-length work vectors whose ghosts (lower-rank rows of
                     // this class) are refreshed after every stage
                     const DevCSR &Mn = ps.ts_nl, &Ml = ps.ts_lo;
-                    double *cur = hk->w0, *nxt = hk->w1;
-                    launch_ts_stage0(Mn, ps.lo, ps.ts_split, b, x, deff, ps.ts_P, cur + ps.lo, s);
+                    double *wcur = hk->w0, *wnxt = hk->w1;
+                    launch_ts_stage0(Mn, ps.lo, ps.ts_split, b, xsrc_of(x), deff, ps.ts_P, wcur + ps.lo, s);
                     for (int st = 0; st < sp.inner; ++st) {
-                        if ((rc = hk->exchange(hk->ctx, cur))) return rc;
-                        launch_ts_inner(Ml, ps.lo, deff, ps.ts_P, cur, 0, cur + ps.lo, nxt + ps.lo, s);
-                        std::swap(cur, nxt);
+                        if ((rc = hk->exchange(hk->ctx, wcur))) return rc;
+                        launch_ts_inner(Ml, ps.lo, deff, ps.ts_P, wcur, 0, wcur + ps.lo, wnxt + ps.lo, s);
+                        std::swap(wcur, wnxt);
                     }
-                    SSS_HIP(hipMemcpyAsync(x + ps.lo, cur + ps.lo, sizeof(double) * (size_t)m, hipMemcpyDeviceToDevice,
+                    SSS_HIP(hipMemcpyAsync(x + ps.lo, wcur + ps.lo, sizeof(double) * (size_t)m, hipMemcpyDeviceToDevice,
                                            s));
+                } else if (sp.kind == SSS_HIP_SMOOTH_JACOBI && nocopy) {
+                    // stage 0 (or the Jacobi pass) writes the other buffer; inner steps read only this
+                    // class's previous iterate, so they alternate between the two buffers in place
+                    double *prev = cur[c] == x ? sp.x2 : x, *next = cur[c];
+                    if (sp.inner > 0)
+                        launch_ts_stage0(ps.ts_nl, ps.lo, ps.ts_split, b, xs, deff, ps.ts_P, prev + ps.lo, s);
+                    else
+                        relax(std::integral_constant<int, 1>(), A.ci, (const double *)nullptr, prev + ps.lo);
+                    for (int st = 0; st < sp.inner; ++st) {
+                        launch_ts_inner(ps.ts_lo, ps.lo, deff, ps.ts_P, prev, 0, prev + ps.lo, next + ps.lo, s);
+                        std::swap(prev, next);
+                    }
+                    cur[c] = prev;
                 } else if (sp.kind == SSS_HIP_SMOOTH_JACOBI && sp.inner > 0) {
                     const DevCSR &Mn = ps.ts_nl, &Ml = ps.ts_lo;
-                    launch_ts_stage0(Mn, ps.lo, ps.ts_split, b, x, deff, ps.ts_P, ps.y, s);
-                    double *cur = ps.y, *nxt = ps.y2;
+                    launch_ts_stage0(Mn, ps.lo, ps.ts_split, b, xsrc_of(x), deff, ps.ts_P, ps.y, s);
+                    double *ycur = ps.y, *ynxt = ps.y2;
                     for (int st = 0; st < sp.inner; ++st) {
-                        launch_ts_inner(Ml, ps.lo, deff, ps.ts_P, cur, ps.lo, cur, nxt, s);
-                        std::swap(cur, nxt);
+                        launch_ts_inner(Ml, ps.lo, deff, ps.ts_P, ycur, ps.lo, ycur, ynxt, s);
+                        std::swap(ycur, ynxt);
                     }
-                    SSS_HIP(hipMemcpyAsync(x + ps.lo, cur, sizeof(double) * (size_t)m, hipMemcpyDeviceToDevice, s));
+                    SSS_HIP(hipMemcpyAsync(x + ps.lo, ycur, sizeof(double) * (size_t)m, hipMemcpyDeviceToDevice, s));
                 } else if (sp.kind == SSS_HIP_SMOOTH_JACOBI) {
                     relax(std::integral_constant<int, 1>(), A.ci, (const double *)nullptr, ps.y);
                     SSS_HIP(hipMemcpyAsync(x + ps.lo, ps.y, sizeof(double) * (size_t)m, hipMemcpyDeviceToDevice, s));
                 } else if (rf && sp.fuse_resid && c == 1 && sw + 1 == sweeps && !hk) {
                     hipLaunchKernelGGL(relax_range<2>, dim3(nb), dim3(kBlock), 0, s, ps.blo, A.blk, A.rp, A.ci, A.v,
                                        sp.diag_pos, ps.lo, b, x, (const double *)nullptr, (double *)nullptr, deff,
-                                       A.pk, A.pv, A.pb, rf->r, rf->partial);
+                                       A.pk, A.pv, A.pb, rf->r, rf->partial, xs);
                     rf->done = true;
                 } else {
                     relax(std::integral_constant<int, 0>(), A.ci, (const double *)nullptr, (double *)nullptr);
@@ -725,6 +754,10 @@ int smoother_run(const SmootherPlan &sp, const DevCSR &A, const double *b, doubl
             }
         }
     }
+    for (int c = 0; c < 2; ++c)   // odd number of writes to a class (odd sweeps x (1 + inner))
+        if (cur[c] != x)
+            SSS_HIP(hipMemcpyAsync(x + sp.pass[c].lo, cur[c] + sp.pass[c].lo,
+                                   sizeof(double) * (size_t)(sp.pass[c].hi - sp.pass[c].lo), hipMemcpyDeviceToDevice, s));
     SSS_HIP(hipGetLastError());
     return 0;
 }

@@ -382,6 +382,21 @@ def test_fused_residual_bitwise(p32_h, smoother, coarse, monkeypatch):
     assert np.array_equal(w1.view(np.uint64), w0.view(np.uint64))
 
 
+@pytest.mark.parametrize("hname", ["p32_h", "a27_h"])
+@pytest.mark.parametrize("smoother,inner", [("hybrid", 0), ("hybrid", 1), ("jacobi", 2)])
+def test_nocopy_jacobi_bitwise(request, hname, smoother, inner, monkeypatch):
+    """C/F-Jacobi and two-stage passes writing into a second x vector and reading each class from
+    where its current values live (SmootherPlan::x2) give the iterates of the copy-per-pass form."""
+    H = request.getfixturevalue(hname)
+    xs = []
+    for nc in ("1", "0"):
+        monkeypatch.setenv("SSS_HIP_NOCOPY", nc)
+        rel, x = _gpu_history(H, smoother, "direct", max_it=6, inner=inner, inner_from=1)
+        xs.append((rel, x))
+    assert np.array_equal(xs[0][1].view(np.uint64), xs[1][1].view(np.uint64))
+    assert np.array_equal(xs[0][0].view(np.uint64), xs[1][0].view(np.uint64))
+
+
 def test_solve_bus_known_answer(bus_h):
     """GPU history equals the reference's printed table."""
     expect = [2.907170e+00, 4.389125e-01, 1.321964e-01, 4.453643e-02, 1.213532e-02, 3.537244e-03, 1.358532e-03,
