@@ -47,6 +47,9 @@ def parse():
     p.add_argument("--grid", "--n", dest="n", type=int, default=400, help="grid edge (400 -> 64M rows)")
     p.add_argument("--mode", default="throughput", choices=["throughput", "parity"])
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--cpu-threads", type=int, default=0,
+                   help="threads of the multi-core CPU baseline in the GPU's mode (default: OMP_NUM_THREADS or 16, "
+                        "at most the host CPUs; 0 disables it with --no-cpu-baseline)")
     p.add_argument("--cpu-n", type=int, default=0, help="grid edge of the CPU sample (default: same workload)")
     p.add_argument("--mode-smoother", default=None, help="override: exact|hybrid|jacobi")
     p.add_argument("--mode-coarse", default=None, help="override: krylov|direct")
@@ -114,26 +117,48 @@ def quiet_call(fn, *a, **kw):
         os.close(saved)
 
 
-def cpu_baseline_worker(H, out: dict):
-    """One outer iteration of the CPU restatement (reference semantics, 1 thread)."""
+def cpu_iterations(H, out: dict, threads: int = 1, iters: int = 1, warmup: int = 0, **mode):
+    """Outer iterations (V-cycle, r = b - A0 x, ||r||) of the CPU restatement oracle/sss_oracle.c.
+    threads = 1 with no mode keys: exactly the reference's serial host path (GS-CF everywhere,
+    CG(beta=1)+GMRES coarse solve).  threads > 1: its row loops on that many host threads (results
+    unchanged).  mode: oracle options, e.g. the GPU throughput mode (smoother=1, inner=1,
+    inner_mask, coarse_mode=1)."""
     import oracle
     ora = oracle.load()
+    ora.ora_set_threads(threads)
     n = H.level(0).A.num_rows
     b = np.ones(n)
     x = np.ones(n)
     from amg_amd._native import SSS_VEC, dptr
     H.mg.cg[0].x = SSS_VEC(n, dptr(x))
     H.mg.cg[0].b = SSS_VEC(n, dptr(b))
-    opts = oracle.opts()
+    opts = oracle.opts(**mode)
+    r = np.empty(n)
+
+    def one():
+        ora.ora_cycle(C.byref(H.mg), C.byref(opts))
+        r[:] = b
+        ora.ora_mv_amxpy(-1.0, C.byref(H.level(0).A), dptr(x), dptr(r), 0)
+        return float(np.sqrt(np.dot(r, r)))
+
+    for _ in range(warmup):
+        one()
     ora.ora_reset_timers()
     t0 = time.perf_counter()
-    ora.ora_cycle(C.byref(H.mg), C.byref(opts))
-    r = np.empty(n)
-    r[:] = b
+    for _ in range(iters):
+        one()
+    dt = (time.perf_counter() - t0) / iters
+    # the fine-level SpMV of the CPU path, for the GB/s column (one r = b - A0 x)
+    t1 = time.perf_counter()
     ora.ora_mv_amxpy(-1.0, C.byref(H.level(0).A), dptr(x), dptr(r), 0)
-    float(np.sqrt(np.dot(r, r)))
-    dt = time.perf_counter() - t0
-    out.update(seconds=dt, coarse_seconds=ora.ora_coarse_seconds())
+    spmv_s = time.perf_counter() - t1
+    out.update(seconds=dt, coarse_seconds=ora.ora_coarse_seconds() / iters, threads=ora.ora_get_threads(),
+               spmv_seconds=spmv_s)
+
+
+def cpu_baseline_worker(H, out: dict):
+    """One outer iteration of the CPU restatement (reference semantics, 1 thread)."""
+    cpu_iterations(H, out, threads=1, iters=1)
 
 
 class Single:
@@ -310,17 +335,39 @@ def main():
             traffic = None
 
     cpu_baseline = None
+    cpu_mt = None
     if cpu_thread is not None:
         cpu_thread.join()
+        cpu_n = args.cpu_n or n
+        a0_bytes = 12 * nnz + 4 * (N + 1) + 24 * N
         if cpu.get("seconds"):
-            cpu_n = args.cpu_n or n
             cpu_baseline = {
                 "value": 1.0 / cpu["seconds"], "unit": "V-cycle iter/s", "cores": 1, "kind": "port",
                 "sample": f"one outer iteration (V-cycle incl. reference CG(beta=1)+GMRES coarse solve, "
                           f"residual, norm) of oracle/sss_oracle.c on the same 7-pt {cpu_n}^3 hierarchy, "
                           f"1 host thread; coarse solve {cpu['coarse_seconds']:.1f} s of {cpu['seconds']:.1f} s",
                 "seconds": cpu["seconds"], "coarse_seconds": cpu["coarse_seconds"],
+                "fine_spmv_GBps": a0_bytes / cpu["spmv_seconds"] / 1e9 if cpu_n == n else None,
             }
+        # the same restatement in the GPU's own mode, its row loops on the host cores, after the GPU
+        # measurements (it would otherwise compete with the launch thread)
+        thr = args.cpu_threads or int(os.environ.get("OMP_NUM_THREADS", "16"))
+        thr = max(1, min(thr, os.cpu_count() or 1))
+        mt = {}
+        mode = {}
+        if args.mode == "throughput":
+            mode = dict(smoother=1, jacobi_from=1, coarse_mode=1 if coarse == "direct" else 0,
+                        inner=inner if smoother != "exact" else 0, inner_mask=~((1 << inner_from) - 1))
+        cpu_iterations(Hc, mt, threads=thr, iters=2, warmup=1, **mode)
+        cpu_mt = {
+            "value": 1.0 / mt["seconds"], "unit": "V-cycle iter/s", "cores": mt["threads"], "kind": "port",
+            "sample": f"2 outer iterations after 1 warm-up, oracle/sss_oracle.c in the GPU's mode "
+                      f"({smoother} smoother, {coarse} coarse solve) on the same 7-pt {cpu_n}^3 hierarchy, "
+                      f"row loops on {mt['threads']} host threads; coarse solve {mt['coarse_seconds']:.2f} s "
+                      f"of {mt['seconds']:.2f} s",
+            "seconds": mt["seconds"], "coarse_seconds": mt["coarse_seconds"],
+            "fine_spmv_GBps": a0_bytes / mt["spmv_seconds"] / 1e9 if cpu_n == n else None,
+        }
 
     rec = {
         "metric": "V-cycle iters/sec + fine-level SpMV GB/s (%HBM peak), 64M-row 7pt Poisson",
@@ -344,9 +391,12 @@ def main():
                      "frac_of_copy_peak": achieved / COPY_PEAK_GBS, "avg_launch_ms": spmv_ms,
                      "bytes_per_launch": spmv_bytes, "traffic": traffic},
         "cpu_baseline": cpu_baseline,
+        "cpu_baseline_same_mode": cpu_mt,
     }
     if cpu_baseline:
         rec["speedup_vs_cpu"] = value / cpu_baseline["value"]
+    if cpu_mt:
+        rec["speedup_vs_cpu_same_mode"] = value / cpu_mt["value"]
     DH.close()
     hb_stop.set()
     if D.rank == 0:

@@ -41,6 +41,8 @@ def load():
         dp, ip = P(C.c_double), P(C.c_int)
         sigs = {
             "ora_opts_default": (None, [P(ORA_OPTS)]),
+            "ora_set_threads": (None, [C.c_int]),
+            "ora_get_threads": (C.c_int, []),
             "ora_mv_amxpy": (None, [C.c_double, P(SSS_MAT), dp, dp, C.c_int]),
             "ora_mv_mxy": (None, [P(SSS_MAT), dp, dp]),
             "ora_mv_acc": (None, [P(SSS_MAT), dp, dp, C.c_int]),

@@ -34,6 +34,7 @@
 #include "sss_oracle.h"
 
 #include <math.h>
+#include <omp.h>
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -116,22 +117,31 @@ static double row_sum(const SSS_MAT *A, const double *x, int i)
     return s;
 }
 
+/* Row loops below may run on several host threads (ora_set_threads; bench.py's multi-core CPU
+ * baseline): every row is still summed sequentially in stored order by one thread, so the
+ * results do not depend on the thread count. */
 void ora_mv_amxpy(double alpha, const SSS_MAT *A, const double *x, double *y, int cap)
 {
     const int m = capped_rows(A->num_rows, cap);
+#pragma omp parallel for schedule(static, 4096)
     for (int i = 0; i < m; ++i) y[i] += row_sum(A, x, i) * alpha;
 }
 
 void ora_mv_mxy(const SSS_MAT *A, const double *x, double *y)
 {
+#pragma omp parallel for schedule(static, 4096)
     for (int i = 0; i < A->num_rows; ++i) y[i] = row_sum(A, x, i);
 }
 
 void ora_mv_acc(const SSS_MAT *A, const double *x, double *y, int cap)
 {
     const int m = capped_rows(A->num_rows, cap);
+#pragma omp parallel for schedule(static, 4096)
     for (int i = 0; i < m; ++i) y[i] += row_sum(A, x, i);
 }
+
+void ora_set_threads(int n) { omp_set_num_threads(n > 0 ? n : 1); }
+int ora_get_threads(void) { return omp_get_max_threads(); }
 
 /* ---------------------------------------------------------------- smoothers */
 /* one Gauss-Seidel pass over the rows selected by want(mark[i]); d is carried (stale) */
@@ -151,12 +161,64 @@ static void gs_pass(double *u, const SSS_MAT *A, const double *b, const int *mar
     }
 }
 
+/* Rows of the class are independent (no same-class off-diagonal entry) and each has exactly one
+ * diagonal entry: then the pass gives the same values in any row order (the carried d is always
+ * the row's own diagonal), so it may run on several threads.  Cached per (matrix, class). */
+static int gs_pass_independent(const SSS_MAT *A, const int *mark, int c_rows)
+{
+    static struct { const int *ci; const int *mark; int c; int ok; } cache[16];
+    static int ncache = 0;
+    for (int q = 0; q < ncache; ++q)
+        if (cache[q].ci == A->col_idx && cache[q].mark == mark && cache[q].c == c_rows) return cache[q].ok;
+    int ok = 1;
+#pragma omp parallel for reduction(&& : ok) schedule(static, 4096)
+    for (int i = 0; i < A->num_rows; ++i) {
+        if ((mark[i] == 1) != c_rows) continue;
+        int nd = 0;
+        for (int k = A->row_ptr[i]; k < A->row_ptr[i + 1]; ++k) {
+            const int j = A->col_idx[k];
+            if (j == i) nd++;
+            else if (j < A->num_rows && (mark[j] == 1) == c_rows) ok = 0;
+        }
+        if (nd != 1) ok = 0;
+    }
+    if (ncache < 16) cache[ncache].ci = A->col_idx, cache[ncache].mark = mark, cache[ncache].c = c_rows,
+                     cache[ncache++].ok = ok;
+    return ok;
+}
+
+static void gs_pass_any(double *u, const SSS_MAT *A, const double *b, const int *mark, int c_rows, double *d)
+{
+    if (omp_get_max_threads() == 1 || !gs_pass_independent(A, mark, c_rows)) {
+        gs_pass(u, A, b, mark, c_rows, d);
+        return;
+    }
+    const int n = A->num_rows;
+#pragma omp parallel for schedule(static, 4096)
+    for (int i = 0; i < n; ++i) {
+        if ((mark[i] == 1) != c_rows) continue;
+        double t = b[i], di = 0.0;
+        for (int k = A->row_ptr[i]; k < A->row_ptr[i + 1]; ++k) {
+            const int j = A->col_idx[k];
+            if (j != i) t -= A->val[k] * u[j];
+            else di = A->val[k];
+        }
+        if ((di >= 0.0 ? di : -di) > SMALLFLOAT) u[i] = t / di;
+    }
+    for (int i = n - 1; i >= 0; --i)   /* the divisor register after the pass: the last row's diagonal */
+        if ((mark[i] == 1) == c_rows) {
+            for (int k = A->row_ptr[i]; k < A->row_ptr[i + 1]; ++k)
+                if (A->col_idx[k] == i) *d = A->val[k];
+            break;
+        }
+}
+
 void ora_gs_cf(double *u, const SSS_MAT *A, const double *b, int sweeps, const int *mark, int order)
 {
     double d = 0.0;
     while (sweeps--) {
-        gs_pass(u, A, b, mark, order ? 0 : 1, &d);
-        gs_pass(u, A, b, mark, order ? 1 : 0, &d);
+        gs_pass_any(u, A, b, mark, order ? 0 : 1, &d);
+        gs_pass_any(u, A, b, mark, order ? 1 : 0, &d);
     }
 }
 
@@ -187,6 +249,7 @@ void ora_cf_jacobi_w(double *u, const SSS_MAT *A, const double *b, int sweeps, c
     while (sweeps--) {
         for (int pass = 0; pass < (mark ? 2 : 1); ++pass) {
             copy(n, u, old);
+#pragma omp parallel for schedule(static, 4096)
             for (int i = 0; i < n; ++i) {
                 double t, d = 0.0, off = 0.0;
                 if (mark && (mark[i] == 1) != pass) continue;
@@ -234,6 +297,7 @@ void ora_cf_twostage(double *u, const SSS_MAT *A, const double *b, int sweeps, c
 #define IN_PASS(r) (!mark || (mark[r] == 1) == pass)
             copy(n, u, old);
             copy(n, u, cur);
+#pragma omp parallel for schedule(static, 4096)
             for (int i = 0; i < n; ++i) {   /* P and stage 0 */
                 double t, d = 0.0;
                 if (!IN_PASS(i)) continue;
@@ -253,6 +317,7 @@ void ora_cf_twostage(double *u, const SSS_MAT *A, const double *b, int sweeps, c
             }
             for (int stage = 1; stage <= inner; ++stage) {
                 copy(n, cur, nxt);
+#pragma omp parallel for schedule(static, 4096)
                 for (int i = 0; i < n; ++i) {
                     double t;
                     if (!IN_PASS(i)) continue;
@@ -542,6 +607,7 @@ static void lu_factor(const SSS_MAT *A)
                 a[(size_t)pr * n + j] = tmp;
             }
         if (a[(size_t)k * n + k] == 0.0) continue;
+#pragma omp parallel for schedule(static, 16)
         for (int i = k + 1; i < n; ++i) {
             double f = a[(size_t)i * n + k] / a[(size_t)k * n + k];
             a[(size_t)i * n + k] = f;

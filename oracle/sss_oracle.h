@@ -30,6 +30,9 @@ typedef struct {
 void ora_opts_default(ora_opts *o);
 
 /* SSS_utils.c:161-201 (+ the row cap of Solve/SSS_cuda.cu:131,152 when cap > 0) */
+/* host threads for the row-parallel loops (results do not depend on it) */
+void ora_set_threads(int n);
+int ora_get_threads(void);
 void ora_mv_amxpy(double alpha, const SSS_MAT *A, const double *x, double *y, int cap);
 void ora_mv_mxy(const SSS_MAT *A, const double *x, double *y);
 void ora_mv_acc(const SSS_MAT *A, const double *x, double *y, int cap);
