@@ -522,6 +522,48 @@ __global__ __launch_bounds__(NT) void k_ldsx(int n, int nchunk, const int *rs, c
     }
 }
 
+// Merged row groups (throughput mode: free order): G consecutive rows' entries merged into one
+// column-sorted list, packed (col << 5) | row-in-group.  One wave per group, lane-strided over the
+// list with U loads in flight; per-lane accumulator per row (select chain), xor-reduced per row.
+// Neighbouring rows share most columns, so 64 consecutive merged entries touch ~G x fewer lines.
+template <int G, int U>
+__global__ __launch_bounds__(kB) void k_merged(int n, const int *gp, const unsigned *mk, const double *mv,
+                                               const double *x, const double *b, double *y)
+{
+    const int g = blockIdx.x * (kB / 64) + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+    const int ng = (n + G - 1) / G;
+    if (g >= ng) return;
+    const int k0 = gp[g], k1 = gp[g + 1];
+    double s[G];
+#pragma unroll
+    for (int u = 0; u < G; ++u) s[u] = 0.0;
+    for (int k = k0 + lane; k < k1; k += 64 * U) {
+        unsigned q[U];
+        double a[U];
+#pragma unroll
+        for (int t = 0; t < U; ++t) {
+            const int kk = k + 64 * t;
+            q[t] = kk < k1 ? mk[kk] : 0u;
+            a[t] = kk < k1 ? mv[kk] : 0.0;
+        }
+#pragma unroll
+        for (int t = 0; t < U; ++t) {
+            const double p = a[t] * x[q[t] >> 5];
+            const unsigned rid = q[t] & 31u;
+#pragma unroll
+            for (int u = 0; u < G; ++u) s[u] += rid == (unsigned)u ? p : 0.0;
+        }
+    }
+#pragma unroll
+    for (int u = 0; u < G; ++u) {
+        double v = s[u];
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+        const int r = g * G + u;
+        if (lane == 0 && r < n) y[r] = b[r] - v;
+    }
+}
+
 struct Lx {
     int K = 0, nchunk = 0, nb = 0;
     int *rs = nullptr, *crp = nullptr;
@@ -529,9 +571,17 @@ struct Lx {
     double *cv = nullptr;
 };
 
+struct Merged {
+    int G = 0;
+    int *gp = nullptr;
+    unsigned *mk = nullptr;
+    double *mv = nullptr;
+};
+
 struct Dev {
     int n = 0, nnz = 0, nblk = 0;
     Lx lx[2];   // K = 8192, 16384
+    Merged mg[3];   // G = 4, 8, 16
     int *rp = nullptr, *ci = nullptr, *blk = nullptr, *pk11 = nullptr, *pk8 = nullptr;
     double *v11 = nullptr, *v8 = nullptr;
     std::vector<int> hrp, hci;
@@ -609,6 +659,7 @@ extern "C" void lab_free()
 {
     for (auto &c : D.cfg) hipFree(c.blk), hipFree(c.pk), hipFree(c.v);
     for (auto &L : D.lx) hipFree(L.rs), hipFree(L.crp), hipFree(L.cci), hipFree(L.cv);
+    for (auto &M : D.mg) hipFree(M.gp), hipFree(M.mk), hipFree(M.mv);
     hipFree(D.rci), hipFree(D.rv);
     hipFree(D.pk11), hipFree(D.pk8), hipFree(D.v11), hipFree(D.v8);
     hipFree(D.rp), hipFree(D.ci), hipFree(D.v), hipFree(D.blk), hipFree(D.x), hipFree(D.b), hipFree(D.y);
@@ -694,6 +745,54 @@ static Lx *lx_get(int slot, int K, int nb)
     hipMalloc(&L.cv, sizeof(double) * (vv.size() + 8));
     hipMemcpy(L.cv, vv.data(), sizeof(double) * vv.size(), hipMemcpyHostToDevice);
     return &L;
+}
+
+static Merged *mg_get(int slot, int G)
+{
+    Merged &M = D.mg[slot];
+    if (M.G) return &M;
+    const int n = D.n, ng = (n + G - 1) / G;
+    const int *rp = D.hrp.data(), *ci = D.hci.data();
+    if (n >= (1 << 27)) return nullptr;
+    std::vector<int> gp(ng + 1);
+    std::vector<unsigned> mk(D.nnz);
+    std::vector<double> mv(D.nnz);
+    std::vector<int> idx;
+    for (int g = 0; g < ng; ++g) {
+        const int r0 = g * G, r1 = std::min(n, r0 + G), a = rp[r0], e = rp[r1];
+        gp[g] = a;
+        idx.resize(e - a);
+        for (int t = 0; t < e - a; ++t) idx[t] = a + t;
+        std::stable_sort(idx.begin(), idx.end(), [&](int p, int q) { return ci[p] < ci[q]; });
+        int r = r0;
+        std::vector<int> rowof(e - a);
+        for (int k = a; k < e; ++k) {
+            while (rp[r + 1] <= k) ++r;
+            rowof[k - a] = r - r0;
+        }
+        for (int t = 0; t < e - a; ++t) {
+            mk[a + t] = ((unsigned)ci[idx[t]] << 5) | (unsigned)rowof[idx[t] - a];
+            mv[a + t] = D.hv[idx[t]];
+        }
+    }
+    gp[ng] = rp[n];
+    M.G = G;
+    hipMalloc(&M.gp, sizeof(int) * gp.size());
+    hipMemcpy(M.gp, gp.data(), sizeof(int) * gp.size(), hipMemcpyHostToDevice);
+    hipMalloc(&M.mk, sizeof(unsigned) * (mk.size() + 8));
+    hipMemcpy(M.mk, mk.data(), sizeof(unsigned) * mk.size(), hipMemcpyHostToDevice);
+    hipMalloc(&M.mv, sizeof(double) * (mv.size() + 8));
+    hipMemcpy(M.mv, mv.data(), sizeof(double) * mv.size(), hipMemcpyHostToDevice);
+    return &M;
+}
+
+template <int G, int U>
+static void launch_mg(int slot)
+{
+    Merged *M = mg_get(slot, G);
+    if (!M) return;
+    const int ng = (D.n + G - 1) / G;
+    hipLaunchKernelGGL((k_merged<G, U>), dim3((ng + 3) / 4), dim3(kB), 0, 0, D.n, M->gp, M->mk, M->mv, D.x, D.b, D.y);
 }
 
 template <int K, int NT, int R, int Q>
@@ -808,6 +907,10 @@ static void launch(int variant)
     case 37: launch_lx<16384, 1024, 2, 4>(1, 256); break;
     case 38: launch_lx<16384, 1024, 8, 1>(1, 256); break;
     case 39: launch_lx<16384, 512, 4, 2>(1, 256); break;
+    case 40: launch_mg<4, 4>(0); break;
+    case 41: launch_mg<8, 4>(1); break;
+    case 42: launch_mg<16, 4>(2); break;
+    case 43: launch_mg<8, 2>(1); break;
     default: break;
     }
 }

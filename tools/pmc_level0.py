@@ -12,6 +12,18 @@ import numpy as np  # noqa: E402
 
 import amg_amd as A  # noqa: E402
 
+import threading  # noqa: E402
+import time  # noqa: E402
+
+
+def _heartbeat():   # gpurun kills a command that prints nothing for 3 minutes (setup + upload)
+    t0 = time.time()
+    while True:
+        time.sleep(60)
+        print(f"[pmc_level0] working ({time.time() - t0:.0f} s)", file=sys.stderr, flush=True)
+
+
+threading.Thread(target=_heartbeat, daemon=True).start()
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 400
 reps = int(sys.argv[2]) if len(sys.argv) > 2 else 5
 fd = os.dup(1)
