@@ -90,11 +90,24 @@ struct DevCSR {
     unsigned *pk = nullptr;
     double *pv = nullptr;
     int2 *pb = nullptr;
-    // kEncFreeOrder on a wave_rows matrix: rows summed in a fixed tree order (64 strided lane
-    // sums, xor-shuffle reduction) over rows stored column-sorted (within [rp, seg) and
-    // [seg, rp+1) when a segment split is given).  Deterministic but NOT the reference order.
+    // kEncFreeOrder on a long-row matrix (>= free_row_min() entries per row on average): rows summed
+    // in a fixed tree order, deterministic but NOT the reference order.  ci/v then hold each row
+    // (or each of its two segments [rp, seg) / [seg, rp+1)) column-sorted for the wave-per-row
+    // kernels (64 lane-strided sums, xor-shuffle reduction) ...
     bool vec_rows = false;
+    // ... and, for matrices with enough rows to fill the chip in groups (merge_group_size), a
+    // merged copy: G consecutive rows' entries of one segment merged into one column-sorted list,
+    // packed col << 3 | row-in-group.  One wave sums a group lane-strided with one accumulator per
+    // row; neighbouring rows share most columns, so a wave's 64 gathers touch ~G x fewer x lines
+    // (the long-row levels are bound by the L2->CU line rate of those gathers, not by HBM).
+    int mg_G = 0;              // 0: no merged copy
+    int mg_ng = 0;             // groups
+    int *mg_gp = nullptr;      // per group: first entry (mg_ng + 1)
+    int *mg_gs = nullptr;      // two-segment matrices: per group, first entry of the second segment
+    unsigned *mg_k = nullptr;
+    double *mg_v = nullptr;
 };
+constexpr int kMergeShift = 3;           // row-in-group bits of a merged entry (G <= 8)
 constexpr int kTileShift = 11;           // log2(kTileEntries)
 constexpr int kTileColBits = 20;         // column offset bits of a packed sorted-tile entry
 static_assert((1 << kTileShift) == kTileEntries, "tile packing");
@@ -109,6 +122,7 @@ int level_encoding(const sss_hip_opts &o);
 void devcsr_free(DevCSR &d);
 int build_row_blocks(const int *h_rp, int n, std::vector<int> &blk, int split = -1);
 int wave_row_min();
+int free_row_min();
 
 // ---- hierarchy internals shared with the distributed engine (sss_hier.hip) ------------------
 // A hierarchy over mg->cg[0 .. num_levels); its L[0] is global level `level_base` (smoother

@@ -231,7 +231,7 @@ int smoother_build(SmootherPlan &sp, const SSS_MAT &A, const int *mark, int kind
         }
     }
     const char *fz = getenv("SSS_HIP_FUSE_RESID");   // 0: never fuse (tests compare both paths)
-    if (!(fz && *fz == '0') && kind != SSS_HIP_SMOOTH_JACOBI && dA && !dA->wave_rows && all_diag && single_diag &&
+    if (!(fz && *fz == '0') && kind != SSS_HIP_SMOOTH_JACOBI && dA && !dA->wave_rows && !dA->vec_rows && all_diag && single_diag &&
         dA->split_row > 0 &&
         dA->split_row < n && sp.pass[0].range && sp.pass[1].range && sp.pass[0].lo == 0 &&
         sp.pass[0].hi == dA->split_row && sp.pass[1].lo == dA->split_row && sp.pass[1].hi == n) {
@@ -486,7 +486,23 @@ __global__ __launch_bounds__(kBlock) void ts_stage0(int lo, DevCSR M, const int 
         const double d = deff[r];
         y[q] = fabs(d) > SMALLFLOAT ? acc / d : x(r);
     };
-    if constexpr (PATH == 2) {
+    if constexpr (PATH >= 3) {   // merged row groups, G = PATH
+        constexpr int G = PATH;
+        const int g = xcd_bid() * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+        if (g >= M.mg_ng) return;
+        auto prod = [&](int c, double a) { return a * x(c); };
+        double sN[G], sL[G];
+        merged_sums<G>(M.mg_gp[g], M.mg_gs[g], M.mg_k, M.mg_v, prod, sN);
+        merged_sums<G>(M.mg_gs[g], M.mg_gp[g + 1], M.mg_k, M.mg_v, prod, sL);
+        const double n_sum = merged_pick<G>(sN), l_sum = merged_pick<G>(sL);
+        const int q = g * G + lane;
+        if (lane < G && q < M.n) {
+            const double Pq = b[lo + q] - n_sum;
+            P[q] = Pq;
+            finish(q, Pq - l_sum);
+        }
+        return;
+    } else if constexpr (PATH == 2) {
         const int q = xcd_bid() * 4 + (threadIdx.x >> 6);
         if (q >= M.n) return;
         auto prod = [&](int c, double a) { return a * x(c); };
@@ -565,7 +581,17 @@ __global__ __launch_bounds__(kBlock) void ts_inner(int lo, DevCSR M, const doubl
         const double d = deff[lo + q];
         y[q] = fabs(d) > SMALLFLOAT ? acc / d : ykeep[q];
     };
-    if constexpr (PATH == 2) {
+    if constexpr (PATH >= 3) {   // merged row groups, G = PATH
+        constexpr int G = PATH;
+        const int g = xcd_bid() * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+        if (g >= M.mg_ng) return;
+        double s[G];
+        merged_sums<G>(M.mg_gp[g], M.mg_gp[g + 1], M.mg_k, M.mg_v, [&](int c, double a) { return a * fetch(c); }, s);
+        const double l_sum = merged_pick<G>(s);
+        const int q = g * G + lane;
+        if (lane < G && q < M.n) finish(q, P[q] - l_sum);
+        return;
+    } else if constexpr (PATH == 2) {
         const int q = xcd_bid() * 4 + (threadIdx.x >> 6);
         if (q >= M.n) return;
         const double acc =
@@ -611,8 +637,12 @@ void launch_ts_stage0(const DevCSR &M, int lo, const int *split, const double *b
                       double *P, double *y, hipStream_t s)
 {
     if (M.n == 0) return;
-    if (M.vec_rows)
-        hipLaunchKernelGGL(ts_stage0<2>, dim3(M.ngrid), dim3(kBlock), 0, s, lo, M, split, b, x, deff, P, y);
+    if (M.mg_G == 8 && M.mg_gs)
+        hipLaunchKernelGGL(ts_stage0<8>, dim3(M.ngrid), dim3(kBlock), 0, s, lo, M, split, b, x, deff, P, y);
+    else if (M.mg_G == 4 && M.mg_gs)
+        hipLaunchKernelGGL(ts_stage0<4>, dim3(M.ngrid), dim3(kBlock), 0, s, lo, M, split, b, x, deff, P, y);
+    else if (M.vec_rows)
+        hipLaunchKernelGGL(ts_stage0<2>, dim3((M.n + 3) / 4), dim3(kBlock), 0, s, lo, M, split, b, x, deff, P, y);
     else if (M.wave_rows)
         hipLaunchKernelGGL(ts_stage0<1>, dim3(M.ngrid), dim3(kBlock), 0, s, lo, M, split, b, x, deff, P, y);
     else
@@ -623,8 +653,12 @@ void launch_ts_inner(const DevCSR &M, int lo, const double *deff, const double *
                      const double *ykeep, double *y, hipStream_t s)
 {
     if (M.n == 0) return;
-    if (M.vec_rows)
-        hipLaunchKernelGGL(ts_inner<2>, dim3(M.ngrid), dim3(kBlock), 0, s, lo, M, deff, P, ycols, col_off, ykeep, y);
+    if (M.mg_G == 8)
+        hipLaunchKernelGGL(ts_inner<8>, dim3(M.ngrid), dim3(kBlock), 0, s, lo, M, deff, P, ycols, col_off, ykeep, y);
+    else if (M.mg_G == 4)
+        hipLaunchKernelGGL(ts_inner<4>, dim3(M.ngrid), dim3(kBlock), 0, s, lo, M, deff, P, ycols, col_off, ykeep, y);
+    else if (M.vec_rows)
+        hipLaunchKernelGGL(ts_inner<2>, dim3((M.n + 3) / 4), dim3(kBlock), 0, s, lo, M, deff, P, ycols, col_off, ykeep, y);
     else if (M.wave_rows)
         hipLaunchKernelGGL(ts_inner<1>, dim3(M.ngrid), dim3(kBlock), 0, s, lo, M, deff, P, ycols, col_off, ykeep, y);
     else
@@ -659,7 +693,7 @@ int smoother_run(const SmootherPlan &sp, const DevCSR &A, const double *b, doubl
             }
             if (ps.range) {
                 const int nb = ps.bhi - ps.blo, m = ps.hi - ps.lo, nw = (m + 3) / 4;
-                const bool wave = A.wave_rows;
+                const bool wave = A.wave_rows || A.vec_rows;
                 const XSrc xs = nocopy ? XSrc{cur[0], cur[1], sp.csplit} : xsrc_of(x);
                 auto relax = [&](auto mode, const int *cols, const double *yp, double *y) {
                     constexpr int M = decltype(mode)::value;

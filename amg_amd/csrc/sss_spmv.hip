@@ -37,6 +37,26 @@ int wave_row_min()
     return (e && *e) ? atoi(e) : kWaveRowMin;
 }
 
+// Free-order threshold (kFreeRowMin; SSS_HIP_FREE_MIN overrides it at upload time).
+int free_row_min()
+{
+    const char *e = getenv("SSS_HIP_FREE_MIN");
+    return (e && *e) ? atoi(e) : kFreeRowMin;
+}
+
+// Rows per merged group for a free-order matrix of n rows (0: wave-per-row kernels).  Measured on
+// 7-pt 400^3 (tools/lab_rows.hip, residual): G = 8 from ~100K rows (level 6: 204 vs 311 us), G = 4
+// from ~12K rows (levels 7-9: 1.1-1.4x), below that too few groups fill the chip (level 10: 32 vs
+// 27 us).  SSS_HIP_MERGE_G / SSS_HIP_MERGE_MIN_ROWS override (tests).
+static int merge_group_size(int n)
+{
+    const char *g = getenv("SSS_HIP_MERGE_G"), *m = getenv("SSS_HIP_MERGE_MIN_ROWS");
+    const int min_rows = (m && *m) ? atoi(m) : 12000;
+    if (n < min_rows) return 0;
+    if (g && *g) return atoi(g) <= 0 ? 0 : atoi(g) >= 8 ? 8 : 4;   // kernel instances: 4 and 8
+    return n >= 80000 ? 8 : 4;
+}
+
 int build_row_blocks(const int *h_rp, int n, std::vector<int> &blk, int split)
 {
     blk.clear();
@@ -129,13 +149,55 @@ static void sort_row_segments(const SSS_MAT &h, const int *seg, std::vector<int>
     });
 }
 
+// Merged row groups of a free-order matrix: group g = rows [gG, gG + G); its entries keep their
+// CSR span [rp[gG], rp[gG + G]) and hold first the first-segment entries of its rows (all entries
+// when seg is null), then the second-segment ones, each part sorted by (column, row).
+static void build_merged(const SSS_MAT &h, const int *seg, int G, std::vector<int> &gp, std::vector<int> &gs,
+                         std::vector<unsigned> &mk, std::vector<double> &mv)
+{
+    const int n = h.num_rows, ng = (n + G - 1) / G;
+    const int *rp = h.row_ptr, *ci = h.col_idx;
+    gp.resize((size_t)ng + 1);
+    gs.resize(seg ? (size_t)ng : 0);
+    mk.resize((size_t)h.num_nnzs);
+    mv.resize((size_t)h.num_nnzs);
+    parallel_chunks(ng, 256, [&](int glo, int ghi) {
+        std::vector<int> idx;
+        for (int g = glo; g < ghi; ++g) {
+            const int r0 = g * G, r1 = std::min(n, r0 + G);
+            int pos = rp[r0];
+            gp[g] = pos;
+            for (int part = 0; part < (seg ? 2 : 1); ++part) {
+                if (part == 1) gs[g] = pos;
+                idx.clear();
+                for (int r = r0; r < r1; ++r) {
+                    const int a = part == 0 ? rp[r] : seg[r], e = (part == 0 && seg) ? seg[r] : rp[r + 1];
+                    for (int k = a; k < e; ++k) idx.push_back(k);
+                }
+                // idx is in (row, stored position) order: a stable sort by column keeps rows ascending
+                std::stable_sort(idx.begin(), idx.end(), [&](int p, int q) { return ci[p] < ci[q]; });
+                for (int k : idx) {
+                    int r = r0;
+                    while (rp[r + 1] <= k) ++r;
+                    mk[pos] = ((unsigned)ci[k] << kMergeShift) | (unsigned)(r - r0);
+                    mv[pos] = h.val[k];
+                    ++pos;
+                }
+            }
+        }
+    });
+    gp[ng] = rp[n];
+}
+
 int devcsr_upload(DevCSR &d, const SSS_MAT &h, int split, int enc, const int *seg)
 {
     d.n = h.num_rows;
     d.ncols = h.num_cols;
     d.nnz = h.num_nnzs;
     d.wave_rows = d.n > 0 && (long long)d.nnz >= (long long)wave_row_min() * d.n;
-    d.vec_rows = d.wave_rows && (enc & kEncFreeOrder);
+    d.vec_rows = d.n > 0 && (enc & kEncFreeOrder) && (long long)d.nnz >= (long long)free_row_min() * d.n;
+    if (d.vec_rows && (unsigned long long)std::max(d.ncols, 1) < (1ull << (32 - kMergeShift)))
+        d.mg_G = merge_group_size(d.n);
     d.rp = dev_alloc<int>((size_t)d.n + 1);
     d.ci = dev_alloc<int>((size_t)d.nnz);
     d.v = dev_alloc<double>((size_t)d.nnz);
@@ -163,12 +225,32 @@ int devcsr_upload(DevCSR &d, const SSS_MAT &h, int split, int enc, const int *se
     d.blk = dev_alloc<int>(blk.size());
     if (!d.blk) return hip_fail(hipErrorOutOfMemory, "hipMalloc(blk)", __FILE__, __LINE__);
     SSS_HIP(hipMemcpy(d.blk, blk.data(), sizeof(int) * blk.size(), hipMemcpyHostToDevice));
-    d.ngrid = d.wave_rows ? (d.n + 3) / 4 : d.nblk;
-    // the tile kernels of a wave_rows matrix never run on the hierarchy; no sorted copy for them
+    d.ngrid = (d.wave_rows || d.vec_rows) ? (d.n + 3) / 4 : d.nblk;
+    if (d.mg_G > 0) {
+        std::vector<int> gp, gs;
+        std::vector<unsigned> mk;
+        std::vector<double> mv;
+        build_merged(h, seg, d.mg_G, gp, gs, mk, mv);
+        d.mg_ng = (int)gp.size() - 1;
+        d.ngrid = (d.mg_ng + 3) / 4;
+        d.mg_gp = dev_alloc<int>(gp.size());
+        d.mg_k = dev_alloc<unsigned>(mk.size());
+        d.mg_v = dev_alloc<double>(mv.size());
+        if (!d.mg_gp || !d.mg_k || !d.mg_v) return hip_fail(hipErrorOutOfMemory, "hipMalloc(merged)", __FILE__, __LINE__);
+        SSS_HIP(hipMemcpy(d.mg_gp, gp.data(), sizeof(int) * gp.size(), hipMemcpyHostToDevice));
+        SSS_HIP(hipMemcpy(d.mg_k, mk.data(), sizeof(unsigned) * mk.size(), hipMemcpyHostToDevice));
+        SSS_HIP(hipMemcpy(d.mg_v, mv.data(), sizeof(double) * mv.size(), hipMemcpyHostToDevice));
+        if (!gs.empty()) {
+            d.mg_gs = dev_alloc<int>(gs.size());
+            if (!d.mg_gs) return hip_fail(hipErrorOutOfMemory, "hipMalloc(merged)", __FILE__, __LINE__);
+            SSS_HIP(hipMemcpy(d.mg_gs, gs.data(), sizeof(int) * gs.size(), hipMemcpyHostToDevice));
+        }
+    }
+    // the tile kernels of a wave-path matrix never run on the hierarchy; no sorted copy for them
     std::vector<unsigned> pk;
     std::vector<double> pv;
     std::vector<int2> pb;
-    if ((enc & kEncSortedTiles) && !d.wave_rows && d.nnz > 0 && build_sorted_tiles(h, blk, pk, pv, pb)) {
+    if ((enc & kEncSortedTiles) && !d.wave_rows && !d.vec_rows && d.nnz > 0 && build_sorted_tiles(h, blk, pk, pv, pb)) {
         d.pk = dev_alloc<unsigned>((size_t)d.nnz);
         d.pv = dev_alloc<double>((size_t)d.nnz);
         d.pb = dev_alloc<int2>(pb.size());
@@ -189,6 +271,10 @@ void devcsr_free(DevCSR &d)
     dev_free(d.pk);
     dev_free(d.pv);
     dev_free(d.pb);
+    dev_free(d.mg_gp);
+    dev_free(d.mg_gs);
+    dev_free(d.mg_k);
+    dev_free(d.mg_v);
     d = DevCSR();
 }
 
@@ -257,11 +343,53 @@ __global__ __launch_bounds__(kBlock) void spmv_wave(int n, const int *__restrict
     }
 }
 
+// Free order, merged row groups (DevCSR::mg_*): one wave per group of G rows, lane u < G writes row u.
+template <int OP, bool NORM, int G>
+__global__ __launch_bounds__(kBlock) void spmv_merged(int n, int ng, const int *__restrict__ gp,
+                                                      const unsigned *__restrict__ mk, const double *__restrict__ mv,
+                                                      const double *__restrict__ x, const double *__restrict__ b,
+                                                      double *__restrict__ y, double alpha, int cap,
+                                                      double *__restrict__ partial)
+{
+    __shared__ double red[kBlock / 64];
+    const int g = xcd_bid() * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+    double sq = 0.0;
+    if (g < ng) {
+        double s[G];
+        merged_sums<G>(gp[g], gp[g + 1], mk, mv, [&](int c, double a) { return a * x[c]; }, s);
+        const double sr = merged_pick<G>(s);
+        const int r = g * G + lane;
+        if (lane < G && r < n) {
+            bool write = true;
+            double out;
+            if constexpr (OP == SSS_HIP_SPMV_MXY) out = sr;
+            else if constexpr (OP == SSS_HIP_SPMV_AMXPY) out = y[r] + sr * alpha;
+            else if constexpr (OP == SSS_HIP_SPMV_RESID) out = b[r] + sr * alpha;
+            else {
+                write = !(cap > 0 && r >= cap);
+                out = write ? y[r] + sr : 0.0;
+            }
+            if (write) y[r] = out;
+            if (NORM) sq = out * out;
+        }
+    }
+    if (NORM) {
+        const double t = block_sum(sq, red);
+        if (threadIdx.x == 0) partial[xcd_bid()] = t;
+    }
+}
+
 template <int OP, bool NORM>
 static void launch_op(const DevCSR &A, double alpha, const double *x, const double *b, double *y, int cap,
                       double *partial, hipStream_t s)
 {
-    if (A.vec_rows)
+    if (A.mg_G == 8)
+        hipLaunchKernelGGL((spmv_merged<OP, NORM, 8>), dim3(A.ngrid), dim3(kBlock), 0, s, A.n, A.mg_ng, A.mg_gp,
+                           A.mg_k, A.mg_v, x, b, y, alpha, cap, partial);
+    else if (A.mg_G == 4)
+        hipLaunchKernelGGL((spmv_merged<OP, NORM, 4>), dim3(A.ngrid), dim3(kBlock), 0, s, A.n, A.mg_ng, A.mg_gp,
+                           A.mg_k, A.mg_v, x, b, y, alpha, cap, partial);
+    else if (A.vec_rows)
         hipLaunchKernelGGL((spmv_wave<OP, NORM, true>), dim3(A.ngrid), dim3(kBlock), 0, s, A.n, A.rp, A.ci, A.v, x,
                            b, y, alpha, cap, partial);
     else if (A.wave_rows)
@@ -293,7 +421,7 @@ int launch_spmv(const DevCSR &A, int op, double alpha, const double *x, const do
 int launch_spmv_blocks(const DevCSR &A, int nblk, int op, double alpha, const double *x, const double *b, double *y,
                        double *partial, hipStream_t s)
 {
-    if (A.wave_rows || nblk > A.nblk || op != SSS_HIP_SPMV_RESID) return ERROR_INPUT_PAR;
+    if (A.wave_rows || A.vec_rows || nblk > A.nblk || op != SSS_HIP_SPMV_RESID) return ERROR_INPUT_PAR;
     if (nblk <= 0) return 0;
     if (partial)
         hipLaunchKernelGGL((spmv_adaptive<SSS_HIP_SPMV_RESID, true>), dim3(nblk), dim3(kBlock), 0, s, A.blk, A.rp,

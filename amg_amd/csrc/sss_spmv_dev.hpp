@@ -229,6 +229,8 @@ __device__ __forceinline__ double csr_block_rows(const int *__restrict__ blk, co
     return contrib;
 }
 
+
+
 }  // namespace sss
 
 namespace sss {
@@ -271,6 +273,8 @@ __device__ __forceinline__ void csr_block_relax(const int *__restrict__ blk, con
     }
 }
 
+
+
 }  // namespace sss
 
 namespace sss {
@@ -283,6 +287,10 @@ namespace sss {
 // (tools/lab_rows.py): the tile path wins up to ~400 entries per row, this path from ~700.
 constexpr int kWaveStage = 256;    // doubles per wave strip (2 KiB; 8 KiB per workgroup)
 constexpr int kWaveRowMin = 600;   // average entries per row from which a matrix uses this path
+// Free order (throughput mode): average entries per row from which a matrix is summed in tree
+// order -- merged row groups beat the bitwise sorted tiles from ~300 (7-pt 400^3 level 5: 183 vs
+// 243 us per residual, level 4 at 199 per row: 145 vs 133 us, tools/lab_rows.hip).
+constexpr int kFreeRowMin = 300;
 
 __device__ __forceinline__ void wave_sync()
 {
@@ -353,6 +361,54 @@ __device__ __forceinline__ double wave_row_sum(int k0, int k1, const int *__rest
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off, 64);
     return s;
+}
+
+
+// Merged row groups (DevCSR::mg_*): entries [k0, k1) of one group's segment, lane-strided with U
+// loads in flight; lane l accumulates its entries in increasing position into the accumulator of
+// the entry's row, then each row's 64 lane sums are xor-reduced.  Fixed order: deterministic.
+// s[u] = sum over the segment's entries of row u of prod(col, val), valid in every lane.
+template <int G, class Prod>
+__device__ __forceinline__ void merged_sums(int k0, int k1, const unsigned *__restrict__ mk,
+                                            const double *__restrict__ mv, Prod prod, double (&s)[G])
+{
+    constexpr int U = 4;
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int u = 0; u < G; ++u) s[u] = 0.0;
+    for (int k = k0 + lane; k < k1; k += 64 * U) {
+        unsigned q[U];
+        double a[U];
+#pragma unroll
+        for (int t = 0; t < U; ++t) {
+            const int kk = k + 64 * t;
+            q[t] = kk < k1 ? mk[kk] : 0u;
+            a[t] = kk < k1 ? mv[kk] : 0.0;
+        }
+#pragma unroll
+        for (int t = 0; t < U; ++t) {
+            if (k + 64 * t >= k1) break;
+            const double p = prod((int)(q[t] >> kMergeShift), a[t]);
+            const unsigned rid = q[t] & ((1u << kMergeShift) - 1);
+#pragma unroll
+            for (int u = 0; u < G; ++u) s[u] += rid == (unsigned)u ? p : 0.0;
+        }
+    }
+#pragma unroll
+    for (int u = 0; u < G; ++u)
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) s[u] += __shfl_xor(s[u], off, 64);
+}
+
+// the row sum this lane reports in a merged-group epilogue (lane u < G owns row u of the group)
+template <int G>
+__device__ __forceinline__ double merged_pick(const double (&s)[G])
+{
+    const int lane = threadIdx.x & 63;
+    double v = 0.0;
+#pragma unroll
+    for (int u = 0; u < G; ++u) v = lane == u ? s[u] : v;
+    return v;
 }
 
 }  // namespace sss

@@ -1,8 +1,10 @@
 """GPU tests of the free summation order (sss_hip_opts.sum_order = 1, throughput mode).
 
-On long-row levels (>= SSS_HIP_WAVE_MIN entries per row on average) the free order sums each
+On long-row levels (>= SSS_HIP_FREE_MIN entries per row on average) the free order sums each
 row with a whole wave in a fixed tree order over a column-sorted copy of the row
-(sss_spmv_dev.hpp wave_row_sum) instead of the reference's sequential CSR order.  The result is
+(sss_spmv_dev.hpp wave_row_sum), or -- levels with enough rows -- G = 4 or 8 neighbouring rows
+merged into one column-sorted list summed by one wave (merged_sums), instead of the reference's
+sequential CSR order.  The result is
 deterministic but not bitwise the oracle's, so the checks here are the SURVEY.md §8c ladder's
 reordered-summation rows:
   * one smoother call per level (C/F-Jacobi and two-stage GS-CF, every level forced onto the
@@ -36,10 +38,18 @@ def a27_h(quiet):
     return build_hierarchy(A.generate(27, 16), quiet)
 
 
-@pytest.fixture
-def all_wave(monkeypatch):
-    """every matrix of the hierarchy on the wave-per-row (tree-summed) kernels"""
+@pytest.fixture(params=["wave", "merged4", "merged8"])
+def all_wave(request, monkeypatch):
+    """every matrix of the hierarchy on the free-order kernels: wave per row (tree sum over the
+    column-sorted row), or merged row groups of 4 / 8 rows (sss_spmv_dev.hpp merged_sums)"""
     monkeypatch.setenv("SSS_HIP_WAVE_MIN", "1")
+    monkeypatch.setenv("SSS_HIP_FREE_MIN", "1")
+    if request.param == "wave":
+        monkeypatch.setenv("SSS_HIP_MERGE_MIN_ROWS", str(1 << 30))
+    else:
+        monkeypatch.setenv("SSS_HIP_MERGE_MIN_ROWS", "1")
+        monkeypatch.setenv("SSS_HIP_MERGE_G", request.param[-1])
+    return request.param
 
 
 @pytest.mark.parametrize("hname", ["p32_h", "a27_h"])

@@ -35,7 +35,7 @@ def main():
     lvl = 0
     for name, s, e in rows:
         dur = (e - s) / 1e3   # us
-        m = re.search(r"(spmv_\w+)<(\d), (true|false)(?:, (?:true|false))?>", name)
+        m = re.search(r"(spmv_\w+)<(\d), (true|false)(?:, \w+)?>", name)
         if m and m.group(2) == "2" and m.group(3) == "true":
             if cur is not None:
                 cur[("out", "resid")] += dur
