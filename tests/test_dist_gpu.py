@@ -25,7 +25,7 @@ def _free_port() -> int:
         return s.getsockname()[1]
 
 
-def _worker(rank, world, port, kind, n, smoother, inner_from, agg_rows, cycles, errq):
+def _worker(rank, world, port, kind, n, smoother, inner_from, agg_rows, cycles, errq, transport="host"):
     try:
         os.environ["MASTER_ADDR"] = "127.0.0.1"
         os.environ["MASTER_PORT"] = str(port)
@@ -38,7 +38,7 @@ def _worker(rank, world, port, kind, n, smoother, inner_from, agg_rows, cycles, 
 
         H = build_hierarchy(A.generate(kind, n), quiet_ctx)
         N = H.level(0).A.num_rows
-        comm = A.Comm(world, rank, "host")
+        comm = A.Comm(world, rank, transport, device=0)
         D = A.DistHierarchy(H, comm, smoother=smoother, coarse="direct", device=0, agg_rows=agg_rows,
                             inner_from=inner_from)
         assert D.nagg >= 2, D.nagg
@@ -83,13 +83,26 @@ def _worker(rank, world, port, kind, n, smoother, inner_from, agg_rows, cycles, 
     (27, 14, "jacobi", 2, 100),    # 27-point: not red-black, C/F-Jacobi forms only
 ])
 def test_dist_equals_single_gpu(kind, n, smoother, inner_from, agg):
+    _run(2, "host", kind, n, smoother, inner_from, agg)
+
+
+@pytest.mark.parametrize("smoother", ["hybrid", "jacobi"])
+def test_dist_rccl_single_rank(smoother):
+    """The RCCL transport on the one GPU a test box has: communicator from a broadcast unique id,
+    the grouped send/recv of the coarse all-gather (no peers) and the ncclAllReduce of ||r||^2 --
+    bitwise the single-GPU engine.  (Two ranks cannot share a GPU under RCCL; the halo send/recv
+    pattern itself is covered by the host-transport tests above, which run the same plan.)"""
+    _run(1, "rccl", 7, 24, smoother, 2, 100)
+
+
+def _run(world, transport, kind, n, smoother, inner_from, agg):
     import torch.multiprocessing as mp
 
     ctx = mp.get_context("spawn")
     errq = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, kind, n, smoother, inner_from, agg, 4, errq))
-             for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, kind, n, smoother, inner_from, agg, 4, errq, transport))
+             for r in range(world)]
     for p in procs:
         p.start()
     for p in procs:
