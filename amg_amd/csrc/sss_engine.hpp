@@ -96,18 +96,18 @@ struct DevCSR {
     // kernels (64 lane-strided sums, xor-shuffle reduction) ...
     bool vec_rows = false;
     // ... and, for matrices with enough rows to fill the chip in groups (merge_group_size), a
-    // merged copy: G consecutive rows' entries of one segment merged into one column-sorted list,
-    // packed col << 3 | row-in-group.  One wave sums a group lane-strided with one accumulator per
+    // merged copy: G consecutive rows' entries merged into one column-sorted list, packed
+    // col << 4 | segment << 3 | row-in-group (segment: 0, or 1 for [seg, rp+1) of two-segment rows).  One wave sums a group lane-strided with one accumulator per
     // row; neighbouring rows share most columns, so a wave's 64 gathers touch ~G x fewer x lines
     // (the long-row levels are bound by the L2->CU line rate of those gathers, not by HBM).
     int mg_G = 0;              // 0: no merged copy
     int mg_ng = 0;             // groups
     int *mg_gp = nullptr;      // per group: first entry (mg_ng + 1)
-    int *mg_gs = nullptr;      // two-segment matrices: per group, first entry of the second segment
+    bool mg_two = false;       // two-segment rows
     unsigned *mg_k = nullptr;
     double *mg_v = nullptr;
 };
-constexpr int kMergeShift = 3;           // row-in-group bits of a merged entry (G <= 8)
+constexpr int kMergeShift = 4;           // segment + row-in-group bits of a merged entry (G <= 8)
 constexpr int kTileShift = 11;           // log2(kTileEntries)
 constexpr int kTileColBits = 20;         // column offset bits of a packed sorted-tile entry
 static_assert((1 << kTileShift) == kTileEntries, "tile packing");

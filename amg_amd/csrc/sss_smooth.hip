@@ -492,8 +492,7 @@ __global__ __launch_bounds__(kBlock) void ts_stage0(int lo, DevCSR M, const int 
         if (g >= M.mg_ng) return;
         auto prod = [&](int c, double a) { return a * x(c); };
         double sN[G], sL[G];
-        merged_sums<G>(M.mg_gp[g], M.mg_gs[g], M.mg_k, M.mg_v, prod, sN);
-        merged_sums<G>(M.mg_gs[g], M.mg_gp[g + 1], M.mg_k, M.mg_v, prod, sL);
+        merged_sums<G, 2>(M.mg_gp[g], M.mg_gp[g + 1], M.mg_k, M.mg_v, prod, sN, sL);
         const double n_sum = merged_pick<G>(sN), l_sum = merged_pick<G>(sL);
         const int q = g * G + lane;
         if (lane < G && q < M.n) {
@@ -585,8 +584,9 @@ __global__ __launch_bounds__(kBlock) void ts_inner(int lo, DevCSR M, const doubl
         constexpr int G = PATH;
         const int g = xcd_bid() * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
         if (g >= M.mg_ng) return;
-        double s[G];
-        merged_sums<G>(M.mg_gp[g], M.mg_gp[g + 1], M.mg_k, M.mg_v, [&](int c, double a) { return a * fetch(c); }, s);
+        double s[G], unused[G];
+        merged_sums<G, 1>(M.mg_gp[g], M.mg_gp[g + 1], M.mg_k, M.mg_v, [&](int c, double a) { return a * fetch(c); }, s,
+                          unused);
         const double l_sum = merged_pick<G>(s);
         const int q = g * G + lane;
         if (lane < G && q < M.n) finish(q, P[q] - l_sum);
@@ -637,9 +637,9 @@ void launch_ts_stage0(const DevCSR &M, int lo, const int *split, const double *b
                       double *P, double *y, hipStream_t s)
 {
     if (M.n == 0) return;
-    if (M.mg_G == 8 && M.mg_gs)
+    if (M.mg_G == 8 && M.mg_two)
         hipLaunchKernelGGL(ts_stage0<8>, dim3(M.ngrid), dim3(kBlock), 0, s, lo, M, split, b, x, deff, P, y);
-    else if (M.mg_G == 4 && M.mg_gs)
+    else if (M.mg_G == 4 && M.mg_two)
         hipLaunchKernelGGL(ts_stage0<4>, dim3(M.ngrid), dim3(kBlock), 0, s, lo, M, split, b, x, deff, P, y);
     else if (M.vec_rows)
         hipLaunchKernelGGL(ts_stage0<2>, dim3((M.n + 3) / 4), dim3(kBlock), 0, s, lo, M, split, b, x, deff, P, y);

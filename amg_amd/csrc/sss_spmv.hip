@@ -149,40 +149,34 @@ static void sort_row_segments(const SSS_MAT &h, const int *seg, std::vector<int>
     });
 }
 
-// Merged row groups of a free-order matrix: group g = rows [gG, gG + G); its entries keep their
-// CSR span [rp[gG], rp[gG + G]) and hold first the first-segment entries of its rows (all entries
-// when seg is null), then the second-segment ones, each part sorted by (column, row).
-static void build_merged(const SSS_MAT &h, const int *seg, int G, std::vector<int> &gp, std::vector<int> &gs,
-                         std::vector<unsigned> &mk, std::vector<double> &mv)
+// Merged row groups of a free-order matrix: group g = rows [gG, gG + G); its entries keep their CSR
+// span [rp[gG], rp[gG + G]), sorted by (column, segment, row); segment 1 = [seg[r], rp[r+1]) of a
+// two-segment row.
+static void build_merged(const SSS_MAT &h, const int *seg, int G, std::vector<int> &gp, std::vector<unsigned> &mk,
+                         std::vector<double> &mv)
 {
     const int n = h.num_rows, ng = (n + G - 1) / G;
     const int *rp = h.row_ptr, *ci = h.col_idx;
     gp.resize((size_t)ng + 1);
-    gs.resize(seg ? (size_t)ng : 0);
     mk.resize((size_t)h.num_nnzs);
     mv.resize((size_t)h.num_nnzs);
     parallel_chunks(ng, 256, [&](int glo, int ghi) {
-        std::vector<int> idx;
+        std::vector<std::pair<unsigned long long, int>> ent;   // ((col << 4 | seg << 3 | row), position)
         for (int g = glo; g < ghi; ++g) {
             const int r0 = g * G, r1 = std::min(n, r0 + G);
+            ent.clear();
+            for (int r = r0; r < r1; ++r)
+                for (int k = rp[r]; k < rp[r + 1]; ++k) {
+                    const unsigned sg = (seg && k >= seg[r]) ? 1u : 0u;
+                    ent.emplace_back(((unsigned long long)ci[k] << kMergeShift) | (sg << 3) | (unsigned)(r - r0), k);
+                }
+            std::sort(ent.begin(), ent.end());
             int pos = rp[r0];
             gp[g] = pos;
-            for (int part = 0; part < (seg ? 2 : 1); ++part) {
-                if (part == 1) gs[g] = pos;
-                idx.clear();
-                for (int r = r0; r < r1; ++r) {
-                    const int a = part == 0 ? rp[r] : seg[r], e = (part == 0 && seg) ? seg[r] : rp[r + 1];
-                    for (int k = a; k < e; ++k) idx.push_back(k);
-                }
-                // idx is in (row, stored position) order: a stable sort by column keeps rows ascending
-                std::stable_sort(idx.begin(), idx.end(), [&](int p, int q) { return ci[p] < ci[q]; });
-                for (int k : idx) {
-                    int r = r0;
-                    while (rp[r + 1] <= k) ++r;
-                    mk[pos] = ((unsigned)ci[k] << kMergeShift) | (unsigned)(r - r0);
-                    mv[pos] = h.val[k];
-                    ++pos;
-                }
+            for (const auto &e : ent) {
+                mk[pos] = (unsigned)e.first;
+                mv[pos] = h.val[e.second];
+                ++pos;
             }
         }
     });
@@ -196,8 +190,10 @@ int devcsr_upload(DevCSR &d, const SSS_MAT &h, int split, int enc, const int *se
     d.nnz = h.num_nnzs;
     d.wave_rows = d.n > 0 && (long long)d.nnz >= (long long)wave_row_min() * d.n;
     d.vec_rows = d.n > 0 && (enc & kEncFreeOrder) && (long long)d.nnz >= (long long)free_row_min() * d.n;
-    if (d.vec_rows && (unsigned long long)std::max(d.ncols, 1) < (1ull << (32 - kMergeShift)))
+    if (d.vec_rows && (unsigned long long)std::max(d.ncols, 1) < (1ull << (32 - kMergeShift))) {
         d.mg_G = merge_group_size(d.n);
+        if (seg && d.mg_G > 4) d.mg_G = 4;   // two segments: 2G accumulators per lane
+    }
     d.rp = dev_alloc<int>((size_t)d.n + 1);
     d.ci = dev_alloc<int>((size_t)d.nnz);
     d.v = dev_alloc<double>((size_t)d.nnz);
@@ -227,10 +223,11 @@ int devcsr_upload(DevCSR &d, const SSS_MAT &h, int split, int enc, const int *se
     SSS_HIP(hipMemcpy(d.blk, blk.data(), sizeof(int) * blk.size(), hipMemcpyHostToDevice));
     d.ngrid = (d.wave_rows || d.vec_rows) ? (d.n + 3) / 4 : d.nblk;
     if (d.mg_G > 0) {
-        std::vector<int> gp, gs;
+        std::vector<int> gp;
         std::vector<unsigned> mk;
         std::vector<double> mv;
-        build_merged(h, seg, d.mg_G, gp, gs, mk, mv);
+        build_merged(h, seg, d.mg_G, gp, mk, mv);
+        d.mg_two = seg != nullptr;
         d.mg_ng = (int)gp.size() - 1;
         d.ngrid = (d.mg_ng + 3) / 4;
         d.mg_gp = dev_alloc<int>(gp.size());
@@ -240,11 +237,6 @@ int devcsr_upload(DevCSR &d, const SSS_MAT &h, int split, int enc, const int *se
         SSS_HIP(hipMemcpy(d.mg_gp, gp.data(), sizeof(int) * gp.size(), hipMemcpyHostToDevice));
         SSS_HIP(hipMemcpy(d.mg_k, mk.data(), sizeof(unsigned) * mk.size(), hipMemcpyHostToDevice));
         SSS_HIP(hipMemcpy(d.mg_v, mv.data(), sizeof(double) * mv.size(), hipMemcpyHostToDevice));
-        if (!gs.empty()) {
-            d.mg_gs = dev_alloc<int>(gs.size());
-            if (!d.mg_gs) return hip_fail(hipErrorOutOfMemory, "hipMalloc(merged)", __FILE__, __LINE__);
-            SSS_HIP(hipMemcpy(d.mg_gs, gs.data(), sizeof(int) * gs.size(), hipMemcpyHostToDevice));
-        }
     }
     // the tile kernels of a wave-path matrix never run on the hierarchy; no sorted copy for them
     std::vector<unsigned> pk;
@@ -272,7 +264,6 @@ void devcsr_free(DevCSR &d)
     dev_free(d.pv);
     dev_free(d.pb);
     dev_free(d.mg_gp);
-    dev_free(d.mg_gs);
     dev_free(d.mg_k);
     dev_free(d.mg_v);
     d = DevCSR();
@@ -355,8 +346,8 @@ __global__ __launch_bounds__(kBlock) void spmv_merged(int n, int ng, const int *
     const int g = xcd_bid() * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
     double sq = 0.0;
     if (g < ng) {
-        double s[G];
-        merged_sums<G>(gp[g], gp[g + 1], mk, mv, [&](int c, double a) { return a * x[c]; }, s);
+        double s[G], unused[G];
+        merged_sums<G, 1>(gp[g], gp[g + 1], mk, mv, [&](int c, double a) { return a * x[c]; }, s, unused);
         const double sr = merged_pick<G>(s);
         const int r = g * G + lane;
         if (lane < G && r < n) {

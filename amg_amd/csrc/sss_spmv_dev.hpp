@@ -364,18 +364,20 @@ __device__ __forceinline__ double wave_row_sum(int k0, int k1, const int *__rest
 }
 
 
-// Merged row groups (DevCSR::mg_*): entries [k0, k1) of one group's segment, lane-strided with U
-// loads in flight; lane l accumulates its entries in increasing position into the accumulator of
-// the entry's row, then each row's 64 lane sums are xor-reduced.  Fixed order: deterministic.
-// s[u] = sum over the segment's entries of row u of prod(col, val), valid in every lane.
-template <int G, class Prod>
+// Merged row groups (DevCSR::mg_*): the entries [k0, k1) of one group, lane-strided with U loads in
+// flight; lane l accumulates its entries in increasing position into the accumulator of the
+// entry's (segment, row), then each accumulator's 64 lane sums are xor-reduced.  Fixed order:
+// deterministic.  s0[u] / s1[u] = sum over row u's first- / second-segment entries of
+// prod(col, val), valid in every lane (S = 1: single-segment matrices, s1 untouched).
+template <int G, int S, class Prod>
 __device__ __forceinline__ void merged_sums(int k0, int k1, const unsigned *__restrict__ mk,
-                                            const double *__restrict__ mv, Prod prod, double (&s)[G])
+                                            const double *__restrict__ mv, Prod prod, double (&s0)[G],
+                                            double (&s1)[G])
 {
     constexpr int U = 4;
     const int lane = threadIdx.x & 63;
 #pragma unroll
-    for (int u = 0; u < G; ++u) s[u] = 0.0;
+    for (int u = 0; u < G; ++u) s0[u] = 0.0, s1[u] = 0.0;
     for (int k = k0 + lane; k < k1; k += 64 * U) {
         unsigned q[U];
         double a[U];
@@ -389,15 +391,21 @@ __device__ __forceinline__ void merged_sums(int k0, int k1, const unsigned *__re
         for (int t = 0; t < U; ++t) {
             if (k + 64 * t >= k1) break;
             const double p = prod((int)(q[t] >> kMergeShift), a[t]);
-            const unsigned rid = q[t] & ((1u << kMergeShift) - 1);
+            const unsigned key = q[t] & ((1u << kMergeShift) - 1);
 #pragma unroll
-            for (int u = 0; u < G; ++u) s[u] += rid == (unsigned)u ? p : 0.0;
+            for (int u = 0; u < G; ++u) {
+                s0[u] += key == (unsigned)u ? p : 0.0;
+                if (S == 2) s1[u] += key == (unsigned)(8 + u) ? p : 0.0;
+            }
         }
     }
 #pragma unroll
     for (int u = 0; u < G; ++u)
 #pragma unroll
-        for (int off = 32; off > 0; off >>= 1) s[u] += __shfl_xor(s[u], off, 64);
+        for (int off = 32; off > 0; off >>= 1) {
+            s0[u] += __shfl_xor(s0[u], off, 64);
+            if (S == 2) s1[u] += __shfl_xor(s1[u], off, 64);
+        }
 }
 
 // the row sum this lane reports in a merged-group epilogue (lane u < G owns row u of the group)
