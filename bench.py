@@ -208,6 +208,30 @@ class Distributed(Single):
         self.DH.upload("x", np.ones(self.rows))
 
 
+def vcycle_bytes(H) -> int:
+    """Algorithmic HBM bytes of one outer iteration, SURVEY.md 8(d): per level l < coarsest, with
+    z = nnz(A_l), p = nnz(P_l) = nnz(R_l), n = n_l, m = n_{l+1}:
+      GS-CF sweep   12z + 4(n+1) + 8n + 8n + 16n + 8n      (x (pre_iter + post_iter) sweeps)
+      residual      12z + 4(n+1) + 24n
+      restriction   12p + 4(m+1) + 8n + 8m
+      prolongation  12p + 4(n+1) + 8m + 16n
+      zero-fill     8m
+    plus the outer residual and norm 12z0 + 4(n0+1) + 24n0 + 8n0; the coarse solve is excluded."""
+    sweeps = H.pars.pre_iter + H.pars.post_iter
+    tot = 0
+    for l in range(H.num_levels - 1):
+        L, Lc = H.level(l), H.level(l + 1)
+        z, n, m, p = L.A.num_nnzs, L.A.num_rows, Lc.A.num_rows, L.P.num_nnzs
+        tot += sweeps * (12 * z + 4 * (n + 1) + 40 * n)
+        tot += 12 * z + 4 * (n + 1) + 24 * n
+        tot += 12 * p + 4 * (m + 1) + 8 * n + 8 * m
+        tot += 12 * p + 4 * (n + 1) + 8 * m + 16 * n
+        tot += 8 * m
+    L0 = H.level(0)
+    tot += 12 * L0.A.num_nnzs + 4 * (L0.A.num_rows + 1) + 32 * L0.A.num_rows
+    return int(tot)
+
+
 def heartbeat(stop: threading.Event, t0: float):
     """A progress line on stderr every 60 s through the long host phases (setup, upload)."""
     while not stop.wait(60.0):
@@ -323,6 +347,7 @@ def main():
             break
     solve_s = time.perf_counter() - t0
     levels = [(H.level(l).A.num_rows, H.level(l).A.num_nnzs) for l in range(H.num_levels)]
+    vbytes = vcycle_bytes(H)
 
     traffic = None
     pmc = ROOT / "profiles" / "r01_level0_spmv_pmc.json"
@@ -390,6 +415,14 @@ def main():
                      "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": achieved / PEAK_HBM_GBS,
                      "frac_of_copy_peak": achieved / COPY_PEAK_GBS, "avg_launch_ms": spmv_ms,
                      "bytes_per_launch": spmv_bytes, "traffic": traffic},
+        "vcycle_roofline": {
+            "bytes_per_step": vbytes, "achieved": vbytes / (ms_per_step * 1e-3) / 1e9, "peak": PEAK_HBM_GBS,
+            "unit": "GB/s", "frac": vbytes / (ms_per_step * 1e-3) / 1e9 / PEAK_HBM_GBS,
+            "definition": "SURVEY.md 8(d) V-cycle algorithmic bytes: per smoothed level 4 GS-CF sweeps, "
+                          "residual, restriction, prolongation, zero-fill; plus the outer residual+norm; "
+                          "coarse solve excluded -- divided by the measured time per outer iteration "
+                          "(whole-job bytes / max-over-ranks time at N > 1)",
+        },
         "cpu_baseline": cpu_baseline,
         "cpu_baseline_same_mode": cpu_mt,
     }
