@@ -486,16 +486,16 @@ __global__ __launch_bounds__(kBlock) void ts_stage0(int lo, DevCSR M, const int 
         const double d = deff[r];
         y[q] = fabs(d) > SMALLFLOAT ? acc / d : x(r);
     };
-    if constexpr (PATH >= 3) {   // merged row groups, G = PATH
+    if constexpr (PATH >= 3) {   // merged row groups, G = PATH: one workgroup per group
         constexpr int G = PATH;
-        const int g = xcd_bid() * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
-        if (g >= M.mg_ng) return;
+        __shared__ double red[8 * G];
+        const int g = xcd_bid();
         auto prod = [&](int c, double a) { return a * x(c); };
         double sN[G], sL[G];
-        merged_sums<G, 2>(M.mg_gp[g], M.mg_gp[g + 1], M.mg_k, M.mg_v, prod, sN, sL);
+        merged_group<G, 2>(M.mg_gp[g], M.mg_gp[g + 1], M.mg_k, M.mg_v, prod, sN, sL, red);
         const double n_sum = merged_pick<G>(sN), l_sum = merged_pick<G>(sL);
-        const int q = g * G + lane;
-        if (lane < G && q < M.n) {
+        const int q = g * G + (int)threadIdx.x;
+        if (threadIdx.x < G && q < M.n) {
             const double Pq = b[lo + q] - n_sum;
             P[q] = Pq;
             finish(q, Pq - l_sum);
@@ -580,16 +580,16 @@ __global__ __launch_bounds__(kBlock) void ts_inner(int lo, DevCSR M, const doubl
         const double d = deff[lo + q];
         y[q] = fabs(d) > SMALLFLOAT ? acc / d : ykeep[q];
     };
-    if constexpr (PATH >= 3) {   // merged row groups, G = PATH
+    if constexpr (PATH >= 3) {   // merged row groups, G = PATH: one workgroup per group
         constexpr int G = PATH;
-        const int g = xcd_bid() * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
-        if (g >= M.mg_ng) return;
+        __shared__ double red[8 * G];
+        const int g = xcd_bid();
         double s[G], unused[G];
-        merged_sums<G, 1>(M.mg_gp[g], M.mg_gp[g + 1], M.mg_k, M.mg_v, [&](int c, double a) { return a * fetch(c); }, s,
-                          unused);
+        merged_group<G, 1>(M.mg_gp[g], M.mg_gp[g + 1], M.mg_k, M.mg_v, [&](int c, double a) { return a * fetch(c); },
+                           s, unused, red);
         const double l_sum = merged_pick<G>(s);
-        const int q = g * G + lane;
-        if (lane < G && q < M.n) finish(q, P[q] - l_sum);
+        const int q = g * G + (int)threadIdx.x;
+        if (threadIdx.x < G && q < M.n) finish(q, P[q] - l_sum);
         return;
     } else if constexpr (PATH == 2) {
         const int q = xcd_bid() * 4 + (threadIdx.x >> 6);

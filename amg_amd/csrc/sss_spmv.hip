@@ -229,7 +229,7 @@ int devcsr_upload(DevCSR &d, const SSS_MAT &h, int split, int enc, const int *se
         build_merged(h, seg, d.mg_G, gp, mk, mv);
         d.mg_two = seg != nullptr;
         d.mg_ng = (int)gp.size() - 1;
-        d.ngrid = (d.mg_ng + 3) / 4;
+        d.ngrid = d.mg_ng;   // one workgroup per group
         d.mg_gp = dev_alloc<int>(gp.size());
         d.mg_k = dev_alloc<unsigned>(mk.size());
         d.mg_v = dev_alloc<double>(mv.size());
@@ -334,7 +334,8 @@ __global__ __launch_bounds__(kBlock) void spmv_wave(int n, const int *__restrict
     }
 }
 
-// Free order, merged row groups (DevCSR::mg_*): one wave per group of G rows, lane u < G writes row u.
+// Free order, merged row groups (DevCSR::mg_*): one workgroup per group of G rows (its 4 waves split
+// the group's entries), thread u < G writes row u.
 template <int OP, bool NORM, int G>
 __global__ __launch_bounds__(kBlock) void spmv_merged(int n, int ng, const int *__restrict__ gp,
                                                       const unsigned *__restrict__ mk, const double *__restrict__ mv,
@@ -342,31 +343,30 @@ __global__ __launch_bounds__(kBlock) void spmv_merged(int n, int ng, const int *
                                                       double *__restrict__ y, double alpha, int cap,
                                                       double *__restrict__ partial)
 {
-    __shared__ double red[kBlock / 64];
-    const int g = xcd_bid() * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+    __shared__ double red[8 * G];
+    __shared__ double nred[kBlock / 64];
+    const int g = xcd_bid();
+    double s[G], unused[G];
+    merged_group<G, 1>(gp[g], gp[g + 1], mk, mv, [&](int c, double a) { return a * x[c]; }, s, unused, red);
+    const double sr = merged_pick<G>(s);
+    const int r = g * G + (int)threadIdx.x;
     double sq = 0.0;
-    if (g < ng) {
-        double s[G], unused[G];
-        merged_sums<G, 1>(gp[g], gp[g + 1], mk, mv, [&](int c, double a) { return a * x[c]; }, s, unused);
-        const double sr = merged_pick<G>(s);
-        const int r = g * G + lane;
-        if (lane < G && r < n) {
-            bool write = true;
-            double out;
-            if constexpr (OP == SSS_HIP_SPMV_MXY) out = sr;
-            else if constexpr (OP == SSS_HIP_SPMV_AMXPY) out = y[r] + sr * alpha;
-            else if constexpr (OP == SSS_HIP_SPMV_RESID) out = b[r] + sr * alpha;
-            else {
-                write = !(cap > 0 && r >= cap);
-                out = write ? y[r] + sr : 0.0;
-            }
-            if (write) y[r] = out;
-            if (NORM) sq = out * out;
+    if (threadIdx.x < G && r < n) {
+        bool write = true;
+        double out;
+        if constexpr (OP == SSS_HIP_SPMV_MXY) out = sr;
+        else if constexpr (OP == SSS_HIP_SPMV_AMXPY) out = y[r] + sr * alpha;
+        else if constexpr (OP == SSS_HIP_SPMV_RESID) out = b[r] + sr * alpha;
+        else {
+            write = !(cap > 0 && r >= cap);
+            out = write ? y[r] + sr : 0.0;
         }
+        if (write) y[r] = out;
+        if (NORM) sq = out * out;
     }
     if (NORM) {
-        const double t = block_sum(sq, red);
-        if (threadIdx.x == 0) partial[xcd_bid()] = t;
+        const double t = block_sum(sq, nred);
+        if (threadIdx.x == 0) partial[g] = t;
     }
 }
 

@@ -408,6 +408,33 @@ __device__ __forceinline__ void merged_sums(int k0, int k1, const unsigned *__re
         }
 }
 
+// One merged group per 256-thread workgroup: the 4 waves take consecutive quarters of the
+// group's entries (merged_sums each), then every thread adds the 4 partials per (segment, row)
+// in wave order (fixed: deterministic).  t0/t1 valid in every thread.  red: 8G doubles of LDS.
+template <int G, int S, class Prod>
+__device__ __forceinline__ void merged_group(int k0, int k1, const unsigned *__restrict__ mk,
+                                             const double *__restrict__ mv, Prod prod, double (&t0)[G],
+                                             double (&t1)[G], double *red)
+{
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int len = k1 - k0, per = (len + 3) >> 2;
+    const int a = k0 + min(len, w * per), e = k0 + min(len, (w + 1) * per);
+    double s0[G], s1[G];
+    merged_sums<G, S>(a, e, mk, mv, prod, s0, s1);
+    if (lane == 0)
+#pragma unroll
+        for (int u = 0; u < G; ++u) {
+            red[(w * 2) * G + u] = s0[u];
+            if (S == 2) red[(w * 2 + 1) * G + u] = s1[u];
+        }
+    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < G; ++u) {
+        t0[u] = ((red[0 * G + u] + red[2 * G + u]) + red[4 * G + u]) + red[6 * G + u];
+        if (S == 2) t1[u] = ((red[1 * G + u] + red[3 * G + u]) + red[5 * G + u]) + red[7 * G + u];
+    }
+}
+
 // the row sum this lane reports in a merged-group epilogue (lane u < G owns row u of the group)
 template <int G>
 __device__ __forceinline__ double merged_pick(const double (&s)[G])
