@@ -45,13 +45,14 @@ int free_row_min()
 }
 
 // Rows per merged group for a free-order matrix of n rows (0: wave-per-row kernels).  Measured on
-// 7-pt 400^3 (tools/lab_rows.hip, residual): G = 8 from ~100K rows (level 6: 204 vs 311 us), G = 4
-// from ~12K rows (levels 7-9: 1.1-1.4x), below that too few groups fill the chip (level 10: 32 vs
-// 27 us).  SSS_HIP_MERGE_G / SSS_HIP_MERGE_MIN_ROWS override (tests).
+// 7-pt 400^3 (tools/lab_rows.hip, residual, one wave per group): G = 8 from ~100K rows (level 6:
+// 204 vs 311 us), G = 4 below (levels 7-9: 1.1-1.4x).  With one workgroup per group (4 waves split
+// the entries) small matrices gain too: from 2,000 rows the V-cycle's levels 9-10 took 0.97 ms
+// against 1.09 ms with 12,000 (tools/gpu/prof.sh).  SSS_HIP_MERGE_G / _MIN_ROWS override (tests).
 static int merge_group_size(int n)
 {
     const char *g = getenv("SSS_HIP_MERGE_G"), *m = getenv("SSS_HIP_MERGE_MIN_ROWS");
-    const int min_rows = (m && *m) ? atoi(m) : 12000;
+    const int min_rows = (m && *m) ? atoi(m) : 2000;
     if (n < min_rows) return 0;
     if (g && *g) return atoi(g) <= 0 ? 0 : atoi(g) >= 8 ? 8 : 4;   // kernel instances: 4 and 8
     return n >= 80000 ? 8 : 4;
