@@ -137,9 +137,14 @@ int level_inner_of(const sss_hip_opts &o, int global_level);
 // sum-of-squares of the written y per row block, for a deterministic fused norm.
 int launch_spmv(const DevCSR &A, int op, double alpha, const double *x, const double *b, double *y,
                 int cap, double *partial, hipStream_t stream);
-// As launch_spmv, tile path only, over the row blocks [0, nblk) of A (nblk <= A.nblk).
-int launch_spmv_blocks(const DevCSR &A, int nblk, int op, double alpha, const double *x, const double *b, double *y,
-                       double *partial, hipStream_t stream);
+// As launch_spmv, tile path only, over the row blocks [blo, bhi) of A (partial indexed by block).
+int launch_spmv_range(const DevCSR &A, int blo, int bhi, int op, double alpha, const double *x, const double *b,
+                      double *y, double *partial, hipStream_t stream);
+inline int launch_spmv_blocks(const DevCSR &A, int nblk, int op, double alpha, const double *x, const double *b,
+                              double *y, double *partial, hipStream_t stream)
+{
+    return launch_spmv_range(A, 0, nblk, op, alpha, x, b, y, partial, stream);
+}
 
 // ---- smoother schedules -------------------------------------------------------------------
 struct PassSchedule {          // rows of one class (F or C), grouped by DAG depth
@@ -185,6 +190,10 @@ struct SmootherPlan {
     // r = b - A x of its rows (ResidFuse): exact GS with depth-1 range passes (a red-black level),
     // every row with exactly one diagonal, no long-row block among the C blocks.
     bool fuse_resid = false;
+    // The F pass has depth 1 (no F-F coupling) and divides every F row by |d| > 1e-20 in every
+    // sweep: it overwrites x_F from C values only, so whatever x_F held before is dead (the
+    // prolongation into F rows before a post-smoother can be skipped).
+    bool f_overwritten = false;
 };
 // Residual fused into the smoother's last pass: r[i] = b[i] - sum_k a_ik x_k (stored order from
 // 0.0, x after the pass) for the C rows, and their per-block sums of squares into partial[block]

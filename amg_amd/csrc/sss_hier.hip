@@ -279,7 +279,9 @@ sss_hip_hier *sss::hier_create_impl(const SSS_AMG *mg, const sss_hip_opts *o, in
                 RelabeledCSR P, R;
                 relabel_csr(C.P, L.perm, inv[l + 1], P);
                 relabel_csr(C.R, pc, inv[l], R);
-                if (devcsr_upload(L.P, P.view(C.P.num_rows, C.P.num_cols), -1, enc) ||
+                // P's rows follow the level's F|C relabeling: blocks split there too, so a
+                // prolongation can be limited to the C rows (SmootherPlan::f_overwritten)
+                if (devcsr_upload(L.P, P.view(C.P.num_rows, C.P.num_cols), rl ? nF[l] : -1, enc) ||
                     devcsr_upload(L.R, R.view(C.R.num_rows, C.R.num_cols), -1, enc))
                     return fail("upload P/R");
             } else if (devcsr_upload(L.P, C.P, -1, enc) || devcsr_upload(L.R, C.R, -1, enc)) {
@@ -456,7 +458,17 @@ static int walk_cycle(sss_hip_hier *h, CoarseFn coarse)
         while (l > 0) {
             l--;
             auto &L = h->L[l];
-            if ((rc = launch_spmv(L.P, SSS_HIP_SPMV_AMXPY, 1.0, h->L[l + 1].x, nullptr, L.x, 0, nullptr, s))) return rc;
+            // x_l += P e.  When the post-smoother's first pass overwrites every F row from C values
+            // only (depth-1 GS F pass, all |d| > 1e-20), the F rows' correction is dead: prolong
+            // into the C rows only (the iterates are bitwise unchanged).
+            if (L.sm.f_overwritten && h->pars.post_iter > 0 && L.P.split_row == L.sm.pass[0].hi &&
+                L.P.split_row > 0 && !L.P.wave_rows && !L.P.vec_rows) {
+                if ((rc = launch_spmv_range(L.P, L.P.split_blk, L.P.nblk, SSS_HIP_SPMV_AMXPY, 1.0, h->L[l + 1].x, nullptr,
+                                            L.x, nullptr, s)))
+                    return rc;
+            } else if ((rc = launch_spmv(L.P, SSS_HIP_SPMV_AMXPY, 1.0, h->L[l + 1].x, nullptr, L.x, 0, nullptr, s))) {
+                return rc;
+            }
             if (l == 0 && L.sm.fuse_resid) {   // the C rows of the outer residual come with the last pass
                 ResidFuse rf;
                 rf.r = L.wp;

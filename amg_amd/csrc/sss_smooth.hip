@@ -230,6 +230,15 @@ int smoother_build(SmootherPlan &sp, const SSS_MAT &A, const int *mark, int kind
             if (!sp.x2) return hip_fail(hipErrorOutOfMemory, "hipMalloc(x2)", __FILE__, __LINE__);
         }
     }
+    {
+        const char *dz = getenv("SSS_HIP_DEAD_PROLONG");   // 0: always prolong into every row (tests)
+        const PassSchedule &F = sp.pass[0];
+        bool ok = !(dz && *dz == '0') && kind != SSS_HIP_SMOOTH_JACOBI && F.range && F.lo == 0 && F.nrows > 0 &&
+                  F.depth <= 1 && single_diag;
+        for (int i = F.lo; ok && i < F.hi; ++i)
+            ok = std::fabs(d_first[i]) > SMALLFLOAT && std::fabs(all_diag ? d_first[i] : d_later[i]) > SMALLFLOAT;
+        sp.f_overwritten = ok;
+    }
     const char *fz = getenv("SSS_HIP_FUSE_RESID");   // 0: never fuse (tests compare both paths)
     if (!(fz && *fz == '0') && kind != SSS_HIP_SMOOTH_JACOBI && dA && !dA->wave_rows && !dA->vec_rows && all_diag && single_diag &&
         dA->split_row > 0 &&

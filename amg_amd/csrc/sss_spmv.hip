@@ -410,17 +410,25 @@ int launch_spmv(const DevCSR &A, int op, double alpha, const double *x, const do
     return 0;
 }
 
-int launch_spmv_blocks(const DevCSR &A, int nblk, int op, double alpha, const double *x, const double *b, double *y,
-                       double *partial, hipStream_t s)
+int launch_spmv_range(const DevCSR &A, int blo, int bhi, int op, double alpha, const double *x, const double *b,
+                      double *y, double *partial, hipStream_t s)
 {
-    if (A.wave_rows || A.vec_rows || nblk > A.nblk || op != SSS_HIP_SPMV_RESID) return ERROR_INPUT_PAR;
-    if (nblk <= 0) return 0;
-    if (partial)
-        hipLaunchKernelGGL((spmv_adaptive<SSS_HIP_SPMV_RESID, true>), dim3(nblk), dim3(kBlock), 0, s, A.blk, A.rp,
-                           A.ci, A.v, x, b, y, alpha, 0, partial, A.pk, A.pv, A.pb);
+    if (A.wave_rows || A.vec_rows || blo < 0 || bhi > A.nblk) return ERROR_INPUT_PAR;
+    if (op != SSS_HIP_SPMV_RESID && op != SSS_HIP_SPMV_AMXPY) return ERROR_INPUT_PAR;
+    const int nb = bhi - blo;
+    if (nb <= 0) return 0;
+    // the kernel indexes blocks from 0: shift the block-indexed arrays
+    const int2 *pb = A.pb ? A.pb + blo : nullptr;
+    double *pp = partial ? partial + blo : nullptr;
+    if (op == SSS_HIP_SPMV_AMXPY)
+        hipLaunchKernelGGL((spmv_adaptive<SSS_HIP_SPMV_AMXPY, false>), dim3(nb), dim3(kBlock), 0, s, A.blk + blo, A.rp,
+                           A.ci, A.v, x, b, y, alpha, 0, pp, A.pk, A.pv, pb);
+    else if (partial)
+        hipLaunchKernelGGL((spmv_adaptive<SSS_HIP_SPMV_RESID, true>), dim3(nb), dim3(kBlock), 0, s, A.blk + blo, A.rp,
+                           A.ci, A.v, x, b, y, alpha, 0, pp, A.pk, A.pv, pb);
     else
-        hipLaunchKernelGGL((spmv_adaptive<SSS_HIP_SPMV_RESID, false>), dim3(nblk), dim3(kBlock), 0, s, A.blk, A.rp,
-                           A.ci, A.v, x, b, y, alpha, 0, partial, A.pk, A.pv, A.pb);
+        hipLaunchKernelGGL((spmv_adaptive<SSS_HIP_SPMV_RESID, false>), dim3(nb), dim3(kBlock), 0, s, A.blk + blo, A.rp,
+                           A.ci, A.v, x, b, y, alpha, 0, pp, A.pk, A.pv, pb);
     SSS_HIP(hipGetLastError());
     return 0;
 }

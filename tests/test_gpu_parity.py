@@ -358,15 +358,18 @@ def test_solve_hybrid_krylov_bitwise(request, hname, inner, inner_from, row_path
     assert np.allclose(rel_g, rel_r, rtol=1e-13, atol=0)
 
 
+@pytest.mark.parametrize("knob", ["SSS_HIP_FUSE_RESID", "SSS_HIP_DEAD_PROLONG"])
 @pytest.mark.parametrize("smoother,coarse", [("exact", "krylov"), ("hybrid", "direct")])
-def test_fused_residual_bitwise(p32_h, smoother, coarse, monkeypatch):
-    """Level 0 of 7-pt Poisson is red-black, so the last C pass of each smoother call also writes
-    the C rows of r = b - A x (ResidFuse).  With fusion on/off: x, the in-cycle residual wp and
-    the outer residual norm are bitwise identical over several cycles."""
+def test_fused_residual_bitwise(p32_h, smoother, coarse, knob, monkeypatch):
+    """Level 0 of 7-pt Poisson is red-black.  SSS_HIP_FUSE_RESID: the last C pass of each smoother
+    call also writes the C rows of r = b - A x (ResidFuse).  SSS_HIP_DEAD_PROLONG: the prolongation
+    skips the F rows, which the post-smoother's first (depth-1) F pass overwrites from C values
+    only.  With each on/off: x, the in-cycle residual wp and the outer residual norm are bitwise
+    identical over several cycles."""
     n = p32_h.level(0).A.num_rows
     out = []
     for fuse in ("1", "0"):
-        monkeypatch.setenv("SSS_HIP_FUSE_RESID", fuse)
+        monkeypatch.setenv(knob, fuse)
         D = A.DeviceHierarchy(p32_h, smoother=smoother, coarse=coarse)
         D.upload(0, "b", np.ones(n))
         D.upload(0, "x", np.ones(n))
