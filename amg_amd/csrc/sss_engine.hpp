@@ -110,6 +110,9 @@ struct DevCSR {
 constexpr int kMergeShift = 4;           // segment + row-in-group bits of a merged entry (G <= 8)
 constexpr int kTileShift = 11;           // log2(kTileEntries)
 constexpr int kTileColBits = 20;         // column offset bits of a packed sorted-tile entry
+// Offsets >= kTileDiagMark mark a diagonal entry: offset - kTileDiagMark = its row in the block (so
+// its column is the block's first row + that), and the staging also keeps its raw value in LDS.
+constexpr unsigned kTileDiagMark = (1u << kTileColBits) - 256;
 static_assert((1 << kTileShift) == kTileEntries, "tile packing");
 static_assert(1 + kTileColBits + kTileShift == 32, "tile packing");
 enum { kEncSortedTiles = 1, kEncFreeOrder = 2 };
@@ -194,6 +197,9 @@ struct SmootherPlan {
     // sweep: it overwrites x_F from C values only, so whatever x_F held before is dead (the
     // prolongation into F rows before a post-smoother can be skipped).
     bool f_overwritten = false;
+    // Every row has exactly one diagonal entry, so every sweep's divisor is the row's own diagonal:
+    // tile passes over a sorted-tile matrix read it from the staged tile instead of d_first/d_later.
+    bool own_diag = false;
 };
 // Residual fused into the smoother's last pass: r[i] = b[i] - sum_k a_ik x_k (stored order from
 // 0.0, x after the pass) for the C rows, and their per-block sums of squares into partial[block]

@@ -56,6 +56,7 @@ int smoother_build(SmootherPlan &sp, const SSS_MAT &A, const int *mark, int kind
     std::vector<int> diag_pos(n, -1);
     bool all_diag = true, single_diag = true;
     int rc;
+    const char *tz = getenv("SSS_HIP_TILE_DIAG");   // 0: divisors from the deff stream (tests)
 
     sp.kind = kind;
     for (int i = 0; i < n; ++i) {
@@ -230,6 +231,7 @@ int smoother_build(SmootherPlan &sp, const SSS_MAT &A, const int *mark, int kind
             if (!sp.x2) return hip_fail(hipErrorOutOfMemory, "hipMalloc(x2)", __FILE__, __LINE__);
         }
     }
+    sp.own_diag = all_diag && single_diag && !(tz && *tz == '0');
     {
         const char *dz = getenv("SSS_HIP_DEAD_PROLONG");   // 0: always prolong into every row (tests)
         const PassSchedule &F = sp.pass[0];
@@ -390,8 +392,10 @@ __global__ __launch_bounds__(kBlock) void relax_range(int blo, const int *__rest
     const int r0 = blk[bid], r1 = blk[bid + 1];
     const int k0 = rp[r0], k1 = rp[r1];
     auto fetch = [&](int c) -> double { return MODE == 1 ? xs(c) : x[c]; };
+    // deff null: the plan's divisor is each row's own diagonal, staged from the sorted tile
+    auto dval = [&](int r) -> double { return deff ? deff[r] : sm.d[r - r0]; };
     auto finish = [&](int r, double acc) {
-        const double d = deff[r];
+        const double d = dval(r);
         if (MODE != 1) {
             if (fabs(d) > SMALLFLOAT) x[r] = acc / d;
         } else {
@@ -403,7 +407,7 @@ __global__ __launch_bounds__(kBlock) void relax_range(int blo, const int *__rest
         int a = 0, e = 0, dp = -1;
         double acc = 0.0, br = 0.0;
         if (r < r1) a = rp[r] - k0, e = rp[r + 1] - k0, dp = diag_pos[r], br = b[r];   // ahead of the tile
-        stage_any(sm.v, k0, k1, ci, v, pk, pv, pb, bid, fetch);
+        stage_any(sm.v, k0, k1, ci, v, pk, pv, pb, bid, r0, deff ? (double *)nullptr : sm.d, fetch);
         __syncthreads();
         double sq = 0.0;
         if (r < r1) {
@@ -414,7 +418,7 @@ __global__ __launch_bounds__(kBlock) void relax_range(int blo, const int *__rest
                 acc = chain_sub(acc, sm.v, dp - k0 + 1, e);
             }
             if constexpr (MODE == 2) {   // plan guarantees one diagonal per row, deff = a_rr
-                const double d = deff[r];
+                const double d = dval(r);
                 const double xn = fabs(d) > SMALLFLOAT ? acc / d : x[r];
                 if (fabs(d) > SMALLFLOAT) x[r] = xn;
                 double s = chain_add(0.0, sm.v, a, dp - k0);
@@ -438,7 +442,7 @@ __global__ __launch_bounds__(kBlock) void relax_range(int blo, const int *__rest
         double acc = b[r];
         for (int base = k0; base < k1; base += kTileEntries) {
             const int m = min(kTileEntries, k1 - base);
-            stage_any(sm.v, base, base + m, ci, v, pk, pv, pb, bid, fetch);
+            stage_any(sm.v, base, base + m, ci, v, pk, pv, pb, bid, r0, deff ? (double *)nullptr : sm.d, fetch);
             __syncthreads();
             if (threadIdx.x == 0) {
                 if (dp >= base && dp < base + m) {
@@ -543,7 +547,7 @@ __global__ __launch_bounds__(kBlock) void ts_stage0(int lo, DevCSR M, const int 
             int a = 0, sp = 0, e = 0;
             double acc = 0.0;
             if (q < q1) a = M.rp[q] - k0, sp = split[q] - k0, e = M.rp[q + 1] - k0, acc = b[lo + q];
-            stage_any(sm.v, k0, k1, M.ci, M.v, M.pk, M.pv, M.pb, bq, [&](int c) -> double { return x(c); });
+            stage_any(sm.v, k0, k1, M.ci, M.v, M.pk, M.pv, M.pb, bq, q0, (double *)nullptr, [&](int c) -> double { return x(c); });
             __syncthreads();
             if (q < q1) {
                 acc = chain_sub(acc, sm.v, a, sp);
@@ -556,7 +560,7 @@ __global__ __launch_bounds__(kBlock) void ts_stage0(int lo, DevCSR M, const int 
             double acc = b[lo + q];
             for (int base = k0; base < k1; base += kTileEntries) {
                 const int m = min(kTileEntries, k1 - base);
-                stage_any(sm.v, base, base + m, M.ci, M.v, M.pk, M.pv, M.pb, bq, [&](int c) -> double { return x(c); });
+                stage_any(sm.v, base, base + m, M.ci, M.v, M.pk, M.pv, M.pb, bq, q0, (double *)nullptr, [&](int c) -> double { return x(c); });
                 __syncthreads();
                 if (threadIdx.x == 0) {
                     if (sp >= base && sp < base + m) {
@@ -624,7 +628,7 @@ __global__ __launch_bounds__(kBlock) void ts_inner(int lo, DevCSR M, const doubl
             int a = 0, e = 0;
             double acc = 0.0;
             if (q < q1) a = M.rp[q] - k0, e = M.rp[q + 1] - k0, acc = P[q];
-            stage_any(sm.v, k0, k1, M.ci, M.v, M.pk, M.pv, M.pb, bq, fetch);
+            stage_any(sm.v, k0, k1, M.ci, M.v, M.pk, M.pv, M.pb, bq, q0, (double *)nullptr, fetch);
             __syncthreads();
             if (q < q1) finish(q, chain_sub(acc, sm.v, a, e));
         } else {
@@ -632,7 +636,7 @@ __global__ __launch_bounds__(kBlock) void ts_inner(int lo, DevCSR M, const doubl
             double acc = P[q];
             for (int base = k0; base < k1; base += kTileEntries) {
                 const int m = min(kTileEntries, k1 - base);
-                stage_any(sm.v, base, base + m, M.ci, M.v, M.pk, M.pv, M.pb, bq, fetch);
+                stage_any(sm.v, base, base + m, M.ci, M.v, M.pk, M.pv, M.pb, bq, q0, (double *)nullptr, fetch);
                 __syncthreads();
                 if (threadIdx.x == 0) acc = chain_sub(acc, sm.v, 0, m);
                 __syncthreads();
@@ -704,6 +708,8 @@ int smoother_run(const SmootherPlan &sp, const DevCSR &A, const double *b, doubl
                 const int nb = ps.bhi - ps.blo, m = ps.hi - ps.lo, nw = (m + 3) / 4;
                 const bool wave = A.wave_rows || A.vec_rows;
                 const XSrc xs = nocopy ? XSrc{cur[0], cur[1], sp.csplit} : xsrc_of(x);
+                // tile passes take each row's divisor from its staged diagonal (no deff stream)
+                const bool tile_d = sp.own_diag && A.pk != nullptr;
                 auto relax = [&](auto mode, const int *cols, const double *yp, double *y) {
                     constexpr int M = decltype(mode)::value;
                     if (wave && A.vec_rows)
@@ -714,8 +720,8 @@ int smoother_run(const SmootherPlan &sp, const DevCSR &A, const double *b, doubl
                                            A.rp, cols, A.v, b, x, yp, y, deff, xs);
                     else
                         hipLaunchKernelGGL(relax_range<M>, dim3(nb), dim3(kBlock), 0, s, ps.blo, A.blk, A.rp, cols,
-                                           A.v, sp.diag_pos, ps.lo, b, x, yp, y, deff, A.pk, A.pv, A.pb,
-                                           (double *)nullptr, (double *)nullptr, xs);
+                                           A.v, sp.diag_pos, ps.lo, b, x, yp, y, tile_d ? nullptr : deff, A.pk,
+                                           A.pv, A.pb, (double *)nullptr, (double *)nullptr, xs);
                 };
                 if (sp.kind == SSS_HIP_SMOOTH_JACOBI && sp.inner > 0 && hk) {
                     // iterates live in full-length work vectors whose ghosts (lower-rank rows of
@@ -757,8 +763,8 @@ int smoother_run(const SmootherPlan &sp, const DevCSR &A, const double *b, doubl
                     SSS_HIP(hipMemcpyAsync(x + ps.lo, ps.y, sizeof(double) * (size_t)m, hipMemcpyDeviceToDevice, s));
                 } else if (rf && sp.fuse_resid && c == 1 && sw + 1 == sweeps && !hk) {
                     hipLaunchKernelGGL(relax_range<2>, dim3(nb), dim3(kBlock), 0, s, ps.blo, A.blk, A.rp, A.ci, A.v,
-                                       sp.diag_pos, ps.lo, b, x, (const double *)nullptr, (double *)nullptr, deff,
-                                       A.pk, A.pv, A.pb, rf->r, rf->partial, xs);
+                                       sp.diag_pos, ps.lo, b, x, (const double *)nullptr, (double *)nullptr,
+                                       tile_d ? nullptr : deff, A.pk, A.pv, A.pb, rf->r, rf->partial, xs);
                     rf->done = true;
                 } else {
                     relax(std::integral_constant<int, 0>(), A.ci, (const double *)nullptr, (double *)nullptr);

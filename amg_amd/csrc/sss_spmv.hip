@@ -85,7 +85,7 @@ static bool build_sorted_tiles(const SSS_MAT &h, const std::vector<int> &blk, st
 {
     const int *rp = h.row_ptr, *ci = h.col_idx;
     const int nb = (int)blk.size() - 1;
-    constexpr long long kSpan = 1ll << kTileColBits;
+    constexpr long long kSpan = kTileDiagMark;   // larger offsets mark diagonal entries
     pk.resize((size_t)h.num_nnzs);
     pv.resize((size_t)h.num_nnzs);
     pb.resize((size_t)std::max(nb, 1));
@@ -110,17 +110,20 @@ static bool build_sorted_tiles(const SSS_MAT &h, const std::vector<int> &blk, st
                 return;
             }
             pb[q] = make_int2(b0, b1);
+            const int r0 = blk[q];
             for (int a = a0; a < e0; a += kTileEntries) {
                 const int e = std::min(e0, a + kTileEntries);
                 idx.resize((size_t)(e - a));
                 for (int t = 0; t < e - a; ++t) idx[t] = a + t;
                 std::stable_sort(idx.begin(), idx.end(), [&](int p, int r) { return ci[p] < ci[r]; });
                 for (int t = 0; t < e - a; ++t) {
-                    const int c = ci[idx[t]];
+                    const int k = idx[t], c = ci[k];
+                    int r = r0;   // the entry's row
+                    while (rp[r + 1] <= k) ++r;
                     const unsigned cl = (cols.size() > 1 && c >= cut) ? 1u : 0u;
-                    const unsigned off = (unsigned)(c - (cl ? b1 : b0));
-                    pk[(size_t)a + t] = (cl << 31) | (off << kTileShift) | (unsigned)(idx[t] - a);
-                    pv[(size_t)a + t] = h.val[idx[t]];
+                    const unsigned off = c == r ? kTileDiagMark + (unsigned)(r - r0) : (unsigned)(c - (cl ? b1 : b0));
+                    pk[(size_t)a + t] = (cl << 31) | (off << kTileShift) | (unsigned)(k - a);
+                    pv[(size_t)a + t] = h.val[k];
                 }
             }
         }

@@ -33,6 +33,7 @@ __device__ __forceinline__ int xcd_bid()
 struct SpmvSmem {
     double v[kTileEntries];    // products a_k * x_{c_k} of the tile
     double red[kBlock / 64];
+    double d[kBlock];          // sorted tiles: the raw diagonal value of each row of the block
 };
 
 // In-order chains over LDS products: 8 reads issued ahead of 8 dependent adds/subtractions,
@@ -143,16 +144,12 @@ __device__ __forceinline__ void stage_products_f(double *__restrict__ sm, int k0
 
 // Column-sorted staging (DevCSR::pk/pv/pb): slot k of the segment [k0, k1) holds the entry packed
 // as cluster << 31 | (col - base[cluster]) << kTileShift | pos, pos = its stored-order position in
-// the segment; the product goes to sm[pos], so the LDS image is exactly stage_products_f's and
-// every chain over it is unchanged.
-__device__ __forceinline__ int sorted_col(unsigned q, int2 base)
-{
-    return (int)((q >> kTileShift) & ((1u << kTileColBits) - 1)) + ((q >> 31) ? base.y : base.x);
-}
-
+// the segment (a diagonal entry: offset kTileDiagMark + its row in the block); the product goes to
+// sm[pos], so the LDS image is exactly stage_products_f's and every chain over it is unchanged.
 template <class Fetch>
 __device__ __forceinline__ void stage_sorted(double *__restrict__ sm, int k0, int k1, const unsigned *__restrict__ pk,
-                                             const double *__restrict__ pv, int2 base, Fetch fetch)
+                                             const double *__restrict__ pv, int2 base, int r0, double *diag,
+                                             Fetch fetch)
 {
     constexpr int U = 8;
     constexpr unsigned kMask = kTileEntries - 1;
@@ -166,21 +163,30 @@ __device__ __forceinline__ void stage_sorted(double *__restrict__ sm, int k0, in
             a[u] = k < k1 ? pv[k] : 0.0;
         }
 #pragma unroll
-        for (int u = 0; u < U; ++u) xv[u] = kb + u * kBlock < k1 ? fetch(sorted_col(q[u], base)) : 0.0;
+        for (int u = 0; u < U; ++u) {
+            const unsigned off = (q[u] >> kTileShift) & ((1u << kTileColBits) - 1);
+            const int c = off >= kTileDiagMark ? r0 + (int)(off - kTileDiagMark) : (int)off + ((q[u] >> 31) ? base.y : base.x);
+            xv[u] = kb + u * kBlock < k1 ? fetch(c) : 0.0;
+        }
 #pragma unroll
         for (int u = 0; u < U; ++u)
-            if (kb + u * kBlock < k1) sm[q[u] & kMask] = a[u] * xv[u];
+            if (kb + u * kBlock < k1) {
+                sm[q[u] & kMask] = a[u] * xv[u];
+                const unsigned off = (q[u] >> kTileShift) & ((1u << kTileColBits) - 1);
+                if (diag && off >= kTileDiagMark) diag[off - kTileDiagMark] = a[u];
+            }
     }
 }
 
-// Stage the products of segment [k0, k1) of block `bid`: from the sorted copy when the matrix has one.
+// Stage the products of segment [k0, k1) of block `bid` (first row r0): from the sorted copy when
+// the matrix has one (then diag[row - r0], if given, receives each row's diagonal value).
 template <class Fetch>
 __device__ __forceinline__ void stage_any(double *__restrict__ sm, int k0, int k1, const int *__restrict__ ci,
                                           const double *__restrict__ v, const unsigned *__restrict__ pk,
-                                          const double *__restrict__ pv, const int2 *__restrict__ pb, int bid,
-                                          Fetch fetch)
+                                          const double *__restrict__ pv, const int2 *__restrict__ pb, int bid, int r0,
+                                          double *diag, Fetch fetch)
 {
-    if (pk) stage_sorted(sm, k0, k1, pk, pv, pb[bid], fetch);
+    if (pk) stage_sorted(sm, k0, k1, pk, pv, pb[bid], r0, diag, fetch);
     else stage_products_f(sm, k0, k1, ci, v, fetch);
 }
 
@@ -207,7 +213,7 @@ __device__ __forceinline__ double csr_block_rows(const int *__restrict__ blk, co
         const int r = r0 + (int)threadIdx.x;
         int ra = 0, re = 0;
         if (r < r1) ra = rp[r], re = rp[r + 1];   // issued ahead of the tile
-        if (pk) stage_sorted(sm.v, k0, k1, pk, pv, pb[bid], fetch);
+        if (pk) stage_sorted(sm.v, k0, k1, pk, pv, pb[bid], r0, (double *)nullptr, fetch);
         else stage_products(sm.v, k0, k1, ci, v, x);
         __syncthreads();
         if (r < r1) {
@@ -218,7 +224,7 @@ __device__ __forceinline__ double csr_block_rows(const int *__restrict__ blk, co
         double s = 0.0;
         for (int base = k0; base < k1; base += kTileEntries) {
             const int m = min(kTileEntries, k1 - base);
-            if (pk) stage_sorted(sm.v, base, base + m, pk, pv, pb[bid], fetch);
+            if (pk) stage_sorted(sm.v, base, base + m, pk, pv, pb[bid], r0, (double *)nullptr, fetch);
             else stage_products(sm.v, base, base + m, ci, v, x);
             __syncthreads();
             if (threadIdx.x == 0) s = chain_add(s, sm.v, 0, m);
