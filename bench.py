@@ -45,6 +45,9 @@ def parse():
     p.add_argument("--steps", type=int, default=10)
     p.add_argument("--warmup", type=int, default=3)
     p.add_argument("--grid", "--n", dest="n", type=int, default=400, help="grid edge (400 -> 64M rows)")
+    p.add_argument("--stencil", type=int, default=7, choices=[7, 27],
+                   help="7: 7-pt Poisson (the metric's workload); 27: the 27-pt anisotropic operator of "
+                        "BASELINE.json configs[4] (SURVEY.md 8(d))")
     p.add_argument("--mode", default="throughput", choices=["throughput", "parity"])
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-threads", type=int, default=0,
@@ -253,7 +256,7 @@ def main():
     sorted_tiles = args.sorted_tiles if args.sorted_tiles is not None else int(os.environ.get("SSS_HIP_SORTED_TILES", "1"))
 
     t0 = time.perf_counter()
-    M = A.generate(7, n)
+    M = A.generate(args.stencil, n)
     H = quiet_call(A.Hierarchy, M)
     setup_s = time.perf_counter() - t0
     A.lib().SSS_mat_destroy(C.byref(M))
@@ -298,7 +301,7 @@ def main():
     if D.rank == 0 and D.world == 1 and not args.no_cpu_baseline:
         Hc = H
         if args.cpu_n and args.cpu_n != n:
-            Mc = A.generate(7, args.cpu_n)
+            Mc = A.generate(args.stencil, args.cpu_n)
             Hc = quiet_call(A.Hierarchy, Mc)
         cpu_thread = threading.Thread(target=cpu_baseline_worker, args=(Hc, cpu), daemon=True)
         cpu_thread.start()
@@ -369,7 +372,7 @@ def main():
             cpu_baseline = {
                 "value": 1.0 / cpu["seconds"], "unit": "V-cycle iter/s", "cores": 1, "kind": "port",
                 "sample": f"one outer iteration (V-cycle incl. reference CG(beta=1)+GMRES coarse solve, "
-                          f"residual, norm) of oracle/sss_oracle.c on the same 7-pt {cpu_n}^3 hierarchy, "
+                          f"residual, norm) of oracle/sss_oracle.c on the same {args.stencil}-pt {cpu_n}^3 hierarchy, "
                           f"1 host thread; coarse solve {cpu['coarse_seconds']:.1f} s of {cpu['seconds']:.1f} s",
                 "seconds": cpu["seconds"], "coarse_seconds": cpu["coarse_seconds"],
                 "fine_spmv_GBps": a0_bytes / cpu["spmv_seconds"] / 1e9 if cpu_n == n else None,
@@ -387,7 +390,7 @@ def main():
         cpu_mt = {
             "value": 1.0 / mt["seconds"], "unit": "V-cycle iter/s", "cores": mt["threads"], "kind": "port",
             "sample": f"2 outer iterations after 1 warm-up, oracle/sss_oracle.c in the GPU's mode "
-                      f"({smoother} smoother, {coarse} coarse solve) on the same 7-pt {cpu_n}^3 hierarchy, "
+                      f"({smoother} smoother, {coarse} coarse solve) on the same {args.stencil}-pt {cpu_n}^3 hierarchy, "
                       f"row loops on {mt['threads']} host threads; coarse solve {mt['coarse_seconds']:.2f} s "
                       f"of {mt['seconds']:.2f} s",
             "seconds": mt["seconds"], "coarse_seconds": mt["coarse_seconds"],
@@ -399,8 +402,8 @@ def main():
         "value": value, "unit": "V-cycle iter/s", "n_gpus": D.world, "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": ms_per_step, "higher_is_better": True,
         "scaling": "strong" if D.world > 1 else "weak", "vs_baseline": None,
-        "dtype": "f64", "data": "synthetic (7-pt Poisson generated in memory, b = x0 = 1)",
-        "config": {"workload": f"poisson7_{n}^3", "rows": N, "nnz": nnz, "levels": len(levels),
+        "dtype": "f64", "data": f"synthetic ({args.stencil}-pt Poisson generated in memory, b = x0 = 1)",
+        "config": {"workload": f"poisson{args.stencil}_{n}^3", "rows": N, "nnz": nnz, "levels": len(levels),
                    "hierarchy": [list(t) for t in levels],
                    "mode": args.mode, "smoother": smoother, "coarse": coarse,
                    "inner": inner if smoother != "exact" else None,

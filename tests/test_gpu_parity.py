@@ -107,6 +107,44 @@ def test_spmv_long_rows_bitwise():
     assert np.array_equal(y_gpu.view(np.uint64), y_ref.view(np.uint64))
 
 
+def _powerlaw_csr(n, banded, seed):
+    """A G3_circuit-sized irregular CSR (BASELINE.json configs[3]; the SuiteSparse file is not in
+    the container): heavy-tailed row lengths 1..~3000 plus a few rows longer than the LDS tile;
+    banded = columns within +-60,000 of the row (the sorted-tile path), else uniform over all columns
+    (sorted tiles refused: stored-order staging)."""
+    rng = np.random.default_rng(seed)
+    lens = np.minimum(1 + rng.zipf(1.8, n), 3000)
+    lens[rng.integers(0, n, 8)] = 6000
+    rp = np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)
+    rows = np.repeat(np.arange(n), lens)
+    if banded:
+        ci = np.clip(rows + rng.integers(-60000, 60001, rp[-1]), 0, n - 1)
+    else:
+        ci = rng.integers(0, n, rp[-1])
+    v = rng.standard_normal(rp[-1])
+    return A.NumpyCSR(rp.astype(np.int32), ci.astype(np.int32), v)
+
+
+@pytest.mark.parametrize("banded", [True, False])
+@pytest.mark.parametrize("op", ["mxy", "resid"])
+def test_spmv_irregular_large_bitwise(banded, op, row_path):
+    """Load-balance path at G3_circuit size (1,585,478 rows): every row sum bitwise the oracle's."""
+    n = 1585478
+    M = _powerlaw_csr(n, banded, 11)
+    rng = np.random.default_rng(12)
+    x = rng.standard_normal(n)
+    b = rng.standard_normal(n)
+    y_gpu = np.zeros(n)
+    y_ref = b.copy() if op == "resid" else np.zeros(n)
+    assert _lib().sss_hip_host_spmv(A.SPMV[op], -1.0 if op == "resid" else 1.0, C.byref(M.mat), dptr(x),
+                                    dptr(b) if op == "resid" else None, dptr(y_gpu), 0) == 0
+    if op == "resid":
+        oracle.load().ora_mv_amxpy(-1.0, C.byref(M.mat), dptr(x), dptr(y_ref), 0)
+    else:
+        oracle.load().ora_mv_mxy(C.byref(M.mat), dptr(x), dptr(y_ref))
+    assert np.array_equal(y_gpu.view(np.uint64), y_ref.view(np.uint64))
+
+
 def test_spmv_empty_rows():
     rp = np.array([0, 0, 2, 2, 3, 3], np.int32)
     ci = np.array([0, 4, 1], np.int32)
