@@ -371,7 +371,7 @@ extern "C" sss_hip_dist *sss_hip_dist_create(const SSS_AMG *mg, const sss_hip_op
     d->nc_all = nt;
     d->d_cown = dev_alloc<double>(d->nc_own);
     d->d_call = dev_alloc<double>(nt);
-    d->partial = dev_alloc<double>((size_t)std::max(d->L[0].A.ngrid, 1));
+    d->partial = dev_alloc<double>((size_t)std::max(d->L[0].A.ngrid, 1) + kFinalScratch);
     d->d_norm = dev_alloc<double>(1);
     if (!d->d_cown || !d->d_call || !d->partial || !d->d_norm ||
         hipHostMalloc((void **)&d->h_norm, sizeof(double)) != hipSuccess)

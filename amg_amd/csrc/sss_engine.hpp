@@ -240,8 +240,10 @@ int smoother_run(const SmootherPlan &sp, const DevCSR &A, const double *b, doubl
                  hipStream_t stream, const PassHooks *hooks = nullptr, ResidFuse *rf = nullptr);
 
 // ---- reductions ----------------------------------------------------------------------------
-// Deterministic sum of `n` partials -> *out (device); optionally sqrt.
-int launch_final_sum(const double *partials, int n, double *out, bool take_sqrt, hipStream_t s);
+// Deterministic sum of `n` partials -> *out (device); optionally sqrt.  `partials` must hold
+// n + kFinalScratch doubles: the tail is scratch for the first of two reduction stages.
+constexpr int kFinalScratch = 256;
+int launch_final_sum(double *partials, int n, double *out, bool take_sqrt, hipStream_t s);
 
 // ---- coarse solvers ------------------------------------------------------------------------
 struct CoarseDirect {

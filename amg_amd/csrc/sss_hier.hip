@@ -296,7 +296,7 @@ sss_hip_hier *sss::hier_create_impl(const SSS_AMG *mg, const sss_hip_opts *o, in
             hipMemset(L.wp, 0, sizeof(double) * n) != hipSuccess)
             return fail("memset");
     }
-    h->partial = dev_alloc<double>((size_t)h->L[0].A.ngrid);
+    h->partial = dev_alloc<double>((size_t)h->L[0].A.ngrid + kFinalScratch);
     h->d_norm = dev_alloc<double>(1);
     if (!h->partial || !h->d_norm || hipHostMalloc((void **)&h->h_norm, sizeof(double)) != hipSuccess)
         return fail("norm buffers");

@@ -437,25 +437,53 @@ int launch_spmv_range(const DevCSR &A, int blo, int bhi, int op, double alpha, c
 }
 
 // ---- deterministic final reduction ----------------------------------------------------------
+// Two fixed-order stages: kFinalChunks workgroups each reduce one contiguous chunk of the partials
+// (lane-strided sums + xor tree + waves in order) into scratch[b]; one workgroup then sums those.
+// A single workgroup streaming all 250,000 level-0 partials took ~100 us; two stages take ~10 us.
+constexpr int kFinalChunks = kFinalScratch;
+
+__device__ __forceinline__ double block_sum_1024(double v, double *red)
+{
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+    __syncthreads();
+    double t = 0.0;
+    if (threadIdx.x == 0)
+        for (int w = 0; w < 1024 / 64; ++w) t += red[w];
+    return t;
+}
+
+__global__ __launch_bounds__(1024) void final_sum_chunks(const double *__restrict__ partials, int n, int chunk,
+                                                         double *__restrict__ scratch)
+{
+    __shared__ double red[1024 / 64];
+    const int a = blockIdx.x * chunk, e = min(n, a + chunk);
+    double v = 0.0;
+    for (int i = a + (int)threadIdx.x; i < e; i += 1024) v += partials[i];
+    const double t = block_sum_1024(v, red);
+    if (threadIdx.x == 0) scratch[blockIdx.x] = t;
+}
+
 __global__ __launch_bounds__(1024) void final_sum_kernel(const double *__restrict__ partials, int n,
                                                          double *__restrict__ out, int take_sqrt)
 {
     __shared__ double red[1024 / 64];
     double v = 0.0;
     for (int i = threadIdx.x; i < n; i += 1024) v += partials[i];
-    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
-    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        double t = 0.0;
-        for (int w = 0; w < 1024 / 64; ++w) t += red[w];
-        *out = take_sqrt ? sqrt(t) : t;
-    }
+    const double t = block_sum_1024(v, red);
+    if (threadIdx.x == 0) *out = take_sqrt ? sqrt(t) : t;
 }
 
-int launch_final_sum(const double *partials, int n, double *out, bool take_sqrt, hipStream_t s)
+// partials must have room for n + kFinalChunks doubles (the tail is the first stage's scratch)
+int launch_final_sum(double *partials, int n, double *out, bool take_sqrt, hipStream_t s)
 {
-    hipLaunchKernelGGL(final_sum_kernel, dim3(1), dim3(1024), 0, s, partials, n, out, take_sqrt ? 1 : 0);
+    if (n > 4 * 1024) {
+        const int chunk = (n + kFinalChunks - 1) / kFinalChunks, nb = (n + chunk - 1) / chunk;
+        hipLaunchKernelGGL(final_sum_chunks, dim3(nb), dim3(1024), 0, s, partials, n, chunk, partials + n);
+        hipLaunchKernelGGL(final_sum_kernel, dim3(1), dim3(1024), 0, s, partials + n, nb, out, take_sqrt ? 1 : 0);
+    } else {
+        hipLaunchKernelGGL(final_sum_kernel, dim3(1), dim3(1024), 0, s, partials, n, out, take_sqrt ? 1 : 0);
+    }
     SSS_HIP(hipGetLastError());
     return 0;
 }
