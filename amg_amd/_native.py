@@ -102,7 +102,7 @@ ABI_SYMBOLS = [
     "SSS_amg_setup", "SSS_amg_coarsen", "SSS_amg_interp", "SSS_amg_interp_trunc", "interp_DIR", "SSS_mat_read",
     "SSS_amg_pars_init", "SSS_amg_pars_print", "mmio_info", "mmio_data",
     "sss_hip_opts_default", "sss_hip_device_count", "sss_hip_hier_create", "sss_hip_hier_destroy",
-    "sss_hip_upload_vec", "sss_hip_download_vec", "sss_hip_cycle", "sss_hip_residual_norm",
+    "sss_hip_upload_vec", "sss_hip_download_vec", "sss_hip_cycle", "sss_hip_residual_norm", "sss_hip_pcg",
     "sss_hip_coarse_solve", "sss_hip_smooth", "sss_hip_sync", "sss_hip_level_info_get", "sss_hip_num_levels",
     "sss_hip_spmv_plan_create", "sss_hip_spmv_plan_destroy", "sss_hip_spmv", "sss_hip_host_spmv",
     "sss_hip_host_smooth", "sss_hip_host_coarse_solve", "sss_hip_time_level0_spmv", "sss_hip_time_iterations",
@@ -158,6 +158,7 @@ def _declare(lib):
         "sss_hip_download_vec": (C.c_int, [C.c_void_p, C.c_int, C.c_int, _dbl_p, C.c_int]),
         "sss_hip_cycle": (C.c_int, [C.c_void_p]),
         "sss_hip_residual_norm": (C.c_int, [C.c_void_p, _dbl_p]),
+        "sss_hip_pcg": (C.c_int, [C.c_void_p, C.c_double, C.c_int, P(C.c_int), _dbl_p, _dbl_p, C.c_int]),
         "sss_hip_coarse_solve": (C.c_int, [C.c_void_p]),
         "sss_hip_smooth": (C.c_int, [C.c_void_p, C.c_int, C.c_int]),
         "sss_hip_sync": (C.c_int, [C.c_void_p]),
@@ -336,6 +337,14 @@ class DeviceHierarchy:
         out = C.c_double()
         self._check(lib().sss_hip_residual_norm(self.h, C.byref(out)), "residual_norm")
         return out.value
+
+    def pcg(self, tol: float, maxit: int = 100):
+        """AMG-preconditioned CG on level 0 (b, x uploaded as for cycle()); returns (iterations,
+        relative residual history)."""
+        hist = np.zeros(max(maxit, 1))
+        its, rel = C.c_int(), C.c_double()
+        self._check(lib().sss_hip_pcg(self.h, tol, maxit, C.byref(its), C.byref(rel), dptr(hist), len(hist)), "pcg")
+        return its.value, hist[: its.value].copy()
 
     def smooth(self, level: int, post: bool):
         self._check(lib().sss_hip_smooth(self.h, level, int(post)), "smooth")

@@ -245,6 +245,16 @@ int smoother_run(const SmootherPlan &sp, const DevCSR &A, const double *b, doubl
 constexpr int kFinalScratch = 256;
 int launch_final_sum(double *partials, int n, double *out, bool take_sqrt, hipStream_t s);
 
+// ---- BLAS-1 for the preconditioned CG (sss_blas.hip) ---------------------------------------
+// dot: partial must hold 1024 + kFinalScratch doubles; *out on the device.
+int launch_dot(int n, const double *a, const double *b, double *partial, double *out, hipStream_t s);
+// y += sign * (*num / *den) * x
+int launch_axpy_ratio(int n, const double *num, const double *den, double sign, const double *x, double *y,
+                      hipStream_t s);
+// p = z + ((*num - *numold) / *den) * p   (numold null: *num / *den)
+int launch_xpby_ratio(int n, const double *num, const double *numold, const double *den, const double *z, double *p,
+                      hipStream_t s);
+
 // ---- coarse solvers ------------------------------------------------------------------------
 struct CoarseDirect {
     int n = 0;

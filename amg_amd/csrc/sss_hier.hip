@@ -11,6 +11,8 @@
 // norm is the only per-iteration device->host transfer.
 #include "sss_engine.hpp"
 
+#include <cmath>
+
 #include <algorithm>
 #include <cstdlib>
 #include <cstring>
@@ -53,6 +55,11 @@ struct sss_hip_hier {
     // the F rows.  Valid from the end of a cycle until level-0 x or b is touched by anything else.
     bool resid_c_ready = false;
     hipGraphExec_t resid_f_exec = nullptr;
+    // AMG-preconditioned CG (sss_hip_pcg): level-0 work vectors, dot partials, device scalars
+    double *pcg_v = nullptr;     // 7 vectors of n0: b, x, r, z, p, q, r_old
+    double *pcg_part = nullptr;
+    double *pcg_s = nullptr;     // device scalars
+    double *pcg_h = nullptr;     // pinned host mirror
 };
 
 static int env_int(const char *name, int dflt)
@@ -130,6 +137,10 @@ static void hier_release(sss_hip_hier *h)
         if (g) (void)hipGraphExecDestroy(g);
     if (h->resid_exec) (void)hipGraphExecDestroy(h->resid_exec);
     if (h->resid_f_exec) (void)hipGraphExecDestroy(h->resid_f_exec);
+    dev_free(h->pcg_v);
+    dev_free(h->pcg_part);
+    dev_free(h->pcg_s);
+    if (h->pcg_h) (void)hipHostFree(h->pcg_h);
     coarse_direct_free(h->direct);
     coarse_krylov_destroy(h->krylov);
     dev_free(h->partial);
@@ -576,6 +587,82 @@ extern "C" int sss_hip_residual_norm(sss_hip_hier *h, double *absres)
     SSS_HIP(hipMemcpyAsync(h->h_norm, h->d_norm, sizeof(double), hipMemcpyDeviceToHost, h->stream));
     SSS_HIP(hipStreamSynchronize(h->stream));
     *absres = *h->h_norm;
+    return 0;
+}
+
+// AMG as a preconditioner (not in the reference, whose CG/GMRES serve only
+// the coarsest level): flexible CG with Polak-Ribiere beta, one V-cycle of this hierarchy (its
+// configured smoothers and coarse solve) per iteration as M^-1.  Right-hand side L0.b, initial
+// guess and result L0.x; iterates until ||r_k|| / ||b|| < tol (recursive residual) or maxit.
+// Dots are fixed-order reductions (deterministic); one 8-byte read-back per iteration.
+extern "C" int sss_hip_pcg(sss_hip_hier *h, double tol, int maxit, int *iters, double *relres, double *hist,
+                           int hist_cap)
+{
+    auto &L = h->L[0];
+    const int n = L.A.n;
+    hipStream_t s = h->stream;
+    if (!h->pcg_v) {
+        h->pcg_v = dev_alloc<double>((size_t)7 * n);
+        h->pcg_part = dev_alloc<double>(1024 + kFinalScratch);
+        h->pcg_s = dev_alloc<double>(8);
+        if (!h->pcg_v || !h->pcg_part || !h->pcg_s) return hip_fail(hipErrorOutOfMemory, "hipMalloc(pcg)", __FILE__, __LINE__);
+        SSS_HIP(hipHostMalloc((void **)&h->pcg_h, 8 * sizeof(double), hipHostMallocDefault));
+    }
+    double *bs = h->pcg_v, *xs = bs + n, *r = xs + n, *z = r + n, *p = z + n, *q = p + n, *ro = q + n;
+    double *rz = h->pcg_s, *pq = h->pcg_s + 1, *rr = h->pcg_s + 2, *rzn = h->pcg_s + 3, *roz = h->pcg_s + 4;
+    const size_t bytes = sizeof(double) * (size_t)n;
+    int rc;
+    auto precondition = [&](const double *rin, double *zout) -> int {   // zout = one V-cycle on (rin, 0)
+        SSS_HIP(hipMemcpyAsync(L.b, rin, bytes, hipMemcpyDeviceToDevice, s));
+        SSS_HIP(hipMemsetAsync(L.x, 0, bytes, s));
+        int c = sss_hip_cycle(h);
+        if (c) return c;
+        SSS_HIP(hipMemcpyAsync(zout, L.x, bytes, hipMemcpyDeviceToDevice, s));
+        return 0;
+    };
+    auto fetch = [&](const double *dv, double *out) -> int {
+        SSS_HIP(hipMemcpyAsync(h->pcg_h, dv, sizeof(double), hipMemcpyDeviceToHost, s));
+        SSS_HIP(hipStreamSynchronize(s));
+        *out = h->pcg_h[0];
+        return 0;
+    };
+    SSS_HIP(hipMemcpyAsync(bs, L.b, bytes, hipMemcpyDeviceToDevice, s));
+    SSS_HIP(hipMemcpyAsync(xs, L.x, bytes, hipMemcpyDeviceToDevice, s));
+    double nb2 = 0.0, rr_h = 0.0, rel = 1.0;
+    if ((rc = launch_dot(n, bs, bs, h->pcg_part, rr, s)) || (rc = fetch(rr, &nb2))) return rc;
+    const double nb = std::sqrt(nb2);
+    int it = 0;
+    if (nb == 0.0) {
+        SSS_HIP(hipMemsetAsync(L.x, 0, bytes, s));
+    } else {
+        if ((rc = launch_spmv(L.A, SSS_HIP_SPMV_RESID, -1.0, xs, bs, r, 0, nullptr, s))) return rc;   // r = b - A x
+        if ((rc = precondition(r, z))) return rc;
+        if ((rc = launch_dot(n, r, z, h->pcg_part, rz, s))) return rc;
+        SSS_HIP(hipMemcpyAsync(p, z, bytes, hipMemcpyDeviceToDevice, s));
+        while (it < maxit) {
+            ++it;
+            if ((rc = launch_spmv(L.A, SSS_HIP_SPMV_MXY, 1.0, p, nullptr, q, 0, nullptr, s))) return rc;   // q = A p
+            if ((rc = launch_dot(n, p, q, h->pcg_part, pq, s))) return rc;
+            if ((rc = launch_axpy_ratio(n, rz, pq, 1.0, p, xs, s))) return rc;                          // x += a p
+            SSS_HIP(hipMemcpyAsync(ro, r, bytes, hipMemcpyDeviceToDevice, s));
+            if ((rc = launch_axpy_ratio(n, rz, pq, -1.0, q, r, s))) return rc;                          // r -= a q
+            if ((rc = launch_dot(n, r, r, h->pcg_part, rr, s)) || (rc = fetch(rr, &rr_h))) return rc;
+            rel = std::sqrt(rr_h) / nb;
+            if (hist && it <= hist_cap) hist[it - 1] = rel;
+            if (rel < tol) break;
+            if ((rc = precondition(r, z))) return rc;
+            if ((rc = launch_dot(n, r, z, h->pcg_part, rzn, s))) return rc;
+            if ((rc = launch_dot(n, ro, z, h->pcg_part, roz, s))) return rc;
+            if ((rc = launch_xpby_ratio(n, rzn, roz, rz, z, p, s))) return rc;   // p = z + ((r-ro).z / rz) p
+            SSS_HIP(hipMemcpyAsync(rz, rzn, sizeof(double), hipMemcpyDeviceToDevice, s));
+        }
+        SSS_HIP(hipMemcpyAsync(L.x, xs, bytes, hipMemcpyDeviceToDevice, s));
+    }
+    SSS_HIP(hipMemcpyAsync(L.b, bs, bytes, hipMemcpyDeviceToDevice, s));
+    SSS_HIP(hipStreamSynchronize(s));
+    h->resid_c_ready = false;
+    if (iters) *iters = it;
+    if (relres) *relres = rel;
     return 0;
 }
 

@@ -670,7 +670,9 @@ void SSS_amg_setup(SSS_AMG *mg, SSS_MAT *A, SSS_AMG_PARS *pars)
         int status;
         memset(&S, 0, sizeof(S));
 
+        const double tc0 = SSS_get_time();
         status = SSS_amg_coarsen(&L->A, &vertices, &L->P, &S, pars);
+        const double tc1 = SSS_get_time();
         if (status < 0) {
             free(S.row_ptr);
             free(S.col_idx);
@@ -694,8 +696,13 @@ void SSS_amg_setup(SSS_AMG *mg, SSS_MAT *A, SSS_AMG_PARS *pars)
         memcpy(L->cfmark.d, vertices.d, (size_t)L->A.num_rows * sizeof(int));
 
         SSS_amg_interp(&L->A, &vertices, &L->P, &S, pars);
+        const double tc2 = SSS_get_time();
         L->R = SSS_mat_trans(&L->P);
+        const double tc3 = SSS_get_time();
         mg->cg[lvl + 1].A = SSS_blas_mat_rap(&L->R, &L->A, &L->P);
+        if (getenv("SSS_SETUP_TIMING"))   /* phase times on stderr (stdout stays the reference's) */
+            fprintf(stderr, "[setup] level %d: coarsen %.3f s, interp %.3f s, transpose %.3f s, RAP %.3f s\n", lvl,
+                    tc1 - tc0, tc2 - tc1, tc3 - tc2, SSS_get_time() - tc3);
         free(S.row_ptr);
         free(S.col_idx);
 

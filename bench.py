@@ -349,6 +349,16 @@ def main():
         if relres < H.pars.tol:
             break
     solve_s = time.perf_counter() - t0
+    pcg = None
+    if D.world == 1 and args.converge_max > 0:
+        # AMG as a CG preconditioner: same problem, same x0, same tolerance
+        DH.set_x_ones()
+        t0 = time.perf_counter()
+        pits, phist = DH.DH.pcg(H.pars.tol, args.converge_max)
+        pcg = {"iterations_to_tol": pits, "final_relres": float(phist[-1]) if len(phist) else None,
+               "time_to_solution_s": time.perf_counter() - t0}
+        print(f"[bench] AMG-PCG: {pits} iterations, relres {pcg['final_relres']:.3e}, "
+              f"{pcg['time_to_solution_s']:.3f} s", file=sys.stderr, flush=True)
     levels = [(H.level(l).A.num_rows, H.level(l).A.num_nnzs) for l in range(H.num_levels)]
     vbytes = vcycle_bytes(H)
 
@@ -411,6 +421,7 @@ def main():
                    "sum_order": "tree (long rows)" if sum_order == 1 else "stored CSR order",
                    "sorted_tiles": bool(sorted_tiles),
                    "iterations_to_tol": its, "final_relres": relres, "time_to_solution_s": solve_s,
+                   "amg_pcg": pcg,
                    "setup_s": setup_s, "upload_s": upload_s,
                    "parallelism": f"rowpart{D.world}" if D.world > 1 else "single-gpu",
                    "transport": transport},

@@ -82,6 +82,12 @@ int sss_hip_download_vec(sss_hip_hier *h, int level, int which, double *dst, int
 int sss_hip_cycle(sss_hip_hier *h);
 /* wp0 = b0 - A0*x0 and ||wp0||_2, returned to the host (synchronises the stream). */
 int sss_hip_residual_norm(sss_hip_hier *h, double *absres);
+/* AMG-preconditioned flexible CG on level 0 (an engine extension -- the
+ * reference's Krylov solvers serve only the coarsest level): right-hand side = the level-0 b
+ * vector, initial guess / result = the level-0 x vector, one V-cycle per iteration as the
+ * preconditioner.  Stops when ||r_k||/||b|| < tol or after maxit iterations; hist (optional)
+ * receives the relative residual of each iteration. */
+int sss_hip_pcg(sss_hip_hier *h, double tol, int maxit, int *iters, double *relres, double *hist, int hist_cap);
 /* The coarsest-level solve alone (on the level vectors of the coarsest level). */
 int sss_hip_coarse_solve(sss_hip_hier *h);
 /* Pre (post = 0) or post (post = 1) smoothing of one level. */
