@@ -103,6 +103,7 @@ ABI_SYMBOLS = [
     "SSS_amg_pars_init", "SSS_amg_pars_print", "mmio_info", "mmio_data",
     "sss_hip_opts_default", "sss_hip_device_count", "sss_hip_hier_create", "sss_hip_hier_destroy",
     "sss_hip_upload_vec", "sss_hip_download_vec", "sss_hip_cycle", "sss_hip_residual_norm", "sss_hip_pcg",
+    "SSS_amg_save", "SSS_amg_load",
     "sss_hip_coarse_solve", "sss_hip_smooth", "sss_hip_sync", "sss_hip_level_info_get", "sss_hip_num_levels",
     "sss_hip_spmv_plan_create", "sss_hip_spmv_plan_destroy", "sss_hip_spmv", "sss_hip_host_spmv",
     "sss_hip_host_smooth", "sss_hip_host_coarse_solve", "sss_hip_time_level0_spmv", "sss_hip_time_iterations",
@@ -159,6 +160,8 @@ def _declare(lib):
         "sss_hip_cycle": (C.c_int, [C.c_void_p]),
         "sss_hip_residual_norm": (C.c_int, [C.c_void_p, _dbl_p]),
         "sss_hip_pcg": (C.c_int, [C.c_void_p, C.c_double, C.c_int, P(C.c_int), _dbl_p, _dbl_p, C.c_int]),
+        "SSS_amg_save": (C.c_int, [P(SSS_AMG), C.c_char_p]),
+        "SSS_amg_load": (C.c_int, [P(SSS_AMG), C.c_char_p]),
         "sss_hip_coarse_solve": (C.c_int, [C.c_void_p]),
         "sss_hip_smooth": (C.c_int, [C.c_void_p, C.c_int, C.c_int]),
         "sss_hip_sync": (C.c_int, [C.c_void_p]),
@@ -264,12 +267,28 @@ def read_mtx(path: str | os.PathLike) -> SSS_MAT:
 
 
 class Hierarchy:
-    """An SSS_AMG built by the (host C, reference-semantics) setup; owns it."""
+    """An SSS_AMG built by the (host C, reference-semantics) setup -- or read back from a file
+    SSS_amg_save wrote (Hierarchy.load) -- owns it."""
 
-    def __init__(self, A: SSS_MAT, pars: SSS_AMG_PARS | None = None):
+    def __init__(self, A: SSS_MAT | None, pars: SSS_AMG_PARS | None = None):
         self.pars = pars if pars is not None else default_pars()
         self.mg = SSS_AMG()
-        lib().SSS_amg_setup(C.byref(self.mg), C.byref(A), C.byref(self.pars))
+        if A is not None:
+            lib().SSS_amg_setup(C.byref(self.mg), C.byref(A), C.byref(self.pars))
+
+    def save(self, path) -> None:
+        rc = lib().SSS_amg_save(C.byref(self.mg), str(path).encode())
+        if rc != 0:
+            raise OSError(f"SSS_amg_save({path}) failed ({rc})")
+
+    @classmethod
+    def load(cls, path) -> "Hierarchy":
+        H = cls(None)
+        rc = lib().SSS_amg_load(C.byref(H.mg), str(path).encode())
+        if rc != 0:
+            raise OSError(f"SSS_amg_load({path}) failed ({rc})")
+        H.pars = H.mg.pars
+        return H
 
     @property
     def num_levels(self) -> int:

@@ -45,6 +45,9 @@ def parse():
     p.add_argument("--steps", type=int, default=10)
     p.add_argument("--warmup", type=int, default=3)
     p.add_argument("--grid", "--n", dest="n", type=int, default=400, help="grid edge (400 -> 64M rows)")
+    p.add_argument("--hier-cache", default=None,
+                   help="binary hierarchy file (SSS_amg_save): loaded when present, else written after setup "
+                        "(rank 0; the other ranks load it)")
     p.add_argument("--stencil", type=int, default=7, choices=[7, 27],
                    help="7: 7-pt Poisson (the metric's workload); 27: the 27-pt anisotropic operator of "
                         "BASELINE.json configs[4] (SURVEY.md 8(d))")
@@ -256,10 +259,24 @@ def main():
     sorted_tiles = args.sorted_tiles if args.sorted_tiles is not None else int(os.environ.get("SSS_HIP_SORTED_TILES", "1"))
 
     t0 = time.perf_counter()
-    M = A.generate(args.stencil, n)
-    H = quiet_call(A.Hierarchy, M)
+    hier_src = None
+    cache = Path(args.hier_cache) if args.hier_cache else None
+    if cache is not None and D.rank == 0 and not cache.exists():
+        M = A.generate(args.stencil, n)
+        H = quiet_call(A.Hierarchy, M)
+        A.lib().SSS_mat_destroy(C.byref(M))
+        H.save(cache)
+        hier_src = "setup (saved)"
+    D.barrier()
+    if cache is not None and (D.rank != 0 or hier_src is None):
+        H = A.Hierarchy.load(cache)
+        hier_src = f"loaded from {cache}"
+    elif cache is None:
+        M = A.generate(args.stencil, n)
+        H = quiet_call(A.Hierarchy, M)
+        A.lib().SSS_mat_destroy(C.byref(M))
+        hier_src = "setup"
     setup_s = time.perf_counter() - t0
-    A.lib().SSS_mat_destroy(C.byref(M))
     N = H.level(0).A.num_rows
     nnz = H.level(0).A.num_nnzs
 
@@ -422,7 +439,7 @@ def main():
                    "sorted_tiles": bool(sorted_tiles),
                    "iterations_to_tol": its, "final_relres": relres, "time_to_solution_s": solve_s,
                    "amg_pcg": pcg,
-                   "setup_s": setup_s, "upload_s": upload_s,
+                   "setup_s": setup_s, "hierarchy": hier_src, "upload_s": upload_s,
                    "parallelism": f"rowpart{D.world}" if D.world > 1 else "single-gpu",
                    "transport": transport},
         "roofline": {"bound": "hbm", "kernel": "spmv_adaptive<RESID> level 0", "achieved": achieved,

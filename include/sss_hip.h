@@ -82,6 +82,13 @@ int sss_hip_download_vec(sss_hip_hier *h, int level, int which, double *dst, int
 int sss_hip_cycle(sss_hip_hier *h);
 /* wp0 = b0 - A0*x0 and ||wp0||_2, returned to the host (synchronises the stream). */
 int sss_hip_residual_norm(sss_hip_hier *h, double *absres);
+/* Binary hierarchy file (engine extension; amg_amd/host/sss_hierio.c): what
+ * the solve phase reads of a set-up SSS_AMG -- parameters and per level A, P, R, cfmark.  Loading
+ * gives a hierarchy field-for-field equal to the one SSS_amg_setup built (free it with
+ * SSS_amg_data_destroy).  0 or ERROR_OPEN_FILE / ERROR_WRONG_FILE. */
+int SSS_amg_save(const SSS_AMG *mg, const char *path);
+int SSS_amg_load(SSS_AMG *mg, const char *path);
+
 /* AMG-preconditioned flexible CG on level 0 (an engine extension -- the
  * reference's Krylov solvers serve only the coarsest level): right-hand side = the level-0 b
  * vector, initial guess / result = the level-0 x vector, one V-cycle per iteration as the
