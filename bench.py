@@ -254,6 +254,10 @@ def main():
     n = args.n
     smoother, coarse = ("hybrid", "direct") if args.mode == "throughput" else ("exact", "krylov")
     smoother = args.mode_smoother or smoother
+    if args.mode_smoother is None and D.world > 1 and args.stencil == 27 and smoother == "hybrid":
+        # level 0 of the 27-point operator is not red-black: its exact GS-CF has intra-class chains
+        # that cannot be split across ranks; the row-partitioned engine smooths it by C/F-Jacobi
+        smoother = "jacobi"
     coarse = args.mode_coarse or coarse
     sum_order = args.sum_order if args.sum_order is not None else (1 if args.mode == "throughput" else 0)
     sorted_tiles = args.sorted_tiles if args.sorted_tiles is not None else int(os.environ.get("SSS_HIP_SORTED_TILES", "1"))

@@ -25,10 +25,13 @@ def _free_port() -> int:
         return s.getsockname()[1]
 
 
-def _worker(rank, world, port, kind, n, smoother, inner_from, agg_rows, cycles, errq, transport="host"):
+def _worker(rank, world, port, kind, n, smoother, inner_from, agg_rows, cycles, errq, transport="host", sum_order=0):
     try:
         os.environ["MASTER_ADDR"] = "127.0.0.1"
         os.environ["MASTER_PORT"] = str(port)
+        if sum_order:   # every level on the free-order kernels, merged row groups wherever possible
+            os.environ["SSS_HIP_FREE_MIN"] = "1"
+            os.environ["SSS_HIP_MERGE_MIN_ROWS"] = "1"
         import torch
         import torch.distributed as dist
 
@@ -40,7 +43,7 @@ def _worker(rank, world, port, kind, n, smoother, inner_from, agg_rows, cycles, 
         N = H.level(0).A.num_rows
         comm = A.Comm(world, rank, transport, device=0)
         D = A.DistHierarchy(H, comm, smoother=smoother, coarse="direct", device=0, agg_rows=agg_rows,
-                            inner_from=inner_from)
+                            inner_from=inner_from, sum_order=sum_order)
         assert D.nagg >= 2, D.nagg
         own = D.hi - D.lo
         D.upload("b", np.ones(own))
@@ -58,7 +61,8 @@ def _worker(rank, world, port, kind, n, smoother, inner_from, agg_rows, cycles, 
             x = np.zeros(N)
             for lo, xo in parts:
                 x[lo:lo + len(xo)] = xo
-            R = A.DeviceHierarchy(H, smoother=smoother, coarse="direct", device=0, inner_from=inner_from)
+            R = A.DeviceHierarchy(H, smoother=smoother, coarse="direct", device=0, inner_from=inner_from,
+                                  sum_order=sum_order)
             R.upload(0, "b", np.ones(N))
             R.upload(0, "x", np.ones(N))
             rel_r = []
@@ -67,9 +71,13 @@ def _worker(rank, world, port, kind, n, smoother, inner_from, agg_rows, cycles, 
                 rel_r.append(R.residual_norm() / np.sqrt(N))
             x_r = R.download(0, "x")
             R.close()
-            assert np.array_equal(x.view(np.uint64), x_r.view(np.uint64)), \
-                f"max |dx| = {np.max(np.abs(x - x_r))}"
-            assert np.allclose(rel, rel_r, rtol=1e-12, atol=0), (rel, rel_r)
+            if sum_order:   # tree-order sums over per-rank row groups: same iterates up to rounding
+                assert np.linalg.norm(x - x_r) <= 1e-10 * np.linalg.norm(x_r), np.max(np.abs(x - x_r))
+                assert np.allclose(rel, rel_r, rtol=1e-8, atol=0), (rel, rel_r)
+            else:
+                assert np.array_equal(x.view(np.uint64), x_r.view(np.uint64)), \
+                    f"max |dx| = {np.max(np.abs(x - x_r))}"
+                assert np.allclose(rel, rel_r, rtol=1e-12, atol=0), (rel, rel_r)
         dist.barrier()
         dist.destroy_process_group()
     except BaseException as e:  # noqa: BLE001
@@ -95,13 +103,22 @@ def test_dist_rccl_single_rank(smoother):
     _run(1, "rccl", 7, 24, smoother, 2, 100)
 
 
-def _run(world, transport, kind, n, smoother, inner_from, agg):
+@pytest.mark.parametrize("kind,n,smoother", [(7, 24, "hybrid"), (27, 14, "jacobi")])
+def test_dist_free_order(kind, n, smoother):
+    """bench.py's N > 1 configuration: throughput mode with the free-order (merged-group) kernels
+    on the row-partitioned engine, against the single-GPU engine in the same mode (27-point:
+    level 0 is not red-black, so its exact GS-CF cannot be split across ranks -- C/F-Jacobi)."""
+    _run(2, "host", kind, n, smoother, 2, 100, sum_order=1)
+
+
+def _run(world, transport, kind, n, smoother, inner_from, agg, sum_order=0):
     import torch.multiprocessing as mp
 
     ctx = mp.get_context("spawn")
     errq = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, kind, n, smoother, inner_from, agg, 4, errq, transport))
+    procs = [ctx.Process(target=_worker,
+                         args=(r, world, port, kind, n, smoother, inner_from, agg, 4, errq, transport, sum_order))
              for r in range(world)]
     for p in procs:
         p.start()
