@@ -443,7 +443,7 @@ def main():
                    "sorted_tiles": bool(sorted_tiles),
                    "iterations_to_tol": its, "final_relres": relres, "time_to_solution_s": solve_s,
                    "amg_pcg": pcg,
-                   "setup_s": setup_s, "hierarchy": hier_src, "upload_s": upload_s,
+                   "setup_s": setup_s, "hierarchy_source": hier_src, "upload_s": upload_s,
                    "parallelism": f"rowpart{D.world}" if D.world > 1 else "single-gpu",
                    "transport": transport},
         "roofline": {"bound": "hbm", "kernel": "spmv_adaptive<RESID> level 0", "achieved": achieved,
