@@ -564,6 +564,52 @@ __global__ __launch_bounds__(kB) void k_merged(int n, const int *gp, const unsig
     }
 }
 
+// Merged groups with LDS accumulators: one workgroup per group of G rows, its 4 waves take quarters
+// of the merged list; each lane accumulates into its private LDS slot acc[w][row][lane] (no select
+// chain, so G can grow: fewer x lines per 64 gathers), then per-row lane trees and waves in order.
+template <int G>
+__global__ __launch_bounds__(kB) void k_mlds(int n, const int *gp, const unsigned *mk, const double *mv,
+                                             const double *x, const double *b, double *y)
+{
+    __shared__ double acc[4][G][64];
+    __shared__ double red[4][G];
+    const int g = blockIdx.x, w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int k0 = gp[g], k1 = gp[g + 1], len = k1 - k0, per = (len + 3) >> 2;
+    const int a = k0 + min(len, w * per), e = k0 + min(len, (w + 1) * per);
+#pragma unroll
+    for (int u = 0; u < G; ++u) acc[w][u][lane] = 0.0;
+    constexpr int U = 4;
+    for (int k = a + lane; k < e; k += 64 * U) {
+        unsigned q[U];
+        double av[U];
+#pragma unroll
+        for (int t = 0; t < U; ++t) {
+            const int kk = k + 64 * t;
+            q[t] = kk < e ? mk[kk] : 0u;
+            av[t] = kk < e ? mv[kk] : 0.0;
+        }
+#pragma unroll
+        for (int t = 0; t < U; ++t) {
+            if (k + 64 * t >= e) break;
+            const double p = av[t] * x[q[t] >> 5];
+            acc[w][q[t] & 31u][lane] += p;
+        }
+    }
+#pragma unroll
+    for (int u = 0; u < G; ++u) {
+        double v = acc[w][u][lane];
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+        if (lane == 0) red[w][u] = v;
+    }
+    __syncthreads();
+    if (threadIdx.x < G) {
+        const int u = threadIdx.x, r = g * G + u;
+        const double t = ((red[0][u] + red[1][u]) + red[2][u]) + red[3][u];
+        if (r < n) y[r] = b[r] - t;
+    }
+}
+
 struct Lx {
     int K = 0, nchunk = 0, nb = 0;
     int *rs = nullptr, *crp = nullptr;
@@ -581,7 +627,7 @@ struct Merged {
 struct Dev {
     int n = 0, nnz = 0, nblk = 0;
     Lx lx[2];   // K = 8192, 16384
-    Merged mg[3];   // G = 4, 8, 16
+    Merged mg[5];   // G = 4, 8, 16, 32, 16(b)
     int *rp = nullptr, *ci = nullptr, *blk = nullptr, *pk11 = nullptr, *pk8 = nullptr;
     double *v11 = nullptr, *v8 = nullptr;
     std::vector<int> hrp, hci;
@@ -911,6 +957,9 @@ static void launch(int variant)
     case 41: launch_mg<8, 4>(1); break;
     case 42: launch_mg<16, 4>(2); break;
     case 43: launch_mg<8, 2>(1); break;
+    case 44: { Merged *M = mg_get(2, 16); if (M) hipLaunchKernelGGL(k_mlds<16>, dim3((D.n + 15) / 16), dim3(kB), 0, 0, D.n, M->gp, M->mk, M->mv, D.x, D.b, D.y); } break;
+    case 45: { Merged *M = mg_get(3, 32); if (M) hipLaunchKernelGGL(k_mlds<32>, dim3((D.n + 31) / 32), dim3(kB), 0, 0, D.n, M->gp, M->mk, M->mv, D.x, D.b, D.y); } break;
+    case 46: { Merged *M = mg_get(1, 8); if (M) hipLaunchKernelGGL(k_mlds<8>, dim3((D.n + 7) / 8), dim3(kB), 0, 0, D.n, M->gp, M->mk, M->mv, D.x, D.b, D.y); } break;
     default: break;
     }
 }

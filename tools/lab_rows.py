@@ -21,7 +21,7 @@ os.dup2(nul, 1)
 H = A.Hierarchy(A.generate(7, N))
 os.dup2(fd, 1)
 print(f"setup {time.time() - t:.1f}s levels={H.num_levels}", flush=True)
-names = ["tile", "wave256", "wave512", "wave1024", "wavedb256", "wavedb512", "mrow4", "mrow8", "mrow16", "mrow32", "lane16", "lane16pf", "lane8pf", "lane32pf", "tilepipe", "wdb256p", "wdb512p", "wdb1024p", "tilesort", "wavesort", "ts2k", "ts4k", "ts8k512", "ts8k1024", "ts16k", "chain2k", "v8u", "v8s", "v16s", "v32s", "v64s", "v64u", "v4s", "v64s8", "lx8k512", "lx8k1024", "lx16k", "lx16kR2Q4", "lx16kR8Q1", "lx16k512", "mg4", "mg8", "mg16", "mg8u2"]
+names = ["tile", "wave256", "wave512", "wave1024", "wavedb256", "wavedb512", "mrow4", "mrow8", "mrow16", "mrow32", "lane16", "lane16pf", "lane8pf", "lane32pf", "tilepipe", "wdb256p", "wdb512p", "wdb1024p", "tilesort", "wavesort", "ts2k", "ts4k", "ts8k512", "ts8k1024", "ts16k", "chain2k", "v8u", "v8s", "v16s", "v32s", "v64s", "v64u", "v4s", "v64s8", "lx8k512", "lx8k1024", "lx16k", "lx16kR2Q4", "lx16kR8Q1", "lx16k512", "mg4", "mg8", "mg16", "mg8u2", "mlds16", "mlds32", "mlds8"]
 sel = [int(a) for a in os.environ.get("LAB_VARIANTS", "0,20,4,26,27,28,29,30,31,32,33").split(",")]
 for l in range(int(os.environ.get('LAB_FROM', '0')), H.num_levels):
     M = H.level(l).A
