@@ -102,6 +102,7 @@ struct DevCSR {
     // (the long-row levels are bound by the L2->CU line rate of those gathers, not by HBM).
     int mg_G = 0;              // 0: no merged copy
     int mg_ng = 0;             // groups
+    int mg_W = 4;              // waves per group (1, 2 or 4): 4 / mg_W groups per workgroup
     int *mg_gp = nullptr;      // per group: first entry (mg_ng + 1)
     bool mg_two = false;       // two-segment rows
     unsigned *mg_k = nullptr;

@@ -499,19 +499,19 @@ __global__ __launch_bounds__(kBlock) void ts_stage0(int lo, DevCSR M, const int 
         const double d = deff[r];
         y[q] = fabs(d) > SMALLFLOAT ? acc / d : x(r);
     };
-    if constexpr (PATH >= 3) {   // merged row groups, G = PATH: one workgroup per group
+    if constexpr (PATH >= 3) {   // merged row groups, G = PATH, M.mg_W waves per group
         constexpr int G = PATH;
         __shared__ double red[8 * G];
-        const int g = xcd_bid();
         auto prod = [&](int c, double a) { return a * x(c); };
-        double sN[G], sL[G];
-        merged_group<G, 2>(M.mg_gp[g], M.mg_gp[g + 1], M.mg_k, M.mg_v, prod, sN, sL, red);
-        const double n_sum = merged_pick<G>(sN), l_sum = merged_pick<G>(sL);
-        const int q = g * G + (int)threadIdx.x;
-        if (threadIdx.x < G && q < M.n) {
-            const double Pq = b[lo + q] - n_sum;
-            P[q] = Pq;
-            finish(q, Pq - l_sum);
+        int g = 0, u = 0;
+        double n_sum = 0.0, l_sum = 0.0;
+        if (merged_block<G, 2>(M.mg_gp, M.mg_ng, M.mg_W, M.mg_k, M.mg_v, prod, red, g, u, n_sum, l_sum)) {
+            const int q = g * G + u;
+            if (q < M.n) {
+                const double Pq = b[lo + q] - n_sum;
+                P[q] = Pq;
+                finish(q, Pq - l_sum);
+            }
         }
         return;
     } else if constexpr (PATH == 2) {
@@ -593,16 +593,16 @@ __global__ __launch_bounds__(kBlock) void ts_inner(int lo, DevCSR M, const doubl
         const double d = deff[lo + q];
         y[q] = fabs(d) > SMALLFLOAT ? acc / d : ykeep[q];
     };
-    if constexpr (PATH >= 3) {   // merged row groups, G = PATH: one workgroup per group
+    if constexpr (PATH >= 3) {   // merged row groups, G = PATH, M.mg_W waves per group
         constexpr int G = PATH;
         __shared__ double red[8 * G];
-        const int g = xcd_bid();
-        double s[G], unused[G];
-        merged_group<G, 1>(M.mg_gp[g], M.mg_gp[g + 1], M.mg_k, M.mg_v, [&](int c, double a) { return a * fetch(c); },
-                           s, unused, red);
-        const double l_sum = merged_pick<G>(s);
-        const int q = g * G + (int)threadIdx.x;
-        if (threadIdx.x < G && q < M.n) finish(q, P[q] - l_sum);
+        int g = 0, u = 0;
+        double l_sum = 0.0, unused = 0.0;
+        if (merged_block<G, 1>(M.mg_gp, M.mg_ng, M.mg_W, M.mg_k, M.mg_v, [&](int c, double a) { return a * fetch(c); },
+                               red, g, u, l_sum, unused)) {
+            const int q = g * G + u;
+            if (q < M.n) finish(q, P[q] - l_sum);
+        }
         return;
     } else if constexpr (PATH == 2) {
         const int q = xcd_bid() * 4 + (threadIdx.x >> 6);

@@ -233,7 +233,12 @@ int devcsr_upload(DevCSR &d, const SSS_MAT &h, int split, int enc, const int *se
         build_merged(h, seg, d.mg_G, gp, mk, mv);
         d.mg_two = seg != nullptr;
         d.mg_ng = (int)gp.size() - 1;
-        d.ngrid = d.mg_ng;   // one workgroup per group
+        // waves per group: 4 (fewer -- longer waves over shorter groups -- measured no better on
+        // 7-pt 400^3: levels 5-10 6.6 ms per V-cycle with W = 1/2 by group size, 6.5 ms with 4)
+        const char *wz = getenv("SSS_HIP_MERGE_W");
+        d.mg_W = (wz && *wz) ? atoi(wz) : 4;
+        d.mg_W = d.mg_W >= 4 ? 4 : d.mg_W >= 2 ? 2 : 1;
+        d.ngrid = (d.mg_ng + 4 / d.mg_W - 1) / (4 / d.mg_W);
         d.mg_gp = dev_alloc<int>(gp.size());
         d.mg_k = dev_alloc<unsigned>(mk.size());
         d.mg_v = dev_alloc<double>(mv.size());
@@ -338,10 +343,9 @@ __global__ __launch_bounds__(kBlock) void spmv_wave(int n, const int *__restrict
     }
 }
 
-// Free order, merged row groups (DevCSR::mg_*): one workgroup per group of G rows (its 4 waves split
-// the group's entries), thread u < G writes row u.
+// Free order, merged row groups (DevCSR::mg_*): W waves per group of G rows (merged_block).
 template <int OP, bool NORM, int G>
-__global__ __launch_bounds__(kBlock) void spmv_merged(int n, int ng, const int *__restrict__ gp,
+__global__ __launch_bounds__(kBlock) void spmv_merged(int n, int ng, int W, const int *__restrict__ gp,
                                                       const unsigned *__restrict__ mk, const double *__restrict__ mv,
                                                       const double *__restrict__ x, const double *__restrict__ b,
                                                       double *__restrict__ y, double alpha, int cap,
@@ -349,28 +353,27 @@ __global__ __launch_bounds__(kBlock) void spmv_merged(int n, int ng, const int *
 {
     __shared__ double red[8 * G];
     __shared__ double nred[kBlock / 64];
-    const int g = xcd_bid();
-    double s[G], unused[G];
-    merged_group<G, 1>(gp[g], gp[g + 1], mk, mv, [&](int c, double a) { return a * x[c]; }, s, unused, red);
-    const double sr = merged_pick<G>(s);
-    const int r = g * G + (int)threadIdx.x;
-    double sq = 0.0;
-    if (threadIdx.x < G && r < n) {
-        bool write = true;
-        double out;
-        if constexpr (OP == SSS_HIP_SPMV_MXY) out = sr;
-        else if constexpr (OP == SSS_HIP_SPMV_AMXPY) out = y[r] + sr * alpha;
-        else if constexpr (OP == SSS_HIP_SPMV_RESID) out = b[r] + sr * alpha;
-        else {
-            write = !(cap > 0 && r >= cap);
-            out = write ? y[r] + sr : 0.0;
+    int g = 0, u = 0;
+    double sr = 0.0, unused = 0.0, sq = 0.0;
+    if (merged_block<G, 1>(gp, ng, W, mk, mv, [&](int c, double a) { return a * x[c]; }, red, g, u, sr, unused)) {
+        const int r = g * G + u;
+        if (r < n) {
+            bool write = true;
+            double out;
+            if constexpr (OP == SSS_HIP_SPMV_MXY) out = sr;
+            else if constexpr (OP == SSS_HIP_SPMV_AMXPY) out = y[r] + sr * alpha;
+            else if constexpr (OP == SSS_HIP_SPMV_RESID) out = b[r] + sr * alpha;
+            else {
+                write = !(cap > 0 && r >= cap);
+                out = write ? y[r] + sr : 0.0;
+            }
+            if (write) y[r] = out;
+            if (NORM) sq = out * out;
         }
-        if (write) y[r] = out;
-        if (NORM) sq = out * out;
     }
     if (NORM) {
         const double t = block_sum(sq, nred);
-        if (threadIdx.x == 0) partial[g] = t;
+        if (threadIdx.x == 0) partial[xcd_bid()] = t;
     }
 }
 
@@ -379,11 +382,11 @@ static void launch_op(const DevCSR &A, double alpha, const double *x, const doub
                       double *partial, hipStream_t s)
 {
     if (A.mg_G == 8)
-        hipLaunchKernelGGL((spmv_merged<OP, NORM, 8>), dim3(A.ngrid), dim3(kBlock), 0, s, A.n, A.mg_ng, A.mg_gp,
-                           A.mg_k, A.mg_v, x, b, y, alpha, cap, partial);
+        hipLaunchKernelGGL((spmv_merged<OP, NORM, 8>), dim3(A.ngrid), dim3(kBlock), 0, s, A.n, A.mg_ng, A.mg_W,
+                           A.mg_gp, A.mg_k, A.mg_v, x, b, y, alpha, cap, partial);
     else if (A.mg_G == 4)
-        hipLaunchKernelGGL((spmv_merged<OP, NORM, 4>), dim3(A.ngrid), dim3(kBlock), 0, s, A.n, A.mg_ng, A.mg_gp,
-                           A.mg_k, A.mg_v, x, b, y, alpha, cap, partial);
+        hipLaunchKernelGGL((spmv_merged<OP, NORM, 4>), dim3(A.ngrid), dim3(kBlock), 0, s, A.n, A.mg_ng, A.mg_W,
+                           A.mg_gp, A.mg_k, A.mg_v, x, b, y, alpha, cap, partial);
     else if (A.vec_rows)
         hipLaunchKernelGGL((spmv_wave<OP, NORM, true>), dim3(A.ngrid), dim3(kBlock), 0, s, A.n, A.rp, A.ci, A.v, x,
                            b, y, alpha, cap, partial);

@@ -414,19 +414,26 @@ __device__ __forceinline__ void merged_sums(int k0, int k1, const unsigned *__re
         }
 }
 
-// One merged group per 256-thread workgroup: the 4 waves take consecutive quarters of the
-// group's entries (merged_sums each), then every thread adds the 4 partials per (segment, row)
-// in wave order (fixed: deterministic).  t0/t1 valid in every thread.  red: 8G doubles of LDS.
+// Merged groups per 256-thread workgroup: W waves per group (W = 1, 2 or 4, DevCSR::mg_W), so
+// 4 / W groups per workgroup; the waves of a group take consecutive 1/W shares of its entries
+// (merged_sums each), then thread t < (4/W) G reports (group t / G, row t % G): the W partials
+// added in wave order (fixed: deterministic).  Returns false for threads without a row.
+// red: 8G doubles of LDS.  Must be reached by every thread of the block.
 template <int G, int S, class Prod>
-__device__ __forceinline__ void merged_group(int k0, int k1, const unsigned *__restrict__ mk,
-                                             const double *__restrict__ mv, Prod prod, double (&t0)[G],
-                                             double (&t1)[G], double *red)
+__device__ __forceinline__ bool merged_block(const int *__restrict__ gp, int ng, int W, const unsigned *__restrict__ mk,
+                                             const double *__restrict__ mv, Prod prod, double *red, int &g_out,
+                                             int &u_out, double &t0, double &t1)
 {
-    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int len = k1 - k0, per = (len + 3) >> 2;
-    const int a = k0 + min(len, w * per), e = k0 + min(len, (w + 1) * per);
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, gpb = 4 / W;
+    const int g = xcd_bid() * gpb + w / W, part = w % W;
     double s0[G], s1[G];
-    merged_sums<G, S>(a, e, mk, mv, prod, s0, s1);
+    if (g < ng) {
+        const int k0 = gp[g], k1 = gp[g + 1], len = k1 - k0, per = (len + W - 1) / W;
+        merged_sums<G, S>(k0 + min(len, part * per), k0 + min(len, (part + 1) * per), mk, mv, prod, s0, s1);
+    } else {
+#pragma unroll
+        for (int u = 0; u < G; ++u) s0[u] = 0.0, s1[u] = 0.0;
+    }
     if (lane == 0)
 #pragma unroll
         for (int u = 0; u < G; ++u) {
@@ -434,22 +441,17 @@ __device__ __forceinline__ void merged_group(int k0, int k1, const unsigned *__r
             if (S == 2) red[(w * 2 + 1) * G + u] = s1[u];
         }
     __syncthreads();
-#pragma unroll
-    for (int u = 0; u < G; ++u) {
-        t0[u] = ((red[0 * G + u] + red[2 * G + u]) + red[4 * G + u]) + red[6 * G + u];
-        if (S == 2) t1[u] = ((red[1 * G + u] + red[3 * G + u]) + red[5 * G + u]) + red[7 * G + u];
+    const int t = threadIdx.x;
+    if (t >= gpb * G) return false;
+    const int gi = t / G, u = t % G, gg = xcd_bid() * gpb + gi;
+    if (gg >= ng) return false;
+    double a0 = red[((gi * W) * 2) * G + u], a1 = S == 2 ? red[((gi * W) * 2 + 1) * G + u] : 0.0;
+    for (int v = 1; v < W; ++v) {
+        a0 += red[((gi * W + v) * 2) * G + u];
+        if (S == 2) a1 += red[((gi * W + v) * 2 + 1) * G + u];
     }
-}
-
-// the row sum this lane reports in a merged-group epilogue (lane u < G owns row u of the group)
-template <int G>
-__device__ __forceinline__ double merged_pick(const double (&s)[G])
-{
-    const int lane = threadIdx.x & 63;
-    double v = 0.0;
-#pragma unroll
-    for (int u = 0; u < G; ++u) v = lane == u ? s[u] : v;
-    return v;
+    g_out = gg, u_out = u, t0 = a0, t1 = a1;
+    return true;
 }
 
 }  // namespace sss

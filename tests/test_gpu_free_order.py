@@ -38,17 +38,19 @@ def a27_h(quiet):
     return build_hierarchy(A.generate(27, 16), quiet)
 
 
-@pytest.fixture(params=["wave", "merged4", "merged8"])
+@pytest.fixture(params=["wave", "merged4", "merged8", "merged4w1", "merged8w2"])
 def all_wave(request, monkeypatch):
     """every matrix of the hierarchy on the free-order kernels: wave per row (tree sum over the
-    column-sorted row), or merged row groups of 4 / 8 rows (sss_spmv_dev.hpp merged_sums)"""
+    column-sorted row), or merged row groups of 4 / 8 rows (sss_spmv_dev.hpp merged_sums) with
+    4 (default for these sizes), 1 or 2 waves per group"""
     monkeypatch.setenv("SSS_HIP_WAVE_MIN", "1")
     monkeypatch.setenv("SSS_HIP_FREE_MIN", "1")
     if request.param == "wave":
         monkeypatch.setenv("SSS_HIP_MERGE_MIN_ROWS", str(1 << 30))
     else:
         monkeypatch.setenv("SSS_HIP_MERGE_MIN_ROWS", "1")
-        monkeypatch.setenv("SSS_HIP_MERGE_G", request.param[-1])
+        monkeypatch.setenv("SSS_HIP_MERGE_G", request.param[6])
+        monkeypatch.setenv("SSS_HIP_MERGE_W", request.param[8] if "w" in request.param else "4")
     return request.param
 
 
