@@ -201,6 +201,10 @@ struct SmootherPlan {
     // Every row has exactly one diagonal entry, so every sweep's divisor is the row's own diagonal:
     // tile passes over a sorted-tile matrix read it from the staged tile instead of d_first/d_later.
     bool own_diag = false;
+    // The outer residual's F half may also compute the next call's first F pass (relax_range<3>):
+    // fuse_resid and f_overwritten hold and no F block is a long row.  smoother_run's pre_f then
+    // skips that pass and lets the first C pass read the F values from pre_f.
+    bool pend_ok = false;
 };
 // Residual fused into the smoother's last pass: r[i] = b[i] - sum_k a_ik x_k (stored order from
 // 0.0, x after the pass) for the C rows, and their per-block sums of squares into partial[block]
@@ -238,7 +242,12 @@ void launch_ts_inner(const DevCSR &M, int lo, const double *deff, const double *
                      const double *ykeep, double *y, hipStream_t s);
 void smoother_free(SmootherPlan &sp);
 int smoother_run(const SmootherPlan &sp, const DevCSR &A, const double *b, double *x, int sweeps,
-                 hipStream_t stream, const PassHooks *hooks = nullptr, ResidFuse *rf = nullptr);
+                 hipStream_t stream, const PassHooks *hooks = nullptr, ResidFuse *rf = nullptr,
+                 const double *pre_f = nullptr);
+// r = b - A x over the F rows (+ per-block partials) and pend = the F pass's GS values from this x
+// (SmootherPlan::pend_ok).
+int launch_f_residual_pending(const SmootherPlan &sp, const DevCSR &A, const double *b, const double *x, double *r,
+                              double *partial, double *pend, hipStream_t s);
 
 // ---- reductions ----------------------------------------------------------------------------
 // Deterministic sum of `n` partials -> *out (device); optionally sqrt.  `partials` must hold

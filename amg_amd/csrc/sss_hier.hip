@@ -55,6 +55,12 @@ struct sss_hip_hier {
     // the F rows.  Valid from the end of a cycle until level-0 x or b is touched by anything else.
     bool resid_c_ready = false;
     hipGraphExec_t resid_f_exec = nullptr;
+    // SmootherPlan::pend_ok on level 0: the residual norm's F half also produced the next cycle's
+    // first F pass (pend_f, F rows); valid while level-0 x and b are untouched.
+    bool pending_f = false;
+    double *pend_f = nullptr;
+    std::vector<hipGraphExec_t> cycle_steps_p;   // cycle graph variant that consumes pend_f
+    bool cycle_graph_ready_p = false;
     // AMG-preconditioned CG (sss_hip_pcg): level-0 work vectors, dot partials, device scalars
     double *pcg_v = nullptr;     // 7 vectors of n0: b, x, r, z, p, q, r_old
     double *pcg_part = nullptr;
@@ -137,6 +143,9 @@ static void hier_release(sss_hip_hier *h)
         if (g) (void)hipGraphExecDestroy(g);
     if (h->resid_exec) (void)hipGraphExecDestroy(h->resid_exec);
     if (h->resid_f_exec) (void)hipGraphExecDestroy(h->resid_f_exec);
+    for (hipGraphExec_t g : h->cycle_steps_p)
+        if (g) (void)hipGraphExecDestroy(g);
+    dev_free(h->pend_f);
     dev_free(h->pcg_v);
     dev_free(h->pcg_part);
     dev_free(h->pcg_s);
@@ -308,6 +317,10 @@ sss_hip_hier *sss::hier_create_impl(const SSS_AMG *mg, const sss_hip_opts *o, in
             return fail("memset");
     }
     h->partial = dev_alloc<double>((size_t)h->L[0].A.ngrid + kFinalScratch);
+    if (h->nl > 1 && h->L[0].sm.pend_ok) {
+        h->pend_f = dev_alloc<double>((size_t)std::max(h->L[0].sm.pass[0].hi, 1));
+        if (!h->pend_f) return fail("pending F pass buffer");
+    }
     h->d_norm = dev_alloc<double>(1);
     if (!h->partial || !h->d_norm || hipHostMalloc((void **)&h->h_norm, sizeof(double)) != hipSuccess)
         return fail("norm buffers");
@@ -370,6 +383,7 @@ extern "C" int sss_hip_upload_vec(sss_hip_hier *h, int level, int which, const d
     double *d = level_vec(h, level, which);
     if (!d || n < 0 || n > h->L[level].A.n) return ERROR_INPUT_PAR;
     h->resid_c_ready = false;
+    h->pending_f = false;
     const auto &perm = h->L[level].perm;
     if (!perm.empty()) {
         if (n != h->L[level].A.n) return ERROR_INPUT_PAR;   // relabeled levels move whole vectors
@@ -427,20 +441,21 @@ extern "C" int sss_hip_smooth(sss_hip_hier *h, int level, int post)
     auto &L = h->L[level];
     const int sweeps = post ? h->pars.post_iter : h->pars.pre_iter;
     h->resid_c_ready = false;
+    h->pending_f = false;
     return smoother_run(L.sm, L.A, L.b, L.x, sweeps, h->stream);
 }
 
 // Smoothing that leaves r = b - A x in wp: fused into the last C pass where the plan allows,
 // then the F rows by a residual SpMV over blocks [0, split_blk); otherwise a full residual SpMV.
 // `partial` (optional): per-block sums of squares of r, for the norm.
-static int smooth_then_residual(sss_hip_hier *h, int l, int post, double *partial)
+static int smooth_then_residual(sss_hip_hier *h, int l, int post, double *partial, const double *pre_f = nullptr)
 {
     auto &L = h->L[l];
     const int sweeps = post ? h->pars.post_iter : h->pars.pre_iter;
     ResidFuse rf;
     rf.r = L.wp;
     rf.partial = partial;
-    int rc = smoother_run(L.sm, L.A, L.b, L.x, sweeps, h->stream, nullptr, &rf);
+    int rc = smoother_run(L.sm, L.A, L.b, L.x, sweeps, h->stream, nullptr, &rf, pre_f);
     if (rc) return rc;
     if (rf.done) return launch_spmv_blocks(L.A, L.A.split_blk, SSS_HIP_SPMV_RESID, -1.0, L.x, L.b, L.wp, partial, h->stream);
     return launch_spmv(L.A, SSS_HIP_SPMV_RESID, -1.0, L.x, L.b, L.wp, 0, partial, h->stream);
@@ -449,7 +464,7 @@ static int smooth_then_residual(sss_hip_hier *h, int l, int post, double *partia
 // Walks SSS_amg_cycle's static control flow, enqueueing kernels; `coarse(h)` is called where
 // the coarsest solve goes.
 template <class CoarseFn>
-static int walk_cycle(sss_hip_hier *h, CoarseFn coarse)
+static int walk_cycle(sss_hip_hier *h, CoarseFn coarse, bool pend = false)
 {
     const int nl = h->nl;
     const int cycle_type = h->pars.cycle_type <= 0 ? 1 : h->pars.cycle_type;
@@ -460,7 +475,8 @@ static int walk_cycle(sss_hip_hier *h, CoarseFn coarse)
         while (l < nl - 1) {
             auto &L = h->L[l];
             visits[l]++;
-            if ((rc = smooth_then_residual(h, l, 0, nullptr))) return rc;
+            const bool first = l == 0 && visits[0] == 1;
+            if ((rc = smooth_then_residual(h, l, 0, nullptr, pend && first ? h->pend_f : nullptr))) return rc;
             if ((rc = launch_spmv(L.R, SSS_HIP_SPMV_MXY, 1.0, L.wp, nullptr, h->L[l + 1].b, 0, nullptr, s))) return rc;
             l++;
             SSS_HIP(hipMemsetAsync(h->L[l].x, 0, sizeof(double) * (size_t)h->L[l].A.n, s));
@@ -506,46 +522,49 @@ static int end_capture(sss_hip_hier *h, hipGraphExec_t *exec)
     return 0;
 }
 
-static int build_cycle_graph(sss_hip_hier *h)
+static int build_cycle_graph(sss_hip_hier *h, bool pend)
 {
+    std::vector<hipGraphExec_t> &steps = pend ? h->cycle_steps_p : h->cycle_steps;
     SSS_HIP(hipStreamBeginCapture(h->stream, hipStreamCaptureModeThreadLocal));
-    int rc = walk_cycle(h, [](sss_hip_hier *hh) -> int {
+    int rc = walk_cycle(h, [&steps](sss_hip_hier *hh) -> int {
         if (hh->coarse_mode == SSS_HIP_COARSE_DIRECT) return sss_hip_coarse_solve(hh);
         hipGraphExec_t seg = nullptr;
         int r = end_capture(hh, &seg);
         if (r) return r;
-        hh->cycle_steps.push_back(seg);
-        hh->cycle_steps.push_back(nullptr);
+        steps.push_back(seg);
+        steps.push_back(nullptr);
         SSS_HIP(hipStreamBeginCapture(hh->stream, hipStreamCaptureModeThreadLocal));
         return 0;
-    });
+    }, pend);
     hipGraphExec_t last = nullptr;
     int rc2 = end_capture(h, &last);
     if (rc) return rc;
     if (rc2) return rc2;
-    h->cycle_steps.push_back(last);
-    h->cycle_graph_ready = true;
+    steps.push_back(last);
+    (pend ? h->cycle_graph_ready_p : h->cycle_graph_ready) = true;
     return 0;
 }
 
-static int cycle_impl(sss_hip_hier *h);
+static int cycle_impl(sss_hip_hier *h, bool pend);
 extern "C" int sss_hip_cycle(sss_hip_hier *h)
 {
+    const bool pend = h->pending_f && h->nl > 1 && h->pars.pre_iter > 0;
     h->resid_c_ready = false;
-    int rc = cycle_impl(h);
+    h->pending_f = false;
+    int rc = cycle_impl(h, pend);
     if (rc) return rc;
     h->resid_c_ready = h->nl > 1 && h->L[0].sm.fuse_resid && h->pars.post_iter > 0;
     return 0;
 }
 
-static int cycle_impl(sss_hip_hier *h)
+static int cycle_impl(sss_hip_hier *h, bool pend)
 {
-    if (!h->opts.use_graph) return walk_cycle(h, [](sss_hip_hier *hh) { return sss_hip_coarse_solve(hh); });
-    if (!h->cycle_graph_ready) {
-        int rc = build_cycle_graph(h);
+    if (!h->opts.use_graph) return walk_cycle(h, [](sss_hip_hier *hh) { return sss_hip_coarse_solve(hh); }, pend);
+    if (!(pend ? h->cycle_graph_ready_p : h->cycle_graph_ready)) {
+        int rc = build_cycle_graph(h, pend);
         if (rc) return rc;
     }
-    for (hipGraphExec_t g : h->cycle_steps) {
+    for (hipGraphExec_t g : (pend ? h->cycle_steps_p : h->cycle_steps)) {
         if (g) SSS_HIP(hipGraphLaunch(g, h->stream));
         else {
             int rc = sss_hip_coarse_solve(h);
@@ -559,8 +578,11 @@ static int cycle_impl(sss_hip_hier *h)
 static int enqueue_residual_norm(sss_hip_hier *h, bool f_only)
 {
     auto &L = h->L[0];
-    int rc = f_only ? launch_spmv_blocks(L.A, L.A.split_blk, SSS_HIP_SPMV_RESID, -1.0, L.x, L.b, L.wp, h->partial, h->stream)
-                    : launch_spmv(L.A, SSS_HIP_SPMV_RESID, -1.0, L.x, L.b, L.wp, 0, h->partial, h->stream);
+    const bool pend = f_only && h->pend_f;   // the F half also precomputes the next first F pass
+    int rc = pend     ? launch_f_residual_pending(L.sm, L.A, L.b, L.x, L.wp, h->partial, h->pend_f, h->stream)
+             : f_only ? launch_spmv_blocks(L.A, L.A.split_blk, SSS_HIP_SPMV_RESID, -1.0, L.x, L.b, L.wp, h->partial,
+                                           h->stream)
+                      : launch_spmv(L.A, SSS_HIP_SPMV_RESID, -1.0, L.x, L.b, L.wp, 0, h->partial, h->stream);
     if (rc) return rc;
     return launch_final_sum(h->partial, L.A.ngrid, h->d_norm, true, h->stream);
 }
@@ -584,6 +606,7 @@ extern "C" int sss_hip_residual_norm(sss_hip_hier *h, double *absres)
         int rc = enqueue_residual_norm(h, f_only);
         if (rc) return rc;
     }
+    h->pending_f = f_only && h->pend_f;
     SSS_HIP(hipMemcpyAsync(h->h_norm, h->d_norm, sizeof(double), hipMemcpyDeviceToHost, h->stream));
     SSS_HIP(hipStreamSynchronize(h->stream));
     *absres = *h->h_norm;
@@ -608,6 +631,7 @@ extern "C" int sss_hip_pcg(sss_hip_hier *h, double tol, int maxit, int *iters, d
         if (!h->pcg_v || !h->pcg_part || !h->pcg_s) return hip_fail(hipErrorOutOfMemory, "hipMalloc(pcg)", __FILE__, __LINE__);
         SSS_HIP(hipHostMalloc((void **)&h->pcg_h, 8 * sizeof(double), hipHostMallocDefault));
     }
+    h->pending_f = false;   // b and x are rewritten below
     double *bs = h->pcg_v, *xs = bs + n, *r = xs + n, *z = r + n, *p = z + n, *q = p + n, *ro = q + n;
     double *rz = h->pcg_s, *pq = h->pcg_s + 1, *rr = h->pcg_s + 2, *rzn = h->pcg_s + 3, *roz = h->pcg_s + 4;
     const size_t bytes = sizeof(double) * (size_t)n;

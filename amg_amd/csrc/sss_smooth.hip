@@ -241,7 +241,8 @@ int smoother_build(SmootherPlan &sp, const SSS_MAT &A, const int *mark, int kind
             ok = std::fabs(d_first[i]) > SMALLFLOAT && std::fabs(all_diag ? d_first[i] : d_later[i]) > SMALLFLOAT;
         sp.f_overwritten = ok;
     }
-    const char *fz = getenv("SSS_HIP_FUSE_RESID");   // 0: never fuse (tests compare both paths)
+    const char *fz = getenv("SSS_HIP_FUSE_RESID");
+    const char *pz = getenv("SSS_HIP_PEND_F");   // 0: never precompute the first F pass (tests)   // 0: never fuse (tests compare both paths)
     if (!(fz && *fz == '0') && kind != SSS_HIP_SMOOTH_JACOBI && dA && !dA->wave_rows && !dA->vec_rows && all_diag && single_diag &&
         dA->split_row > 0 &&
         dA->split_row < n && sp.pass[0].range && sp.pass[1].range && sp.pass[0].lo == 0 &&
@@ -252,6 +253,9 @@ int smoother_build(SmootherPlan &sp, const SSS_MAT &A, const int *mark, int kind
         for (int q = dA->split_blk; q < dA->nblk && short_blocks; ++q)
             short_blocks = rp[blk[q + 1]] - rp[blk[q]] <= kTileEntries;
         sp.fuse_resid = short_blocks;
+        bool f_short = true;
+        for (int q = 0; q < dA->split_blk && f_short; ++q) f_short = rp[blk[q + 1]] - rp[blk[q]] <= kTileEntries;
+        sp.pend_ok = short_blocks && f_short && sp.f_overwritten && !(pz && *pz == '0');
     }
     if (kind == SSS_HIP_SMOOTH_JACOBI) {
         if ((rc = upload_doubles(&sp.d_first, last_diag))) return rc;   // Jacobi: row's own diagonal
@@ -371,6 +375,8 @@ __global__ __launch_bounds__(kBlock) void relax_wave(int m, const int *__restric
 // Class pass over rows [lo, hi) of a relabeled level, blocks [blo, ...) of its own CSR.
 //   MODE 0: GS-CF pass of depth 1, in place (x[r] = t / d).
 //   MODE 1: C/F-Jacobi pass / two-stage stage 0: y[r - lo] = t / d, every x from before the pass.
+//   MODE 3: the residual of the row with x unchanged (rr, partial, as the residual SpMV) and the
+//           GS value the pass's MODE 0 would write, into y[r - lo] (SmootherPlan::pend_ok).
 //   MODE 2: MODE 0, then the residual of the updated row (ResidFuse, sss_engine.hpp):
 //           rr[r] = b_r - (sum of a_k x_k in stored order from 0.0), the diagonal product formed
 //           with the new x_r -- exactly the residual SpMV's chain, since in a depth-1 pass no
@@ -391,7 +397,7 @@ __global__ __launch_bounds__(kBlock) void relax_range(int blo, const int *__rest
     const int bid = blo + xcd_bid();
     const int r0 = blk[bid], r1 = blk[bid + 1];
     const int k0 = rp[r0], k1 = rp[r1];
-    auto fetch = [&](int c) -> double { return MODE == 1 ? xs(c) : x[c]; };
+    auto fetch = [&](int c) -> double { return xs(c); };
     // deff null: the plan's divisor is each row's own diagonal, staged from the sorted tile
     auto dval = [&](int r) -> double { return deff ? deff[r] : sm.d[r - r0]; };
     auto finish = [&](int r, double acc) {
@@ -427,17 +433,23 @@ __global__ __launch_bounds__(kBlock) void relax_range(int blo, const int *__rest
                 const double out = br + s * -1.0;
                 rr[r] = out;
                 sq = out * out;
+            } else if constexpr (MODE == 3) {   // residual of the row (x unchanged) + its GS value
+                const double out = br + chain_add(0.0, sm.v, a, e) * -1.0;
+                rr[r] = out;
+                sq = out * out;
+                const double d = dval(r);
+                y[r - lo] = fabs(d) > SMALLFLOAT ? acc / d : x[r];
             } else {
                 finish(r, acc);
             }
         }
-        if constexpr (MODE == 2) {
+        if constexpr (MODE >= 2) {
             if (partial) {
                 const double t = block_sum(sq, sm.red);
                 if (threadIdx.x == 0) partial[bid] = t;
             }
         }
-    } else if constexpr (MODE != 2) {   // MODE 2 plans have no long-row block
+    } else if constexpr (MODE < 2) {   // MODE 2 / 3 plans have no long-row block
         const int r = r0, dp = diag_pos[r];
         double acc = b[r];
         for (int base = k0; base < k1; base += kTileEntries) {
@@ -678,6 +690,19 @@ void launch_ts_inner(const DevCSR &M, int lo, const double *deff, const double *
         hipLaunchKernelGGL(ts_inner<0>, dim3(M.nblk), dim3(kBlock), 0, s, lo, M, deff, P, ycols, col_off, ykeep, y);
 }
 
+int launch_f_residual_pending(const SmootherPlan &sp, const DevCSR &A, const double *b, const double *x, double *r,
+                              double *partial, double *pend, hipStream_t s)
+{
+    if (!sp.pend_ok) return ERROR_INPUT_PAR;
+    const PassSchedule &F = sp.pass[0];
+    const double *deff = (sp.own_diag && A.pk) ? nullptr : sp.d_first;
+    hipLaunchKernelGGL(relax_range<3>, dim3(F.bhi - F.blo), dim3(kBlock), 0, s, F.blo, A.blk, A.rp, A.ci, A.v,
+                       sp.diag_pos, F.lo, b, const_cast<double *>(x), (const double *)nullptr, pend, deff, A.pk, A.pv,
+                       A.pb, r, partial, xsrc_of(x));
+    SSS_HIP(hipGetLastError());
+    return 0;
+}
+
 __global__ __launch_bounds__(kBlock) void scatter_rows(int m, const int *__restrict__ map, const double *__restrict__ y,
                                                        double *__restrict__ x)
 {
@@ -686,9 +711,10 @@ __global__ __launch_bounds__(kBlock) void scatter_rows(int m, const int *__restr
 }
 
 int smoother_run(const SmootherPlan &sp, const DevCSR &A, const double *b, double *x, int sweeps, hipStream_t s,
-                 const PassHooks *hk, ResidFuse *rf)
+                 const PassHooks *hk, ResidFuse *rf, const double *pre_f)
 {
     if (rf) rf->done = false;
+    if (pre_f && (!sp.pend_ok || hk || sweeps < 1)) return ERROR_INPUT_PAR;
     const int n = A.n;
     if (n == 0) return 0;
     int rc;
@@ -700,6 +726,7 @@ int smoother_run(const SmootherPlan &sp, const DevCSR &A, const double *b, doubl
         for (int c = 0; c < 2; ++c) {
             const PassSchedule &ps = sp.pass[c];
             if (ps.nrows == 0) continue;
+            if (pre_f && sw == 0 && c == 0) continue;   // computed with the last residual (pre_f)
             if (hk) {   // distributed level: refresh x's ghosts; only contiguous passes qualify
                 if (!ps.range) return ERROR_INPUT_PAR;
                 if ((rc = hk->exchange(hk->ctx, x))) return rc;
@@ -707,7 +734,8 @@ int smoother_run(const SmootherPlan &sp, const DevCSR &A, const double *b, doubl
             if (ps.range) {
                 const int nb = ps.bhi - ps.blo, m = ps.hi - ps.lo, nw = (m + 3) / 4;
                 const bool wave = A.wave_rows || A.vec_rows;
-                const XSrc xs = nocopy ? XSrc{cur[0], cur[1], sp.csplit} : xsrc_of(x);
+                XSrc xs = nocopy ? XSrc{cur[0], cur[1], sp.csplit} : xsrc_of(x);
+                if (pre_f && sw == 0) xs = XSrc{pre_f, x, sp.pass[0].hi};   // this sweep's F values
                 // tile passes take each row's divisor from its staged diagonal (no deff stream)
                 const bool tile_d = sp.own_diag && A.pk != nullptr;
                 auto relax = [&](auto mode, const int *cols, const double *yp, double *y) {
@@ -769,6 +797,8 @@ int smoother_run(const SmootherPlan &sp, const DevCSR &A, const double *b, doubl
                 } else {
                     relax(std::integral_constant<int, 0>(), A.ci, (const double *)nullptr, (double *)nullptr);
                 }
+                if (pre_f && sw == 0 && c == 1 && sweeps == 1)   // no later F pass overwrites x_F
+                    SSS_HIP(hipMemcpyAsync(x, pre_f, sizeof(double) * (size_t)sp.pass[0].hi, hipMemcpyDeviceToDevice, s));
                 continue;
             }
             if (sp.kind == SSS_HIP_SMOOTH_JACOBI) {

@@ -2,8 +2,8 @@
 
     python tools/level_breakdown.py gpurun_out/prof_x/run_results.db [bench.json]
 
-Walks the kernels in start order.  A cycle ends at the fused residual-norm kernel
-(spmv_*<2, true>); inside a cycle, a restriction (spmv_*<0, ...>, SSS_HIP_SPMV_MXY) moves the
+Walks the kernels in start order.  A cycle ends at the residual-norm kernel
+(spmv_*<2, true>, or relax_range<3> when it also computes the next first F pass); inside a cycle, a restriction (spmv_*<0, ...>, SSS_HIP_SPMV_MXY) moves the
 level counter down, a prolongation (spmv_*<1, ...>) moves it up, the dense GEMV / Krylov kernels
 are the coarsest level.  Prints, per level, the kernel time of one average cycle split into
 smoother / residual / restriction / prolongation / other, and, when the bench JSON (its
@@ -36,7 +36,9 @@ def main():
     for name, s, e in rows:
         dur = (e - s) / 1e3   # us
         m = re.search(r"(spmv_\w+)<(\d), (true|false)(?:, \w+)?>", name)
-        if m and m.group(2) == "2" and m.group(3) == "true":
+        # the outer residual norm ends a cycle: the fused-norm SpMV, or relax_range<3> (its F half
+        # fused with the next cycle's first F pass, SmootherPlan::pend_ok)
+        if (m and m.group(2) == "2" and m.group(3) == "true") or "relax_range<3>" in name:
             if cur is not None:
                 cur[("out", "resid")] += dur
                 cycles.append(cur)
