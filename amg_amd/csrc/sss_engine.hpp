@@ -205,6 +205,8 @@ struct SmootherPlan {
     // fuse_resid and f_overwritten hold and no F block is a long row.  smoother_run's pre_f then
     // skips that pass and lets the first C pass read the F values from pre_f.
     bool pend_ok = false;
+    // Every value of A is finite: a pass over a zero iterate reduces to t = b (zero_first_pass).
+    bool finite = false;
 };
 // Residual fused into the smoother's last pass: r[i] = b[i] - sum_k a_ik x_k (stored order from
 // 0.0, x after the pass) for the C rows, and their per-block sums of squares into partial[block]
@@ -243,7 +245,7 @@ void launch_ts_inner(const DevCSR &M, int lo, const double *deff, const double *
 void smoother_free(SmootherPlan &sp);
 int smoother_run(const SmootherPlan &sp, const DevCSR &A, const double *b, double *x, int sweeps,
                  hipStream_t stream, const PassHooks *hooks = nullptr, ResidFuse *rf = nullptr,
-                 const double *pre_f = nullptr);
+                 const double *pre_f = nullptr, bool x_zero = false);
 // r = b - A x over the F rows (+ per-block partials) and pend = the F pass's GS values from this x
 // (SmootherPlan::pend_ok).
 int launch_f_residual_pending(const SmootherPlan &sp, const DevCSR &A, const double *b, const double *x, double *r,

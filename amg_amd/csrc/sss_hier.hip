@@ -448,14 +448,15 @@ extern "C" int sss_hip_smooth(sss_hip_hier *h, int level, int post)
 // Smoothing that leaves r = b - A x in wp: fused into the last C pass where the plan allows,
 // then the F rows by a residual SpMV over blocks [0, split_blk); otherwise a full residual SpMV.
 // `partial` (optional): per-block sums of squares of r, for the norm.
-static int smooth_then_residual(sss_hip_hier *h, int l, int post, double *partial, const double *pre_f = nullptr)
+static int smooth_then_residual(sss_hip_hier *h, int l, int post, double *partial, const double *pre_f = nullptr,
+                                bool x_zero = false)
 {
     auto &L = h->L[l];
     const int sweeps = post ? h->pars.post_iter : h->pars.pre_iter;
     ResidFuse rf;
     rf.r = L.wp;
     rf.partial = partial;
-    int rc = smoother_run(L.sm, L.A, L.b, L.x, sweeps, h->stream, nullptr, &rf, pre_f);
+    int rc = smoother_run(L.sm, L.A, L.b, L.x, sweeps, h->stream, nullptr, &rf, pre_f, x_zero);
     if (rc) return rc;
     if (rf.done) return launch_spmv_blocks(L.A, L.A.split_blk, SSS_HIP_SPMV_RESID, -1.0, L.x, L.b, L.wp, partial, h->stream);
     return launch_spmv(L.A, SSS_HIP_SPMV_RESID, -1.0, L.x, L.b, L.wp, 0, partial, h->stream);
@@ -476,7 +477,8 @@ static int walk_cycle(sss_hip_hier *h, CoarseFn coarse, bool pend = false)
             auto &L = h->L[l];
             visits[l]++;
             const bool first = l == 0 && visits[0] == 1;
-            if ((rc = smooth_then_residual(h, l, 0, nullptr, pend && first ? h->pend_f : nullptr))) return rc;
+            // levels >= 1 were just zeroed by the descent: the first pass may skip its products
+            if ((rc = smooth_then_residual(h, l, 0, nullptr, pend && first ? h->pend_f : nullptr, l > 0))) return rc;
             if ((rc = launch_spmv(L.R, SSS_HIP_SPMV_MXY, 1.0, L.wp, nullptr, h->L[l + 1].b, 0, nullptr, s))) return rc;
             l++;
             SSS_HIP(hipMemsetAsync(h->L[l].x, 0, sizeof(double) * (size_t)h->L[l].A.n, s));

@@ -233,6 +233,12 @@ int smoother_build(SmootherPlan &sp, const SSS_MAT &A, const int *mark, int kind
     }
     sp.own_diag = all_diag && single_diag && !(tz && *tz == '0');
     {
+        const char *zz = getenv("SSS_HIP_ZERO_FIRST");   // 0: run the first pass on a zero x in full (tests)
+        bool fin = !(zz && *zz == '0');
+        for (int k = 0; fin && k < rp[n]; ++k) fin = std::isfinite(v[k]);
+        sp.finite = fin;
+    }
+    {
         const char *dz = getenv("SSS_HIP_DEAD_PROLONG");   // 0: always prolong into every row (tests)
         const PassSchedule &F = sp.pass[0];
         bool ok = !(dz && *dz == '0') && kind != SSS_HIP_SMOOTH_JACOBI && F.range && F.lo == 0 && F.nrows > 0 &&
@@ -690,6 +696,42 @@ void launch_ts_inner(const DevCSR &M, int lo, const double *deff, const double *
         hipLaunchKernelGGL(ts_inner<0>, dim3(M.nblk), dim3(kBlock), 0, s, lo, M, deff, P, ycols, col_off, ykeep, y);
 }
 
+// First pass of a smoother call on a zero iterate (C/F-Jacobi pass or two-stage stage 0 right after
+// the cycle zeroed x): every product a_k * x_k is +-0.0, so t = b - (a_1 x_1) - (a_2 x_2) - ... is
+// exactly b -- except b == -0.0 with a summed value whose sign bit is set (its product -0.0 turns
+// -0.0 into +0.0), which is order-independent.  The pass then reads no matrix entries (the rare
+// -0.0 rows scan their values).  Requires finite matrix values (SmootherPlan::finite).
+__device__ __forceinline__ double zero_x_sum(double t, const int *__restrict__ ci, const double *__restrict__ v, int a,
+                                             int e, int skip_col)
+{
+    if (t == 0.0 && signbit(t))
+        for (int k = a; k < e; ++k)
+            if (ci[k] != skip_col && signbit(v[k])) return 0.0;
+    return t;
+}
+
+template <bool TWO>
+__global__ __launch_bounds__(kBlock) void zero_first_pass(int lo, int m, const int *__restrict__ rp,
+                                                          const int *__restrict__ ci, const double *__restrict__ v,
+                                                          const int *__restrict__ split, const double *__restrict__ b,
+                                                          const double *__restrict__ deff, double *__restrict__ P,
+                                                          double *__restrict__ y)
+{
+    const int q = blockIdx.x * kBlock + threadIdx.x;
+    if (q >= m) return;
+    const int r = lo + q;
+    double t;
+    if (TWO) {   // rows of the pass's [N | L] matrix (local numbering): P = b - N x, t = P - L x
+        const double Pq = zero_x_sum(b[r], ci, v, rp[q], split[q], -1);
+        P[q] = Pq;
+        t = zero_x_sum(Pq, ci, v, split[q], rp[q + 1], -1);
+    } else {     // rows of the level matrix: every entry but the diagonal
+        t = zero_x_sum(b[r], ci, v, rp[r], rp[r + 1], r);
+    }
+    const double d = deff[r];
+    y[q] = fabs(d) > SMALLFLOAT ? t / d : 0.0;   // a row that keeps its value keeps x_r = +0.0
+}
+
 int launch_f_residual_pending(const SmootherPlan &sp, const DevCSR &A, const double *b, const double *x, double *r,
                               double *partial, double *pend, hipStream_t s)
 {
@@ -711,7 +753,7 @@ __global__ __launch_bounds__(kBlock) void scatter_rows(int m, const int *__restr
 }
 
 int smoother_run(const SmootherPlan &sp, const DevCSR &A, const double *b, double *x, int sweeps, hipStream_t s,
-                 const PassHooks *hk, ResidFuse *rf, const double *pre_f)
+                 const PassHooks *hk, ResidFuse *rf, const double *pre_f, bool x_zero)
 {
     if (rf) rf->done = false;
     if (pre_f && (!sp.pend_ok || hk || sweeps < 1)) return ERROR_INPUT_PAR;
@@ -768,7 +810,15 @@ int smoother_run(const SmootherPlan &sp, const DevCSR &A, const double *b, doubl
                     // stage 0 (or the Jacobi pass) writes the other buffer; inner steps read only this
                     // class's previous iterate, so they alternate between the two buffers in place
                     double *prev = cur[c] == x ? sp.x2 : x, *next = cur[c];
-                    if (sp.inner > 0)
+                    const bool zfirst = x_zero && sw == 0 && c == 0 && sp.finite;
+                    const int zg = (m + kBlock - 1) / kBlock;
+                    if (zfirst && sp.inner > 0)
+                        hipLaunchKernelGGL(zero_first_pass<true>, dim3(zg), dim3(kBlock), 0, s, ps.lo, m, ps.ts_nl.rp,
+                                           ps.ts_nl.ci, ps.ts_nl.v, ps.ts_split, b, deff, ps.ts_P, prev + ps.lo);
+                    else if (zfirst)
+                        hipLaunchKernelGGL(zero_first_pass<false>, dim3(zg), dim3(kBlock), 0, s, ps.lo, m, A.rp, A.ci,
+                                           A.v, (const int *)nullptr, b, deff, (double *)nullptr, prev + ps.lo);
+                    else if (sp.inner > 0)
                         launch_ts_stage0(ps.ts_nl, ps.lo, ps.ts_split, b, xs, deff, ps.ts_P, prev + ps.lo, s);
                     else
                         relax(std::integral_constant<int, 1>(), A.ci, (const double *)nullptr, prev + ps.lo);

@@ -63,7 +63,7 @@ def main():
         if "dense_gemv" in name or "k_" in name.split("(")[0]:
             cur[("coarse", "solve")] += dur
             continue
-        if any(k in name for k in ("relax", "ts_", "gs_", "scatter")):
+        if any(k in name for k in ("relax", "ts_", "gs_", "scatter", "zero_first_pass")):
             cur[(lvl, "smooth")] += dur
         else:
             cur[(lvl, "other")] += dur
