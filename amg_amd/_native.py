@@ -109,7 +109,8 @@ ABI_SYMBOLS = [
     "sss_hip_host_smooth", "sss_hip_host_coarse_solve", "sss_hip_time_level0_spmv", "sss_hip_time_iterations",
     "sss_gen_stencil",
     "sss_hip_rccl_unique_id", "sss_hip_comm_rccl", "sss_hip_comm_host", "sss_hip_comm_destroy",
-    "sss_hip_dist_create", "sss_hip_dist_destroy", "sss_hip_dist_info", "sss_hip_dist_upload_vec",
+    "sss_hip_dist_create", "sss_hip_dist_destroy", "sss_hip_dist_info", "sss_hip_dist_level_flags",
+    "sss_hip_dist_upload_vec",
     "sss_hip_dist_download_vec", "sss_hip_dist_cycle", "sss_hip_dist_residual_norm", "sss_hip_dist_sync",
     "sss_hip_dist_time_level0_spmv",
     "sss_part_plan_create", "sss_part_plan_destroy", "sss_part_plan_nagg", "sss_part_plan_level",
@@ -180,6 +181,7 @@ def _declare(lib):
         "sss_hip_dist_create": (C.c_void_p, [P(SSS_AMG), P(SSS_HIP_OPTS), C.c_void_p, C.c_int]),
         "sss_hip_dist_destroy": (None, [C.c_void_p]),
         "sss_hip_dist_info": (C.c_int, [C.c_void_p, _int_p, _int_p, _int_p, _int_p]),
+        "sss_hip_dist_level_flags": (C.c_int, [C.c_void_p, C.c_int]),
         "sss_hip_dist_upload_vec": (C.c_int, [C.c_void_p, C.c_int, _dbl_p, C.c_int]),
         "sss_hip_dist_download_vec": (C.c_int, [C.c_void_p, C.c_int, _dbl_p, C.c_int]),
         "sss_hip_dist_cycle": (C.c_int, [C.c_void_p]),
@@ -573,6 +575,13 @@ class DistHierarchy:
         lo, hi, nagg, g = C.c_int(), C.c_int(), C.c_int(), C.c_int()
         lib().sss_hip_dist_info(self.d, C.byref(lo), C.byref(hi), C.byref(nagg), C.byref(g))
         self.lo, self.hi, self.nagg, self.nghost0 = lo.value, hi.value, nagg.value, g.value
+
+    def level_flags(self, l: int) -> dict:
+        """Exact eliminations in force on partitioned level l (agreed over the ranks)."""
+        f = lib().sss_hip_dist_level_flags(self.d, l)
+        if f < 0:
+            raise ValueError(f"no partitioned level {l}")
+        return {"zero_first": bool(f & 1), "fused_residual": bool(f & 2), "dead_prolong": bool(f & 4)}
 
     def _check(self, rc, what):
         if rc != 0:

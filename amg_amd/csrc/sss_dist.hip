@@ -94,6 +94,7 @@ struct sss_hip_dist {
     std::vector<double> h_cown, h_call;
     double *partial = nullptr, *d_norm = nullptr, *h_norm = nullptr;
     std::vector<double> stage;
+    bool resid_c_ready = false;   // the last cycle's final C pass left r_C and its partials (level 0)
 };
 
 namespace {
@@ -138,7 +139,7 @@ int hook_exchange(void *ctx, double *vec)
     return exchange(h->d, h->l, vec);
 }
 
-int smooth(sss_hip_dist *d, int l, int post)
+int smooth(sss_hip_dist *d, int l, int post, ResidFuse *rf = nullptr, bool x_zero = false)
 {
     DLevel &L = d->L[l];
     HookCtx hc{d, l};
@@ -148,7 +149,56 @@ int smooth(sss_hip_dist *d, int l, int post)
     hk.w0 = L.w0;
     hk.w1 = L.w1;
     const int sweeps = post ? d->pars.post_iter : d->pars.pre_iter;
-    return smoother_run(L.sm, L.A, L.b, L.x, sweeps, d->stream, &hk);
+    return smoother_run(L.sm, L.A, L.b, L.x, sweeps, d->stream, &hk, rf, nullptr, x_zero);
+}
+
+// Sum of n doubles over the ranks, on the host (set-up time only).
+int allreduce_host(sss_hip_dist *d, double *v, int n)
+{
+    sss_hip_comm *c = d->comm;
+    if (c->host) return c->t.allreduce_sum(c->t.ctx, v, n) ? ERROR_MISC : 0;
+    double *dv = dev_alloc<double>((size_t)n);
+    if (!dv) return ERROR_MISC;
+    SSS_HIP(hipMemcpyAsync(dv, v, sizeof(double) * n, hipMemcpyHostToDevice, d->stream));
+    SSS_NCCL(ncclAllReduce(dv, dv, (size_t)n, ncclDouble, ncclSum, c->nccl, d->stream));
+    SSS_HIP(hipMemcpyAsync(v, dv, sizeof(double) * n, hipMemcpyDeviceToHost, d->stream));
+    SSS_HIP(hipStreamSynchronize(d->stream));
+    dev_free(dv);
+    return 0;
+}
+
+// The exact eliminations of the single-GPU cycle, made safe across ranks: the fused C-row residual
+// needs no C row coupled to a ghost C row (whose new value would arrive only with the next
+// exchange), the dead F-row prolongation no F row coupled to a ghost F row (a neighbour would read
+// the skipped correction), and the zero-first pass (which also skips its exchange) finite values --
+// each agreed over every rank so all ranks run the same exchanges.
+int agree_eliminations(sss_hip_dist *d, const PartPlan &plan)
+{
+    const int nagg = d->nagg;
+    std::vector<double> veto((size_t)3 * nagg, 0.0);
+    for (int l = 0; l < nagg; ++l) {
+        const PartLevel &P = plan.L[l];
+        SmootherPlan &sp = d->L[l].sm;
+        const int *rp = P.A.rp.data(), *ci = P.A.ci.data();
+        bool c_ghost_c = false, f_ghost_f = false;
+        for (int c = 0; c < 2; ++c)
+            for (int i = sp.pass[c].lo; i < sp.pass[c].hi && sp.pass[c].nrows > 0; ++i)
+                for (int k = rp[i]; k < rp[i + 1]; ++k)
+                    if (ci[k] >= P.m && P.gclass[ci[k] - P.m] == c) (c ? c_ghost_c : f_ghost_f) = true;
+        veto[3 * l + 0] = sp.finite ? 0.0 : 1.0;
+        veto[3 * l + 1] = (sp.fuse_resid && !c_ghost_c) ? 0.0 : 1.0;
+        veto[3 * l + 2] = (sp.f_overwritten && !f_ghost_f) ? 0.0 : 1.0;
+    }
+    int rc = allreduce_host(d, veto.data(), (int)veto.size());
+    if (rc) return rc;
+    for (int l = 0; l < nagg; ++l) {
+        SmootherPlan &sp = d->L[l].sm;
+        sp.finite = veto[3 * l + 0] == 0.0;
+        sp.fuse_resid = veto[3 * l + 1] == 0.0;
+        sp.f_overwritten = veto[3 * l + 2] == 0.0;
+        sp.pend_ok = false;
+    }
+    return 0;
 }
 
 int allgather_coarse(sss_hip_dist *d)
@@ -334,7 +384,7 @@ extern "C" sss_hip_dist *sss_hip_dist_create(const SSS_AMG *mg, const sss_hip_op
         if (l + 1 == d->nagg && !tinv.empty())
             for (int &j : P.P.ci) j = tinv[j];
         SSS_MAT Pv = P.P.view(), Rv = P.R.view();
-        if (devcsr_upload(L.P, Pv, -1, enc) || devcsr_upload(L.R, Rv, -1, enc)) return fail("upload P/R");
+        if (devcsr_upload(L.P, Pv, P.nF, enc) || devcsr_upload(L.R, Rv, -1, enc)) return fail("upload P/R");
         const size_t nv = (size_t)(L.m + L.g);
         L.b = dev_alloc<double>(nv);
         L.x = dev_alloc<double>(nv);
@@ -376,6 +426,7 @@ extern "C" sss_hip_dist *sss_hip_dist_create(const SSS_AMG *mg, const sss_hip_op
     if (!d->d_cown || !d->d_call || !d->partial || !d->d_norm ||
         hipHostMalloc((void **)&d->h_norm, sizeof(double)) != hipSuccess)
         return fail("buffers");
+    if (agree_eliminations(d, plan)) return fail("agreeing the exact eliminations");
     if (hipStreamSynchronize(d->stream) != hipSuccess) return fail("sync");
     return d;
 }
@@ -398,11 +449,19 @@ static double *dist_vec(sss_hip_dist *d, int which)
     return which == SSS_HIP_VEC_B ? L.b : which == SSS_HIP_VEC_X ? L.x : which == SSS_HIP_VEC_WP ? L.wp : nullptr;
 }
 
+extern "C" int sss_hip_dist_level_flags(sss_hip_dist *d, int l)
+{
+    if (!d || l < 0 || l >= d->nagg) return ERROR_INPUT_PAR;
+    const SmootherPlan &sp = d->L[l].sm;
+    return (sp.finite ? 1 : 0) | (sp.fuse_resid ? 2 : 0) | (sp.f_overwritten ? 4 : 0);
+}
+
 extern "C" int sss_hip_dist_upload_vec(sss_hip_dist *d, int which, const double *own, int n)
 {
     double *v = dist_vec(d, which);
     DLevel &L = d->L[0];
     if (!v || n != L.m) return ERROR_INPUT_PAR;
+    d->resid_c_ready = false;
     d->stage.resize(std::max(n, 1));
     for (int i = 0; i < n; ++i) d->stage[i] = own[L.perm[i] - L.lo];
     SSS_HIP(hipMemcpyAsync(v, d->stage.data(), sizeof(double) * n, hipMemcpyHostToDevice, d->stream));
@@ -427,11 +486,16 @@ extern "C" int sss_hip_dist_cycle(sss_hip_dist *d)
     const hipStream_t s = d->stream;
     const int nagg = d->nagg;
     int rc;
+    d->resid_c_ready = false;
     for (int l = 0; l < nagg; ++l) {   // descent
         DLevel &L = d->L[l];
-        if ((rc = smooth(d, l, 0))) return rc;
+        ResidFuse rf;   // the last C pass may form the residual's C rows (then only F rows remain)
+        rf.r = L.wp;
+        if ((rc = smooth(d, l, 0, &rf, l > 0))) return rc;   // levels >= 1 were just zeroed
         if ((rc = exchange(d, l, L.x))) return rc;
-        if ((rc = launch_spmv(L.A, SSS_HIP_SPMV_RESID, -1.0, L.x, L.b, L.wp, 0, nullptr, s))) return rc;
+        if (rf.done) rc = launch_spmv_blocks(L.A, L.A.split_blk, SSS_HIP_SPMV_RESID, -1.0, L.x, L.b, L.wp, nullptr, s);
+        else rc = launch_spmv(L.A, SSS_HIP_SPMV_RESID, -1.0, L.x, L.b, L.wp, 0, nullptr, s);
+        if (rc) return rc;
         if ((rc = exchange(d, l, L.wp))) return rc;
         if (l + 1 < nagg) {
             DLevel &C = d->L[l + 1];
@@ -459,8 +523,22 @@ extern "C" int sss_hip_dist_cycle(sss_hip_dist *d)
         } else {
             xc = hier_vec(d->tail, 0, SSS_HIP_VEC_X);
         }
-        if ((rc = launch_spmv(L.P, SSS_HIP_SPMV_AMXPY, 1.0, xc, nullptr, L.x, 0, nullptr, s))) return rc;
-        if ((rc = smooth(d, l, 1))) return rc;
+        // dead F-row correction (see walk_cycle in sss_hier.hip): prolong into the C rows only
+        if (L.sm.f_overwritten && d->pars.post_iter > 0 && L.P.split_row == L.sm.pass[0].hi && L.P.split_row > 0 &&
+            !L.P.wave_rows && !L.P.vec_rows)
+            rc = launch_spmv_range(L.P, L.P.split_blk, L.P.nblk, SSS_HIP_SPMV_AMXPY, 1.0, xc, nullptr, L.x, nullptr, s);
+        else
+            rc = launch_spmv(L.P, SSS_HIP_SPMV_AMXPY, 1.0, xc, nullptr, L.x, 0, nullptr, s);
+        if (rc) return rc;
+        if (l == 0 && L.sm.fuse_resid && d->pars.post_iter > 0) {   // outer residual's C rows
+            ResidFuse rf;
+            rf.r = L.wp;
+            rf.partial = d->partial;
+            if ((rc = smooth(d, l, 1, &rf))) return rc;
+            d->resid_c_ready = rf.done;
+        } else if ((rc = smooth(d, l, 1))) {
+            return rc;
+        }
     }
     return 0;
 }
@@ -470,7 +548,12 @@ extern "C" int sss_hip_dist_residual_norm(sss_hip_dist *d, double *absres)
     DLevel &L = d->L[0];
     int rc;
     if ((rc = exchange(d, 0, L.x))) return rc;
-    if ((rc = launch_spmv(L.A, SSS_HIP_SPMV_RESID, -1.0, L.x, L.b, L.wp, 0, d->partial, d->stream))) return rc;
+    if (d->resid_c_ready)   // C rows and their partials came with the cycle's last pass
+        rc = launch_spmv_blocks(L.A, L.A.split_blk, SSS_HIP_SPMV_RESID, -1.0, L.x, L.b, L.wp, d->partial, d->stream);
+    else
+        rc = launch_spmv(L.A, SSS_HIP_SPMV_RESID, -1.0, L.x, L.b, L.wp, 0, d->partial, d->stream);
+    d->resid_c_ready = false;
+    if (rc) return rc;
     if ((rc = launch_final_sum(d->partial, L.A.ngrid, d->d_norm, false, d->stream))) return rc;
     if ((rc = allreduce_norm(d))) return rc;
     *absres = std::sqrt(*d->h_norm);
@@ -483,6 +566,7 @@ extern "C" int sss_hip_dist_time_level0_spmv(sss_hip_dist *d, int reps, double *
     hipEvent_t e0, e1;
     SSS_HIP(hipEventCreate(&e0));
     SSS_HIP(hipEventCreate(&e1));
+    d->resid_c_ready = false;   // overwrites wp
     SSS_HIP(hipStreamSynchronize(d->stream));
     SSS_HIP(hipEventRecord(e0, d->stream));
     for (int r = 0; r < reps; ++r) {

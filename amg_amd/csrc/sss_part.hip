@@ -160,7 +160,11 @@ int part_plan_build(PartPlan &p, const SSS_AMG *mg, int nranks, int rank, int ag
         }
         const int *mark = mg->cg[l].cfmark.d;
         P.gcls.resize(P.g);
-        for (int k = 0; k < P.g; ++k) P.gcls[k] = P.ghosts[k] < P.lo ? (mark[P.ghosts[k]] == 1) : -1;
+        P.gclass.resize(P.g);
+        for (int k = 0; k < P.g; ++k) {
+            P.gclass[k] = mark[P.ghosts[k]] == 1;
+            P.gcls[k] = P.ghosts[k] < P.lo ? P.gclass[k] : -1;
+        }
     }
 
     // pass 3: local matrices

@@ -41,6 +41,7 @@ struct PartLevel {
     std::vector<int> ghosts;   // ghost k (local id m + k) -> global id, ascending
     std::vector<int> mark;     // cfmark in local order
     std::vector<int> gcls;     // per ghost: class (0 F, 1 C) if owned by a lower rank, else -1
+    std::vector<int> gclass;   // per ghost: class (0 F, 1 C), whoever owns it
     HostMat A;                 // m x (m + g)
     HostMat P;                 // m x (next level local ids), or global coarse ids when l + 1 == nagg
     HostMat R;                 // own coarse rows (next level local order, or global order at nagg) x (m + g)

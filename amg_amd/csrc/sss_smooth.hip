@@ -769,9 +769,13 @@ int smoother_run(const SmootherPlan &sp, const DevCSR &A, const double *b, doubl
             const PassSchedule &ps = sp.pass[c];
             if (ps.nrows == 0) continue;
             if (pre_f && sw == 0 && c == 0) continue;   // computed with the last residual (pre_f)
+            // first pass on a just-zeroed iterate (C/F-Jacobi / two-stage): t = b, no matrix read
+            const bool zfirst = x_zero && sw == 0 && c == 0 && sp.finite && sp.kind == SSS_HIP_SMOOTH_JACOBI;
             if (hk) {   // distributed level: refresh x's ghosts; only contiguous passes qualify
                 if (!ps.range) return ERROR_INPUT_PAR;
-                if ((rc = hk->exchange(hk->ctx, x))) return rc;
+                // a zeroed x has zero ghosts (the descent clears own rows and ghosts); `finite` is
+                // agreed over the ranks, so every rank skips this exchange together
+                if (!zfirst && (rc = hk->exchange(hk->ctx, x))) return rc;
             }
             if (ps.range) {
                 const int nb = ps.bhi - ps.blo, m = ps.hi - ps.lo, nw = (m + 3) / 4;
@@ -798,7 +802,11 @@ int smoother_run(const SmootherPlan &sp, const DevCSR &A, const double *b, doubl
                     // this class) are refreshed after every stage
                     const DevCSR &Mn = ps.ts_nl, &Ml = ps.ts_lo;
                     double *wcur = hk->w0, *wnxt = hk->w1;
-                    launch_ts_stage0(Mn, ps.lo, ps.ts_split, b, xsrc_of(x), deff, ps.ts_P, wcur + ps.lo, s);
+                    if (zfirst)
+                        hipLaunchKernelGGL(zero_first_pass<true>, dim3((m + kBlock - 1) / kBlock), dim3(kBlock), 0, s,
+                                           ps.lo, m, Mn.rp, Mn.ci, Mn.v, ps.ts_split, b, deff, ps.ts_P, wcur + ps.lo);
+                    else
+                        launch_ts_stage0(Mn, ps.lo, ps.ts_split, b, xsrc_of(x), deff, ps.ts_P, wcur + ps.lo, s);
                     for (int st = 0; st < sp.inner; ++st) {
                         if ((rc = hk->exchange(hk->ctx, wcur))) return rc;
                         launch_ts_inner(Ml, ps.lo, deff, ps.ts_P, wcur, 0, wcur + ps.lo, wnxt + ps.lo, s);
@@ -810,7 +818,6 @@ int smoother_run(const SmootherPlan &sp, const DevCSR &A, const double *b, doubl
                     // stage 0 (or the Jacobi pass) writes the other buffer; inner steps read only this
                     // class's previous iterate, so they alternate between the two buffers in place
                     double *prev = cur[c] == x ? sp.x2 : x, *next = cur[c];
-                    const bool zfirst = x_zero && sw == 0 && c == 0 && sp.finite;
                     const int zg = (m + kBlock - 1) / kBlock;
                     if (zfirst && sp.inner > 0)
                         hipLaunchKernelGGL(zero_first_pass<true>, dim3(zg), dim3(kBlock), 0, s, ps.lo, m, ps.ts_nl.rp,
@@ -836,10 +843,15 @@ int smoother_run(const SmootherPlan &sp, const DevCSR &A, const double *b, doubl
                         std::swap(ycur, ynxt);
                     }
                     SSS_HIP(hipMemcpyAsync(x + ps.lo, ycur, sizeof(double) * (size_t)m, hipMemcpyDeviceToDevice, s));
+                } else if (sp.kind == SSS_HIP_SMOOTH_JACOBI && zfirst) {
+                    // the pass reads no x at all, so it may write x in place
+                    hipLaunchKernelGGL(zero_first_pass<false>, dim3((m + kBlock - 1) / kBlock), dim3(kBlock), 0, s,
+                                       ps.lo, m, A.rp, A.ci, A.v, (const int *)nullptr, b, deff, (double *)nullptr,
+                                       x + ps.lo);
                 } else if (sp.kind == SSS_HIP_SMOOTH_JACOBI) {
                     relax(std::integral_constant<int, 1>(), A.ci, (const double *)nullptr, ps.y);
                     SSS_HIP(hipMemcpyAsync(x + ps.lo, ps.y, sizeof(double) * (size_t)m, hipMemcpyDeviceToDevice, s));
-                } else if (rf && sp.fuse_resid && c == 1 && sw + 1 == sweeps && !hk) {
+                } else if (rf && sp.fuse_resid && c == 1 && sw + 1 == sweeps) {
                     hipLaunchKernelGGL(relax_range<2>, dim3(nb), dim3(kBlock), 0, s, ps.blo, A.blk, A.rp, A.ci, A.v,
                                        sp.diag_pos, ps.lo, b, x, (const double *)nullptr, (double *)nullptr,
                                        tile_d ? nullptr : deff, A.pk, A.pv, A.pb, rf->r, rf->partial, xs);

@@ -171,6 +171,9 @@ sss_hip_dist *sss_hip_dist_create(const SSS_AMG *mg, const sss_hip_opts *o, sss_
 void sss_hip_dist_destroy(sss_hip_dist *d);
 /* own rows [lo, hi) of level 0 in the original numbering; nagg = number of partitioned levels */
 int sss_hip_dist_info(sss_hip_dist *d, int *lo, int *hi, int *nagg, int *nghost0);
+/* exact eliminations in force on partitioned level l (agreed over the ranks), a bit mask:
+ * 1 zero-first pass, 2 fused C-row residual, 4 dead F-row prolongation.  <0: bad level. */
+int sss_hip_dist_level_flags(sss_hip_dist *d, int l);
 /* level-0 vectors, the rank's own rows in the original order (n = hi - lo) */
 int sss_hip_dist_upload_vec(sss_hip_dist *d, int which, const double *own, int n);
 int sss_hip_dist_download_vec(sss_hip_dist *d, int which, double *own, int n);

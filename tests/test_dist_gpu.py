@@ -45,6 +45,12 @@ def _worker(rank, world, port, kind, n, smoother, inner_from, agg_rows, cycles, 
         D = A.DistHierarchy(H, comm, smoother=smoother, coarse="direct", device=0, agg_rows=agg_rows,
                             inner_from=inner_from, sum_order=sum_order)
         assert D.nagg >= 2, D.nagg
+        if kind == 7 and smoother == "hybrid" and not sum_order:
+            # red-black level 0: the fused C-row residual and the dead F-row prolongation hold
+            # across the rank cut; every level's first pre-smoothing pass starts from zero
+            f0 = D.level_flags(0)
+            assert f0["fused_residual"] and f0["dead_prolong"], f0
+        assert all(D.level_flags(l)["zero_first"] for l in range(D.nagg))
         own = D.hi - D.lo
         D.upload("b", np.ones(own))
         D.upload("x", np.ones(own))
