@@ -74,6 +74,7 @@ struct DevCSR {
     double *v = nullptr;
     int nblk = 0;          // SpMV row blocks
     int *blk = nullptr;    // block -> first row (nblk + 1 entries)
+    int2 *bk = nullptr;    // block -> {first row, first entry} (nblk + 1): one load, no rp[blk[.]] chain
     int split_row = -1;    // class split row the blocks were cut at (-1: none)
     int split_blk = 0;     // index of the block starting at split_row
     bool wave_rows = false;  // long rows: wave-per-row kernels (avg nnz/row >= kWaveRowMin)
@@ -125,6 +126,7 @@ int devcsr_upload(DevCSR &d, const SSS_MAT &h, int split = -1, int enc = 0, cons
 int level_encoding(const sss_hip_opts &o);
 void devcsr_free(DevCSR &d);
 int build_row_blocks(const int *h_rp, int n, std::vector<int> &blk, int split = -1);
+int upload_block_bounds(int2 **dst, const std::vector<int> &blk, const int *h_rp);
 int wave_row_min();
 int free_row_min();
 

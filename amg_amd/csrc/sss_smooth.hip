@@ -390,7 +390,7 @@ __global__ __launch_bounds__(kBlock) void relax_wave(int m, const int *__restric
 // t = b_r - sum over off-diagonal entries in stored order (diag_pos skips the diagonal); rows with
 // |d| <= 1e-20 keep their value.
 template <int MODE>
-__global__ __launch_bounds__(kBlock) void relax_range(int blo, const int *__restrict__ blk, const int *__restrict__ rp,
+__global__ __launch_bounds__(kBlock) void relax_range(int blo, const int2 *__restrict__ blk, const int *__restrict__ rp,
                                                       const int *__restrict__ ci, const double *__restrict__ v,
                                                       const int *__restrict__ diag_pos, int lo,
                                                       const double *__restrict__ b, double *x,
@@ -401,8 +401,8 @@ __global__ __launch_bounds__(kBlock) void relax_range(int blo, const int *__rest
 {
     __shared__ SpmvSmem sm;
     const int bid = blo + xcd_bid();
-    const int r0 = blk[bid], r1 = blk[bid + 1];
-    const int k0 = rp[r0], k1 = rp[r1];
+    const int2 ba = blk[bid], be = blk[bid + 1];
+    const int r0 = ba.x, r1 = be.x, k0 = ba.y, k1 = be.y;
     auto fetch = [&](int c) -> double { return xs(c); };
     // deff null: the plan's divisor is each row's own diagonal, staged from the sorted tile
     auto dval = [&](int r) -> double { return deff ? deff[r] : sm.d[r - r0]; };
@@ -558,8 +558,9 @@ __global__ __launch_bounds__(kBlock) void ts_stage0(int lo, DevCSR M, const int 
         return;
     } else {
         __shared__ SpmvSmem sm;
-        const int bq = xcd_bid(), q0 = M.blk[bq], q1 = M.blk[bq + 1];
-        const int k0 = M.rp[q0], k1 = M.rp[q1];
+        const int bq = xcd_bid();
+        const BlockBounds bb = block_bounds(M.bk, M.rp, bq);
+        const int q0 = bb.r0, q1 = bb.r1, k0 = bb.k0, k1 = bb.k1;
         if (k1 - k0 <= kTileEntries) {
             const int q = q0 + (int)threadIdx.x;
             int a = 0, sp = 0, e = 0;
@@ -639,8 +640,9 @@ __global__ __launch_bounds__(kBlock) void ts_inner(int lo, DevCSR M, const doubl
         return;
     } else {
         __shared__ SpmvSmem sm;
-        const int bq = xcd_bid(), q0 = M.blk[bq], q1 = M.blk[bq + 1];
-        const int k0 = M.rp[q0], k1 = M.rp[q1];
+        const int bq = xcd_bid();
+        const BlockBounds bb = block_bounds(M.bk, M.rp, bq);
+        const int q0 = bb.r0, q1 = bb.r1, k0 = bb.k0, k1 = bb.k1;
         if (k1 - k0 <= kTileEntries) {
             const int q = q0 + (int)threadIdx.x;
             int a = 0, e = 0;
@@ -738,7 +740,7 @@ int launch_f_residual_pending(const SmootherPlan &sp, const DevCSR &A, const dou
     if (!sp.pend_ok) return ERROR_INPUT_PAR;
     const PassSchedule &F = sp.pass[0];
     const double *deff = (sp.own_diag && A.pk) ? nullptr : sp.d_first;
-    hipLaunchKernelGGL(relax_range<3>, dim3(F.bhi - F.blo), dim3(kBlock), 0, s, F.blo, A.blk, A.rp, A.ci, A.v,
+    hipLaunchKernelGGL(relax_range<3>, dim3(F.bhi - F.blo), dim3(kBlock), 0, s, F.blo, A.bk, A.rp, A.ci, A.v,
                        sp.diag_pos, F.lo, b, const_cast<double *>(x), (const double *)nullptr, pend, deff, A.pk, A.pv,
                        A.pb, r, partial, xsrc_of(x));
     SSS_HIP(hipGetLastError());
@@ -793,7 +795,7 @@ int smoother_run(const SmootherPlan &sp, const DevCSR &A, const double *b, doubl
                         hipLaunchKernelGGL((relax_range_wave<M, false>), dim3(nw), dim3(kBlock), 0, s, ps.lo, ps.hi,
                                            A.rp, cols, A.v, b, x, yp, y, deff, xs);
                     else
-                        hipLaunchKernelGGL(relax_range<M>, dim3(nb), dim3(kBlock), 0, s, ps.blo, A.blk, A.rp, cols,
+                        hipLaunchKernelGGL(relax_range<M>, dim3(nb), dim3(kBlock), 0, s, ps.blo, A.bk, A.rp, cols,
                                            A.v, sp.diag_pos, ps.lo, b, x, yp, y, tile_d ? nullptr : deff, A.pk,
                                            A.pv, A.pb, (double *)nullptr, (double *)nullptr, xs);
                 };
@@ -852,7 +854,7 @@ int smoother_run(const SmootherPlan &sp, const DevCSR &A, const double *b, doubl
                     relax(std::integral_constant<int, 1>(), A.ci, (const double *)nullptr, ps.y);
                     SSS_HIP(hipMemcpyAsync(x + ps.lo, ps.y, sizeof(double) * (size_t)m, hipMemcpyDeviceToDevice, s));
                 } else if (rf && sp.fuse_resid && c == 1 && sw + 1 == sweeps) {
-                    hipLaunchKernelGGL(relax_range<2>, dim3(nb), dim3(kBlock), 0, s, ps.blo, A.blk, A.rp, A.ci, A.v,
+                    hipLaunchKernelGGL(relax_range<2>, dim3(nb), dim3(kBlock), 0, s, ps.blo, A.bk, A.rp, A.ci, A.v,
                                        sp.diag_pos, ps.lo, b, x, (const double *)nullptr, (double *)nullptr,
                                        tile_d ? nullptr : deff, A.pk, A.pv, A.pb, rf->r, rf->partial, xs);
                     rf->done = true;

@@ -58,6 +58,17 @@ static int merge_group_size(int n)
     return n >= 80000 ? 8 : 4;
 }
 
+// {first row, first entry} of every block, so a block's bounds are one independent load.
+int upload_block_bounds(int2 **dst, const std::vector<int> &blk, const int *h_rp)
+{
+    std::vector<int2> bk(blk.size());
+    for (size_t q = 0; q < blk.size(); ++q) bk[q] = make_int2(blk[q], h_rp[blk[q]]);
+    *dst = dev_alloc<int2>(bk.size());
+    if (!*dst) return hip_fail(hipErrorOutOfMemory, "hipMalloc(bk)", __FILE__, __LINE__);
+    SSS_HIP(hipMemcpy(*dst, bk.data(), sizeof(int2) * bk.size(), hipMemcpyHostToDevice));
+    return 0;
+}
+
 int build_row_blocks(const int *h_rp, int n, std::vector<int> &blk, int split)
 {
     blk.clear();
@@ -225,6 +236,7 @@ int devcsr_upload(DevCSR &d, const SSS_MAT &h, int split, int enc, const int *se
     d.blk = dev_alloc<int>(blk.size());
     if (!d.blk) return hip_fail(hipErrorOutOfMemory, "hipMalloc(blk)", __FILE__, __LINE__);
     SSS_HIP(hipMemcpy(d.blk, blk.data(), sizeof(int) * blk.size(), hipMemcpyHostToDevice));
+    if (int rc = upload_block_bounds(&d.bk, blk, h.row_ptr)) return rc;
     d.ngrid = (d.wave_rows || d.vec_rows) ? (d.n + 3) / 4 : d.nblk;
     if (d.mg_G > 0) {
         std::vector<int> gp;
@@ -269,6 +281,7 @@ void devcsr_free(DevCSR &d)
     dev_free(d.ci);
     dev_free(d.v);
     dev_free(d.blk);
+    dev_free(d.bk);
     dev_free(d.pk);
     dev_free(d.pv);
     dev_free(d.pb);
@@ -280,7 +293,7 @@ void devcsr_free(DevCSR &d)
 
 // ---- kernel -------------------------------------------------------------------------------
 template <int OP, bool NORM>
-__global__ __launch_bounds__(kBlock) void spmv_adaptive(const int *__restrict__ blk, const int *__restrict__ rp,
+__global__ __launch_bounds__(kBlock) void spmv_adaptive(const int2 *__restrict__ blk, const int *__restrict__ rp,
                                                         const int *__restrict__ ci, const double *__restrict__ v,
                                                         const double *__restrict__ x, const double *__restrict__ b,
                                                         double *__restrict__ y, double alpha, int cap,
@@ -394,7 +407,7 @@ static void launch_op(const DevCSR &A, double alpha, const double *x, const doub
         hipLaunchKernelGGL((spmv_wave<OP, NORM, false>), dim3(A.ngrid), dim3(kBlock), 0, s, A.n, A.rp, A.ci, A.v, x,
                            b, y, alpha, cap, partial);
     else
-        hipLaunchKernelGGL((spmv_adaptive<OP, NORM>), dim3(A.nblk), dim3(kBlock), 0, s, A.blk, A.rp, A.ci, A.v, x,
+        hipLaunchKernelGGL((spmv_adaptive<OP, NORM>), dim3(A.nblk), dim3(kBlock), 0, s, A.bk, A.rp, A.ci, A.v, x,
                            b, y, alpha, cap, partial, A.pk, A.pv, A.pb);
 }
 
@@ -427,13 +440,13 @@ int launch_spmv_range(const DevCSR &A, int blo, int bhi, int op, double alpha, c
     const int2 *pb = A.pb ? A.pb + blo : nullptr;
     double *pp = partial ? partial + blo : nullptr;
     if (op == SSS_HIP_SPMV_AMXPY)
-        hipLaunchKernelGGL((spmv_adaptive<SSS_HIP_SPMV_AMXPY, false>), dim3(nb), dim3(kBlock), 0, s, A.blk + blo, A.rp,
+        hipLaunchKernelGGL((spmv_adaptive<SSS_HIP_SPMV_AMXPY, false>), dim3(nb), dim3(kBlock), 0, s, A.bk + blo, A.rp,
                            A.ci, A.v, x, b, y, alpha, 0, pp, A.pk, A.pv, pb);
     else if (partial)
-        hipLaunchKernelGGL((spmv_adaptive<SSS_HIP_SPMV_RESID, true>), dim3(nb), dim3(kBlock), 0, s, A.blk + blo, A.rp,
+        hipLaunchKernelGGL((spmv_adaptive<SSS_HIP_SPMV_RESID, true>), dim3(nb), dim3(kBlock), 0, s, A.bk + blo, A.rp,
                            A.ci, A.v, x, b, y, alpha, 0, pp, A.pk, A.pv, pb);
     else
-        hipLaunchKernelGGL((spmv_adaptive<SSS_HIP_SPMV_RESID, false>), dim3(nb), dim3(kBlock), 0, s, A.blk + blo, A.rp,
+        hipLaunchKernelGGL((spmv_adaptive<SSS_HIP_SPMV_RESID, false>), dim3(nb), dim3(kBlock), 0, s, A.bk + blo, A.rp,
                            A.ci, A.v, x, b, y, alpha, 0, pp, A.pk, A.pv, pb);
     SSS_HIP(hipGetLastError());
     return 0;
@@ -509,8 +522,10 @@ extern "C" sss_hip_spmv_plan *sss_hip_spmv_plan_create(int n, int nnz, const int
     p->csr.wave_rows = n > 0 && (long long)nnz >= (long long)sss::wave_row_min() * n;
     p->csr.ngrid = p->csr.wave_rows ? (n + 3) / 4 : p->csr.nblk;
     p->csr.blk = sss::dev_alloc<int>(blk.size());
-    if (!p->csr.blk || hipMemcpy(p->csr.blk, blk.data(), sizeof(int) * blk.size(), hipMemcpyHostToDevice) != hipSuccess) {
+    if (!p->csr.blk || hipMemcpy(p->csr.blk, blk.data(), sizeof(int) * blk.size(), hipMemcpyHostToDevice) != hipSuccess ||
+        sss::upload_block_bounds(&p->csr.bk, blk, h_rp)) {
         sss::dev_free(p->csr.blk);
+        sss::dev_free(p->csr.bk);
         delete p;
         return nullptr;
     }
@@ -521,6 +536,7 @@ extern "C" void sss_hip_spmv_plan_destroy(sss_hip_spmv_plan *p)
 {
     if (!p) return;
     sss::dev_free(p->csr.blk);
+    sss::dev_free(p->csr.bk);
     delete p;
 }
 

@@ -195,8 +195,24 @@ __device__ __forceinline__ void stage_any(double *__restrict__ sm, int k0, int k
 // independent x gathers, all in flight).  Phase 2: one thread per row adds its products from
 // LDS in stored order starting from 0.0 (SSS_utils.c:174).  Rows longer than the tile are
 // processed alone, tile by tile, with thread 0 carrying the chain.
-template <class Epi>
-__device__ __forceinline__ double csr_block_rows(const int *__restrict__ blk, const int *__restrict__ rp,
+// A block's row and entry bounds: from {row, entry} pairs (one load each side) or from the
+// first-row array through row_ptr.
+struct BlockBounds {
+    int r0, r1, k0, k1;
+};
+__device__ __forceinline__ BlockBounds block_bounds(const int2 *__restrict__ bk, const int *__restrict__, int bid)
+{
+    const int2 a = bk[bid], e = bk[bid + 1];
+    return {a.x, e.x, a.y, e.y};
+}
+__device__ __forceinline__ BlockBounds block_bounds(const int *__restrict__ blk, const int *__restrict__ rp, int bid)
+{
+    const int r0 = blk[bid], r1 = blk[bid + 1];
+    return {r0, r1, rp[r0], rp[r1]};
+}
+
+template <class Epi, class BlkT>
+__device__ __forceinline__ double csr_block_rows(const BlkT *__restrict__ blk, const int *__restrict__ rp,
                                                  const int *__restrict__ ci, const double *__restrict__ v,
                                                  const double *__restrict__ x, SpmvSmem &sm, Epi epi,
                                                  const unsigned *__restrict__ pk = nullptr,
@@ -205,8 +221,8 @@ __device__ __forceinline__ double csr_block_rows(const int *__restrict__ blk, co
 {
     auto fetch = [&](int c) -> double { return x[c]; };
     const int bid = xcd_bid();
-    const int r0 = blk[bid], r1 = blk[bid + 1];
-    const int k0 = rp[r0], k1 = rp[r1];
+    const BlockBounds bb = block_bounds(blk, rp, bid);
+    const int r0 = bb.r0, r1 = bb.r1, k0 = bb.k0, k1 = bb.k1;
     const int cnt = k1 - k0;
     double contrib = 0.0;
     if (cnt <= kTileEntries) {
