@@ -138,6 +138,7 @@ def _declare(lib):
         "SSS_amg_setup": (None, [P(SSS_AMG), P(SSS_MAT), P(SSS_AMG_PARS)]),
         "SSS_amg_data_destroy": (None, [P(SSS_AMG)]),
         "SSS_amg_solve": (SSS_RTN, [P(SSS_AMG), P(SSS_VEC), P(SSS_VEC)]),
+        "SSS_print_itinfo": (None, [C.c_int, C.c_int, C.c_double, C.c_double, C.c_double]),
         "SSS_amg_cycle": (None, [P(SSS_AMG)]),
         "SSS_solver_amg": (SSS_RTN, [P(SSS_MAT), P(SSS_VEC), P(SSS_VEC), P(SSS_AMG_PARS)]),
         "SSS_mat_read": (None, [C.c_char_p, P(SSS_MAT)]),

@@ -41,21 +41,29 @@ COPY_PEAK_GBS = 6290.0      # measured float4 copy peak (same source)
 
 def parse():
     p = argparse.ArgumentParser()
-    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--gpus", type=int, default=None,
+                   help="ranks (one per GPU); without WORLD_SIZE in the environment and N > 1 the bench "
+                        "launches N ranks itself (torch.distributed.run) before touching the GPU")
     p.add_argument("--steps", type=int, default=10)
     p.add_argument("--warmup", type=int, default=3)
-    p.add_argument("--grid", "--n", dest="n", type=int, default=400, help="grid edge (400 -> 64M rows)")
+    p.add_argument("--grid", "--n", dest="n", type=int, default=None,
+                   help="grid edge (default: the BASELINE.json config of the rank count -- N=1, 2: 400 "
+                        "(64M rows); N=4: 27-pt 256; N=8: 512)")
+    p.add_argument("--probe-ranks", action="store_true",
+                   help="print one line per rank (rank, world size) and exit before any GPU call (tests)")
     p.add_argument("--hier-cache", default=None,
                    help="binary hierarchy file (SSS_amg_save): loaded when present, else written after setup "
                         "(rank 0; the other ranks load it)")
-    p.add_argument("--stencil", type=int, default=7, choices=[7, 27],
+    p.add_argument("--stencil", type=int, default=None, choices=[7, 27],
                    help="7: 7-pt Poisson (the metric's workload); 27: the 27-pt anisotropic operator of "
-                        "BASELINE.json configs[4] (SURVEY.md 8(d))")
+                        "BASELINE.json configs[4] (SURVEY.md 8(d)); default 27 at N=4, else 7")
     p.add_argument("--mode", default="throughput", choices=["throughput", "parity"])
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-threads", type=int, default=0,
-                   help="threads of the multi-core CPU baseline in the GPU's mode (default: OMP_NUM_THREADS or 16, "
-                        "at most the host CPUs; 0 disables it with --no-cpu-baseline)")
+                   help="threads of the multi-core CPU baseline in the GPU's mode (default: every CPU this "
+                        "process may run on -- affinity mask, capped by the cgroup CPU quota)")
+    p.add_argument("--cpu-iters", type=int, default=5, help="timed CPU-baseline iterations (median reported)")
+    p.add_argument("--cpu-warmup", type=int, default=1, help="untimed CPU-baseline iterations first")
     p.add_argument("--cpu-n", type=int, default=0, help="grid edge of the CPU sample (default: same workload)")
     p.add_argument("--mode-smoother", default=None, help="override: exact|hybrid|jacobi")
     p.add_argument("--mode-coarse", default=None, help="override: krylov|direct")
@@ -149,22 +157,65 @@ def cpu_iterations(H, out: dict, threads: int = 1, iters: int = 1, warmup: int =
 
     for _ in range(warmup):
         one()
-    ora.ora_reset_timers()
-    t0 = time.perf_counter()
+    per, coarse = [], []
     for _ in range(iters):
+        ora.ora_reset_timers()
+        t0 = time.perf_counter()
         one()
-    dt = (time.perf_counter() - t0) / iters
-    # the fine-level SpMV of the CPU path, for the GB/s column (one r = b - A0 x)
-    t1 = time.perf_counter()
-    ora.ora_mv_amxpy(-1.0, C.byref(H.level(0).A), dptr(x), dptr(r), 0)
-    spmv_s = time.perf_counter() - t1
-    out.update(seconds=dt, coarse_seconds=ora.ora_coarse_seconds() / iters, threads=ora.ora_get_threads(),
-               spmv_seconds=spmv_s)
+        per.append(time.perf_counter() - t0)
+        coarse.append(ora.ora_coarse_seconds())
+    # the fine-level SpMV of the CPU path, for the GB/s column (one r = b - A0 x), median of 3
+    sp = []
+    for _ in range(3):
+        t1 = time.perf_counter()
+        ora.ora_mv_amxpy(-1.0, C.byref(H.level(0).A), dptr(x), dptr(r), 0)
+        sp.append(time.perf_counter() - t1)
+    out.update(seconds=float(np.median(per)), seconds_all=per, coarse_seconds=float(np.median(coarse)),
+               threads=ora.ora_get_threads(), spmv_seconds=float(np.median(sp)), iters=iters, warmup=warmup)
 
 
-def cpu_baseline_worker(H, out: dict):
-    """One outer iteration of the CPU restatement (reference semantics, 1 thread)."""
-    cpu_iterations(H, out, threads=1, iters=1)
+def host_cpus() -> dict:
+    """What the CPU baseline ran on: logical CPUs of the machine, the ones this process may use
+    (affinity mask, capped by the cgroup v2 CPU quota), the CPU model and the NUMA node count."""
+    info = {"nproc_machine": os.cpu_count()}
+    try:
+        usable = len(os.sched_getaffinity(0))
+    except AttributeError:
+        usable = os.cpu_count() or 1
+    try:
+        q, per = Path("/sys/fs/cgroup/cpu.max").read_text().split()[:2]
+        if q != "max":
+            info["cgroup_cpu_quota"] = int(q) / int(per)
+            usable = max(1, min(usable, int(int(q) // int(per))))
+    except (OSError, ValueError):
+        pass
+    info["usable_cpus"] = usable
+    try:
+        for line in Path("/proc/cpuinfo").read_text().splitlines():
+            if line.startswith("model name"):
+                info["model"] = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    try:
+        info["numa_nodes"] = len([d for d in os.listdir("/sys/devices/system/node") if d.startswith("node")])
+    except OSError:
+        pass
+    return info
+
+
+def spawn_ranks(n: int) -> int:
+    """Launch this script as n ranks under torch.distributed.run (child process; this process
+    never initialises the GPU) and return its exit code."""
+    import socket
+    import subprocess
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr=127.0.0.1", f"--master-port={port}", str(Path(__file__).resolve())] + sys.argv[1:]
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY=os.environ.get("HSA_ENABLE_IPC_MODE_LEGACY", "0"))
+    return subprocess.call(cmd, env=env)
 
 
 class Single:
@@ -246,7 +297,22 @@ def heartbeat(stop: threading.Event, t0: float):
 
 def main():
     args = parse()
+    ws = os.environ.get("WORLD_SIZE")
+    if ws is None and args.gpus is not None and args.gpus > 1:
+        sys.exit(spawn_ranks(args.gpus))   # before anything touches the GPU
     D = Dist()
+    if args.gpus is not None and args.gpus != D.world:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={D.world}")
+    if args.probe_ranks:
+        print(json.dumps({"rank": D.rank, "world": D.world, "local_rank": D.local_rank}), flush=True)
+        D.close()
+        return
+    # the BASELINE.json config of this rank count (configs[2]: 512^3 on 8 GPUs; configs[4]: 27-pt
+    # 256^3 on 4 GPUs; the metric's 64M-row 400^3 otherwise)
+    if args.stencil is None:
+        args.stencil = 27 if D.world == 4 and args.n is None else 7
+    if args.n is None:
+        args.n = 256 if args.stencil == 27 else {8: 512}.get(D.world, 400)
     hb_stop = threading.Event()
     threading.Thread(target=heartbeat, args=(hb_stop, time.perf_counter()), daemon=True).start()
     import amg_amd as A
@@ -317,16 +383,6 @@ def main():
     eng.set_ones()
     DH = eng
 
-    cpu = {}
-    cpu_thread = None
-    if D.rank == 0 and D.world == 1 and not args.no_cpu_baseline:
-        Hc = H
-        if args.cpu_n and args.cpu_n != n:
-            Mc = A.generate(args.stencil, args.cpu_n)
-            Hc = quiet_call(A.Hierarchy, Mc)
-        cpu_thread = threading.Thread(target=cpu_baseline_worker, args=(Hc, cpu), daemon=True)
-        cpu_thread.start()
-
     for _ in range(args.warmup):
         DH.cycle()
         DH.residual_norm()
@@ -393,46 +449,59 @@ def main():
         except Exception:
             traffic = None
 
+    # CPU baselines, rank 0 at N = 1 only, after every GPU measurement: the
+    # median of --cpu-iters outer iterations after --cpu-warmup, on the same hierarchy
     cpu_baseline = None
     cpu_mt = None
-    if cpu_thread is not None:
-        cpu_thread.join()
+    if D.rank == 0 and D.world == 1 and not args.no_cpu_baseline:
+        hb_stop.set()
+        hb_stop = threading.Event()
+        threading.Thread(target=heartbeat, args=(hb_stop, time.perf_counter()), daemon=True).start()
+        Hc = H
+        if args.cpu_n and args.cpu_n != n:
+            Mc = A.generate(args.stencil, args.cpu_n)
+            Hc = quiet_call(A.Hierarchy, Mc)
         cpu_n = args.cpu_n or n
+        hostinfo = host_cpus()
         a0_bytes = 12 * nnz + 4 * (N + 1) + 24 * N
-        if cpu.get("seconds"):
-            cpu_baseline = {
-                "value": 1.0 / cpu["seconds"], "unit": "V-cycle iter/s", "cores": 1, "kind": "port",
-                "sample": f"one outer iteration (V-cycle incl. reference CG(beta=1)+GMRES coarse solve, "
-                          f"residual, norm) of oracle/sss_oracle.c on the same {args.stencil}-pt {cpu_n}^3 hierarchy, "
-                          f"1 host thread; coarse solve {cpu['coarse_seconds']:.1f} s of {cpu['seconds']:.1f} s",
-                "seconds": cpu["seconds"], "coarse_seconds": cpu["coarse_seconds"],
-                "fine_spmv_GBps": a0_bytes / cpu["spmv_seconds"] / 1e9 if cpu_n == n else None,
-            }
-        # the same restatement in the GPU's own mode, its row loops on the host cores, after the GPU
-        # measurements (it would otherwise compete with the launch thread)
-        thr = args.cpu_threads or int(os.environ.get("OMP_NUM_THREADS", "16"))
-        thr = max(1, min(thr, os.cpu_count() or 1))
+        print("[bench] CPU baseline: reference semantics, 1 thread", file=sys.stderr, flush=True)
+        cpu = {}
+        cpu_iterations(Hc, cpu, threads=1, iters=args.cpu_iters, warmup=args.cpu_warmup)
+        cpu_baseline = {
+            "value": 1.0 / cpu["seconds"], "unit": "V-cycle iter/s", "cores": 1, "kind": "port",
+            "sample": f"median of {args.cpu_iters} outer iterations after {args.cpu_warmup} warm-up (V-cycle incl. the "
+                      f"reference CG(beta=1)+GMRES coarse solve, residual, norm) of oracle/sss_oracle.c with the "
+                      f"reference semantics on the same {args.stencil}-pt {cpu_n}^3 hierarchy, 1 host thread, run "
+                      f"after the GPU measurements; coarse solve {cpu['coarse_seconds']:.1f} s of {cpu['seconds']:.1f} s",
+            "seconds": cpu["seconds"], "seconds_all": cpu["seconds_all"], "coarse_seconds": cpu["coarse_seconds"],
+            "fine_spmv_GBps": a0_bytes / cpu["spmv_seconds"] / 1e9 if cpu_n == n else None,
+            "host": hostinfo,
+        }
+        # the same restatement in the GPU's own mode, its row loops on every usable host CPU
+        thr = args.cpu_threads or hostinfo["usable_cpus"]
+        print(f"[bench] CPU baseline: GPU's mode, {thr} threads", file=sys.stderr, flush=True)
         mt = {}
         mode = {}
         if args.mode == "throughput":
             mode = dict(smoother=1, jacobi_from=1, coarse_mode=1 if coarse == "direct" else 0,
                         inner=inner if smoother != "exact" else 0, inner_mask=~((1 << inner_from) - 1))
-        cpu_iterations(Hc, mt, threads=thr, iters=2, warmup=1, **mode)
+        cpu_iterations(Hc, mt, threads=thr, iters=args.cpu_iters, warmup=args.cpu_warmup, **mode)
         cpu_mt = {
             "value": 1.0 / mt["seconds"], "unit": "V-cycle iter/s", "cores": mt["threads"], "kind": "port",
-            "sample": f"2 outer iterations after 1 warm-up, oracle/sss_oracle.c in the GPU's mode "
-                      f"({smoother} smoother, {coarse} coarse solve) on the same {args.stencil}-pt {cpu_n}^3 hierarchy, "
-                      f"row loops on {mt['threads']} host threads; coarse solve {mt['coarse_seconds']:.2f} s "
-                      f"of {mt['seconds']:.2f} s",
-            "seconds": mt["seconds"], "coarse_seconds": mt["coarse_seconds"],
+            "sample": f"median of {args.cpu_iters} outer iterations after {args.cpu_warmup} warm-up, "
+                      f"oracle/sss_oracle.c in the GPU's mode ({smoother} smoother, {coarse} coarse solve) on the same "
+                      f"{args.stencil}-pt {cpu_n}^3 hierarchy, row loops on {mt['threads']} host threads; coarse solve "
+                      f"{mt['coarse_seconds']:.2f} s of {mt['seconds']:.2f} s",
+            "seconds": mt["seconds"], "seconds_all": mt["seconds_all"], "coarse_seconds": mt["coarse_seconds"],
             "fine_spmv_GBps": a0_bytes / mt["spmv_seconds"] / 1e9 if cpu_n == n else None,
+            "host": hostinfo,
         }
 
     rec = {
         "metric": "V-cycle iters/sec + fine-level SpMV GB/s (%HBM peak), 64M-row 7pt Poisson",
         "value": value, "unit": "V-cycle iter/s", "n_gpus": D.world, "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": ms_per_step, "higher_is_better": True,
-        "scaling": "strong" if D.world > 1 else "weak", "vs_baseline": None,
+        "scaling": "strong" if D.world > 1 else None, "vs_baseline": None,
         "dtype": "f64", "data": f"synthetic ({args.stencil}-pt Poisson generated in memory, b = x0 = 1)",
         "config": {"workload": f"poisson{args.stencil}_{n}^3", "rows": N, "nnz": nnz, "levels": len(levels),
                    "hierarchy": [list(t) for t in levels],

@@ -96,6 +96,8 @@ def load_ref():
             "SSS_blas_array_dot": (C.c_double, [C.c_int, dp, dp]),
             "SSS_blas_array_norm2": (C.c_double, [C.c_int, dp]),
             "SSS_ivec_create": (SSS_IVEC, [C.c_int]),
+            # Solve/SSS_SOLVE.c, its SSS_amg_cycle resolved to ora_cycle (ref_cycle_glue.c)
+            "SSS_amg_solve": (SSS_RTN, [P(SSS_AMG), P(SSS_VEC), P(SSS_VEC)]),
         }
         for name, (res, args) in sigs.items():
             fn = getattr(lib, name)

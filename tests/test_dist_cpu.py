@@ -142,3 +142,25 @@ def test_partition_products_world2(kind, n, agg):
         errs.append(errq.get())
     assert not errs, "\n".join(errs)
     assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
+
+
+def test_bench_gpus_n_launches_n_ranks():
+    """`bench.py --gpus 2` without WORLD_SIZE launches two ranks itself (torch.distributed.run, a
+    child process, before any GPU call); each rank sees world size 2."""
+    import json
+    import subprocess
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    r = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--gpus", "2", "--probe-ranks"], capture_output=True,
+                       text=True, env=env, timeout=240)
+    assert r.returncode == 0, r.stderr[-2000:]
+    recs = [json.loads(l) for l in r.stdout.splitlines() if l.startswith('{"rank"')]
+    assert sorted(x["rank"] for x in recs) == [0, 1]
+    assert all(x["world"] == 2 for x in recs)
+
+
+def test_bench_gpus_mismatch_fails_loudly():
+    import subprocess
+    env = dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--gpus", "2", "--probe-ranks"], capture_output=True,
+                       text=True, env=env, timeout=120)
+    assert r.returncode != 0 and "WORLD_SIZE" in r.stderr
