@@ -153,6 +153,18 @@ inline int launch_spmv_blocks(const DevCSR &A, int nblk, int op, double alpha, c
 }
 
 // ---- smoother schedules -------------------------------------------------------------------
+// One-launch exact GS-CF pass (sss_gs_persist.hip): engine 0 = one launch per DAG depth,
+// 1 = chip-wide dataflow ("flow"), 2 = single-CU ("cu").
+struct GsPersist {
+    int engine = 0;
+    int lo = 0, hi = 0;                 // the pass's contiguous rows
+    bool wave = false;                  // flow: one long row per ticket (else 64 rows of one depth)
+    int nchunks = 0, grid = 0;
+    int *ck = nullptr;                  // flow, short rows: chunk -> first position (nchunks + 1)
+    int *h_off = nullptr;               // cu: depth offsets (depth + 1)
+    unsigned *ctl = nullptr;            // epoch, ticket, exit count, error
+    unsigned long long *gran = nullptr; // flow: two {epoch, half of x_i} granules per row
+};
 struct PassSchedule {          // rows of one class (F or C), grouped by DAG depth
     int depth = 0;
     std::vector<int> h_off;    // depth + 1 offsets into rows
@@ -176,7 +188,13 @@ struct PassSchedule {          // rows of one class (F or C), grouped by DAG dep
     DevCSR sub;
     int *map = nullptr;        // local row -> global row
     double *y = nullptr;       // Jacobi: new values of this class, scattered after the pass
+    GsPersist gp;              // exact GS with depth > 1: one launch per pass when set up
 };
+int gs_persist_build(PassSchedule &ps, const SSS_MAT &A, int lo, int hi, bool long_rows);
+void gs_persist_free(PassSchedule &ps);
+int gs_persist_run(const PassSchedule &ps, const DevCSR &A, const double *b, double *x, const double *deff,
+                   hipStream_t s);
+int gs_persist_error(const PassSchedule &ps, unsigned *out);
 struct SmootherPlan {
     int kind = SSS_HIP_SMOOTH_EXACT;
     PassSchedule pass[2];      // [0] = F pass (mark != 1), [1] = C pass (mark == 1)

@@ -1,0 +1,410 @@
+// sss_gs_persist.hip — exact GS-CF class passes with intra-class couplings as ONE launch per pass
+// (replaces the one-launch-per-DAG-depth schedule of sss_smooth.hip for SSS_amg_smoother_gs_cf,
+// Solve/SSS_smooth.c:4-87; results bitwise identical: every row forms
+//     t = b_i - sum_{k: j_k != i} a_k x_{j_k}    in stored order from b_i, then x_i = t / d
+// with exactly the x values the sequential reference reads).
+//
+// Two engines, chosen per pass at plan time by a cost estimate (SSS_HIP_GS_ENGINE overrides):
+//
+//  * "cu"   — the whole pass in ONE workgroup of 16 waves (one CU).  Rows are taken in depth order
+//             from an LDS ticket; a row of depth d waits until every row of depth d-1 has finished
+//             (per-depth completion counters in LDS, workgroup-scope release/acquire), so the
+//             hand-off between dependent rows costs an LDS round trip, not a cross-CU hop.  Made for
+//             the deep, narrow coarse levels (a few rows per depth, hundreds of entries per row):
+//             there the pass is bound by the chain of dependent rows, and one CU streams the rows
+//             fast enough.  A wave loads its row's first strip before it waits.
+//  * "flow" — dataflow over the whole chip: waves dequeue chunks (one long row, or up to 64 short
+//             rows of one depth) in depth order from an agent-scope ticket and start as soon as the
+//             rows they read are done.  A finished row publishes its value as two self-validating
+//             8-byte granules {epoch, half of x_i} (sc1 stores; MI355X_MICROARCH.md Valid forms, R2:
+//             the data is the flag); a reader of a same-class lower neighbour re-reads its granules
+//             (sc1 loads) until both tags carry this launch's epoch.  Old values (same class, j > i)
+//             and the other class's values are read from x with plain loads: they do not change
+//             during the pass, because a same-class upper neighbour j of i reads x_i and therefore
+//             waits for i (the pass requires a structurally symmetric same-class coupling, checked
+//             at plan time).  Made for the wide levels (thousands of short rows per depth).
+//
+// Both engines need the pass's rows to be a contiguous range [lo, hi) (relabeled levels) and make
+// progress without any residency assumption (tickets are handed out in depth order, a wave only
+// waits for rows whose tickets were handed out earlier).  Every spin is bounded: a pass that
+// stalls for ~0.5 s gives up and sets an error word (the engine reports it; results are then
+// garbage, but no wave spins forever).
+#include "sss_engine.hpp"
+#include "sss_spmv_dev.hpp"
+
+#include <cmath>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+
+namespace sss {
+
+constexpr int kCuWaves = 16;               // waves of the single-CU engine (1024 threads)
+constexpr int kCuMaxDepth = 7168;          // LDS completion counters (28 KiB)
+constexpr int kSpinLimit = 1 << 22;        // LDS polls before a cu wave gives up (~0.5 s with s_sleep)
+constexpr int kFlowSpinLimit = 1 << 18;    // granule polls before a flow wave gives up (~0.5 s)
+
+// control words of a flow pass: [0] epoch of the last completed launch, [1] ticket, [2] waves that
+// have exited, [3] error (stall) flag
+enum { kCtlEpoch = 0, kCtlTicket = 1, kCtlExit = 2, kCtlErr = 3, kCtlWords = 4 };
+
+#define RLX_AGENT __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT
+
+__device__ __forceinline__ double x_own(double *x, int i)   // a row's own value, never via the scalar cache
+{
+    return __longlong_as_double(
+        (long long)__hip_atomic_load(reinterpret_cast<unsigned long long *>(x + i), RLX_AGENT));
+}
+
+// ---- flow engine -------------------------------------------------------------------------------
+__device__ __forceinline__ bool granule_get(const unsigned long long *g, unsigned epoch, double &val)
+{
+    const unsigned long long a = __hip_atomic_load(const_cast<unsigned long long *>(g), RLX_AGENT);
+    const unsigned long long c = __hip_atomic_load(const_cast<unsigned long long *>(g + 1), RLX_AGENT);
+    if ((unsigned)(a >> 32) != epoch || (unsigned)(c >> 32) != epoch) return false;
+    val = __longlong_as_double((long long)((c << 32) | (a & 0xffffffffull)));
+    return true;
+}
+__device__ __forceinline__ void granule_put(unsigned long long *g, unsigned epoch, double v)
+{
+    const unsigned long long u = (unsigned long long)__double_as_longlong(v);
+    __hip_atomic_store(g, ((unsigned long long)epoch << 32) | (u & 0xffffffffull), RLX_AGENT);
+    __hip_atomic_store(g + 1, ((unsigned long long)epoch << 32) | (u >> 32), RLX_AGENT);
+}
+// x_j of a same-class lower neighbour: spin on its granules (bounded)
+__device__ __forceinline__ double granule_wait(const unsigned long long *g, unsigned epoch, unsigned *err)
+{
+    double v = 0.0;
+    for (int s = 0; !granule_get(g, epoch, v); ++s) {
+        // give up after the limit, or at once when another wave already did (checked every 64 polls)
+        if (s >= kFlowSpinLimit || ((s & 63) == 63 && __hip_atomic_load(err, RLX_AGENT))) {
+            __hip_atomic_store(err, 1u, RLX_AGENT);
+            return 0.0;
+        }
+        __builtin_amdgcn_s_sleep(1);
+    }
+    return v;
+}
+
+__device__ __forceinline__ void flow_exit(unsigned *ctl, unsigned epoch)
+{
+    // the last wave out resets the ticket and the exit count and publishes the epoch for the next
+    // launch (visible to it across the kernel boundary)
+    const unsigned total = gridDim.x * (blockDim.x >> 6);
+    if ((threadIdx.x & 63) == 0 && __hip_atomic_fetch_add(&ctl[kCtlExit], 1u, RLX_AGENT) == total - 1) {
+        __hip_atomic_store(&ctl[kCtlTicket], 0u, RLX_AGENT);
+        __hip_atomic_store(&ctl[kCtlExit], 0u, RLX_AGENT);
+        __hip_atomic_store(&ctl[kCtlEpoch], epoch, RLX_AGENT);
+    }
+}
+
+__device__ __forceinline__ int flow_ticket(unsigned *ctl)
+{
+    int p = 0;
+    if ((threadIdx.x & 63) == 0) p = (int)__hip_atomic_fetch_add(&ctl[kCtlTicket], 1u, RLX_AGENT);
+    return __shfl(p, 0, 64);
+}
+
+// one long row per ticket, the whole wave on it (lane 0 runs the stored-order chain)
+__global__ __launch_bounds__(kBlock) void gs_flow_wave(int nrows, const int *__restrict__ rows,
+                                                       const int *__restrict__ rp, const int *__restrict__ ci,
+                                                       const double *__restrict__ v, const double *__restrict__ b,
+                                                       double *x, const double *__restrict__ deff,
+                                                       unsigned long long *gran, int lo, unsigned *ctl)
+{
+    __shared__ double strips[4][kWaveStage];
+    double *strip = strips[threadIdx.x >> 6];
+    const int lane = threadIdx.x & 63;
+    const unsigned epoch = __hip_atomic_load(&ctl[kCtlEpoch], RLX_AGENT) + 1u;
+    unsigned *err = &ctl[kCtlErr];
+    for (;;) {
+        const int p = flow_ticket(ctl);
+        if (p >= nrows) break;
+        const int i = rows[p];
+        const int k0 = rp[i], k1 = rp[i + 1];
+        auto prod = [&](int c, double a) -> double {
+            if (c == i) return 0.0;   // the diagonal: subtracting +0.0 is the identity
+            const double xv = (c >= lo && c < i) ? granule_wait(gran + 2 * (size_t)(c - lo), epoch, err) : x[c];
+            return a * xv;
+        };
+        const double acc = wave_row_chain<true>(k0, k1, ci, v, prod, b[i], strip);
+        if (lane == 0) {
+            const double d = deff[i];
+            const double xn = fabs(d) > SMALLFLOAT ? acc / d : x_own(x, i);
+            x[i] = xn;
+            granule_put(gran + 2 * (size_t)(i - lo), epoch, xn);
+        }
+    }
+    flow_exit(ctl, epoch);
+}
+
+// up to 64 rows of one depth per ticket, one per lane
+__global__ __launch_bounds__(kBlock) void gs_flow_thread(int nchunks, const int *__restrict__ ck,
+                                                         const int *__restrict__ rows, const int *__restrict__ rp,
+                                                         const int *__restrict__ ci, const double *__restrict__ v,
+                                                         const double *__restrict__ b, double *x,
+                                                         const double *__restrict__ deff, unsigned long long *gran,
+                                                         int lo, unsigned *ctl)
+{
+    const int lane = threadIdx.x & 63;
+    const unsigned epoch = __hip_atomic_load(&ctl[kCtlEpoch], RLX_AGENT) + 1u;
+    unsigned *err = &ctl[kCtlErr];
+    for (;;) {
+        const int q = flow_ticket(ctl);
+        if (q >= nchunks) break;
+        const int p = ck[q] + lane;
+        if (p >= ck[q + 1]) continue;
+        const int i = rows[p];
+        const int k0 = rp[i], k1 = rp[i + 1];
+        double acc = b[i];
+        constexpr int U = 8;
+        for (int k = k0; k < k1; k += U) {
+            int c[U];
+            double a[U], xv[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                c[u] = k + u < k1 ? ci[k + u] : i;
+                a[u] = k + u < k1 ? v[k + u] : 0.0;
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u) xv[u] = (c[u] >= lo && c[u] < i) ? 0.0 : x[c[u]];
+#pragma unroll
+            for (int u = 0; u < U; ++u)
+                if (c[u] >= lo && c[u] < i) xv[u] = granule_wait(gran + 2 * (size_t)(c[u] - lo), epoch, err);
+#pragma unroll
+            for (int u = 0; u < U; ++u)
+                if (c[u] != i) acc -= a[u] * xv[u];
+        }
+        const double d = deff[i];
+        const double xn = fabs(d) > SMALLFLOAT ? acc / d : x_own(x, i);
+        x[i] = xn;
+        granule_put(gran + 2 * (size_t)(i - lo), epoch, xn);
+    }
+    flow_exit(ctl, epoch);
+}
+
+// ---- single-CU engine --------------------------------------------------------------------------
+// One workgroup of kCuWaves waves.  h_off[d] .. h_off[d+1]: positions of depth d in `rows`.
+__global__ __launch_bounds__(64 * kCuWaves) void gs_cu(int nrows, int ndepth, const int *__restrict__ rows,
+                                                       const int *__restrict__ h_off, const int *__restrict__ rp,
+                                                       const int *__restrict__ ci, const double *__restrict__ v,
+                                                       const double *__restrict__ b, double *x,
+                                                       const double *__restrict__ deff, unsigned *err)
+{
+    __shared__ int done[kCuMaxDepth];
+    __shared__ int ticket, abort_flag;
+    __shared__ double strips[kCuWaves][kWaveStage];
+    for (int t = threadIdx.x; t < ndepth; t += blockDim.x) done[t] = 0;
+    if (threadIdx.x == 0) ticket = 0, abort_flag = 0;
+    __syncthreads();
+    const int lane = threadIdx.x & 63;
+    double *strip = strips[threadIdx.x >> 6];
+    constexpr int U = kWaveStage / 64;
+    int d = 0;
+    for (;;) {
+        int p = 0;
+        if (lane == 0) p = __hip_atomic_fetch_add(&ticket, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        p = __shfl(p, 0, 64);
+        if (p >= nrows) break;
+        while (p >= h_off[d + 1]) ++d;   // tickets rise, so each wave's depth only moves forward
+        const int i = rows[p];
+        const int k0 = rp[i], k1 = rp[i + 1];
+        // the first strip's entries do not depend on the pass: load them before waiting
+        int c[U];
+        double a[U];
+        {
+            const int m = min(kWaveStage, k1 - k0);
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int q = lane + 64 * u;
+                c[u] = q < m ? ci[k0 + q] : 0;
+                a[u] = q < m ? v[k0 + q] : 0.0;
+            }
+        }
+        if (d > 0) {
+            const int need = h_off[d] - h_off[d - 1];
+            for (int s = 0; __hip_atomic_load(&done[d - 1], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < need; ++s) {
+                // give up after the limit, or at once when another wave of the pass already did
+                if (s >= kSpinLimit || __hip_atomic_load(&abort_flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) {
+                    if (lane == 0) {
+                        __hip_atomic_store(err, 1u, RLX_AGENT);
+                        __hip_atomic_store(&abort_flag, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    }
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(1);
+            }
+        }
+        double acc = b[i];
+        for (int base = k0; base < k1; base += kWaveStage) {
+            const int m = min(kWaveStage, k1 - base);
+            if (base != k0) {
+#pragma unroll
+                for (int u = 0; u < U; ++u) {
+                    const int q = lane + 64 * u;
+                    c[u] = q < m ? ci[base + q] : 0;
+                    a[u] = q < m ? v[base + q] : 0.0;
+                }
+            }
+            double xv[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int q = lane + 64 * u;
+                xv[u] = (q < m && c[u] != i) ? x[c[u]] : 0.0;
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int q = lane + 64 * u;
+                if (q < m) strip[q] = c[u] == i ? 0.0 : a[u] * xv[u];
+            }
+            wave_sync();
+            if (lane == 0) acc = chain_sub(acc, strip, 0, m);
+            wave_sync();
+        }
+        if (lane == 0) {
+            const double dd = deff[i];
+            if (fabs(dd) > SMALLFLOAT) x[i] = acc / dd;
+            // release: the x store above is visible to every wave of the workgroup that acquires
+            // this counter
+            __hip_atomic_fetch_add(&done[d], 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+    }
+}
+
+// ---- planning ----------------------------------------------------------------------------------
+static const char *gs_engine_env()
+{
+    const char *e = getenv("SSS_HIP_GS_ENGINE");
+    return e ? e : "auto";
+}
+
+// Rows of the pass are ps.h_off-ordered by depth; A is the level matrix (host), [lo, hi) the pass's
+// contiguous row range.  Chooses the engine and builds its device data.
+int gs_persist_build(PassSchedule &ps, const SSS_MAT &A, int lo, int hi, bool long_rows)
+{
+    GsPersist &g = ps.gp;
+    g = GsPersist();
+    const std::string want = gs_engine_env();
+    if (want == "launch" || ps.depth <= 1 || ps.nrows == 0) return 0;
+    const int *rp = A.row_ptr, *ci = A.col_idx;
+    long long nnz = 0;
+    for (int i = lo; i < hi; ++i) nnz += rp[i + 1] - rp[i];
+    const double bytes = 12.0 * (double)nnz + 44.0 * (double)(hi - lo);
+    const double avg = (double)nnz / std::max(1, hi - lo);
+    // cost estimates (seconds) per pass; constants measured on MI355X
+    const double t_launch = ps.depth * 5.0e-6 + bytes / 2.0e12;
+    const double t_flow = ps.depth * 2.0e-6 + bytes / 2.5e12;
+    const double t_cu = std::max(bytes / 9.0e10, ps.depth * (0.4e-6 + 0.5 * avg * 3.5e-9));
+    int engine = 0;
+    if (want == "cu") engine = 2;
+    else if (want == "flow") engine = 1;
+    else engine = t_cu <= t_flow ? 2 : 1;
+    if (engine == 2 && ps.depth > kCuMaxDepth) engine = 1;
+    if (engine == 0 || (want == "auto" && std::min(t_cu, t_flow) >= t_launch)) return 0;
+    if (engine == 1) {
+        // the flow engine needs every same-class coupling in both directions (see the header)
+        bool sym = true;
+        std::vector<char> bad(1, 0);
+        parallel_chunks(hi - lo, 4096, [&](int a, int e) {
+            for (int i = lo + a; i < lo + e && !bad[0]; ++i)
+                for (int k = rp[i]; k < rp[i + 1]; ++k) {
+                    const int j = ci[k];
+                    if (j == i || j < lo || j >= hi) continue;
+                    bool found = false;
+                    for (int t = rp[j]; t < rp[j + 1] && !found; ++t) found = ci[t] == i;
+                    if (!found) {
+                        bad[0] = 1;
+                        break;
+                    }
+                }
+        });
+        sym = !bad[0];
+        if (!sym) {
+            if (ps.depth <= kCuMaxDepth) engine = 2;
+            else return 0;
+        }
+    }
+    g.engine = engine;
+    g.lo = lo;
+    g.hi = hi;
+    if (engine == 2) {
+        std::vector<int> off(ps.h_off.begin(), ps.h_off.end());
+        g.h_off = dev_alloc<int>(off.size());
+        g.ctl = dev_alloc<unsigned>(kCtlWords);
+        if (!g.h_off || !g.ctl) return hip_fail(hipErrorOutOfMemory, "hipMalloc(gs cu)", __FILE__, __LINE__);
+        SSS_HIP(hipMemcpy(g.h_off, off.data(), sizeof(int) * off.size(), hipMemcpyHostToDevice));
+        SSS_HIP(hipMemset(g.ctl, 0, sizeof(unsigned) * kCtlWords));
+        return 0;
+    }
+    g.wave = long_rows;
+    g.gran = dev_alloc<unsigned long long>(2 * (size_t)(hi - lo));
+    g.ctl = dev_alloc<unsigned>(kCtlWords);
+    if (!g.gran || !g.ctl) return hip_fail(hipErrorOutOfMemory, "hipMalloc(gs flow)", __FILE__, __LINE__);
+    SSS_HIP(hipMemset(g.gran, 0, sizeof(unsigned long long) * 2 * (size_t)(hi - lo)));
+    SSS_HIP(hipMemset(g.ctl, 0, sizeof(unsigned) * kCtlWords));
+    if (!g.wave) {   // chunks: up to 64 rows of one depth
+        std::vector<int> ck;
+        for (int l = 0; l < ps.depth; ++l)
+            for (int s = ps.h_off[l]; s < ps.h_off[l + 1]; s += 64) ck.push_back(s);
+        ck.push_back(ps.nrows);
+        g.nchunks = (int)ck.size() - 1;
+        g.ck = dev_alloc<int>(ck.size());
+        if (!g.ck) return hip_fail(hipErrorOutOfMemory, "hipMalloc(gs chunks)", __FILE__, __LINE__);
+        SSS_HIP(hipMemcpy(g.ck, ck.data(), sizeof(int) * ck.size(), hipMemcpyHostToDevice));
+    } else {
+        g.nchunks = ps.nrows;
+    }
+    int cus = 256;
+    {
+        int dev = 0;
+        hipDeviceProp_t prop;
+        if (hipGetDevice(&dev) == hipSuccess && hipGetDeviceProperties(&prop, dev) == hipSuccess)
+            cus = prop.multiProcessorCount;
+    }
+    // enough waves to keep every CU streaming, no more than there are tickets
+    const int waves = std::min(g.nchunks, cus * 8);
+    g.grid = std::max(1, (waves + 3) / 4);
+    return 0;
+}
+
+void gs_persist_free(PassSchedule &ps)
+{
+    GsPersist &g = ps.gp;
+    dev_free(g.h_off);
+    dev_free(g.ctl);
+    dev_free(g.gran);
+    dev_free(g.ck);
+    g = GsPersist();
+}
+
+int gs_persist_run(const PassSchedule &ps, const DevCSR &A, const double *b, double *x, const double *deff,
+                   hipStream_t s)
+{
+    const GsPersist &g = ps.gp;
+    if (g.engine == 2) {
+        hipLaunchKernelGGL(gs_cu, dim3(1), dim3(64 * kCuWaves), 0, s, ps.nrows, ps.depth, ps.rows, g.h_off, A.rp, A.ci,
+                           A.v, b, x, deff, g.ctl + kCtlErr);
+    } else if (g.engine == 1 && g.wave) {
+        hipLaunchKernelGGL(gs_flow_wave, dim3(g.grid), dim3(kBlock), 0, s, ps.nrows, ps.rows, A.rp, A.ci, A.v, b, x,
+                           deff, g.gran, g.lo, g.ctl);
+    } else if (g.engine == 1) {
+        hipLaunchKernelGGL(gs_flow_thread, dim3(g.grid), dim3(kBlock), 0, s, g.nchunks, g.ck, ps.rows, A.rp, A.ci, A.v,
+                           b, x, deff, g.gran, g.lo, g.ctl);
+    } else {
+        return ERROR_INPUT_PAR;
+    }
+    SSS_HIP(hipGetLastError());
+    return 0;
+}
+
+int gs_persist_error(const PassSchedule &ps, unsigned *out)
+{
+    *out = 0;
+    if (!ps.gp.ctl) return 0;
+    unsigned e = 0;
+    SSS_HIP(hipMemcpy(&e, ps.gp.ctl + kCtlErr, sizeof(unsigned), hipMemcpyDeviceToHost));
+    *out = e;
+    return 0;
+}
+
+}  // namespace sss

@@ -342,15 +342,17 @@ sss_hip_hier *sss::hier_create_impl(const SSS_AMG *mg, const sss_hip_opts *o, in
         const auto &sm = h->L[l].sm;
         long long per_sweep = 0;
         for (const auto &ps : sm.pass)
-            per_sweep += ps.nrows == 0 ? 0 : ps.compact ? (sm.kind == SSS_HIP_SMOOTH_JACOBI ? 2 + sm.inner : 1) : ps.depth;
+            per_sweep += ps.nrows == 0 ? 0
+                         : ps.compact ? (sm.kind == SSS_HIP_SMOOTH_JACOBI ? 2 + sm.inner : 1)
+                         : ps.gp.engine ? 1 : ps.depth;
         launches += per_sweep * (h->pars.pre_iter + h->pars.post_iter) + 4;
     }
     if (launches > 4096) h->opts.use_graph = 0;
     if (h->opts.verbose) {
         for (int l = 0; l < h->nl; ++l)
-            fprintf(stderr, "[sss_hip] level %d: n=%d nnz=%d blocks=%d dagF=%d dagC=%d kind=%d\n", l, h->L[l].A.n,
-                    h->L[l].A.nnz, h->L[l].A.nblk, h->L[l].sm.pass[0].depth, h->L[l].sm.pass[1].depth,
-                    h->L[l].sm.kind);
+            fprintf(stderr, "[sss_hip] level %d: n=%d nnz=%d blocks=%d dagF=%d dagC=%d kind=%d gs engine F/C=%d/%d\n", l,
+                    h->L[l].A.n, h->L[l].A.nnz, h->L[l].A.nblk, h->L[l].sm.pass[0].depth, h->L[l].sm.pass[1].depth,
+                    h->L[l].sm.kind, h->L[l].sm.pass[0].gp.engine, h->L[l].sm.pass[1].gp.engine);
     }
     return h;
 }
@@ -710,6 +712,11 @@ extern "C" int sss_hip_level_info_get(sss_hip_hier *h, int level, sss_hip_level_
     out->dag_f = L.sm.pass[0].depth;
     out->dag_c = L.sm.pass[1].depth;
     out->smoother_kind = L.sm.kind;
+    out->gs_engine_f = L.sm.pass[0].gp.engine;
+    out->gs_engine_c = L.sm.pass[1].gp.engine;
+    unsigned ef = 0, ec = 0;
+    if (gs_persist_error(L.sm.pass[0], &ef) || gs_persist_error(L.sm.pass[1], &ec)) return ERROR_MISC;
+    out->gs_stall = (int)(ef | ec);
     return 0;
 }
 

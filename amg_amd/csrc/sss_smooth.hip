@@ -171,6 +171,22 @@ int smoother_build(SmootherPlan &sp, const SSS_MAT &A, const int *mark, int kind
         }
     }
     if ((rc = upload_ints(&sp.cls, cls))) return rc;
+    // exact GS passes with intra-class chains: one launch per pass where the class is contiguous
+    if (kind == SSS_HIP_SMOOTH_EXACT && !gcls && A.num_cols == n) {
+        for (int c = 0; c < 2; ++c) {
+            PassSchedule &ps = sp.pass[c];
+            if (ps.compact || ps.depth <= 1 || ps.nrows == 0) continue;
+            int lo = -1, hi = -1;
+            bool contiguous = true;
+            for (int i = 0; i < n && contiguous; ++i) {
+                if (cls[i] != c) continue;
+                if (lo < 0) lo = i;
+                else if (i != hi) contiguous = false;
+                hi = i + 1;
+            }
+            if (contiguous && (rc = gs_persist_build(ps, A, lo, hi, sp.long_rows))) return rc;
+        }
+    }
     if (kind == SSS_HIP_SMOOTH_JACOBI && inner > 0 && sp.pass[0].range == (sp.pass[0].nrows > 0) &&
         sp.pass[1].range == (sp.pass[1].nrows > 0)) {
         sp.inner = inner;
@@ -286,6 +302,7 @@ void smoother_free(SmootherPlan &sp)
         devcsr_free(ps.ts_lo);
         dev_free(ps.ts_split);
         dev_free(ps.ts_P);
+        gs_persist_free(ps);
     }
     if (sp.d_later != sp.d_first) dev_free(sp.d_later);
     dev_free(sp.d_first);
@@ -883,6 +900,10 @@ int smoother_run(const SmootherPlan &sp, const DevCSR &A, const double *b, doubl
                 else
                     hipLaunchKernelGGL(relax_compact<true>, dim3(ps.sub.nblk), dim3(kBlock), 0, s, ps.sub.blk,
                                        ps.sub.rp, ps.sub.ci, ps.sub.v, ps.map, b, x, (double *)nullptr, deff);
+                continue;
+            }
+            if (ps.gp.engine) {
+                if ((rc = gs_persist_run(ps, A, b, x, deff, s))) return rc;
                 continue;
             }
             for (int l = 0; l < ps.depth; ++l) {

@@ -101,9 +101,12 @@ int sss_hip_coarse_solve(sss_hip_hier *h);
 int sss_hip_smooth(sss_hip_hier *h, int level, int post);
 int sss_hip_sync(sss_hip_hier *h);
 
-/* Per-level statistics for reporting: rows, nnz(A), nnz(P), smoother DAG depths. */
+/* Per-level statistics for reporting: rows, nnz(A), nnz(P), smoother DAG depths; the exact GS
+ * engine of the F / C pass (0: one launch per DAG depth, 1: chip-wide dataflow, 2: single CU) and
+ * whether a one-launch pass ever gave up waiting (gs_stall != 0: results invalid). */
 typedef struct sss_hip_level_info {
     int rows, nnz, nnz_p, dag_f, dag_c, smoother_kind;
+    int gs_engine_f, gs_engine_c, gs_stall;
 } sss_hip_level_info;
 int sss_hip_level_info_get(sss_hip_hier *h, int level, sss_hip_level_info *out);
 int sss_hip_num_levels(sss_hip_hier *h);

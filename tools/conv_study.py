@@ -57,9 +57,15 @@ def main():
     out = {"n": a.n, "stencil": a.stencil, "levels": [(H.level(l).A.num_rows, H.level(l).A.num_nnzs)
                                                       for l in range(H.num_levels)], "modes": {}}
     normb = float(np.sqrt(N))
+    import os
     for m in a.modes.split(","):
+        base, _, eng = m.partition("@")   # parity@cu: exact GS engine override (SSS_HIP_GS_ENGINE)
+        if eng:
+            os.environ["SSS_HIP_GS_ENGINE"] = eng
+        else:
+            os.environ.pop("SSS_HIP_GS_ENGINE", None)
         t0 = time.perf_counter()
-        D = A.DeviceHierarchy(H, device=0, **mode_kwargs(m))
+        D = A.DeviceHierarchy(H, device=0, **mode_kwargs(base))
         up = time.perf_counter() - t0
         D.upload(0, "b", np.ones(N))
         D.upload(0, "x", np.ones(N))
@@ -74,12 +80,16 @@ def main():
             if rel < H.pars.tol or not np.isfinite(rel):
                 break
         x = D.download(0, "x")
+        info = [D.level_info(l) for l in range(H.num_levels - 1)]
+        engines = [(i.gs_engine_f, i.gs_engine_c) for i in info]
+        stall = any(i.gs_stall for i in info)
         D.close()
         out["modes"][m] = {"upload_s": up, "relres": hist, "iters": len(hist),
-                           "ms_per_iter_median": float(np.median(times) * 1e3),
+                           "ms_per_iter_median": float(np.median(times) * 1e3), "gs_engines": engines,
+                           "gs_stall": stall,
                            "sum_x": float(x.sum()), "x_sample": x[:: max(1, N // 4096)].tolist()}
-        print(f"[conv] {m}: {len(hist)} iterations, upload {up:.1f} s, median {np.median(times) * 1e3:.2f} ms",
-              file=sys.stderr, flush=True)
+        print(f"[conv] {m}: {len(hist)} iterations, upload {up:.1f} s, median {np.median(times) * 1e3:.2f} ms, "
+              f"gs engines {engines}, stall {stall}", file=sys.stderr, flush=True)
     # pairwise x differences (sampled) against the first mode
     modes = list(out["modes"])
     if modes:
