@@ -98,11 +98,14 @@ __device__ __forceinline__ void flow_exit(unsigned *ctl, unsigned epoch)
     }
 }
 
+// Next ticket for the whole wave.  Every lane takes part in the atomic (lane 0 adds 1, the others
+// 0) and the result is read from the first lane into a scalar register: the loop around it then
+// has a uniform exit, so the compiler keeps the wave converged (a lane-0-only atomic followed by a
+// __shfl lets the structurizer split the loop and broadcast from an inactive lane).
 __device__ __forceinline__ int flow_ticket(unsigned *ctl)
 {
-    int p = 0;
-    if ((threadIdx.x & 63) == 0) p = (int)__hip_atomic_fetch_add(&ctl[kCtlTicket], 1u, RLX_AGENT);
-    return __shfl(p, 0, 64);
+    const unsigned inc = (threadIdx.x & 63) == 0 ? 1u : 0u;
+    return __builtin_amdgcn_readfirstlane((int)__hip_atomic_fetch_add(&ctl[kCtlTicket], inc, RLX_AGENT));
 }
 
 // one long row per ticket, the whole wave on it (lane 0 runs the stored-order chain)
@@ -202,9 +205,8 @@ __global__ __launch_bounds__(64 * kCuWaves) void gs_cu(int nrows, int ndepth, co
     constexpr int U = kWaveStage / 64;
     int d = 0;
     for (;;) {
-        int p = 0;
-        if (lane == 0) p = __hip_atomic_fetch_add(&ticket, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        p = __shfl(p, 0, 64);
+        const int p = __builtin_amdgcn_readfirstlane(
+            __hip_atomic_fetch_add(&ticket, lane == 0 ? 1 : 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
         if (p >= nrows) break;
         while (p >= h_off[d + 1]) ++d;   // tickets rise, so each wave's depth only moves forward
         const int i = rows[p];

@@ -1,6 +1,10 @@
-set -o pipefail
-cd $GRAFT_REPO_ROOT
-timeout -k 10 400 python -u -m pytest tests/test_gpu_gs_engines.py -x -v --timeout 300 --timeout-method thread > gpurun_out/gs_tests.log 2>&1 || { echo TESTS_FAILED; tail -30 gpurun_out/gs_tests.log; exit 1; }
-tail -3 gpurun_out/gs_tests.log
-timeout -k 10 600 python -u tools/conv_study.py --n 256 --modes parity@cu,parity@flow,exact-direct --maxit 3 --json gpurun_out/conv256_gs.json > gpurun_out/conv256_gs.log 2>&1
-grep "\[conv\]" gpurun_out/conv256_gs.log | tail -12
+# One-launch exact GS engines: GPU tests, then 256^3 parity-mode V-cycle times per engine.
+cd "$GRAFT_REPO_ROOT" || exit 1
+timeout -k 10 400 python -u -m pytest tests/test_gpu_gs_engines.py -x -v --timeout 120 --timeout-method thread > gpurun_out/gs_tests.log 2>&1
+rc=$?
+tail -5 gpurun_out/gs_tests.log
+[ $rc -eq 0 ] || exit $rc
+timeout -k 10 600 python -u tools/conv_study.py --n 256 --modes ${GS_MODES:-parity@cu,parity@flow,parity} --maxit ${GS_MAXIT:-3} --json gpurun_out/conv256_gs.json > gpurun_out/conv256_gs.log 2>&1
+rc=$?
+grep "\[conv\]" gpurun_out/conv256_gs.log
+exit $rc
