@@ -158,7 +158,7 @@ inline int launch_spmv_blocks(const DevCSR &A, int nblk, int op, double alpha, c
 struct GsPersist {
     int engine = 0;
     int lo = 0, hi = 0;                 // the pass's contiguous rows
-    bool wave = false;                  // flow: one long row per ticket (else 64 rows of one depth)
+    int G = 64;                         // flow: lanes per row (64 / G rows of one depth per ticket)
     int nchunks = 0, grid = 0;
     int *ck = nullptr;                  // flow, short rows: chunk -> first position (nchunks + 1)
     int *h_off = nullptr;               // cu: depth offsets (depth + 1)

@@ -9,13 +9,13 @@
 //  * "cu"   — the whole pass in ONE workgroup of 16 waves (one CU).  Rows are taken in depth order
 //             from an LDS ticket; a row of depth d waits until every row of depth d-1 has finished
 //             (per-depth completion counters in LDS, workgroup-scope release/acquire), so the
-//             hand-off between dependent rows costs an LDS round trip, not a cross-CU hop.  Made for
-//             the deep, narrow coarse levels (a few rows per depth, hundreds of entries per row):
-//             there the pass is bound by the chain of dependent rows, and one CU streams the rows
-//             fast enough.  A wave loads its row's first strip before it waits.
-//  * "flow" — dataflow over the whole chip: waves dequeue chunks (one long row, or up to 64 short
-//             rows of one depth) in depth order from an agent-scope ticket and start as soon as the
-//             rows they read are done.  A finished row publishes its value as two self-validating
+//             hand-off between dependent rows costs an LDS round trip, not a cross-CU hop.  Kept
+//             for comparison (SSS_HIP_GS_ENGINE=cu): measured slower than flow on every level of
+//             7-pt 256^3 -- one CU streams too slowly, and a dependent step is dominated by the
+//             row's own in-order chain either way.
+//  * "flow" — dataflow over the whole chip (the default): waves dequeue chunks (64 / G rows of one
+//             depth, G lanes per row) in depth order from an agent-scope ticket, stage every product
+//             they can form before waiting, and finish as soon as the rows they read are done.  A finished row publishes its value as two self-validating
 //             8-byte granules {epoch, half of x_i} (sc1 stores; MI355X_MICROARCH.md Valid forms, R2:
 //             the data is the flag); a reader of a same-class lower neighbour re-reads its granules
 //             (sc1 loads) until both tags carry this launch's epoch.  Old values (same class, j > i)
@@ -81,7 +81,8 @@ __device__ __forceinline__ double granule_wait(const unsigned long long *g, unsi
             __hip_atomic_store(err, 1u, RLX_AGENT);
             return 0.0;
         }
-        __builtin_amdgcn_s_sleep(1);
+        if (s < 16) __builtin_amdgcn_s_sleep(1);   // back off: polls load the memory system
+        else __builtin_amdgcn_s_sleep(8);
     }
     return v;
 }
@@ -108,80 +109,116 @@ __device__ __forceinline__ int flow_ticket(unsigned *ctl)
     return __builtin_amdgcn_readfirstlane((int)__hip_atomic_fetch_add(&ctl[kCtlTicket], inc, RLX_AGENT));
 }
 
-// one long row per ticket, the whole wave on it (lane 0 runs the stored-order chain)
-__global__ __launch_bounds__(kBlock) void gs_flow_wave(int nrows, const int *__restrict__ rows,
-                                                       const int *__restrict__ rp, const int *__restrict__ ci,
-                                                       const double *__restrict__ v, const double *__restrict__ b,
-                                                       double *x, const double *__restrict__ deff,
-                                                       unsigned long long *gran, int lo, unsigned *ctl)
+// s - p[a] - p[a+1] - ... - p[e-1] in order, with the next batch's LDS reads issued before the
+// current batch's subtractions (the chain is one dependent fp64 subtraction per entry)
+__device__ __forceinline__ double chain_sub_pipe(double s, const double *p, int a, int e)
 {
-    __shared__ double strips[4][kWaveStage];
-    double *strip = strips[threadIdx.x >> 6];
-    const int lane = threadIdx.x & 63;
-    const unsigned epoch = __hip_atomic_load(&ctl[kCtlEpoch], RLX_AGENT) + 1u;
-    unsigned *err = &ctl[kCtlErr];
-    for (;;) {
-        const int p = flow_ticket(ctl);
-        if (p >= nrows) break;
-        const int i = rows[p];
-        const int k0 = rp[i], k1 = rp[i + 1];
-        auto prod = [&](int c, double a) -> double {
-            if (c == i) return 0.0;   // the diagonal: subtracting +0.0 is the identity
-            const double xv = (c >= lo && c < i) ? granule_wait(gran + 2 * (size_t)(c - lo), epoch, err) : x[c];
-            return a * xv;
-        };
-        const double acc = wave_row_chain<true>(k0, k1, ci, v, prod, b[i], strip);
-        if (lane == 0) {
-            const double d = deff[i];
-            const double xn = fabs(d) > SMALLFLOAT ? acc / d : x_own(x, i);
-            x[i] = xn;
-            granule_put(gran + 2 * (size_t)(i - lo), epoch, xn);
+    int k = a;
+    if (e - k >= 16) {
+        double c0 = p[k], c1 = p[k + 1], c2 = p[k + 2], c3 = p[k + 3];
+        double c4 = p[k + 4], c5 = p[k + 5], c6 = p[k + 6], c7 = p[k + 7];
+        for (k += 8; k + 8 <= e; k += 8) {
+            const double n0 = p[k], n1 = p[k + 1], n2 = p[k + 2], n3 = p[k + 3];
+            const double n4 = p[k + 4], n5 = p[k + 5], n6 = p[k + 6], n7 = p[k + 7];
+            s -= c0; s -= c1; s -= c2; s -= c3; s -= c4; s -= c5; s -= c6; s -= c7;
+            c0 = n0, c1 = n1, c2 = n2, c3 = n3, c4 = n4, c5 = n5, c6 = n6, c7 = n7;
         }
+        s -= c0; s -= c1; s -= c2; s -= c3; s -= c4; s -= c5; s -= c6; s -= c7;
     }
-    flow_exit(ctl, epoch);
+    for (; k < e; ++k) s -= p[k];
+    return s;
 }
 
-// up to 64 rows of one depth per ticket, one per lane
-__global__ __launch_bounds__(kBlock) void gs_flow_thread(int nchunks, const int *__restrict__ ck,
-                                                         const int *__restrict__ rows, const int *__restrict__ rp,
-                                                         const int *__restrict__ ci, const double *__restrict__ v,
-                                                         const double *__restrict__ b, double *x,
-                                                         const double *__restrict__ deff, unsigned long long *gran,
-                                                         int lo, unsigned *ctl)
+constexpr int kGroupBuf = 2048;   // staged products per wave (16 KiB; 64 KiB per workgroup)
+
+// R = 64 / G rows of one depth per ticket, G lanes per row.  Per row and per round of up to
+// 32 G entries: (A) the G lanes load the entries and form every product whose x is final --
+// the other class, same-class upper neighbours (old values) and lower neighbours whose granules
+// are already published -- into the wave's LDS row buffer, keeping a bit per still-pending entry;
+// (B) they wait for the pending granules and fill those products; (C) the row's first lane runs
+// the stored-order chain over the buffer.  A row never waits before all its own loads are issued.
+template <int G>
+__global__ __launch_bounds__(kBlock) void gs_flow_group(int nchunks, const int *__restrict__ ck,
+                                                        const int *__restrict__ rows, const int *__restrict__ rp,
+                                                        const int *__restrict__ ci, const double *__restrict__ v,
+                                                        const double *__restrict__ b, double *x,
+                                                        const double *__restrict__ deff, unsigned long long *gran,
+                                                        int lo, unsigned *ctl)
 {
-    const int lane = threadIdx.x & 63;
+    constexpr int R = 64 / G, CAP = kGroupBuf / R, U = 8;
+    static_assert(CAP / G == 32, "one pending bit per staged entry of a lane");
+    __shared__ double buf[kBlock / 64][kGroupBuf];
+    const int lane = threadIdx.x & 63, grp = lane / G, gl = lane % G;
+    double *mine = buf[threadIdx.x >> 6] + grp * CAP;
     const unsigned epoch = __hip_atomic_load(&ctl[kCtlEpoch], RLX_AGENT) + 1u;
     unsigned *err = &ctl[kCtlErr];
     for (;;) {
         const int q = flow_ticket(ctl);
         if (q >= nchunks) break;
-        const int p = ck[q] + lane;
-        if (p >= ck[q + 1]) continue;
-        const int i = rows[p];
-        const int k0 = rp[i], k1 = rp[i + 1];
-        double acc = b[i];
-        constexpr int U = 8;
-        for (int k = k0; k < k1; k += U) {
-            int c[U];
-            double a[U], xv[U];
-#pragma unroll
-            for (int u = 0; u < U; ++u) {
-                c[u] = k + u < k1 ? ci[k + u] : i;
-                a[u] = k + u < k1 ? v[k + u] : 0.0;
-            }
-#pragma unroll
-            for (int u = 0; u < U; ++u) xv[u] = (c[u] >= lo && c[u] < i) ? 0.0 : x[c[u]];
-#pragma unroll
-            for (int u = 0; u < U; ++u)
-                if (c[u] >= lo && c[u] < i) xv[u] = granule_wait(gran + 2 * (size_t)(c[u] - lo), epoch, err);
-#pragma unroll
-            for (int u = 0; u < U; ++u)
-                if (c[u] != i) acc -= a[u] * xv[u];
+        const int p = ck[q] + grp;
+        const bool active = p < ck[q + 1];
+        int i = -1, k0 = 0, len = 0;
+        double acc = 0.0;
+        if (active) {
+            i = rows[p];
+            k0 = rp[i];
+            len = rp[i + 1] - k0;
+            acc = b[i];
         }
-        const double d = deff[i];
-        const double xn = fabs(d) > SMALLFLOAT ? acc / d : x_own(x, i);
-        x[i] = xn;
-        granule_put(gran + 2 * (size_t)(i - lo), epoch, xn);
+        int maxlen = len;
+        for (int off = 32; off > 0; off >>= 1) maxlen = max(maxlen, __shfl_xor(maxlen, off, 64));
+        maxlen = __builtin_amdgcn_readfirstlane(maxlen);
+        for (int base = 0; base < maxlen; base += CAP) {
+            const int m = active ? min(CAP, len - base) : 0;
+            const int nj = m > gl ? (m - gl + G - 1) / G : 0;   // this lane's entries t = gl + G j
+            const int kb = k0 + base;
+            unsigned pend = 0;
+            for (int j0 = 0; j0 < nj; j0 += U) {   // (A)
+                int c[U];
+                double a[U], xv[U];
+#pragma unroll
+                for (int u = 0; u < U; ++u) {
+                    const int t = gl + G * (j0 + u);
+                    c[u] = j0 + u < nj ? ci[kb + t] : i;
+                    a[u] = j0 + u < nj ? v[kb + t] : 0.0;
+                }
+#pragma unroll
+                for (int u = 0; u < U; ++u) {
+                    xv[u] = 0.0;
+                    if (c[u] != i && !(c[u] >= lo && c[u] < i)) xv[u] = x[c[u]];
+                }
+#pragma unroll
+                for (int u = 0; u < U; ++u) {
+                    if (j0 + u >= nj) continue;
+                    const int t = gl + G * (j0 + u);
+                    double val = 0.0;   // the diagonal: subtracting +0.0 is the identity
+                    if (c[u] >= lo && c[u] < i) {
+                        double g = 0.0;
+                        if (granule_get(gran + 2 * (size_t)(c[u] - lo), epoch, g)) val = a[u] * g;
+                        else pend |= 1u << (j0 + u);
+                    } else if (c[u] != i) {
+                        val = a[u] * xv[u];
+                    }
+                    mine[t] = val;
+                }
+            }
+            while (pend) {   // (B)
+                const int j = __builtin_ctz(pend);
+                pend &= pend - 1;
+                const int t = gl + G * j;
+                const int c = ci[kb + t];
+                mine[t] = v[kb + t] * granule_wait(gran + 2 * (size_t)(c - lo), epoch, err);
+            }
+            wave_sync();
+            if (gl == 0 && m > 0) acc = chain_sub_pipe(acc, mine, 0, m);   // (C)
+            wave_sync();
+        }
+        if (active && gl == 0) {
+            const double d = deff[i];
+            const double xn = fabs(d) > SMALLFLOAT ? acc / d : x_own(x, i);
+            x[i] = xn;
+            granule_put(gran + 2 * (size_t)(i - lo), epoch, xn);
+        }
     }
     flow_exit(ctl, epoch);
 }
@@ -291,18 +328,14 @@ int gs_persist_build(PassSchedule &ps, const SSS_MAT &A, int lo, int hi, bool lo
     const int *rp = A.row_ptr, *ci = A.col_idx;
     long long nnz = 0;
     for (int i = lo; i < hi; ++i) nnz += rp[i + 1] - rp[i];
-    const double bytes = 12.0 * (double)nnz + 44.0 * (double)(hi - lo);
     const double avg = (double)nnz / std::max(1, hi - lo);
-    // cost estimates (seconds) per pass; constants measured on MI355X
-    const double t_launch = ps.depth * 5.0e-6 + bytes / 2.0e12;
-    const double t_flow = ps.depth * 2.0e-6 + bytes / 2.5e12;
-    const double t_cu = std::max(bytes / 9.0e10, ps.depth * (0.4e-6 + 0.5 * avg * 3.5e-9));
-    int engine = 0;
-    if (want == "cu") engine = 2;
-    else if (want == "flow") engine = 1;
-    else engine = t_cu <= t_flow ? 2 : 1;
+    // Engine choice.  Measured on MI355X (7-pt 256^3, 2-sweep pre-smoother per level, tools/
+    // gs_level_times.py): flow beats one launch per depth on every level (level 1:
+    // 23 vs 68 ms, level 4: 18 vs 42, level 8: 107 vs 216), the single-CU engine loses to flow
+    // everywhere (one CU streams too slowly and the chain of a long row is the same either way),
+    // so "auto" is flow, and cu only on request.
+    int engine = want == "cu" ? 2 : 1;
     if (engine == 2 && ps.depth > kCuMaxDepth) engine = 1;
-    if (engine == 0 || (want == "auto" && std::min(t_cu, t_flow) >= t_launch)) return 0;
     if (engine == 1) {
         // the flow engine needs every same-class coupling in both directions (see the header)
         bool sym = true;
@@ -338,23 +371,26 @@ int gs_persist_build(PassSchedule &ps, const SSS_MAT &A, int lo, int hi, bool lo
         SSS_HIP(hipMemset(g.ctl, 0, sizeof(unsigned) * kCtlWords));
         return 0;
     }
-    g.wave = long_rows;
+    // lanes per row from the average row length: about 8 entries per lane and round
+    g.G = avg <= 24 ? 4 : avg <= 48 ? 8 : avg <= 96 ? 16 : avg <= 192 ? 32 : 64;
+    if (const char *gg = getenv("SSS_HIP_GS_LANES")) g.G = atoi(gg);
+    if (g.G != 4 && g.G != 8 && g.G != 16 && g.G != 32 && g.G != 64) g.G = 64;
+    (void)long_rows;
     g.gran = dev_alloc<unsigned long long>(2 * (size_t)(hi - lo));
     g.ctl = dev_alloc<unsigned>(kCtlWords);
     if (!g.gran || !g.ctl) return hip_fail(hipErrorOutOfMemory, "hipMalloc(gs flow)", __FILE__, __LINE__);
     SSS_HIP(hipMemset(g.gran, 0, sizeof(unsigned long long) * 2 * (size_t)(hi - lo)));
     SSS_HIP(hipMemset(g.ctl, 0, sizeof(unsigned) * kCtlWords));
-    if (!g.wave) {   // chunks: up to 64 rows of one depth
+    {   // chunks: up to 64 / G rows of one depth
+        const int R = 64 / g.G;
         std::vector<int> ck;
         for (int l = 0; l < ps.depth; ++l)
-            for (int s = ps.h_off[l]; s < ps.h_off[l + 1]; s += 64) ck.push_back(s);
+            for (int s0 = ps.h_off[l]; s0 < ps.h_off[l + 1]; s0 += R) ck.push_back(s0);
         ck.push_back(ps.nrows);
         g.nchunks = (int)ck.size() - 1;
         g.ck = dev_alloc<int>(ck.size());
         if (!g.ck) return hip_fail(hipErrorOutOfMemory, "hipMalloc(gs chunks)", __FILE__, __LINE__);
         SSS_HIP(hipMemcpy(g.ck, ck.data(), sizeof(int) * ck.size(), hipMemcpyHostToDevice));
-    } else {
-        g.nchunks = ps.nrows;
     }
     int cus = 256;
     {
@@ -363,8 +399,12 @@ int gs_persist_build(PassSchedule &ps, const SSS_MAT &A, int lo, int hi, bool lo
         if (hipGetDevice(&dev) == hipSuccess && hipGetDeviceProperties(&prop, dev) == hipSuccess)
             cus = prop.multiProcessorCount;
     }
-    // enough waves to keep every CU streaming, no more than there are tickets
-    const int waves = std::min(g.nchunks, cus * 8);
+    // waves in flight: a few per ticket of one depth (more only spin on rows of later depths, and
+    // their polls load the memory system), capped by the tickets and by 8 per CU
+    const double per_depth = (double)g.nchunks / std::max(1, ps.depth);
+    int waves = (int)std::min<double>(1024.0, std::max(32.0, 4.0 * per_depth));
+    if (const char *w = getenv("SSS_HIP_GS_WAVES")) waves = std::max(1, atoi(w));
+    waves = std::min(waves, std::min(g.nchunks, cus * 8));
     g.grid = std::max(1, (waves + 3) / 4);
     return 0;
 }
@@ -386,12 +426,18 @@ int gs_persist_run(const PassSchedule &ps, const DevCSR &A, const double *b, dou
     if (g.engine == 2) {
         hipLaunchKernelGGL(gs_cu, dim3(1), dim3(64 * kCuWaves), 0, s, ps.nrows, ps.depth, ps.rows, g.h_off, A.rp, A.ci,
                            A.v, b, x, deff, g.ctl + kCtlErr);
-    } else if (g.engine == 1 && g.wave) {
-        hipLaunchKernelGGL(gs_flow_wave, dim3(g.grid), dim3(kBlock), 0, s, ps.nrows, ps.rows, A.rp, A.ci, A.v, b, x,
-                           deff, g.gran, g.lo, g.ctl);
     } else if (g.engine == 1) {
-        hipLaunchKernelGGL(gs_flow_thread, dim3(g.grid), dim3(kBlock), 0, s, g.nchunks, g.ck, ps.rows, A.rp, A.ci, A.v,
-                           b, x, deff, g.gran, g.lo, g.ctl);
+        auto go = [&](auto kern) {
+            hipLaunchKernelGGL(kern, dim3(g.grid), dim3(kBlock), 0, s, g.nchunks, g.ck, ps.rows, A.rp, A.ci, A.v, b, x,
+                               deff, g.gran, g.lo, g.ctl);
+        };
+        switch (g.G) {
+        case 4: go(gs_flow_group<4>); break;
+        case 8: go(gs_flow_group<8>); break;
+        case 16: go(gs_flow_group<16>); break;
+        case 32: go(gs_flow_group<32>); break;
+        default: go(gs_flow_group<64>); break;
+        }
     } else {
         return ERROR_INPUT_PAR;
     }
