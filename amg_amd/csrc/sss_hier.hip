@@ -11,6 +11,8 @@
 // norm is the only per-iteration device->host transfer.
 #include "sss_engine.hpp"
 
+#include <chrono>
+
 #include <cmath>
 
 #include <algorithm>
@@ -270,23 +272,29 @@ sss_hip_hier *sss::hier_create_impl(const SSS_AMG *mg, const sss_hip_opts *o, in
             for (int i = 0; i < n; ++i) inv[l][perm[i]] = i;
         }
 
+    const bool timing = getenv("SSS_HIP_TIMING") != nullptr;   // per-level upload phases on stderr
+    auto now = [] { return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count(); };
     for (int l = 0; l < h->nl; ++l) {
         const SSS_AMG_COMP &C = mg->cg[l];
         auto &L = h->L[l];
         const int n = C.A.num_rows;
         const bool rl = !L.perm.empty();
+        double t_a = now(), t_rel = 0, t_up = 0, t_sm = 0;
         // the coarsest operator only feeds the coarse solver: stored order there
         const int enc = l + 1 < h->nl ? level_encoding(h->opts) : (level_encoding(h->opts) & kEncSortedTiles);
         if (rl) {
             RelabeledCSR B;
             relabel_csr(C.A, L.perm, inv[l], B);
             SSS_MAT Av = B.view(n, C.A.num_cols);
+            t_rel = now();
             if (devcsr_upload(L.A, Av, nF[l], enc)) return fail("upload A");
+            t_up = now();
             std::vector<int> mark(n);
             for (int i = 0; i < n; ++i) mark[i] = C.cfmark.d[L.perm[i]];
             if (smoother_build(L.sm, Av, mark.data(), level_smoother_kind(h->opts, h->level_base + l), &L.A,
                                level_inner(h->opts, h->level_base + l), nullptr, enc))
                 return fail("smoother plan");
+            t_sm = now();
         } else {
             if (devcsr_upload(L.A, C.A, -1, enc)) return fail("upload A");
             if (l < h->nl - 1 && smoother_build(L.sm, C.A, C.cfmark.d, level_smoother_kind(h->opts, h->level_base + l),
@@ -308,6 +316,9 @@ sss_hip_hier *sss::hier_create_impl(const SSS_AMG *mg, const sss_hip_opts *o, in
                 return fail("upload P/R");
             }
         }
+        if (timing)
+            fprintf(stderr, "[sss_hip] upload level %d: relabel %.2f s, A %.2f s, smoother plan %.2f s, P/R %.2f s\n", l,
+                    rl ? t_rel - t_a : 0.0, rl ? t_up - t_rel : 0.0, rl ? t_sm - t_up : 0.0, now() - (rl ? t_sm : t_a));
         L.b = dev_alloc<double>((size_t)n);
         L.x = dev_alloc<double>((size_t)n);
         L.wp = dev_alloc<double>((size_t)n);

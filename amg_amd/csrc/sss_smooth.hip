@@ -22,6 +22,7 @@
 #include "sss_spmv_dev.hpp"
 
 #include <algorithm>
+#include <chrono>
 #include <cstdlib>
 #include <type_traits>
 #include <cmath>
@@ -58,6 +59,9 @@ int smoother_build(SmootherPlan &sp, const SSS_MAT &A, const int *mark, int kind
     int rc;
     const char *tz = getenv("SSS_HIP_TILE_DIAG");   // 0: divisors from the deff stream (tests)
 
+    const bool timing = getenv("SSS_HIP_TIMING") != nullptr;
+    auto now = [] { return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count(); };
+    double t0 = now(), t_sched = 0, t_persist = 0, t_two = 0;
     sp.kind = kind;
     for (int i = 0; i < n; ++i) {
         cls[i] = mark ? (mark[i] == 1 ? 1 : 0) : 0;
@@ -171,6 +175,7 @@ int smoother_build(SmootherPlan &sp, const SSS_MAT &A, const int *mark, int kind
         }
     }
     if ((rc = upload_ints(&sp.cls, cls))) return rc;
+    t_sched = now();
     // exact GS passes with intra-class chains: one launch per pass where the class is contiguous
     if (kind == SSS_HIP_SMOOTH_EXACT && !gcls && A.num_cols == n) {
         for (int c = 0; c < 2; ++c) {
@@ -187,6 +192,7 @@ int smoother_build(SmootherPlan &sp, const SSS_MAT &A, const int *mark, int kind
             if (contiguous && (rc = gs_persist_build(ps, A, lo, hi, sp.long_rows))) return rc;
         }
     }
+    t_persist = now();
     if (kind == SSS_HIP_SMOOTH_JACOBI && inner > 0 && sp.pass[0].range == (sp.pass[0].nrows > 0) &&
         sp.pass[1].range == (sp.pass[1].nrows > 0)) {
         sp.inner = inner;
@@ -234,6 +240,7 @@ int smoother_build(SmootherPlan &sp, const SSS_MAT &A, const int *mark, int kind
             if (!ps.ts_P) return hip_fail(hipErrorOutOfMemory, "hipMalloc(P)", __FILE__, __LINE__);
         }
     }
+    t_two = now();
     if (sp.pass[0].range || sp.pass[1].range)
         if ((rc = upload_ints(&sp.diag_pos, diag_pos))) return rc;
     const char *nc = getenv("SSS_HIP_NOCOPY");   // 0: C/F-Jacobi through per-pass copies (tests)
@@ -279,6 +286,9 @@ int smoother_build(SmootherPlan &sp, const SSS_MAT &A, const int *mark, int kind
         for (int q = 0; q < dA->split_blk && f_short; ++q) f_short = rp[blk[q + 1]] - rp[blk[q]] <= kTileEntries;
         sp.pend_ok = short_blocks && f_short && sp.f_overwritten && !(pz && *pz == '0');
     }
+    if (timing)
+        fprintf(stderr, "[sss_hip]   smoother plan n=%d: schedule %.2f s, one-launch GS %.2f s, two-stage %.2f s, rest %.2f s\n",
+                n, t_sched - t0, t_persist - t_sched, t_two - t_persist, now() - t_two);
     if (kind == SSS_HIP_SMOOTH_JACOBI) {
         if ((rc = upload_doubles(&sp.d_first, last_diag))) return rc;   // Jacobi: row's own diagonal
         sp.d_later = sp.d_first;
