@@ -32,6 +32,7 @@
 #include "sss_engine.hpp"
 #include "sss_spmv_dev.hpp"
 
+#include <algorithm>
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
@@ -339,15 +340,29 @@ int gs_persist_build(PassSchedule &ps, const SSS_MAT &A, int lo, int hi, bool lo
     if (engine == 1) {
         // the flow engine needs every same-class coupling in both directions (see the header)
         bool sym = true;
+        // each row's same-class columns, sorted, then every coupling looked up in its partner row
+        const int m = hi - lo;
+        std::vector<long long> off((size_t)m + 1, 0);
+        for (int q = 0; q < m; ++q) {
+            long long c = 0;
+            for (int k = rp[lo + q]; k < rp[lo + q + 1]; ++k) c += (ci[k] >= lo && ci[k] < hi && ci[k] != lo + q);
+            off[q + 1] = off[q] + c;
+        }
+        std::vector<int> cols((size_t)off[m]);
+        parallel_chunks(m, 4096, [&](int a, int e) {
+            for (int q = a; q < e; ++q) {
+                long long o = off[q];
+                for (int k = rp[lo + q]; k < rp[lo + q + 1]; ++k)
+                    if (ci[k] >= lo && ci[k] < hi && ci[k] != lo + q) cols[(size_t)o++] = ci[k];
+                std::sort(cols.begin() + off[q], cols.begin() + off[q + 1]);
+            }
+        });
         std::vector<char> bad(1, 0);
-        parallel_chunks(hi - lo, 4096, [&](int a, int e) {
-            for (int i = lo + a; i < lo + e && !bad[0]; ++i)
-                for (int k = rp[i]; k < rp[i + 1]; ++k) {
-                    const int j = ci[k];
-                    if (j == i || j < lo || j >= hi) continue;
-                    bool found = false;
-                    for (int t = rp[j]; t < rp[j + 1] && !found; ++t) found = ci[t] == i;
-                    if (!found) {
+        parallel_chunks(m, 4096, [&](int a, int e) {
+            for (int q = a; q < e && !bad[0]; ++q)
+                for (long long t = off[q]; t < off[q + 1]; ++t) {
+                    const int j = cols[(size_t)t] - lo;
+                    if (!std::binary_search(cols.begin() + off[j], cols.begin() + off[j + 1], lo + q)) {
                         bad[0] = 1;
                         break;
                     }

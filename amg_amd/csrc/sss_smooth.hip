@@ -63,19 +63,33 @@ int smoother_build(SmootherPlan &sp, const SSS_MAT &A, const int *mark, int kind
     auto now = [] { return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count(); };
     double t0 = now(), t_sched = 0, t_persist = 0, t_two = 0;
     sp.kind = kind;
-    for (int i = 0; i < n; ++i) {
-        cls[i] = mark ? (mark[i] == 1 ? 1 : 0) : 0;
-        for (int k = rp[i]; k < rp[i + 1]; ++k)
-            if (ci[k] == i) {
-                last_diag[i] = v[k];
-                if (has_diag[i]) single_diag = false;
-                has_diag[i] = 1;
-                diag_pos[i] = k;
+    {   // classes, diagonals (row-parallel)
+        std::atomic<bool> all{true}, single{true};
+        parallel_chunks(n, 1 << 16, [&](int lo, int hi) {
+            bool a = true, s1 = true;
+            for (int i = lo; i < hi; ++i) {
+                cls[i] = mark ? (mark[i] == 1 ? 1 : 0) : 0;
+                for (int k = rp[i]; k < rp[i + 1]; ++k)
+                    if (ci[k] == i) {
+                        last_diag[i] = v[k];
+                        if (has_diag[i]) s1 = false;
+                        has_diag[i] = 1;
+                        diag_pos[i] = k;
+                    }
+                a = a && has_diag[i];
             }
-        all_diag = all_diag && has_diag[i];
+            if (!a) all = false;
+            if (!s1) single = false;
+        });
+        all_diag = all;
+        single_diag = single;
     }
-    // stale-d resolution: simulate the divisor register over two sweeps of (F pass, C pass)
-    {
+    // stale-d resolution: simulate the divisor register over two sweeps of (F pass, C pass); with
+    // a diagonal in every row it is each row's own last diagonal entry
+    if (all_diag) {
+        d_first = last_diag;
+        d_later = last_diag;
+    } else {
         double d = 0.0;
         for (int sweep = 0; sweep < 2; ++sweep)
             for (int c = 0; c < 2; ++c)
@@ -89,16 +103,29 @@ int smoother_build(SmootherPlan &sp, const SSS_MAT &A, const int *mark, int kind
     long long nnz_total = rp[n];
     // exact GS depth launches hold few rows each: a wave per row pays from short lengths on
     sp.long_rows = n > 0 && nnz_total >= (long long)std::min(32, wave_row_min()) * n;
-    for (int i = 0; i < n; ++i) {
-        int dep = pushed[i];
-        for (int k = rp[i]; k < rp[i + 1]; ++k) {
-            const int j = ci[k];
-            if (j < i && cls[j] == cls[i]) dep = std::max(dep, depth[j] + 1);
-        }
-        depth[i] = dep;
-        for (int k = rp[i]; k < rp[i + 1]; ++k) {
-            const int j = ci[k];
-            if (j > i && j < n && cls[j] == cls[i]) pushed[j] = std::max(pushed[j], dep + 1);
+    std::atomic<bool> coupled{false};   // any same-class off-diagonal entry at all?
+    parallel_chunks(n, 1 << 16, [&](int lo, int hi) {
+        for (int i = lo; i < hi && !coupled; ++i)
+            for (int k = rp[i]; k < rp[i + 1]; ++k) {
+                const int j = ci[k];
+                if (j != i && j < n && cls[j] == cls[i]) {
+                    coupled = true;
+                    break;
+                }
+            }
+    });
+    if (coupled) {   // red-black levels (no coupling) keep depth 0 everywhere
+        for (int i = 0; i < n; ++i) {
+            int dep = pushed[i];
+            for (int k = rp[i]; k < rp[i + 1]; ++k) {
+                const int j = ci[k];
+                if (j < i && cls[j] == cls[i]) dep = std::max(dep, depth[j] + 1);
+            }
+            depth[i] = dep;
+            for (int k = rp[i]; k < rp[i + 1]; ++k) {
+                const int j = ci[k];
+                if (j > i && j < n && cls[j] == cls[i]) pushed[j] = std::max(pushed[j], dep + 1);
+            }
         }
     }
     for (int c = 0; c < 2; ++c) {
@@ -199,28 +226,47 @@ int smoother_build(SmootherPlan &sp, const SSS_MAT &A, const int *mark, int kind
         for (auto &ps : sp.pass) {
             if (ps.nrows == 0) continue;
             const int m = ps.hi - ps.lo;
-            std::vector<int> nrp(1, 0), nci, lrp(1, 0), lci, split(m);
-            std::vector<double> nv, lv;
-            for (int i = ps.lo; i < ps.hi; ++i) {
-                // L_i: same class, j < i in the global order -- own rows of the pass below i, or
-                // (distributed levels) ghost columns of this class owned by lower ranks
-                const int c = (int)(&ps - sp.pass);
-                auto lower = [&](int j) { return j < n ? (j >= ps.lo && j < i) : (gcls && gcls[j - n] == c); };
-                for (int k = rp[i]; k < rp[i + 1]; ++k) {   // N_i: off-diagonal, not same-class lower
-                    const int j = ci[k];
-                    if (j != i && !lower(j)) nci.push_back(j), nv.push_back(v[k]);
+            const int c = (int)(&ps - sp.pass);
+            // L_i: same class, j < i in the global order -- own rows of the pass below i, or
+            // (distributed levels) ghost columns of this class owned by lower ranks
+            auto lower = [&](int i, int j) { return j < n ? (j >= ps.lo && j < i) : (gcls && gcls[j - n] == c); };
+            // two row-parallel passes: count, then fill at the prefix offsets (same order as a
+            // sequential build: N_i entries in stored order, then L_i entries in stored order)
+            std::vector<int> nrp((size_t)m + 1, 0), lrp((size_t)m + 1, 0), split(m);
+            parallel_chunks(m, 1 << 14, [&](int a, int e) {
+                for (int q = a; q < e; ++q) {
+                    const int i = ps.lo + q;
+                    int nn = 0, nl = 0;
+                    for (int k = rp[i]; k < rp[i + 1]; ++k) {
+                        const int j = ci[k];
+                        if (lower(i, j)) ++nl;
+                        else if (j != i) ++nn;
+                    }
+                    nrp[q + 1] = nn + nl;
+                    lrp[q + 1] = nl;
                 }
-                split[i - ps.lo] = (int)nci.size();
-                for (int k = rp[i]; k < rp[i + 1]; ++k) {   // L_i
-                    const int j = ci[k];
-                    if (lower(j)) {
-                        nci.push_back(j), nv.push_back(v[k]);
-                        lci.push_back(j), lv.push_back(v[k]);
+            });
+            for (int q = 0; q < m; ++q) nrp[q + 1] += nrp[q], lrp[q + 1] += lrp[q];
+            std::vector<int> nci((size_t)nrp[m]), lci((size_t)lrp[m]);
+            std::vector<double> nv((size_t)nrp[m]), lv((size_t)lrp[m]);
+            parallel_chunks(m, 1 << 14, [&](int a, int e) {
+                for (int q = a; q < e; ++q) {
+                    const int i = ps.lo + q;
+                    int o = nrp[q], ol = lrp[q];
+                    for (int k = rp[i]; k < rp[i + 1]; ++k) {   // N_i: off-diagonal, not same-class lower
+                        const int j = ci[k];
+                        if (j != i && !lower(i, j)) nci[o] = j, nv[o] = v[k], ++o;
+                    }
+                    split[q] = o;
+                    for (int k = rp[i]; k < rp[i + 1]; ++k) {   // L_i
+                        const int j = ci[k];
+                        if (lower(i, j)) {
+                            nci[o] = j, nv[o] = v[k], ++o;
+                            lci[ol] = j, lv[ol] = v[k], ++ol;
+                        }
                     }
                 }
-                nrp.push_back((int)nci.size());
-                lrp.push_back((int)lci.size());
-            }
+            });
             auto mk = [&](std::vector<int> &r, std::vector<int> &c, std::vector<double> &w) {
                 SSS_MAT M;
                 M.num_rows = m;
@@ -257,8 +303,12 @@ int smoother_build(SmootherPlan &sp, const SSS_MAT &A, const int *mark, int kind
     sp.own_diag = all_diag && single_diag && !(tz && *tz == '0');
     {
         const char *zz = getenv("SSS_HIP_ZERO_FIRST");   // 0: run the first pass on a zero x in full (tests)
-        bool fin = !(zz && *zz == '0');
-        for (int k = 0; fin && k < rp[n]; ++k) fin = std::isfinite(v[k]);
+        std::atomic<bool> fin{!(zz && *zz == '0')};
+        if (fin)
+            parallel_chunks(n, 1 << 16, [&](int lo, int hi) {
+                for (int k = rp[lo]; k < rp[hi] && fin; ++k)
+                    if (!std::isfinite(v[k])) fin = false;
+            });
         sp.finite = fin;
     }
     {

@@ -102,13 +102,16 @@ static bool build_sorted_tiles(const SSS_MAT &h, const std::vector<int> &blk, st
     pb.resize((size_t)std::max(nb, 1));
     std::atomic<int> ok{1};
     parallel_chunks(nb, 512, [&](int qlo, int qhi) {
-        std::vector<int> idx, cols;
+        std::vector<int> idx, cols, rowof;
         for (int q = qlo; q < qhi; ++q) {
             const int a0 = rp[blk[q]], e0 = rp[blk[q + 1]];
             if (a0 == e0) {
                 pb[q] = make_int2(0, 0);
                 continue;
             }
+            rowof.resize((size_t)(e0 - a0));   // entry position -> its row (one pass over the block)
+            for (int r = blk[q]; r < blk[q + 1]; ++r)
+                for (int k = rp[r]; k < rp[r + 1]; ++k) rowof[(size_t)(k - a0)] = r;
             cols.assign(ci + a0, ci + e0);
             std::sort(cols.begin(), cols.end());
             size_t gap = 0;   // cut after cols[gap]
@@ -129,8 +132,7 @@ static bool build_sorted_tiles(const SSS_MAT &h, const std::vector<int> &blk, st
                 std::stable_sort(idx.begin(), idx.end(), [&](int p, int r) { return ci[p] < ci[r]; });
                 for (int t = 0; t < e - a; ++t) {
                     const int k = idx[t], c = ci[k];
-                    int r = r0;   // the entry's row
-                    while (rp[r + 1] <= k) ++r;
+                    const int r = rowof[(size_t)(k - a0)];   // the entry's row
                     const unsigned cl = (cols.size() > 1 && c >= cut) ? 1u : 0u;
                     const unsigned off = c == r ? kTileDiagMark + (unsigned)(r - r0) : (unsigned)(c - (cl ? b1 : b0));
                     pk[(size_t)a + t] = (cl << 31) | (off << kTileShift) | (unsigned)(k - a);
