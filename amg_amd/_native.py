@@ -114,7 +114,8 @@ ABI_SYMBOLS = [
     "sss_hip_dist_upload_vec",
     "sss_hip_dist_download_vec", "sss_hip_dist_cycle", "sss_hip_dist_residual_norm", "sss_hip_dist_sync",
     "sss_hip_dist_time_level0_spmv",
-    "sss_part_plan_create", "sss_part_plan_destroy", "sss_part_plan_nagg", "sss_part_plan_level",
+    "sss_part_plan_create", "sss_part_plan_destroy", "sss_part_save", "sss_part_plan_load",
+    "sss_hip_dist_create_from_files", "sss_hip_dist_level_size", "sss_part_plan_nagg", "sss_part_plan_level",
     "sss_part_plan_matrix", "sss_part_plan_ids", "sss_part_plan_halo",
 ]
 
@@ -183,6 +184,7 @@ def _declare(lib):
         "sss_hip_dist_create": (C.c_void_p, [P(SSS_AMG), P(SSS_HIP_OPTS), C.c_void_p, C.c_int]),
         "sss_hip_dist_destroy": (None, [C.c_void_p]),
         "sss_hip_dist_info": (C.c_int, [C.c_void_p, _int_p, _int_p, _int_p, _int_p]),
+        "sss_hip_dist_level_size": (C.c_int, [C.c_void_p, C.c_int, _int_p, _int_p, P(C.c_longlong)]),
         "sss_hip_dist_level_flags": (C.c_int, [C.c_void_p, C.c_int]),
         "sss_hip_dist_upload_vec": (C.c_int, [C.c_void_p, C.c_int, _dbl_p, C.c_int]),
         "sss_hip_dist_download_vec": (C.c_int, [C.c_void_p, C.c_int, _dbl_p, C.c_int]),
@@ -191,6 +193,9 @@ def _declare(lib):
         "sss_hip_dist_sync": (C.c_int, [C.c_void_p]),
         "sss_hip_dist_time_level0_spmv": (C.c_int, [C.c_void_p, C.c_int, _dbl_p]),
         "sss_part_plan_create": (C.c_void_p, [P(SSS_AMG), C.c_int, C.c_int, C.c_int]),
+        "sss_part_save": (C.c_int, [P(SSS_AMG), C.c_int, C.c_int, C.c_char_p]),
+        "sss_part_plan_load": (C.c_void_p, [C.c_char_p]),
+        "sss_hip_dist_create_from_files": (C.c_void_p, [C.c_char_p, P(SSS_HIP_OPTS), C.c_void_p]),
         "sss_part_plan_destroy": (None, [C.c_void_p]),
         "sss_part_plan_nagg": (C.c_int, [C.c_void_p]),
         "sss_part_plan_level": (C.c_int, [C.c_void_p, C.c_int, _int_p, _int_p, _int_p, _int_p]),
@@ -410,15 +415,34 @@ def device_count() -> int:
 
 
 # ---------------------------------------------------------------- row-partitioned multi-GPU
-class PartPlan:
-    """Host-only view of one rank's partition of a hierarchy (sss_part_plan_*)."""
+def part_save(H: "Hierarchy", nranks: int, prefix, agg_rows: int = 0) -> None:
+    """Partition set of H for nranks ranks (sss_part_save): prefix.r<rank> files + prefix.tail."""
+    rc = lib().sss_part_save(C.byref(H.mg), nranks, agg_rows, str(prefix).encode())
+    if rc != 0:
+        raise OSError(f"sss_part_save({prefix}) failed ({rc})")
 
-    def __init__(self, H: "Hierarchy", nranks: int, rank: int, agg_rows: int = 0):
+
+class PartPlan:
+    """Host-only view of one rank's partition of a hierarchy (sss_part_plan_*), built from the
+    global hierarchy, or read back from its partition file (PartPlan.load)."""
+
+    def __init__(self, H: "Hierarchy | None", nranks: int = 1, rank: int = 0, agg_rows: int = 0):
         self.H = H
-        self.p = lib().sss_part_plan_create(C.byref(H.mg), nranks, rank, agg_rows)
-        if not self.p:
-            raise RuntimeError("sss_part_plan_create failed")
-        self.nagg = lib().sss_part_plan_nagg(self.p)
+        self.p = None
+        if H is not None:
+            self.p = lib().sss_part_plan_create(C.byref(H.mg), nranks, rank, agg_rows)
+            if not self.p:
+                raise RuntimeError("sss_part_plan_create failed")
+            self.nagg = lib().sss_part_plan_nagg(self.p)
+
+    @classmethod
+    def load(cls, path) -> "PartPlan":
+        pp = cls(None)
+        pp.p = lib().sss_part_plan_load(str(path).encode())
+        if not pp.p:
+            raise OSError(f"sss_part_plan_load({path}) failed")
+        pp.nagg = lib().sss_part_plan_nagg(pp.p)
+        return pp
 
     def level(self, l: int):
         lo, hi, m, g = C.c_int(), C.c_int(), C.c_int(), C.c_int()
@@ -554,11 +578,13 @@ class Comm:
 
 
 class DistHierarchy:
-    """Row-partitioned device hierarchy (sss_hip_dist_*): this rank's rows of every level."""
+    """Row-partitioned device hierarchy (sss_hip_dist_*): this rank's rows of every level, built
+    from the global hierarchy H, or (H None, parts = a partition-set prefix) from this rank's
+    partition file and the tail file only."""
 
-    def __init__(self, H: "Hierarchy", comm: Comm, smoother: str = "hybrid", coarse: str = "direct",
+    def __init__(self, H: "Hierarchy | None", comm: Comm, smoother: str = "hybrid", coarse: str = "direct",
                  device: int = -1, agg_rows: int = 0, inner: int | None = None, inner_from: int | None = None,
-                 sorted_tiles: int | None = None, sum_order: int | None = None):
+                 sorted_tiles: int | None = None, sum_order: int | None = None, parts=None):
         o = SSS_HIP_OPTS()
         lib().sss_hip_opts_default(C.byref(o))
         o.smoother, o.coarse, o.device = SMOOTH[smoother], COARSE[coarse], device
@@ -571,12 +597,21 @@ class DistHierarchy:
         if inner_from is not None:
             o.inner_from = inner_from
         self.H, self.comm = H, comm
-        self.d = lib().sss_hip_dist_create(C.byref(H.mg), C.byref(o), comm.c, agg_rows)
+        if H is None:
+            self.d = lib().sss_hip_dist_create_from_files(str(parts).encode(), C.byref(o), comm.c)
+        else:
+            self.d = lib().sss_hip_dist_create(C.byref(H.mg), C.byref(o), comm.c, agg_rows)
         if not self.d:
             raise RuntimeError("sss_hip_dist_create failed")
         lo, hi, nagg, g = C.c_int(), C.c_int(), C.c_int(), C.c_int()
         lib().sss_hip_dist_info(self.d, C.byref(lo), C.byref(hi), C.byref(nagg), C.byref(g))
         self.lo, self.hi, self.nagg, self.nghost0 = lo.value, hi.value, nagg.value, g.value
+
+    def level_size(self, l: int):
+        """(own rows, ghosts, nonzeros) of this rank's partitioned level l"""
+        m, g, z = C.c_int(), C.c_int(), C.c_longlong()
+        self._check(lib().sss_hip_dist_level_size(self.d, l, C.byref(m), C.byref(g), C.byref(z)), "level size")
+        return m.value, g.value, z.value
 
     def level_flags(self, l: int) -> dict:
         """Exact eliminations in force on partitioned level l (agreed over the ranks)."""

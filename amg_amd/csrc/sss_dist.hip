@@ -95,6 +95,8 @@ struct sss_hip_dist {
     double *partial = nullptr, *d_norm = nullptr, *h_norm = nullptr;
     std::vector<double> stage;
     bool resid_c_ready = false;   // the last cycle's final C pass left r_C and its partials (level 0)
+    SSS_AMG tail_host{};          // the tail levels read from a partition set (file-built engines)
+    bool own_tail_host = false;
 };
 
 namespace {
@@ -260,6 +262,7 @@ void release(sss_hip_dist *d)
         dev_free(L.halo.d_sbuf);
     }
     if (d->tail) sss_hip_hier_destroy(d->tail);
+    if (d->own_tail_host) SSS_amg_data_destroy(&d->tail_host);
     dev_free(d->d_cown);
     dev_free(d->d_call);
     dev_free(d->d_tail_perm);
@@ -323,14 +326,11 @@ extern "C" void sss_hip_comm_destroy(sss_hip_comm *c)
     delete c;
 }
 
-extern "C" sss_hip_dist *sss_hip_dist_create(const SSS_AMG *mg, const sss_hip_opts *o, sss_hip_comm *c, int agg_rows)
+// The engine of one rank from its partition `plan` and the replicated tail hierarchy `tailmg`
+// (its cg[0] is global level plan.nagg).  Takes ownership of d.
+static sss_hip_dist *dist_create_impl(sss_hip_dist *d, PartPlan &plan, const SSS_AMG *tailmg)
 {
-    if (!mg || !c || sss_hip_device_count() <= 0) return nullptr;
-    auto *d = new sss_hip_dist();
-    d->comm = c;
-    d->pars = mg->pars;
-    if (o) d->opts = *o;
-    else sss_hip_opts_default(&d->opts);
+    sss_hip_comm *c = d->comm;
     auto fail = [&](const char *what) {
         fprintf(stderr, "### ERROR: sss_hip_dist_create (rank %d): %s\n", c->rank, what);
         release(d);
@@ -339,25 +339,18 @@ extern "C" sss_hip_dist *sss_hip_dist_create(const SSS_AMG *mg, const sss_hip_op
     if (d->pars.cycle_type > 1) return fail("only V-cycles are distributed");
     if (d->opts.device >= 0 && hipSetDevice(d->opts.device) != hipSuccess) return fail("hipSetDevice");
     if (hipStreamCreateWithFlags(&d->stream, hipStreamNonBlocking) != hipSuccess) return fail("stream");
-    if (agg_rows <= 0) {
-        const char *e = getenv("SSS_HIP_AGG_ROWS");
-        agg_rows = (e && *e) ? atoi(e) : 20000;
-    }
-    PartPlan plan;
-    if (part_plan_build(plan, mg, c->nranks, c->rank, agg_rows)) return fail("partition");
+    if (plan.nranks != c->nranks || plan.rank != c->rank) return fail("partition made for another rank layout");
     d->nagg = plan.nagg;
     if (d->nagg < 1) return fail("hierarchy too shallow to partition");
+    if (tailmg->num_levels != plan.nl - plan.nagg) return fail("tail levels do not match the partition");
 
     // replicated tail first: its level-0 relabeling fixes the column ids of P_{nagg-1}
-    SSS_AMG sub = *mg;
-    sub.cg = mg->cg + d->nagg;
-    sub.num_levels = mg->num_levels - d->nagg;
     sss_hip_opts to = d->opts;
     to.use_graph = 0;
-    d->tail = hier_create_impl(&sub, &to, d->nagg, d->stream);
+    d->tail = hier_create_impl(tailmg, &to, d->nagg, d->stream);
     if (!d->tail) return fail("replicated coarse levels");
     const std::vector<int> &tperm = hier_perm(d->tail, 0);
-    const int nt = mg->cg[d->nagg].A.num_rows;
+    const int nt = tailmg->cg[0].A.num_rows;
     std::vector<int> tinv;
     if (!tperm.empty()) {
         tinv.resize(nt);
@@ -431,6 +424,57 @@ extern "C" sss_hip_dist *sss_hip_dist_create(const SSS_AMG *mg, const sss_hip_op
     return d;
 }
 
+static sss_hip_dist *dist_new(const SSS_AMG_PARS &pars, const sss_hip_opts *o, sss_hip_comm *c)
+{
+    auto *d = new sss_hip_dist();
+    d->comm = c;
+    d->pars = pars;
+    if (o) d->opts = *o;
+    else sss_hip_opts_default(&d->opts);
+    return d;
+}
+
+static int agg_rows_or_default(int agg_rows)
+{
+    if (agg_rows > 0) return agg_rows;
+    const char *e = getenv("SSS_HIP_AGG_ROWS");
+    return (e && *e) ? atoi(e) : 20000;
+}
+
+extern "C" sss_hip_dist *sss_hip_dist_create(const SSS_AMG *mg, const sss_hip_opts *o, sss_hip_comm *c, int agg_rows)
+{
+    if (!mg || !c || sss_hip_device_count() <= 0) return nullptr;
+    PartPlan plan;
+    if (part_plan_build(plan, mg, c->nranks, c->rank, agg_rows_or_default(agg_rows))) {
+        fprintf(stderr, "### ERROR: sss_hip_dist_create (rank %d): partition\n", c->rank);
+        return nullptr;
+    }
+    SSS_AMG sub = *mg;
+    sub.cg = mg->cg + plan.nagg;
+    sub.num_levels = mg->num_levels - plan.nagg;
+    return dist_create_impl(dist_new(mg->pars, o, c), plan, &sub);
+}
+
+extern "C" sss_hip_dist *sss_hip_dist_create_from_files(const char *prefix, const sss_hip_opts *o, sss_hip_comm *c)
+{
+    if (!prefix || !c || sss_hip_device_count() <= 0) return nullptr;
+    PartPlan plan;
+    SSS_AMG_PARS pars;
+    const std::string part = part_file_name(prefix, c->rank), tail = part_tail_name(prefix);
+    if (part_plan_read(plan, pars, part.c_str())) {
+        fprintf(stderr, "### ERROR: sss_hip_dist_create_from_files (rank %d): cannot read %s\n", c->rank, part.c_str());
+        return nullptr;
+    }
+    sss_hip_dist *d = dist_new(pars, o, c);
+    if (SSS_amg_load(&d->tail_host, tail.c_str())) {
+        fprintf(stderr, "### ERROR: sss_hip_dist_create_from_files (rank %d): cannot read %s\n", c->rank, tail.c_str());
+        release(d);
+        return nullptr;
+    }
+    d->own_tail_host = true;
+    return dist_create_impl(d, plan, &d->tail_host);
+}
+
 extern "C" void sss_hip_dist_destroy(sss_hip_dist *d) { release(d); }
 
 extern "C" int sss_hip_dist_info(sss_hip_dist *d, int *lo, int *hi, int *nagg, int *nghost0)
@@ -440,6 +484,15 @@ extern "C" int sss_hip_dist_info(sss_hip_dist *d, int *lo, int *hi, int *nagg, i
     *hi = d->L[0].hi;
     *nagg = d->nagg;
     *nghost0 = d->L[0].g;
+    return 0;
+}
+
+extern "C" int sss_hip_dist_level_size(sss_hip_dist *d, int l, int *m, int *g, long long *nnz)
+{
+    if (!d || l < 0 || l >= d->nagg) return ERROR_INPUT_PAR;
+    *m = d->L[l].m;
+    *g = d->L[l].g;
+    *nnz = d->L[l].A.nnz;
     return 0;
 }
 

@@ -67,6 +67,9 @@ void parallel_chunks(int n, int grain, Fn fn)
     for (auto &t : th) t.join();
 }
 
+// Host -> device copy through pinned staging buffers (sss_spmv.hip); returns 0 or an error code.
+int h2d(void *dst, const void *src, size_t bytes);
+
 // CSR matrix resident in HBM, plus its CSR-adaptive row blocking for SpMV.
 struct DevCSR {
     int n = 0, ncols = 0, nnz = 0;

@@ -3,11 +3,17 @@
 #include "sss_part.hpp"
 
 #include <algorithm>
+#include <cstdint>
+#include <cstdio>
+#include <cstring>
+#include <string>
 #include <thread>
 
 #include "../../include/sss_hip.h"
 
 namespace sss {
+
+constexpr int kMaxPartLevels = max_AMG_LVL;
 
 namespace {
 
@@ -189,9 +195,187 @@ int part_plan_build(PartPlan &p, const SSS_AMG *mg, int nranks, int rank, int ag
 
 }  // namespace sss
 
+namespace sss {
+
+// ---- partition files -------------------------------------------------------------------------
+// Layout (little-endian, native LP64):  "SSSPART1"  int32 version=1  int32 sizeof(SSS_AMG_PARS)
+//   SSS_AMG_PARS  int32 nranks, rank, nl, nagg;  nagg+1 cut vectors;  per level l < nagg:
+//   int32 lo, hi, m, g, nF;  int vectors perm, ghosts, mark, gcls, gclass;  matrices A, P, R;
+//   int vectors sdst, scount, sidx, rsrc, rcount.   vector := int64 count + data;
+//   matrix := int32 rows, cols + int vectors rp, ci + double vector v.
+namespace {
+const char kPartMagic[8] = {'S', 'S', 'S', 'P', 'A', 'R', 'T', '1'};
+
+struct Out {
+    FILE *f;
+    bool bad = false;
+    void raw(const void *p, size_t n)
+    {
+        if (!bad && n && fwrite(p, 1, n, f) != n) bad = true;
+    }
+    void i32(int v)
+    {
+        const int32_t x = v;
+        raw(&x, sizeof(x));
+    }
+    template <class T>
+    void vec(const std::vector<T> &v)
+    {
+        const int64_t n = (int64_t)v.size();
+        raw(&n, sizeof(n));
+        raw(v.data(), sizeof(T) * v.size());
+    }
+    void mat(const HostMat &m)
+    {
+        i32(m.rows);
+        i32(m.cols);
+        vec(m.rp);
+        vec(m.ci);
+        vec(m.v);
+    }
+};
+struct In {
+    FILE *f;
+    bool bad = false;
+    void raw(void *p, size_t n)
+    {
+        if (!bad && n && fread(p, 1, n, f) != n) bad = true;
+    }
+    int i32()
+    {
+        int32_t x = 0;
+        raw(&x, sizeof(x));
+        return x;
+    }
+    template <class T>
+    void vec(std::vector<T> &v)
+    {
+        int64_t n = 0;
+        raw(&n, sizeof(n));
+        if (bad || n < 0 || n > ((int64_t)1 << 40)) {
+            bad = true;
+            return;
+        }
+        v.resize((size_t)n);
+        raw(v.data(), sizeof(T) * (size_t)n);
+    }
+    void mat(HostMat &m)
+    {
+        m.rows = i32();
+        m.cols = i32();
+        vec(m.rp);
+        vec(m.ci);
+        vec(m.v);
+        if (!bad && (m.rp.size() != (size_t)m.rows + 1 || m.ci.size() != m.v.size() ||
+                     (size_t)m.rp.back() != m.ci.size()))
+            bad = true;
+    }
+};
+}  // namespace
+
+int part_plan_write(const PartPlan &p, const SSS_AMG_PARS &pars, const char *path)
+{
+    FILE *f = fopen(path, "wb");
+    if (!f) return ERROR_OPEN_FILE;
+    Out o{f};
+    o.raw(kPartMagic, sizeof(kPartMagic));
+    o.i32(1);
+    o.i32((int)sizeof(SSS_AMG_PARS));
+    o.raw(&pars, sizeof(pars));
+    o.i32(p.nranks);
+    o.i32(p.rank);
+    o.i32(p.nl);
+    o.i32(p.nagg);
+    for (const auto &c : p.cut) o.vec(c);
+    for (const auto &L : p.L) {
+        o.i32(L.lo), o.i32(L.hi), o.i32(L.m), o.i32(L.g), o.i32(L.nF);
+        o.vec(L.perm), o.vec(L.ghosts), o.vec(L.mark), o.vec(L.gcls), o.vec(L.gclass);
+        o.mat(L.A), o.mat(L.P), o.mat(L.R);
+        o.vec(L.sdst), o.vec(L.scount), o.vec(L.sidx), o.vec(L.rsrc), o.vec(L.rcount);
+    }
+    const bool bad = o.bad;
+    return (fclose(f) != 0 || bad) ? ERROR_OPEN_FILE : 0;
+}
+
+int part_plan_read(PartPlan &p, SSS_AMG_PARS &pars, const char *path)
+{
+    FILE *f = fopen(path, "rb");
+    if (!f) return ERROR_OPEN_FILE;
+    In in{f};
+    char magic[8];
+    in.raw(magic, sizeof(magic));
+    if (in.bad || memcmp(magic, kPartMagic, sizeof(magic)) || in.i32() != 1 || in.i32() != (int)sizeof(SSS_AMG_PARS)) {
+        fclose(f);
+        return ERROR_WRONG_FILE;
+    }
+    in.raw(&pars, sizeof(pars));
+    p = PartPlan();
+    p.nranks = in.i32();
+    p.rank = in.i32();
+    p.nl = in.i32();
+    p.nagg = in.i32();
+    if (in.bad || p.nranks < 1 || p.rank < 0 || p.rank >= p.nranks || p.nagg < 1 || p.nagg >= p.nl ||
+        p.nl > kMaxPartLevels) {
+        fclose(f);
+        return ERROR_WRONG_FILE;
+    }
+    p.cut.resize((size_t)p.nagg + 1);
+    for (auto &c : p.cut) {
+        in.vec(c);
+        if (c.size() != (size_t)p.nranks + 1) in.bad = true;
+    }
+    p.L.resize((size_t)p.nagg);
+    for (auto &L : p.L) {
+        L.lo = in.i32(), L.hi = in.i32(), L.m = in.i32(), L.g = in.i32(), L.nF = in.i32();
+        in.vec(L.perm), in.vec(L.ghosts), in.vec(L.mark), in.vec(L.gcls), in.vec(L.gclass);
+        in.mat(L.A), in.mat(L.P), in.mat(L.R);
+        in.vec(L.sdst), in.vec(L.scount), in.vec(L.sidx), in.vec(L.rsrc), in.vec(L.rcount);
+        if (!in.bad && (L.perm.size() != (size_t)L.m || L.ghosts.size() != (size_t)L.g || L.mark.size() != (size_t)L.m))
+            in.bad = true;
+    }
+    const bool bad = in.bad;
+    fclose(f);
+    return bad ? ERROR_WRONG_FILE : 0;
+}
+
+std::string part_file_name(const char *prefix, int rank) { return std::string(prefix) + ".r" + std::to_string(rank); }
+std::string part_tail_name(const char *prefix) { return std::string(prefix) + ".tail"; }
+
+}  // namespace sss
+
 struct sss_part_plan {
     sss::PartPlan p;
 };
+
+extern "C" int sss_part_save(const SSS_AMG *mg, int nranks, int agg_rows, const char *prefix)
+{
+    if (!mg || nranks < 1 || !prefix) return ERROR_INPUT_PAR;
+    if (agg_rows <= 0) agg_rows = 20000;
+    int nagg = -1;
+    for (int r = 0; r < nranks; ++r) {   // one rank's plan in memory at a time
+        sss::PartPlan plan;
+        int rc = sss::part_plan_build(plan, mg, nranks, r, agg_rows);
+        if (rc) return rc;
+        if (plan.nagg < 1) return ERROR_INPUT_PAR;
+        nagg = plan.nagg;
+        if ((rc = sss::part_plan_write(plan, mg->pars, sss::part_file_name(prefix, r).c_str()))) return rc;
+    }
+    SSS_AMG tail = *mg;   // the replicated levels, as their own hierarchy
+    tail.cg = mg->cg + nagg;
+    tail.num_levels = mg->num_levels - nagg;
+    return SSS_amg_save(&tail, sss::part_tail_name(prefix).c_str());
+}
+
+extern "C" sss_part_plan *sss_part_plan_load(const char *path)
+{
+    auto *pp = new sss_part_plan();
+    SSS_AMG_PARS pars;
+    if (sss::part_plan_read(pp->p, pars, path)) {
+        delete pp;
+        return nullptr;
+    }
+    return pp;
+}
 
 extern "C" sss_part_plan *sss_part_plan_create(const SSS_AMG *mg, int nranks, int rank, int agg_rows)
 {

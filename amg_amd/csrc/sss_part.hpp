@@ -12,6 +12,7 @@
 // and of P_{l-1}'s own fine rows, so one halo plan serves every vector of the level.
 #pragma once
 
+#include <string>
 #include <vector>
 
 #include "../../include/sss_amg.h"
@@ -59,5 +60,13 @@ struct PartPlan {
 // agg_rows: the first level l >= 1 with at most agg_rows rows, and every level below it, is
 // replicated (the coarsest always is).  Returns 0 or an SSS error code.
 int part_plan_build(PartPlan &p, const SSS_AMG *mg, int nranks, int rank, int agg_rows);
+
+// Partition file of one rank (sss_part_save): its PartPlan plus the solve parameters.  The
+// replicated tail levels (cg[nagg..]) live in a separate hierarchy file (SSS_amg_save format)
+// that every rank loads.  Returns 0 or ERROR_OPEN_FILE / ERROR_WRONG_FILE.
+int part_plan_write(const PartPlan &p, const SSS_AMG_PARS &pars, const char *path);
+int part_plan_read(PartPlan &p, SSS_AMG_PARS &pars, const char *path);
+std::string part_file_name(const char *prefix, int rank);   // prefix.r<rank>
+std::string part_tail_name(const char *prefix);             // prefix.tail
 
 }  // namespace sss

@@ -34,15 +34,13 @@ static int upload_ints(int **dst, const std::vector<int> &src)
 {
     *dst = dev_alloc<int>(src.size());
     if (!*dst) return hip_fail(hipErrorOutOfMemory, "hipMalloc(ints)", __FILE__, __LINE__);
-    if (!src.empty()) SSS_HIP(hipMemcpy(*dst, src.data(), sizeof(int) * src.size(), hipMemcpyHostToDevice));
-    return 0;
+    return src.empty() ? 0 : h2d(*dst, src.data(), sizeof(int) * src.size());
 }
 static int upload_doubles(double **dst, const std::vector<double> &src)
 {
     *dst = dev_alloc<double>(src.size());
     if (!*dst) return hip_fail(hipErrorOutOfMemory, "hipMalloc(doubles)", __FILE__, __LINE__);
-    if (!src.empty()) SSS_HIP(hipMemcpy(*dst, src.data(), sizeof(double) * src.size(), hipMemcpyHostToDevice));
-    return 0;
+    return src.empty() ? 0 : h2d(*dst, src.data(), sizeof(double) * src.size());
 }
 
 int smoother_build(SmootherPlan &sp, const SSS_MAT &A, const int *mark, int kind, const DevCSR *dA, int inner,

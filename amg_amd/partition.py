@@ -1,0 +1,73 @@
+"""Partition set of a stencil hierarchy for a row-partitioned multi-GPU solve (host only).
+
+    python -m amg_amd.partition --stencil 7 --n 512 --ranks 8 --prefix /tmp/sss_parts/part
+
+Builds the global hierarchy once (the reference-semantics host setup), writes one partition file
+per rank (prefix.r<rank>: its rows, ghosts and halo lists of every partitioned level) and the
+replicated coarse tail (prefix.tail), then a manifest (prefix.json: global level sizes, timings,
+this process's peak host memory).  Run as its own process so that no solve rank ever holds the
+global hierarchy (sss_hip_dist_create_from_files); it never touches the GPU.
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes as C
+import json
+import os
+import resource
+import sys
+import time
+from pathlib import Path
+
+
+def level_table(H) -> list:
+    out = []
+    for l in range(H.num_levels):
+        L = H.level(l)
+        last = l + 1 == H.num_levels
+        out.append({"rows": L.A.num_rows, "nnz": L.A.num_nnzs, "nnz_p": 0 if last else L.P.num_nnzs,
+                    "rows_next": 0 if last else H.level(l + 1).A.num_rows})
+    return out
+
+
+def build(stencil: int, n: int, ranks: int, prefix: Path, agg_rows: int = 0) -> dict:
+    from . import _native as N
+    t0 = time.perf_counter()
+    M = N.generate(stencil, n)
+    sys.stdout.flush()
+    saved = os.dup(1)
+    os.dup2(2, 1)   # the setup's level table goes to stderr
+    try:
+        H = N.Hierarchy(M)
+    finally:
+        C.CDLL(None).fflush(None)
+        os.dup2(saved, 1)
+        os.close(saved)
+    N.lib().SSS_mat_destroy(C.byref(M))
+    t1 = time.perf_counter()
+    prefix.parent.mkdir(parents=True, exist_ok=True)
+    N.part_save(H, ranks, prefix, agg_rows)
+    t2 = time.perf_counter()
+    man = {"stencil": stencil, "n": n, "ranks": ranks, "agg_rows": agg_rows, "levels": level_table(H),
+           "pars": {"pre_iter": H.pars.pre_iter, "post_iter": H.pars.post_iter, "tol": H.pars.tol},
+           "setup_s": t1 - t0, "partition_s": t2 - t1,
+           "peak_rss_gb": resource.getrusage(resource.RUSAGE_SELF).ru_maxrss / 2**20}
+    H.close()
+    Path(str(prefix) + ".json").write_text(json.dumps(man))
+    return man
+
+
+def main():
+    p = argparse.ArgumentParser()
+    p.add_argument("--stencil", type=int, default=7)
+    p.add_argument("--n", type=int, required=True)
+    p.add_argument("--ranks", type=int, required=True)
+    p.add_argument("--prefix", required=True)
+    p.add_argument("--agg-rows", type=int, default=0)
+    a = p.parse_args()
+    man = build(a.stencil, a.n, a.ranks, Path(a.prefix), a.agg_rows)
+    print(json.dumps({k: v for k, v in man.items() if k != "levels"}), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -251,11 +251,9 @@ class Single:
 class Distributed(Single):
     """N > 1: this rank's rows of the row-partitioned engine (sss_hip_dist_*)."""
 
-    def __init__(self, DD, H):
+    def __init__(self, DD):
         self.DH = DD
-        self.rows, self.ghosts = DD.hi - DD.lo, DD.nghost0
-        rp = np.ctypeslib.as_array(H.level(0).A.row_ptr, shape=(H.level(0).A.num_rows + 1,))
-        self.nnz = int(rp[DD.hi] - rp[DD.lo])
+        self.rows, self.ghosts, self.nnz = DD.level_size(0)
 
     def set_ones(self):
         self.DH.upload("b", np.ones(self.rows))
@@ -265,7 +263,7 @@ class Distributed(Single):
         self.DH.upload("x", np.ones(self.rows))
 
 
-def vcycle_bytes(H) -> int:
+def vcycle_bytes(levels: list, sweeps: int) -> int:
     """Algorithmic HBM bytes of one outer iteration, SURVEY.md 8(d): per level l < coarsest, with
     z = nnz(A_l), p = nnz(P_l) = nnz(R_l), n = n_l, m = n_{l+1}:
       GS-CF sweep   12z + 4(n+1) + 8n + 8n + 16n + 8n      (x (pre_iter + post_iter) sweeps)
@@ -273,20 +271,26 @@ def vcycle_bytes(H) -> int:
       restriction   12p + 4(m+1) + 8n + 8m
       prolongation  12p + 4(n+1) + 8m + 16n
       zero-fill     8m
-    plus the outer residual and norm 12z0 + 4(n0+1) + 24n0 + 8n0; the coarse solve is excluded."""
-    sweeps = H.pars.pre_iter + H.pars.post_iter
+    plus the outer residual and norm 12z0 + 4(n0+1) + 24n0 + 8n0; the coarse solve is excluded.
+    levels: per level {"rows", "nnz", "nnz_p", "rows_next"} (amg_amd.partition.level_table)."""
     tot = 0
-    for l in range(H.num_levels - 1):
-        L, Lc = H.level(l), H.level(l + 1)
-        z, n, m, p = L.A.num_nnzs, L.A.num_rows, Lc.A.num_rows, L.P.num_nnzs
+    for L in levels[:-1]:
+        z, n, m, p = L["nnz"], L["rows"], L["rows_next"], L["nnz_p"]
         tot += sweeps * (12 * z + 4 * (n + 1) + 40 * n)
         tot += 12 * z + 4 * (n + 1) + 24 * n
         tot += 12 * p + 4 * (m + 1) + 8 * n + 8 * m
         tot += 12 * p + 4 * (n + 1) + 8 * m + 16 * n
         tot += 8 * m
-    L0 = H.level(0)
-    tot += 12 * L0.A.num_nnzs + 4 * (L0.A.num_rows + 1) + 32 * L0.A.num_rows
+    L0 = levels[0]
+    tot += 12 * L0["nnz"] + 4 * (L0["rows"] + 1) + 32 * L0["rows"]
     return int(tot)
+
+
+def part_prefix(stencil: int, n: int, world: int) -> Path:
+    """Where the partition set of a multi-rank run lives (SSS_PART_DIR, default /tmp); reused by
+    later runs of the same configuration."""
+    base = Path(os.environ.get("SSS_PART_DIR", "/tmp")) / f"sss_parts_{stencil}pt_{n}_{world}r"
+    return base / "part"
 
 
 def heartbeat(stop: threading.Event, t0: float):
@@ -304,7 +308,9 @@ def main():
     if args.gpus is not None and args.gpus != D.world:
         raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={D.world}")
     if args.probe_ranks:
-        print(json.dumps({"rank": D.rank, "world": D.world, "local_rank": D.local_rank}), flush=True)
+        # one write() per line: the ranks share the launcher's stdout pipe
+        sys.stdout.write(json.dumps({"rank": D.rank, "world": D.world, "local_rank": D.local_rank}) + "\n")
+        sys.stdout.flush()
         D.close()
         return
     # the BASELINE.json config of this rank count (configs[2]: 512^3 on 8 GPUs; configs[4]: 27-pt
@@ -330,25 +336,45 @@ def main():
 
     t0 = time.perf_counter()
     hier_src = None
-    cache = Path(args.hier_cache) if args.hier_cache else None
-    if cache is not None and D.rank == 0 and not cache.exists():
-        M = A.generate(args.stencil, n)
-        H = quiet_call(A.Hierarchy, M)
-        A.lib().SSS_mat_destroy(C.byref(M))
-        H.save(cache)
-        hier_src = "setup (saved)"
-    D.barrier()
-    if cache is not None and (D.rank != 0 or hier_src is None):
-        H = A.Hierarchy.load(cache)
-        hier_src = f"loaded from {cache}"
-    elif cache is None:
-        M = A.generate(args.stencil, n)
-        H = quiet_call(A.Hierarchy, M)
-        A.lib().SSS_mat_destroy(C.byref(M))
-        hier_src = "setup"
+    H = None
+    if D.world == 1:
+        cache = Path(args.hier_cache) if args.hier_cache else None
+        if cache is not None and cache.exists():
+            H = A.Hierarchy.load(cache)
+            hier_src = f"loaded from {cache}"
+        else:
+            M = A.generate(args.stencil, n)
+            H = quiet_call(A.Hierarchy, M)
+            A.lib().SSS_mat_destroy(C.byref(M))
+            hier_src = "setup"
+            if cache is not None:
+                H.save(cache)
+                hier_src = "setup (saved)"
+        from amg_amd.partition import level_table
+        table = level_table(H)
+        pars = {"pre_iter": H.pars.pre_iter, "post_iter": H.pars.post_iter, "tol": H.pars.tol}
+    else:
+        # rows partitioned over the ranks: a separate host process builds the global hierarchy and
+        # writes one partition file per rank (amg_amd/partition.py); each rank then reads only its
+        # rows, ghosts and the replicated coarse tail -- no rank ever holds the global hierarchy
+        prefix = part_prefix(args.stencil, n, D.world)
+        manifest = Path(str(prefix) + ".json")
+        if D.rank == 0 and not manifest.exists():
+            import subprocess
+            subprocess.run([sys.executable, "-m", "amg_amd.partition", "--stencil", str(args.stencil), "--n", str(n),
+                            "--ranks", str(D.world), "--prefix", str(prefix)], check=True, cwd=str(ROOT),
+                           stdout=sys.stderr)
+            hier_src = f"partition set written to {prefix.parent}"
+        D.barrier()
+        man = json.loads(manifest.read_text())
+        table, pars = man["levels"], man["pars"]
+        hier_src = hier_src or f"partition set read from {prefix.parent}"
+        if D.rank == 0:
+            print(f"[bench] partition set: setup {man['setup_s']:.1f} s, partition {man['partition_s']:.1f} s, "
+                  f"peak host memory of the partitioning process {man['peak_rss_gb']:.1f} GB", file=sys.stderr, flush=True)
     setup_s = time.perf_counter() - t0
-    N = H.level(0).A.num_rows
-    nnz = H.level(0).A.num_nnzs
+    N = table[0]["rows"]
+    nnz = table[0]["nnz"]
 
     t0 = time.perf_counter()
     inner = args.inner if args.inner is not None else int(os.environ.get("SSS_HIP_INNER", "1"))
@@ -375,9 +401,9 @@ def main():
             transport = "host-gloo"
         else:
             transport = "rccl"
-        DD = A.DistHierarchy(H, comm, smoother=smoother, coarse=coarse, device=dev, inner=args.inner,
-                             inner_from=args.inner_from, sum_order=sum_order, sorted_tiles=sorted_tiles)
-        eng = Distributed(DD, H)
+        DD = A.DistHierarchy(None, comm, smoother=smoother, coarse=coarse, device=dev, inner=args.inner,
+                             inner_from=args.inner_from, sum_order=sum_order, sorted_tiles=sorted_tiles, parts=prefix)
+        eng = Distributed(DD)
     upload_s = time.perf_counter() - t0
     print(f"[bench] setup {setup_s:.1f} s, upload {upload_s:.1f} s", file=sys.stderr, flush=True)
     eng.set_ones()
@@ -423,7 +449,7 @@ def main():
         relres = DH.residual_norm() / sumb
         its += 1
         print(f"[bench] converge iteration {its}: relres {relres:.6e}", file=sys.stderr, flush=True)
-        if relres < H.pars.tol:
+        if relres < pars["tol"]:
             break
     solve_s = time.perf_counter() - t0
     pcg = None
@@ -431,13 +457,15 @@ def main():
         # AMG as a CG preconditioner: same problem, same x0, same tolerance
         DH.set_x_ones()
         t0 = time.perf_counter()
-        pits, phist = DH.DH.pcg(H.pars.tol, args.converge_max)
+        pits, phist = DH.DH.pcg(pars["tol"], args.converge_max)
         pcg = {"iterations_to_tol": pits, "final_relres": float(phist[-1]) if len(phist) else None,
                "time_to_solution_s": time.perf_counter() - t0}
         print(f"[bench] AMG-PCG: {pits} iterations, relres {pcg['final_relres']:.3e}, "
               f"{pcg['time_to_solution_s']:.3f} s", file=sys.stderr, flush=True)
-    levels = [(H.level(l).A.num_rows, H.level(l).A.num_nnzs) for l in range(H.num_levels)]
-    vbytes = vcycle_bytes(H)
+    levels = [(L["rows"], L["nnz"]) for L in table]
+    vbytes = vcycle_bytes(table, pars["pre_iter"] + pars["post_iter"])
+    import resource
+    rss_gb = D.max(resource.getrusage(resource.RUSAGE_SELF).ru_maxrss / 2**20)   # peak over the ranks
 
     traffic = None
     pmc = ROOT / "profiles" / "r01_level0_spmv_pmc.json"
@@ -514,6 +542,7 @@ def main():
                    "amg_pcg": pcg,
                    "setup_s": setup_s, "hierarchy_source": hier_src, "upload_s": upload_s,
                    "parallelism": f"rowpart{D.world}" if D.world > 1 else "single-gpu",
+                   "host_peak_rss_gb_max_over_ranks": rss_gb,
                    "transport": transport},
         "roofline": {"bound": "hbm", "kernel": "spmv_adaptive<RESID> level 0", "achieved": achieved,
                      "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": achieved / PEAK_HBM_GBS,

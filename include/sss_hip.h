@@ -171,9 +171,15 @@ void sss_hip_comm_destroy(sss_hip_comm *c);
 /* mg: the global hierarchy (every rank runs the same host setup).  V-cycles only.
  * agg_rows <= 0: SSS_HIP_AGG_ROWS or 20000. */
 sss_hip_dist *sss_hip_dist_create(const SSS_AMG *mg, const sss_hip_opts *o, sss_hip_comm *c, int agg_rows);
+/* The same engine from a partition set written by sss_part_save: rank r reads only
+ * prefix.r<r> (its rows, ghosts, halo lists) and prefix.tail (the replicated coarse levels), so
+ * no rank holds the global hierarchy (the 512^3 8-GPU configuration). */
+sss_hip_dist *sss_hip_dist_create_from_files(const char *prefix, const sss_hip_opts *o, sss_hip_comm *c);
 void sss_hip_dist_destroy(sss_hip_dist *d);
 /* own rows [lo, hi) of level 0 in the original numbering; nagg = number of partitioned levels */
 int sss_hip_dist_info(sss_hip_dist *d, int *lo, int *hi, int *nagg, int *nghost0);
+/* Own rows, ghosts and nonzeros of this rank's partitioned level l. */
+int sss_hip_dist_level_size(sss_hip_dist *d, int l, int *m, int *g, long long *nnz);
 /* exact eliminations in force on partitioned level l (agreed over the ranks), a bit mask:
  * 1 zero-first pass, 2 fused C-row residual, 4 dead F-row prolongation.  <0: bad level. */
 int sss_hip_dist_level_flags(sss_hip_dist *d, int l);
@@ -192,6 +198,12 @@ int sss_hip_dist_time_level0_spmv(sss_hip_dist *d, int reps, double *avg_ms);
  * Arrays stay owned by the plan. */
 typedef struct sss_part_plan sss_part_plan;
 sss_part_plan *sss_part_plan_create(const SSS_AMG *mg, int nranks, int rank, int agg_rows);
+/* Partition set of the global hierarchy for nranks ranks: prefix.r0 .. prefix.r<nranks-1> (one
+ * rank's plan each, built one at a time) and prefix.tail (levels >= nagg, SSS_amg_save format).
+ * Host only.  Returns 0 or an SSS error code. */
+int sss_part_save(const SSS_AMG *mg, int nranks, int agg_rows, const char *prefix);
+/* One rank's plan read back from its partition file (prefix.r<rank>). */
+sss_part_plan *sss_part_plan_load(const char *path);
 void sss_part_plan_destroy(sss_part_plan *p);
 int sss_part_plan_nagg(const sss_part_plan *p);
 /* own range, own count, ghost count of level l (l <= nagg for the range; m/g for l < nagg) */

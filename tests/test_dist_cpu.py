@@ -46,7 +46,7 @@ def _halo_exchange(dist, torch, halo, local, m):
         off += len(t)
 
 
-def _worker(rank, world, port, kind, n, agg_rows, errq):
+def _worker(rank, world, port, kind, n, agg_rows, errq, prefix=None):
     try:
         os.environ["MASTER_ADDR"] = "127.0.0.1"
         os.environ["MASTER_PORT"] = str(port)
@@ -60,7 +60,17 @@ def _worker(rank, world, port, kind, n, agg_rows, errq):
         from conftest import build_hierarchy, quiet_ctx
 
         H = build_hierarchy(A.generate(kind, n), quiet_ctx)
-        plan = A.PartPlan(H, world, rank, agg_rows)
+        if prefix is None:
+            plan = A.PartPlan(H, world, rank, agg_rows)
+        else:   # this rank's partition file only; the global H serves as the checker
+            plan = A.PartPlan.load(f"{prefix}.r{rank}")
+            ref = A.PartPlan(H, world, rank, agg_rows)
+            assert plan.nagg == ref.nagg
+            for l in range(plan.nagg):
+                assert plan.level(l) == ref.level(l)
+                for w in "APR":
+                    a, b = A.csr_arrays(plan.matrix(l, w)), A.csr_arrays(ref.matrix(l, w))
+                    assert all(np.array_equal(x.view(np.uint8), y.view(np.uint8)) for x, y in zip(a, b)), (l, w)
         ora = oracle.load()
         assert plan.nagg >= 2, plan.nagg
         # ranges tile every partitioned level
@@ -125,14 +135,13 @@ def _worker(rank, world, port, kind, n, agg_rows, errq):
         errq.put(f"rank {rank}: {e!r}\n{traceback.format_exc()}")
 
 
-@pytest.mark.parametrize("kind,n,agg", [(7, 20, 60), (27, 12, 40)])
-def test_partition_products_world2(kind, n, agg):
+def _run_world2(kind, n, agg, prefix=None):
     import torch.multiprocessing as mp
 
     ctx = mp.get_context("spawn")
     errq = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, kind, n, agg, errq)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, kind, n, agg, errq, prefix)) for r in range(2)]
     for p in procs:
         p.start()
     for p in procs:
@@ -142,6 +151,30 @@ def test_partition_products_world2(kind, n, agg):
         errs.append(errq.get())
     assert not errs, "\n".join(errs)
     assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
+
+
+@pytest.mark.parametrize("kind,n,agg", [(7, 20, 60), (27, 12, 40)])
+def test_partition_products_world2(kind, n, agg):
+    _run_world2(kind, n, agg)
+
+
+@pytest.mark.parametrize("kind,n,agg", [(7, 20, 60), (27, 12, 40)])
+def test_partition_files_world2(kind, n, agg, tmp_path):
+    """The same contract with each rank reading only its partition file (sss_part_save /
+    sss_part_plan_load): the file round-trips the plan bitwise, and the products match."""
+    import amg_amd as A
+    from conftest import build_hierarchy, quiet_ctx
+    H = build_hierarchy(A.generate(kind, n), quiet_ctx)
+    prefix = tmp_path / "part"
+    A.part_save(H, 2, prefix, agg)
+    assert (tmp_path / "part.r0").exists() and (tmp_path / "part.r1").exists() and (tmp_path / "part.tail").exists()
+    T = A.Hierarchy.load(tmp_path / "part.tail")
+    plan0 = A.PartPlan.load(tmp_path / "part.r0")
+    assert T.num_levels == H.num_levels - plan0.nagg
+    for l in range(T.num_levels):   # the replicated tail is the global hierarchy's levels >= nagg
+        a, b = A.csr_arrays(T.level(l).A), A.csr_arrays(H.level(plan0.nagg + l).A)
+        assert all(np.array_equal(x.view(np.uint8), y.view(np.uint8)) for x, y in zip(a, b))
+    _run_world2(kind, n, agg, str(prefix))
 
 
 def test_bench_gpus_n_launches_n_ranks():

@@ -25,7 +25,8 @@ def _free_port() -> int:
         return s.getsockname()[1]
 
 
-def _worker(rank, world, port, kind, n, smoother, inner_from, agg_rows, cycles, errq, transport="host", sum_order=0):
+def _worker(rank, world, port, kind, n, smoother, inner_from, agg_rows, cycles, errq, transport="host", sum_order=0,
+            parts=None):
     try:
         os.environ["MASTER_ADDR"] = "127.0.0.1"
         os.environ["MASTER_PORT"] = str(port)
@@ -42,8 +43,12 @@ def _worker(rank, world, port, kind, n, smoother, inner_from, agg_rows, cycles, 
         H = build_hierarchy(A.generate(kind, n), quiet_ctx)
         N = H.level(0).A.num_rows
         comm = A.Comm(world, rank, transport, device=0)
-        D = A.DistHierarchy(H, comm, smoother=smoother, coarse="direct", device=0, agg_rows=agg_rows,
-                            inner_from=inner_from, sum_order=sum_order)
+        if parts is None:
+            D = A.DistHierarchy(H, comm, smoother=smoother, coarse="direct", device=0, agg_rows=agg_rows,
+                                inner_from=inner_from, sum_order=sum_order)
+        else:   # this rank's partition file and the tail file only
+            D = A.DistHierarchy(None, comm, smoother=smoother, coarse="direct", device=0, inner_from=inner_from,
+                                sum_order=sum_order, parts=parts)
         assert D.nagg >= 2, D.nagg
         if kind == 7 and smoother == "hybrid" and not sum_order:
             # red-black level 0: the fused C-row residual and the dead F-row prolongation hold
@@ -117,14 +122,28 @@ def test_dist_free_order(kind, n, smoother):
     _run(2, "host", kind, n, smoother, 2, 100, sum_order=1)
 
 
-def _run(world, transport, kind, n, smoother, inner_from, agg, sum_order=0):
+@pytest.mark.parametrize("kind,n,smoother,sum_order", [(7, 24, "hybrid", 0), (27, 14, "jacobi", 0), (7, 24, "hybrid", 1)])
+def test_dist_from_partition_files(kind, n, smoother, sum_order, tmp_path):
+    """Engines built from a partition set (sss_part_save -> sss_hip_dist_create_from_files, the
+    path bench.py takes at N > 1): every rank reads only its own file and the tail, and the
+    iterates are those of one GPU."""
+    import amg_amd as A
+    from conftest import build_hierarchy, quiet_ctx
+    H = build_hierarchy(A.generate(kind, n), quiet_ctx)
+    A.part_save(H, 2, tmp_path / "part", 100)
+    H.close()
+    _run(2, "host", kind, n, smoother, 2, 100, sum_order=sum_order, parts=str(tmp_path / "part"))
+
+
+def _run(world, transport, kind, n, smoother, inner_from, agg, sum_order=0, parts=None):
     import torch.multiprocessing as mp
 
     ctx = mp.get_context("spawn")
     errq = ctx.Queue()
     port = _free_port()
     procs = [ctx.Process(target=_worker,
-                         args=(r, world, port, kind, n, smoother, inner_from, agg, 4, errq, transport, sum_order))
+                         args=(r, world, port, kind, n, smoother, inner_from, agg, 4, errq, transport, sum_order,
+                               parts))
              for r in range(world)]
     for p in procs:
         p.start()
