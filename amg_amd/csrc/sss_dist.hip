@@ -20,6 +20,7 @@
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
+#include <functional>
 #include <vector>
 
 #include "sss_engine.hpp"
@@ -51,15 +52,28 @@ struct DLevel {
     SmootherPlan sm;
     double *b = nullptr, *x = nullptr, *wp = nullptr, *w0 = nullptr, *w1 = nullptr;
     Halo halo;
+    // per row block of A, R and P: does the block read a ghost value?  (halo overlap)
+    std::vector<char> ghostA, ghostR, ghostP;
 };
 
-__global__ void pack_kernel(int n, const int *__restrict__ idx, const double *__restrict__ v, double *__restrict__ out)
+// Per row block of a local matrix: 1 if any entry reads a column >= own (a ghost).
+std::vector<char> block_ghost_flags(const HostMat &M, int own, const std::vector<int> &blk)
+{
+    std::vector<char> f(blk.empty() ? 0 : blk.size() - 1, 0);
+    for (size_t q = 0; q + 1 < blk.size(); ++q)
+        for (int k = M.rp[blk[q]]; k < M.rp[blk[q + 1]] && !f[q]; ++k) f[q] = M.ci[k] >= own;
+    return f;
+}
+
+__global__ __launch_bounds__(256) void pack_kernel(int n, const int *__restrict__ idx, const double *__restrict__ v,
+                                                    double *__restrict__ out)
 {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i < n) out[i] = v[idx[i]];
 }
 
-__global__ void gather_kernel(int n, const int *__restrict__ idx, const double *__restrict__ v, double *__restrict__ out)
+__global__ __launch_bounds__(256) void gather_kernel(int n, const int *__restrict__ idx, const double *__restrict__ v,
+                                                      double *__restrict__ out)
 {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i < n) out[i] = v[idx[i]];
@@ -97,11 +111,19 @@ struct sss_hip_dist {
     bool resid_c_ready = false;   // the last cycle's final C pass left r_C and its partials (level 0)
     SSS_AMG tail_host{};          // the tail levels read from a partition set (file-built engines)
     bool own_tail_host = false;
+    // halo overlap: RCCL send/recv on a second stream while the engine stream runs interior blocks
+    hipStream_t cstream = nullptr;
+    hipEvent_t ev_packed = nullptr, ev_halo = nullptr;
+    int overlap = 1;   // 0 off, 1 on (RCCL), 2 also split the launches over the host transport (tests)
 };
 
 namespace {
 
-int exchange(sss_hip_dist *d, int l, double *vec)
+// Halo of level l for vec (own values first, ghosts after): pack the values peers need, send them
+// and receive the ghosts.  RCCL: the grouped send/recv runs on the communication stream once the
+// pack has run; exchange_end makes the engine stream wait for it, so work enqueued in between (the
+// blocks that read no ghost) overlaps the transfer.  Host transport: synchronous, in _begin.
+int exchange_begin(sss_hip_dist *d, int l, double *vec)
 {
     DLevel &L = d->L[l];
     Halo &H = L.halo;
@@ -109,14 +131,23 @@ int exchange(sss_hip_dist *d, int l, double *vec)
     const hipStream_t s = d->stream;
     if (H.nsend == 0 && H.nrecv == 0) return 0;
     const int ns = H.soff.empty() ? 0 : H.soff.back();
-    if (ns > 0) hipLaunchKernelGGL(pack_kernel, dim3((ns + 255) / 256), dim3(256), 0, s, ns, H.d_sidx, vec, H.d_sbuf);
+    if (ns > 0) {
+        hipLaunchKernelGGL(pack_kernel, dim3((ns + 255) / 256), dim3(256), 0, s, ns, H.d_sidx, vec, H.d_sbuf);
+        SSS_HIP(hipGetLastError());
+    }
     if (!c->host) {
+        SSS_HIP(hipEventRecord(d->ev_packed, s));
+        SSS_HIP(hipStreamWaitEvent(d->cstream, d->ev_packed, 0));
         SSS_NCCL(ncclGroupStart());
-        for (int i = 0; i < H.nsend; ++i)
-            SSS_NCCL(ncclSend(H.d_sbuf + H.soff[i], (size_t)H.scount[i], ncclDouble, H.sdst[i], c->nccl, s));
-        for (int i = 0; i < H.nrecv; ++i)
-            SSS_NCCL(ncclRecv(vec + L.m + H.roff[i], (size_t)H.rcount[i], ncclDouble, H.rsrc[i], c->nccl, s));
-        SSS_NCCL(ncclGroupEnd());
+        ncclResult_t r = ncclSuccess;
+        for (int i = 0; i < H.nsend && r == ncclSuccess; ++i)
+            r = ncclSend(H.d_sbuf + H.soff[i], (size_t)H.scount[i], ncclDouble, H.sdst[i], c->nccl, d->cstream);
+        for (int i = 0; i < H.nrecv && r == ncclSuccess; ++i)
+            r = ncclRecv(vec + L.m + H.roff[i], (size_t)H.rcount[i], ncclDouble, H.rsrc[i], c->nccl, d->cstream);
+        const ncclResult_t e = ncclGroupEnd();   // always close the group, also after a failed call
+        if (r != ncclSuccess) return nccl_fail(r, "ncclSend/ncclRecv (halo)");
+        if (e != ncclSuccess) return nccl_fail(e, "ncclGroupEnd (halo)");
+        SSS_HIP(hipEventRecord(d->ev_halo, d->cstream));
         return 0;
     }
     H.h_sbuf.resize(std::max(ns, 1));
@@ -129,6 +160,74 @@ int exchange(sss_hip_dist *d, int l, double *vec)
     if (L.g > 0) SSS_HIP(hipMemcpyAsync(vec + L.m, H.h_rbuf.data(), sizeof(double) * L.g, hipMemcpyHostToDevice, s));
     SSS_HIP(hipStreamSynchronize(s));   // the staging buffer is reused by the next exchange
     return 0;
+}
+
+int exchange_end(sss_hip_dist *d, int l)
+{
+    const Halo &H = d->L[l].halo;
+    if (d->comm->host || (H.nsend == 0 && H.nrecv == 0)) return 0;
+    SSS_HIP(hipStreamWaitEvent(d->stream, d->ev_halo, 0));
+    return 0;
+}
+
+int exchange(sss_hip_dist *d, int l, double *vec)
+{
+    int rc = exchange_begin(d, l, vec);
+    return rc ? rc : exchange_end(d, l);
+}
+
+// launch(b0, b1) over the row blocks [blo, bhi) of a matrix whose per-block ghost flags are
+// `ghost`, with vec's halo of level l refreshed in between: the runs of blocks that read no ghost
+// go first, overlapping the transfer, the others after it (everything after the exchange when
+// there is too little interior work or the transport is synchronous).
+int split_launch(sss_hip_dist *d, int l, double *vec, const std::vector<char> &ghost, int blo, int bhi,
+                 const std::function<void(int, int)> &launch)
+{
+    int interior = 0, runs = 0;
+    for (int q = blo; q < bhi; ++q) {
+        interior += !ghost[q];
+        runs += q == blo || ghost[q] != ghost[q - 1];
+    }
+    const Halo &H = d->L[l].halo;
+    const bool halo = H.nsend > 0 || H.nrecv > 0;
+    if (!d->overlap || (d->comm->host && d->overlap < 2) || !halo || interior * 4 < (bhi - blo) || runs > 16) {
+        int rc = exchange(d, l, vec);
+        if (rc) return rc;
+        if (bhi > blo) launch(blo, bhi);
+        SSS_HIP(hipGetLastError());
+        return 0;
+    }
+    int rc = exchange_begin(d, l, vec);
+    if (rc) return rc;
+    for (int pass = 0; pass < 2; ++pass) {   // interior runs, then (after the halo) ghost-reading runs
+        if (pass == 1 && (rc = exchange_end(d, l))) return rc;
+        for (int q = blo; q < bhi;) {
+            int e = q + 1;
+            while (e < bhi && ghost[e] == ghost[q]) ++e;
+            if ((ghost[q] != 0) == (pass == 1)) launch(q, e);
+            q = e;
+        }
+    }
+    SSS_HIP(hipGetLastError());
+    return 0;
+}
+
+// wp = b - A x over this rank's rows of level l (x's halo refreshed, overlapping the interior
+// blocks), or over the F rows only when the smoother's last pass already formed the C rows
+// (c_done); per-block sums of squares into partial when given.
+int residual(sss_hip_dist *d, int l, bool c_done, double *partial)
+{
+    DLevel &L = d->L[l];
+    const int bhi = c_done ? L.A.split_blk : L.A.nblk;
+    if (L.A.wave_rows || L.A.vec_rows) {
+        int rc = exchange(d, l, L.x);
+        return rc ? rc : launch_spmv(L.A, SSS_HIP_SPMV_RESID, -1.0, L.x, L.b, L.wp, 0, partial, d->stream);
+    }
+    int lrc = 0;
+    const int rc = split_launch(d, l, L.x, L.ghostA, 0, bhi, [&](int b0, int b1) {
+        lrc = lrc ? lrc : launch_spmv_range(L.A, b0, b1, SSS_HIP_SPMV_RESID, -1.0, L.x, L.b, L.wp, partial, d->stream);
+    });
+    return rc ? rc : lrc;
 }
 
 struct HookCtx {
@@ -148,6 +247,9 @@ int smooth(sss_hip_dist *d, int l, int post, ResidFuse *rf = nullptr, bool x_zer
     PassHooks hk;
     hk.ctx = &hc;
     hk.exchange = hook_exchange;
+    hk.split = [d, l](double *vec, int blo, int bhi, const std::function<void(int, int)> &launch) {
+        return split_launch(d, l, vec, d->L[l].ghostA, blo, bhi, launch);
+    };
     hk.w0 = L.w0;
     hk.w1 = L.w1;
     const int sweeps = post ? d->pars.post_iter : d->pars.pre_iter;
@@ -161,12 +263,15 @@ int allreduce_host(sss_hip_dist *d, double *v, int n)
     if (c->host) return c->t.allreduce_sum(c->t.ctx, v, n) ? ERROR_MISC : 0;
     double *dv = dev_alloc<double>((size_t)n);
     if (!dv) return ERROR_MISC;
-    SSS_HIP(hipMemcpyAsync(dv, v, sizeof(double) * n, hipMemcpyHostToDevice, d->stream));
-    SSS_NCCL(ncclAllReduce(dv, dv, (size_t)n, ncclDouble, ncclSum, c->nccl, d->stream));
-    SSS_HIP(hipMemcpyAsync(v, dv, sizeof(double) * n, hipMemcpyDeviceToHost, d->stream));
-    SSS_HIP(hipStreamSynchronize(d->stream));
+    int rc = 0;
+    if (hipMemcpyAsync(dv, v, sizeof(double) * n, hipMemcpyHostToDevice, d->stream) != hipSuccess) rc = ERROR_MISC;
+    ncclResult_t r = rc ? ncclSuccess : ncclAllReduce(dv, dv, (size_t)n, ncclDouble, ncclSum, c->nccl, d->stream);
+    if (r != ncclSuccess) rc = nccl_fail(r, "ncclAllReduce (set-up)");
+    if (!rc && (hipMemcpyAsync(v, dv, sizeof(double) * n, hipMemcpyDeviceToHost, d->stream) != hipSuccess ||
+                hipStreamSynchronize(d->stream) != hipSuccess))
+        rc = ERROR_MISC;
     dev_free(dv);
-    return 0;
+    return rc;
 }
 
 // The exact eliminations of the single-GPU cycle, made safe across ranks: the fused C-row residual
@@ -270,6 +375,9 @@ void release(sss_hip_dist *d)
     dev_free(d->d_norm);
     if (d->h_norm) (void)hipHostFree(d->h_norm);
     if (d->stream) (void)hipStreamDestroy(d->stream);
+    if (d->cstream) (void)hipStreamDestroy(d->cstream);
+    if (d->ev_packed) (void)hipEventDestroy(d->ev_packed);
+    if (d->ev_halo) (void)hipEventDestroy(d->ev_halo);
     delete d;
 }
 
@@ -344,81 +452,103 @@ static sss_hip_dist *dist_create_impl(sss_hip_dist *d, PartPlan &plan, const SSS
     if (d->nagg < 1) return fail("hierarchy too shallow to partition");
     if (tailmg->num_levels != plan.nl - plan.nagg) return fail("tail levels do not match the partition");
 
-    // replicated tail first: its level-0 relabeling fixes the column ids of P_{nagg-1}
-    sss_hip_opts to = d->opts;
-    to.use_graph = 0;
-    d->tail = hier_create_impl(tailmg, &to, d->nagg, d->stream);
-    if (!d->tail) return fail("replicated coarse levels");
-    const std::vector<int> &tperm = hier_perm(d->tail, 0);
-    const int nt = tailmg->cg[0].A.num_rows;
-    std::vector<int> tinv;
-    if (!tperm.empty()) {
-        tinv.resize(nt);
-        for (int i = 0; i < nt; ++i) tinv[tperm[i]] = i;
-        if (upload_ints(&d->d_tail_perm, tperm)) return fail("tail perm");
-    }
+    if (hipStreamCreateWithFlags(&d->cstream, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreateWithFlags(&d->ev_packed, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&d->ev_halo, hipEventDisableTiming) != hipSuccess)
+        return fail("communication stream");
+    if (const char *ov = getenv("SSS_HIP_OVERLAP")) d->overlap = atoi(ov);
 
-    for (int l = 0; l < d->nagg; ++l) {
-        PartLevel &P = plan.L[l];
-        DLevel &L = d->L[l];
-        L.lo = P.lo;
-        L.hi = P.hi;
-        L.m = P.m;
-        L.g = P.g;
-        L.perm = P.perm;
-        const int kind = level_kind_of(d->opts, l), inner = level_inner_of(d->opts, l);
-        SSS_MAT Av = P.A.view();
-        const int enc = level_encoding(d->opts);
-        if (devcsr_upload(L.A, Av, P.nF, enc)) return fail("upload A");
-        if (smoother_build(L.sm, Av, P.mark.data(), kind, &L.A, inner, P.gcls.data(), enc))
-            return fail("smoother plan");
-        for (const auto &ps : L.sm.pass)
-            if (ps.nrows > 0 && !ps.range) return fail("level needs an exact GS-CF chain across ranks (not distributed)");
-        if (l + 1 == d->nagg && !tinv.empty())
-            for (int &j : P.P.ci) j = tinv[j];
-        SSS_MAT Pv = P.P.view(), Rv = P.R.view();
-        if (devcsr_upload(L.P, Pv, P.nF, enc) || devcsr_upload(L.R, Rv, -1, enc)) return fail("upload P/R");
-        const size_t nv = (size_t)(L.m + L.g);
-        L.b = dev_alloc<double>(nv);
-        L.x = dev_alloc<double>(nv);
-        L.wp = dev_alloc<double>(nv);
-        L.w0 = dev_alloc<double>(nv);
-        L.w1 = dev_alloc<double>(nv);
-        if (!L.b || !L.x || !L.wp || !L.w0 || !L.w1) return fail("vectors");
-        for (double *v : {L.b, L.x, L.wp, L.w0, L.w1})
-            if (hipMemset(v, 0, sizeof(double) * nv) != hipSuccess) return fail("memset");
-        Halo &H = L.halo;
-        H.sdst = P.sdst;
-        H.scount = P.scount;
-        H.rsrc = P.rsrc;
-        H.rcount = P.rcount;
-        H.nsend = (int)H.sdst.size();
-        H.nrecv = (int)H.rsrc.size();
-        H.soff.assign(1, 0);
-        for (int x : H.scount) H.soff.push_back(H.soff.back() + x);
-        H.roff.assign(1, 0);
-        for (int x : H.rcount) H.roff.push_back(H.roff.back() + x);
-        if (upload_ints(&H.d_sidx, P.sidx)) return fail("halo");
-        H.d_sbuf = dev_alloc<double>(P.sidx.size());
-        if (!H.d_sbuf) return fail("halo buffer");
-    }
-    // all-gather layout of level nagg
-    const auto &cut = plan.cut[d->nagg];
-    d->counts.resize(c->nranks);
-    d->displs.resize(c->nranks);
-    for (int q = 0; q < c->nranks; ++q) {
-        d->counts[q] = cut[q + 1] - cut[q];
-        d->displs[q] = cut[q];
-    }
-    d->nc_own = d->counts[c->rank];
-    d->nc_all = nt;
-    d->d_cown = dev_alloc<double>(d->nc_own);
-    d->d_call = dev_alloc<double>(nt);
-    d->partial = dev_alloc<double>((size_t)std::max(d->L[0].A.ngrid, 1) + kFinalScratch);
-    d->d_norm = dev_alloc<double>(1);
-    if (!d->d_cown || !d->d_call || !d->partial || !d->d_norm ||
-        hipHostMalloc((void **)&d->h_norm, sizeof(double)) != hipSuccess)
-        return fail("buffers");
+    // Everything below can fail on one rank only (memory, a level this rank cannot smooth): each
+    // rank records its failure, and all of them agree on the outcome with one collective before the
+    // first collective of the set-up, so no rank is left waiting in it.
+    const char *err = [&]() -> const char * {
+        // replicated tail first: its level-0 relabeling fixes the column ids of P_{nagg-1}
+        sss_hip_opts to = d->opts;
+        to.use_graph = 0;
+        d->tail = hier_create_impl(tailmg, &to, d->nagg, d->stream);
+        if (!d->tail) return "replicated coarse levels";
+        const std::vector<int> &tperm = hier_perm(d->tail, 0);
+        const int nt = tailmg->cg[0].A.num_rows;
+        std::vector<int> tinv;
+        if (!tperm.empty()) {
+            tinv.resize(nt);
+            for (int i = 0; i < nt; ++i) tinv[tperm[i]] = i;
+            if (upload_ints(&d->d_tail_perm, tperm)) return "tail perm";
+        }
+        for (int l = 0; l < d->nagg; ++l) {
+            PartLevel &P = plan.L[l];
+            DLevel &L = d->L[l];
+            L.lo = P.lo;
+            L.hi = P.hi;
+            L.m = P.m;
+            L.g = P.g;
+            L.perm = P.perm;
+            const int kind = level_kind_of(d->opts, l), inner = level_inner_of(d->opts, l);
+            SSS_MAT Av = P.A.view();
+            const int enc = level_encoding(d->opts);
+            if (devcsr_upload(L.A, Av, P.nF, enc)) return "upload A";
+            if (smoother_build(L.sm, Av, P.mark.data(), kind, &L.A, inner, P.gcls.data(), enc)) return "smoother plan";
+            for (const auto &ps : L.sm.pass)
+                if (ps.nrows > 0 && !ps.range) return "level needs an exact GS-CF chain across ranks (not distributed)";
+            if (l + 1 == d->nagg && !tinv.empty())
+                for (int &j : P.P.ci) j = tinv[j];
+            SSS_MAT Pv = P.P.view(), Rv = P.R.view();
+            if (devcsr_upload(L.P, Pv, P.nF, enc) || devcsr_upload(L.R, Rv, -1, enc)) return "upload P/R";
+            {   // which row blocks read ghosts (the same blockings the uploads made)
+                std::vector<int> blk;
+                build_row_blocks(P.A.rp.data(), P.A.rows, blk, P.nF);
+                L.ghostA = block_ghost_flags(P.A, L.m, blk);
+                build_row_blocks(P.R.rp.data(), P.R.rows, blk, -1);
+                L.ghostR = block_ghost_flags(P.R, L.m, blk);
+                build_row_blocks(P.P.rp.data(), P.P.rows, blk, P.nF);
+                L.ghostP = block_ghost_flags(P.P, l + 1 < d->nagg ? plan.L[l + 1].m : P.P.cols, blk);
+            }
+            const size_t nv = (size_t)(L.m + L.g);
+            L.b = dev_alloc<double>(nv);
+            L.x = dev_alloc<double>(nv);
+            L.wp = dev_alloc<double>(nv);
+            L.w0 = dev_alloc<double>(nv);
+            L.w1 = dev_alloc<double>(nv);
+            if (!L.b || !L.x || !L.wp || !L.w0 || !L.w1) return "vectors";
+            for (double *v : {L.b, L.x, L.wp, L.w0, L.w1})
+                if (hipMemset(v, 0, sizeof(double) * nv) != hipSuccess) return "memset";
+            Halo &H = L.halo;
+            H.sdst = P.sdst;
+            H.scount = P.scount;
+            H.rsrc = P.rsrc;
+            H.rcount = P.rcount;
+            H.nsend = (int)H.sdst.size();
+            H.nrecv = (int)H.rsrc.size();
+            H.soff.assign(1, 0);
+            for (int x : H.scount) H.soff.push_back(H.soff.back() + x);
+            H.roff.assign(1, 0);
+            for (int x : H.rcount) H.roff.push_back(H.roff.back() + x);
+            if (upload_ints(&H.d_sidx, P.sidx)) return "halo";
+            H.d_sbuf = dev_alloc<double>(P.sidx.size());
+            if (!H.d_sbuf) return "halo buffer";
+        }
+        // all-gather layout of level nagg
+        const auto &cut = plan.cut[d->nagg];
+        d->counts.resize(c->nranks);
+        d->displs.resize(c->nranks);
+        for (int q = 0; q < c->nranks; ++q) {
+            d->counts[q] = cut[q + 1] - cut[q];
+            d->displs[q] = cut[q];
+        }
+        d->nc_own = d->counts[c->rank];
+        d->nc_all = nt;
+        d->d_cown = dev_alloc<double>(d->nc_own);
+        d->d_call = dev_alloc<double>(nt);
+        d->partial = dev_alloc<double>((size_t)std::max(d->L[0].A.ngrid, 1) + kFinalScratch);
+        d->d_norm = dev_alloc<double>(1);
+        if (!d->d_cown || !d->d_call || !d->partial || !d->d_norm ||
+            hipHostMalloc((void **)&d->h_norm, sizeof(double)) != hipSuccess)
+            return "buffers";
+        return nullptr;
+    }();
+    double failed = err ? 1.0 : 0.0;
+    if (allreduce_host(d, &failed, 1)) return fail("agreeing the set-up status");
+    if (failed > 0.0) return fail(err ? err : "another rank failed its set-up");
     if (agree_eliminations(d, plan)) return fail("agreeing the exact eliminations");
     if (hipStreamSynchronize(d->stream) != hipSuccess) return fail("sync");
     return d;
@@ -545,17 +675,22 @@ extern "C" int sss_hip_dist_cycle(sss_hip_dist *d)
         ResidFuse rf;   // the last C pass may form the residual's C rows (then only F rows remain)
         rf.r = L.wp;
         if ((rc = smooth(d, l, 0, &rf, l > 0))) return rc;   // levels >= 1 were just zeroed
-        if ((rc = exchange(d, l, L.x))) return rc;
-        if (rf.done) rc = launch_spmv_blocks(L.A, L.A.split_blk, SSS_HIP_SPMV_RESID, -1.0, L.x, L.b, L.wp, nullptr, s);
-        else rc = launch_spmv(L.A, SSS_HIP_SPMV_RESID, -1.0, L.x, L.b, L.wp, 0, nullptr, s);
+        if ((rc = residual(d, l, rf.done, nullptr))) return rc;
+        double *rdst = l + 1 < nagg ? d->L[l + 1].b : d->d_cown;   // restriction wp -> coarse b
+        if (!L.R.wave_rows && !L.R.vec_rows) {
+            int lrc = 0;
+            rc = split_launch(d, l, L.wp, L.ghostR, 0, L.R.nblk, [&](int b0, int b1) {
+                lrc = lrc ? lrc : launch_spmv_range(L.R, b0, b1, SSS_HIP_SPMV_MXY, 1.0, L.wp, nullptr, rdst, nullptr, s);
+            });
+            rc = rc ? rc : lrc;
+        } else if (!(rc = exchange(d, l, L.wp))) {
+            rc = launch_spmv(L.R, SSS_HIP_SPMV_MXY, 1.0, L.wp, nullptr, rdst, 0, nullptr, s);
+        }
         if (rc) return rc;
-        if ((rc = exchange(d, l, L.wp))) return rc;
         if (l + 1 < nagg) {
             DLevel &C = d->L[l + 1];
-            if ((rc = launch_spmv(L.R, SSS_HIP_SPMV_MXY, 1.0, L.wp, nullptr, C.b, 0, nullptr, s))) return rc;
             SSS_HIP(hipMemsetAsync(C.x, 0, sizeof(double) * (size_t)(C.m + C.g), s));
         } else {
-            if ((rc = launch_spmv(L.R, SSS_HIP_SPMV_MXY, 1.0, L.wp, nullptr, d->d_cown, 0, nullptr, s))) return rc;
             if ((rc = allgather_coarse(d))) return rc;
             double *tb = hier_vec(d->tail, 0, SSS_HIP_VEC_B), *tx = hier_vec(d->tail, 0, SSS_HIP_VEC_X);
             if (d->d_tail_perm)
@@ -569,20 +704,23 @@ extern "C" int sss_hip_dist_cycle(sss_hip_dist *d)
     if ((rc = sss_hip_cycle(d->tail))) return rc;   // replicated levels, same stream
     for (int l = nagg - 1; l >= 0; --l) {           // ascent
         DLevel &L = d->L[l];
-        const double *xc;
-        if (l + 1 < nagg) {
-            if ((rc = exchange(d, l + 1, d->L[l + 1].x))) return rc;
-            xc = d->L[l + 1].x;
-        } else {
-            xc = hier_vec(d->tail, 0, SSS_HIP_VEC_X);
-        }
+        double *xc = l + 1 < nagg ? d->L[l + 1].x : hier_vec(d->tail, 0, SSS_HIP_VEC_X);
         // dead F-row correction (see walk_cycle in sss_hier.hip): prolong into the C rows only
-        if (L.sm.f_overwritten && d->pars.post_iter > 0 && L.P.split_row == L.sm.pass[0].hi && L.P.split_row > 0 &&
-            !L.P.wave_rows && !L.P.vec_rows)
-            rc = launch_spmv_range(L.P, L.P.split_blk, L.P.nblk, SSS_HIP_SPMV_AMXPY, 1.0, xc, nullptr, L.x, nullptr, s);
-        else
-            rc = launch_spmv(L.P, SSS_HIP_SPMV_AMXPY, 1.0, xc, nullptr, L.x, 0, nullptr, s);
-        if (rc) return rc;
+        const bool tile = !L.P.wave_rows && !L.P.vec_rows;
+        const bool dead_f = L.sm.f_overwritten && d->pars.post_iter > 0 && L.P.split_row == L.sm.pass[0].hi &&
+                            L.P.split_row > 0 && tile;
+        int lrc = 0;
+        auto prolong = [&](int b0, int b1) {
+            lrc = lrc ? lrc : launch_spmv_range(L.P, b0, b1, SSS_HIP_SPMV_AMXPY, 1.0, xc, nullptr, L.x, nullptr, s);
+        };
+        if (l + 1 < nagg && tile) {   // the coarse correction's halo overlaps the interior blocks
+            rc = split_launch(d, l + 1, xc, L.ghostP, dead_f ? L.P.split_blk : 0, L.P.nblk, prolong);
+        } else {
+            if (l + 1 < nagg && (rc = exchange(d, l + 1, xc))) return rc;
+            if (dead_f) prolong(L.P.split_blk, L.P.nblk);
+            else rc = launch_spmv(L.P, SSS_HIP_SPMV_AMXPY, 1.0, xc, nullptr, L.x, 0, nullptr, s);
+        }
+        if (rc || (rc = lrc)) return rc;
         if (l == 0 && L.sm.fuse_resid && d->pars.post_iter > 0) {   // outer residual's C rows
             ResidFuse rf;
             rf.r = L.wp;
@@ -599,12 +737,8 @@ extern "C" int sss_hip_dist_cycle(sss_hip_dist *d)
 extern "C" int sss_hip_dist_residual_norm(sss_hip_dist *d, double *absres)
 {
     DLevel &L = d->L[0];
-    int rc;
-    if ((rc = exchange(d, 0, L.x))) return rc;
-    if (d->resid_c_ready)   // C rows and their partials came with the cycle's last pass
-        rc = launch_spmv_blocks(L.A, L.A.split_blk, SSS_HIP_SPMV_RESID, -1.0, L.x, L.b, L.wp, d->partial, d->stream);
-    else
-        rc = launch_spmv(L.A, SSS_HIP_SPMV_RESID, -1.0, L.x, L.b, L.wp, 0, d->partial, d->stream);
+    // C rows and their partials may have come with the cycle's last pass
+    int rc = residual(d, 0, d->resid_c_ready, d->partial);
     d->resid_c_ready = false;
     if (rc) return rc;
     if ((rc = launch_final_sum(d->partial, L.A.ngrid, d->d_norm, false, d->stream))) return rc;

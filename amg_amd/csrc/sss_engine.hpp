@@ -11,6 +11,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <functional>
 #include <cstdio>
 #include <thread>
 #include <vector>
@@ -246,10 +247,14 @@ struct ResidFuse {
 // Distributed levels: called before every class pass with x (exchange its ghosts), and after each
 // two-stage stage with the stage's full-length work vector; w0/w1 are full-length (own + ghost) work
 // vectors the two-stage form then writes its iterates into.
+// split (optional): refresh vec's ghosts while launching the row blocks [blo, bhi) of the level
+// matrix -- launch(b0, b1) for the blocks that read no ghost while the halo is in flight, then for
+// the others (or everything after a plain exchange).  Each row is computed exactly as in one launch.
 struct PassHooks {
     void *ctx = nullptr;
     int (*exchange)(void *ctx, double *vec) = nullptr;
     double *w0 = nullptr, *w1 = nullptr;
+    std::function<int(double *vec, int blo, int bhi, const std::function<void(int, int)> &launch)> split;
 };
 int smoother_build(SmootherPlan &sp, const SSS_MAT &A, const int *mark, int kind, const DevCSR *dA = nullptr,
                    int inner = 0, const int *gcls = nullptr, int enc = 0);

@@ -848,11 +848,16 @@ int smoother_run(const SmootherPlan &sp, const DevCSR &A, const double *b, doubl
             if (pre_f && sw == 0 && c == 0) continue;   // computed with the last residual (pre_f)
             // first pass on a just-zeroed iterate (C/F-Jacobi / two-stage): t = b, no matrix read
             const bool zfirst = x_zero && sw == 0 && c == 0 && sp.finite && sp.kind == SSS_HIP_SMOOTH_JACOBI;
+            // a plain tile-path relaxation pass (exact depth-1 GS-CF, or C/F-Jacobi) can overlap the
+            // halo with its interior blocks (PassHooks::split)
+            const bool fused_pass = rf && sp.fuse_resid && c == 1 && sw + 1 == sweeps;
+            const bool split_pass = hk && hk->split && !zfirst && !(A.wave_rows || A.vec_rows) && ps.range &&
+                                    (sp.kind != SSS_HIP_SMOOTH_JACOBI || sp.inner == 0) && !nocopy;
             if (hk) {   // distributed level: refresh x's ghosts; only contiguous passes qualify
                 if (!ps.range) return ERROR_INPUT_PAR;
                 // a zeroed x has zero ghosts (the descent clears own rows and ghosts); `finite` is
                 // agreed over the ranks, so every rank skips this exchange together
-                if (!zfirst && (rc = hk->exchange(hk->ctx, x))) return rc;
+                if (!zfirst && !split_pass && (rc = hk->exchange(hk->ctx, x))) return rc;
             }
             if (ps.range) {
                 const int nb = ps.bhi - ps.blo, m = ps.hi - ps.lo, nw = (m + 3) / 4;
@@ -861,7 +866,7 @@ int smoother_run(const SmootherPlan &sp, const DevCSR &A, const double *b, doubl
                 if (pre_f && sw == 0) xs = XSrc{pre_f, x, sp.pass[0].hi};   // this sweep's F values
                 // tile passes take each row's divisor from its staged diagonal (no deff stream)
                 const bool tile_d = sp.own_diag && A.pk != nullptr;
-                auto relax = [&](auto mode, const int *cols, const double *yp, double *y) {
+                auto relax = [&](auto mode, const int *cols, const double *yp, double *y) -> int {
                     constexpr int M = decltype(mode)::value;
                     if (wave && A.vec_rows)
                         hipLaunchKernelGGL((relax_range_wave<M, true>), dim3(nw), dim3(kBlock), 0, s, ps.lo, ps.hi,
@@ -869,11 +874,18 @@ int smoother_run(const SmootherPlan &sp, const DevCSR &A, const double *b, doubl
                     else if (wave)
                         hipLaunchKernelGGL((relax_range_wave<M, false>), dim3(nw), dim3(kBlock), 0, s, ps.lo, ps.hi,
                                            A.rp, cols, A.v, b, x, yp, y, deff, xs);
-                    else
-                        hipLaunchKernelGGL(relax_range<M>, dim3(nb), dim3(kBlock), 0, s, ps.blo, A.bk, A.rp, cols,
-                                           A.v, sp.diag_pos, ps.lo, b, x, yp, y, tile_d ? nullptr : deff, A.pk,
-                                           A.pv, A.pb, (double *)nullptr, (double *)nullptr, xs);
+                    else {
+                        auto go = [&](int b0, int b1) {
+                            hipLaunchKernelGGL(relax_range<M>, dim3(b1 - b0), dim3(kBlock), 0, s, b0, A.bk, A.rp,
+                                               cols, A.v, sp.diag_pos, ps.lo, b, x, yp, y, tile_d ? nullptr : deff,
+                                               A.pk, A.pv, A.pb, (double *)nullptr, (double *)nullptr, xs);
+                        };
+                        if (split_pass) return hk->split(x, ps.blo, ps.bhi, go);
+                        go(ps.blo, ps.bhi);
+                    }
+                    return 0;
                 };
+                (void)nb;
                 if (sp.kind == SSS_HIP_SMOOTH_JACOBI && sp.inner > 0 && hk) {
                     // iterates live in full-length work vectors whose ghosts (lower-rank rows of
                     // this class) are refreshed after every stage
@@ -904,8 +916,8 @@ int smoother_run(const SmootherPlan &sp, const DevCSR &A, const double *b, doubl
                                            A.v, (const int *)nullptr, b, deff, (double *)nullptr, prev + ps.lo);
                     else if (sp.inner > 0)
                         launch_ts_stage0(ps.ts_nl, ps.lo, ps.ts_split, b, xs, deff, ps.ts_P, prev + ps.lo, s);
-                    else
-                        relax(std::integral_constant<int, 1>(), A.ci, (const double *)nullptr, prev + ps.lo);
+                    else if ((rc = relax(std::integral_constant<int, 1>(), A.ci, (const double *)nullptr, prev + ps.lo)))
+                        return rc;
                     for (int st = 0; st < sp.inner; ++st) {
                         launch_ts_inner(ps.ts_lo, ps.lo, deff, ps.ts_P, prev, 0, prev + ps.lo, next + ps.lo, s);
                         std::swap(prev, next);
@@ -926,15 +938,22 @@ int smoother_run(const SmootherPlan &sp, const DevCSR &A, const double *b, doubl
                                        ps.lo, m, A.rp, A.ci, A.v, (const int *)nullptr, b, deff, (double *)nullptr,
                                        x + ps.lo);
                 } else if (sp.kind == SSS_HIP_SMOOTH_JACOBI) {
-                    relax(std::integral_constant<int, 1>(), A.ci, (const double *)nullptr, ps.y);
+                    if ((rc = relax(std::integral_constant<int, 1>(), A.ci, (const double *)nullptr, ps.y))) return rc;
                     SSS_HIP(hipMemcpyAsync(x + ps.lo, ps.y, sizeof(double) * (size_t)m, hipMemcpyDeviceToDevice, s));
-                } else if (rf && sp.fuse_resid && c == 1 && sw + 1 == sweeps) {
-                    hipLaunchKernelGGL(relax_range<2>, dim3(nb), dim3(kBlock), 0, s, ps.blo, A.bk, A.rp, A.ci, A.v,
-                                       sp.diag_pos, ps.lo, b, x, (const double *)nullptr, (double *)nullptr,
-                                       tile_d ? nullptr : deff, A.pk, A.pv, A.pb, rf->r, rf->partial, xs);
+                } else if (fused_pass) {
+                    auto go = [&](int b0, int b1) {
+                        hipLaunchKernelGGL(relax_range<2>, dim3(b1 - b0), dim3(kBlock), 0, s, b0, A.bk, A.rp, A.ci,
+                                           A.v, sp.diag_pos, ps.lo, b, x, (const double *)nullptr, (double *)nullptr,
+                                           tile_d ? nullptr : deff, A.pk, A.pv, A.pb, rf->r, rf->partial, xs);
+                    };
+                    if (split_pass) {
+                        if ((rc = hk->split(x, ps.blo, ps.bhi, go))) return rc;
+                    } else {
+                        go(ps.blo, ps.bhi);
+                    }
                     rf->done = true;
-                } else {
-                    relax(std::integral_constant<int, 0>(), A.ci, (const double *)nullptr, (double *)nullptr);
+                } else if ((rc = relax(std::integral_constant<int, 0>(), A.ci, (const double *)nullptr, (double *)nullptr))) {
+                    return rc;
                 }
                 if (pre_f && sw == 0 && c == 1 && sweeps == 1)   // no later F pass overwrites x_F
                     SSS_HIP(hipMemcpyAsync(x, pre_f, sizeof(double) * (size_t)sp.pass[0].hi, hipMemcpyDeviceToDevice, s));

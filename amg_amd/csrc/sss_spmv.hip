@@ -480,7 +480,7 @@ int launch_spmv_range(const DevCSR &A, int blo, int bhi, int op, double alpha, c
                       double *y, double *partial, hipStream_t s)
 {
     if (A.wave_rows || A.vec_rows || blo < 0 || bhi > A.nblk) return ERROR_INPUT_PAR;
-    if (op != SSS_HIP_SPMV_RESID && op != SSS_HIP_SPMV_AMXPY) return ERROR_INPUT_PAR;
+    if (op != SSS_HIP_SPMV_RESID && op != SSS_HIP_SPMV_AMXPY && op != SSS_HIP_SPMV_MXY) return ERROR_INPUT_PAR;
     const int nb = bhi - blo;
     if (nb <= 0) return 0;
     // the kernel indexes blocks from 0: shift the block-indexed arrays
@@ -488,6 +488,9 @@ int launch_spmv_range(const DevCSR &A, int blo, int bhi, int op, double alpha, c
     double *pp = partial ? partial + blo : nullptr;
     if (op == SSS_HIP_SPMV_AMXPY)
         hipLaunchKernelGGL((spmv_adaptive<SSS_HIP_SPMV_AMXPY, false>), dim3(nb), dim3(kBlock), 0, s, A.bk + blo, A.rp,
+                           A.ci, A.v, x, b, y, alpha, 0, pp, A.pk, A.pv, pb);
+    else if (op == SSS_HIP_SPMV_MXY)
+        hipLaunchKernelGGL((spmv_adaptive<SSS_HIP_SPMV_MXY, false>), dim3(nb), dim3(kBlock), 0, s, A.bk + blo, A.rp,
                            A.ci, A.v, x, b, y, alpha, 0, pp, A.pk, A.pv, pb);
     else if (partial)
         hipLaunchKernelGGL((spmv_adaptive<SSS_HIP_SPMV_RESID, true>), dim3(nb), dim3(kBlock), 0, s, A.bk + blo, A.rp,

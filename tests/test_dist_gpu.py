@@ -122,6 +122,15 @@ def test_dist_free_order(kind, n, smoother):
     _run(2, "host", kind, n, smoother, 2, 100, sum_order=1)
 
 
+@pytest.mark.parametrize("kind,n,smoother", [(7, 24, "hybrid"), (7, 24, "jacobi"), (27, 14, "jacobi")])
+def test_dist_overlap_split_launches(kind, n, smoother, monkeypatch):
+    """The halo-overlap launch order (blocks that read no ghost first, the others after the
+    halo; SSS_HIP_OVERLAP=2 applies it over the synchronous host transport too): every row block
+    is launched exactly once with the right inputs -- still bitwise the single-GPU engine."""
+    monkeypatch.setenv("SSS_HIP_OVERLAP", "2")
+    _run(2, "host", kind, n, smoother, 2, 100)
+
+
 @pytest.mark.parametrize("kind,n,smoother,sum_order", [(7, 24, "hybrid", 0), (27, 14, "jacobi", 0), (7, 24, "hybrid", 1)])
 def test_dist_from_partition_files(kind, n, smoother, sum_order, tmp_path):
     """Engines built from a partition set (sss_part_save -> sss_hip_dist_create_from_files, the
