@@ -163,6 +163,7 @@ struct GsPersist {
     int engine = 0;
     int lo = 0, hi = 0;                 // the pass's contiguous rows
     int G = 64;                         // flow: lanes per row (64 / G rows of one depth per ticket)
+    bool natural = false, desc = false; // natural-order GS (x = t * d), descending row order
     int nchunks = 0, grid = 0;
     int *ck = nullptr;                  // flow, short rows: chunk -> first position (nchunks + 1)
     int *h_off = nullptr;               // cu: depth offsets (depth + 1)
@@ -194,13 +195,22 @@ struct PassSchedule {          // rows of one class (F or C), grouped by DAG dep
     double *y = nullptr;       // Jacobi: new values of this class, scattered after the pass
     GsPersist gp;              // exact GS with depth > 1: one launch per pass when set up
 };
-int gs_persist_build(PassSchedule &ps, const SSS_MAT &A, int lo, int hi, bool long_rows);
+// natural: x_i = t * d (unguarded, d = 1 / a_ii); desc: rows taken in descending order (the
+// rows a row waits for are the same-pass rows above it)
+int gs_persist_build(PassSchedule &ps, const SSS_MAT &A, int lo, int hi, bool long_rows, bool natural = false,
+                     bool desc = false);
 void gs_persist_free(PassSchedule &ps);
 int gs_persist_run(const PassSchedule &ps, const DevCSR &A, const double *b, double *x, const double *deff,
                    hipStream_t s);
 int gs_persist_error(const PassSchedule &ps, unsigned *out);
 struct SmootherPlan {
     int kind = SSS_HIP_SMOOTH_EXACT;
+    // Natural-order GS (SSS_amg_smoother_gs, Solve/SSS_smooth.c:90-137: cf_order = 0 or no C/F
+    // marker): pass[0] = the rows ascending (pre-smoother), pass[1] = descending (post), each one
+    // class; x_i = t * d with d = 1 / a_ii carried across rows (d_first/d_later per direction:
+    // d_first, d_later for pass[0]; nd_first, nd_later for pass[1]).
+    bool natural = false;
+    double *nd_first = nullptr, *nd_later = nullptr;
     PassSchedule pass[2];      // [0] = F pass (mark != 1), [1] = C pass (mark == 1)
     double *d_first = nullptr; // effective divisor for the first sweep of a call
     double *d_later = nullptr; // ... for later sweeps (aliases d_first when all rows have a diagonal)
@@ -258,6 +268,8 @@ struct PassHooks {
 };
 int smoother_build(SmootherPlan &sp, const SSS_MAT &A, const int *mark, int kind, const DevCSR *dA = nullptr,
                    int inner = 0, const int *gcls = nullptr, int enc = 0);
+// Natural-order GS over the rows [lo, hi) (both directions; see SmootherPlan::natural).
+int smoother_build_natural(SmootherPlan &sp, const SSS_MAT &A, int lo, int hi);
 // Where a pass reads its x values from: columns < split from f, the others from c.  The no-copy
 // C/F-Jacobi form keeps each class's current values in x or in the plan's second vector x2.
 struct XSrc {
@@ -273,7 +285,7 @@ void launch_ts_inner(const DevCSR &M, int lo, const double *deff, const double *
 void smoother_free(SmootherPlan &sp);
 int smoother_run(const SmootherPlan &sp, const DevCSR &A, const double *b, double *x, int sweeps,
                  hipStream_t stream, const PassHooks *hooks = nullptr, ResidFuse *rf = nullptr,
-                 const double *pre_f = nullptr, bool x_zero = false);
+                 const double *pre_f = nullptr, bool x_zero = false, bool post = false);
 // r = b - A x over the F rows (+ per-block partials) and pend = the F pass's GS values from this x
 // (SmootherPlan::pend_ok).
 int launch_f_residual_pending(const SmootherPlan &sp, const DevCSR &A, const double *b, const double *x, double *r,

@@ -37,6 +37,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <string>
+#include <type_traits>
 
 namespace sss {
 
@@ -138,15 +139,17 @@ constexpr int kGroupBuf = 2048;   // staged products per wave (16 KiB; 64 KiB pe
 // are already published -- into the wave's LDS row buffer, keeping a bit per still-pending entry;
 // (B) they wait for the pending granules and fill those products; (C) the row's first lane runs
 // the stored-order chain over the buffer.  A row never waits before all its own loads are issued.
-template <int G>
+template <int G, bool NAT, bool DESC>
 __global__ __launch_bounds__(kBlock) void gs_flow_group(int nchunks, const int *__restrict__ ck,
                                                         const int *__restrict__ rows, const int *__restrict__ rp,
                                                         const int *__restrict__ ci, const double *__restrict__ v,
                                                         const double *__restrict__ b, double *x,
                                                         const double *__restrict__ deff, unsigned long long *gran,
-                                                        int lo, unsigned *ctl)
+                                                        int lo, int hi, unsigned *ctl)
 {
     constexpr int R = 64 / G, CAP = kGroupBuf / R, U = 8;
+    // a same-pass row this row reads the NEW value of (published by its granules)
+    auto dynamic = [&](int c, int i) { return DESC ? (c > i && c < hi) : (c >= lo && c < i); };
     static_assert(CAP / G == 32, "one pending bit per staged entry of a lane");
     __shared__ double buf[kBlock / 64][kGroupBuf];
     const int lane = threadIdx.x & 63, grp = lane / G, gl = lane % G;
@@ -186,14 +189,14 @@ __global__ __launch_bounds__(kBlock) void gs_flow_group(int nchunks, const int *
 #pragma unroll
                 for (int u = 0; u < U; ++u) {
                     xv[u] = 0.0;
-                    if (c[u] != i && !(c[u] >= lo && c[u] < i)) xv[u] = x[c[u]];
+                    if (c[u] != i && !dynamic(c[u], i)) xv[u] = x[c[u]];
                 }
 #pragma unroll
                 for (int u = 0; u < U; ++u) {
                     if (j0 + u >= nj) continue;
                     const int t = gl + G * (j0 + u);
                     double val = 0.0;   // the diagonal: subtracting +0.0 is the identity
-                    if (c[u] >= lo && c[u] < i) {
+                    if (dynamic(c[u], i)) {
                         double g = 0.0;
                         if (granule_get(gran + 2 * (size_t)(c[u] - lo), epoch, g)) val = a[u] * g;
                         else pend |= 1u << (j0 + u);
@@ -216,7 +219,8 @@ __global__ __launch_bounds__(kBlock) void gs_flow_group(int nchunks, const int *
         }
         if (active && gl == 0) {
             const double d = deff[i];
-            const double xn = fabs(d) > SMALLFLOAT ? acc / d : x_own(x, i);
+            // natural order (Solve/SSS_smooth.c:112): x_i = t * d, d the carried reciprocal
+            const double xn = NAT ? acc * d : fabs(d) > SMALLFLOAT ? acc / d : x_own(x, i);
             x[i] = xn;
             granule_put(gran + 2 * (size_t)(i - lo), epoch, xn);
         }
@@ -320,11 +324,14 @@ static const char *gs_engine_env()
 
 // Rows of the pass are ps.h_off-ordered by depth; A is the level matrix (host), [lo, hi) the pass's
 // contiguous row range.  Chooses the engine and builds its device data.
-int gs_persist_build(PassSchedule &ps, const SSS_MAT &A, int lo, int hi, bool long_rows)
+int gs_persist_build(PassSchedule &ps, const SSS_MAT &A, int lo, int hi, bool long_rows, bool natural, bool desc)
 {
     GsPersist &g = ps.gp;
     g = GsPersist();
-    const std::string want = gs_engine_env();
+    g.natural = natural;
+    g.desc = desc;
+    std::string want = gs_engine_env();
+    if ((natural || desc) && want == "cu") want = "flow";   // the single-CU engine runs GS-CF passes only
     if (want == "launch" || ps.depth <= 1 || ps.nrows == 0) return 0;
     const int *rp = A.row_ptr, *ci = A.col_idx;
     long long nnz = 0;
@@ -444,15 +451,23 @@ int gs_persist_run(const PassSchedule &ps, const DevCSR &A, const double *b, dou
     } else if (g.engine == 1) {
         auto go = [&](auto kern) {
             hipLaunchKernelGGL(kern, dim3(g.grid), dim3(kBlock), 0, s, g.nchunks, g.ck, ps.rows, A.rp, A.ci, A.v, b, x,
-                               deff, g.gran, g.lo, g.ctl);
+                               deff, g.gran, g.lo, g.hi, g.ctl);
         };
-        switch (g.G) {
-        case 4: go(gs_flow_group<4>); break;
-        case 8: go(gs_flow_group<8>); break;
-        case 16: go(gs_flow_group<16>); break;
-        case 32: go(gs_flow_group<32>); break;
-        default: go(gs_flow_group<64>); break;
-        }
+        auto by_g = [&](auto nat, auto desc) {
+            constexpr bool N = decltype(nat)::value, D = decltype(desc)::value;
+            switch (g.G) {
+            case 4: go(gs_flow_group<4, N, D>); break;
+            case 8: go(gs_flow_group<8, N, D>); break;
+            case 16: go(gs_flow_group<16, N, D>); break;
+            case 32: go(gs_flow_group<32, N, D>); break;
+            default: go(gs_flow_group<64, N, D>); break;
+            }
+        };
+        using T = std::true_type;
+        using F = std::false_type;
+        if (g.natural && g.desc) by_g(T(), T());
+        else if (g.natural) by_g(T(), F());
+        else by_g(F(), F());
     } else {
         return ERROR_INPUT_PAR;
     }

@@ -127,6 +127,13 @@ int sss::level_encoding(const sss_hip_opts &o)
 }
 int sss::level_inner_of(const sss_hip_opts &o, int l) { return level_inner(o, l); }
 
+// Natural-order GS (SSS_amg_smoother_pre/post with cf_order = 0, Solve/SSS_smooth.c:171-176,
+// 256-260) on the levels the reference would smooth by GS
+static bool natural_level(const sss_hip_hier *h, int gl)
+{
+    return h->pars.cf_order == 0 && h->pars.smoother == SSS_SM_GS && level_smoother_kind(h->opts, gl) == SSS_HIP_SMOOTH_EXACT;
+}
+
 static void hier_release(sss_hip_hier *h)
 {
     if (!h) return;
@@ -260,6 +267,7 @@ sss_hip_hier *sss::hier_create_impl(const SSS_AMG *mg, const sss_hip_opts *o, in
             // two-stage levels need contiguous classes; otherwise follow opts.relabel
             const int gl = h->level_base + l;
             const bool two_stage = level_inner(h->opts, gl) > 0;
+            if (natural_level(h, gl)) continue;   // the natural order is the stored row order
             if (!two_stage && !(h->opts.relabel == 1 || (h->opts.relabel == 2 && gl > 0))) continue;
             auto &perm = h->L[l].perm;
             perm.reserve(n);
@@ -297,9 +305,12 @@ sss_hip_hier *sss::hier_create_impl(const SSS_AMG *mg, const sss_hip_opts *o, in
             t_sm = now();
         } else {
             if (devcsr_upload(L.A, C.A, -1, enc)) return fail("upload A");
-            if (l < h->nl - 1 && smoother_build(L.sm, C.A, C.cfmark.d, level_smoother_kind(h->opts, h->level_base + l),
-                                                nullptr, 0, nullptr, enc))
+            if (l < h->nl - 1 && natural_level(h, h->level_base + l)) {
+                if (smoother_build_natural(L.sm, C.A, 0, n)) return fail("smoother plan");
+            } else if (l < h->nl - 1 && smoother_build(L.sm, C.A, C.cfmark.d, level_smoother_kind(h->opts, h->level_base + l),
+                                                       nullptr, 0, nullptr, enc)) {
                 return fail("smoother plan");
+            }
         }
         if (l < h->nl - 1) {
             const auto &pc = h->L[l + 1].perm;   // (filled above for every relabeled level)
@@ -455,7 +466,7 @@ extern "C" int sss_hip_smooth(sss_hip_hier *h, int level, int post)
     const int sweeps = post ? h->pars.post_iter : h->pars.pre_iter;
     h->resid_c_ready = false;
     h->pending_f = false;
-    return smoother_run(L.sm, L.A, L.b, L.x, sweeps, h->stream);
+    return smoother_run(L.sm, L.A, L.b, L.x, sweeps, h->stream, nullptr, nullptr, nullptr, false, post != 0);
 }
 
 // Smoothing that leaves r = b - A x in wp: fused into the last C pass where the plan allows,
@@ -469,7 +480,7 @@ static int smooth_then_residual(sss_hip_hier *h, int l, int post, double *partia
     ResidFuse rf;
     rf.r = L.wp;
     rf.partial = partial;
-    int rc = smoother_run(L.sm, L.A, L.b, L.x, sweeps, h->stream, nullptr, &rf, pre_f, x_zero);
+    int rc = smoother_run(L.sm, L.A, L.b, L.x, sweeps, h->stream, nullptr, &rf, pre_f, x_zero, post != 0);
     if (rc) return rc;
     if (rf.done) return launch_spmv_blocks(L.A, L.A.split_blk, SSS_HIP_SPMV_RESID, -1.0, L.x, L.b, L.wp, partial, h->stream);
     return launch_spmv(L.A, SSS_HIP_SPMV_RESID, -1.0, L.x, L.b, L.wp, 0, partial, h->stream);
@@ -515,7 +526,8 @@ static int walk_cycle(sss_hip_hier *h, CoarseFn coarse, bool pend = false)
                 ResidFuse rf;
                 rf.r = L.wp;
                 rf.partial = h->partial;
-                if ((rc = smoother_run(L.sm, L.A, L.b, L.x, h->pars.post_iter, s, nullptr, &rf))) return rc;
+                if ((rc = smoother_run(L.sm, L.A, L.b, L.x, h->pars.post_iter, s, nullptr, &rf, nullptr, false, true)))
+                    return rc;
             } else if ((rc = sss_hip_smooth(h, l, 1))) {
                 return rc;
             }
@@ -801,24 +813,32 @@ extern "C" int sss_hip_host_smooth(const SSS_SMTR *s, int post)
     if (sss_hip_device_count() <= 0) return ERROR_MISC;
     const int n = s->A->num_rows;
     const int use_cf = s->cf_order && s->ordering;
-    if (!use_cf && s->smoother == SSS_SM_GS) {
-        fprintf(stderr, "### ERROR: natural-order Gauss-Seidel (cf_order = 0) is not offered by the GPU engine\n");
+    const bool natural = !use_cf && s->smoother == SSS_SM_GS;
+    // natural order (Solve/SSS_smooth.c:171-176, 256-260): pre i = istart .. iend, post i = iend ..
+    // istart, by istep; a loop whose bounds are crossed for its direction runs no row
+    const int i1 = post ? s->iend : s->istart, in = post ? s->istart : s->iend, step = s->istep;
+    if (natural && step != 1 && step != -1) {
+        fprintf(stderr, "### ERROR: natural-order Gauss-Seidel on the GPU needs istep = +1 or -1 (got %d)\n", step);
         return ERROR_INPUT_PAR;
     }
+    const bool desc = step < 0;
+    const int lo = desc ? in : i1, hi = (desc ? i1 : in) + 1;
+    if (natural && (lo < 0 || hi > n)) return ERROR_INPUT_PAR;
+    if (natural && lo >= hi) return 0;
     HostCSR M;
     SmootherPlan sp;
     if (devcsr_upload(M.d, *s->A)) return ERROR_MISC;
-    if (smoother_build(sp, *s->A, use_cf ? s->ordering : nullptr,
-                       s->smoother == SSS_SM_JACOBI ? SSS_HIP_SMOOTH_JACOBI : SSS_HIP_SMOOTH_EXACT)) {
+    if (natural ? smoother_build_natural(sp, *s->A, lo, hi)
+                : smoother_build(sp, *s->A, use_cf ? s->ordering : nullptr,
+                                 s->smoother == SSS_SM_JACOBI ? SSS_HIP_SMOOTH_JACOBI : SSS_HIP_SMOOTH_EXACT)) {
         smoother_free(sp);
         return ERROR_MISC;
     }
-    (void)post;
     double *dx = dev_alloc<double>((size_t)n), *db = dev_alloc<double>((size_t)n);
     int rc = (!dx || !db) ? ERROR_ALLOC_MEM : 0;
     if (!rc && hipMemcpy(dx, s->x->d, sizeof(double) * n, hipMemcpyHostToDevice) != hipSuccess) rc = ERROR_MISC;
     if (!rc && hipMemcpy(db, s->b->d, sizeof(double) * n, hipMemcpyHostToDevice) != hipSuccess) rc = ERROR_MISC;
-    if (!rc) rc = smoother_run(sp, M.d, db, dx, s->nsweeps, nullptr);
+    if (!rc) rc = smoother_run(sp, M.d, db, dx, s->nsweeps, nullptr, nullptr, nullptr, nullptr, false, natural && desc);
     if (!rc && hipMemcpy(s->x->d, dx, sizeof(double) * n, hipMemcpyDeviceToHost) != hipSuccess) rc = ERROR_MISC;
     dev_free(dx);
     dev_free(db);

@@ -364,6 +364,8 @@ void smoother_free(SmootherPlan &sp)
     }
     if (sp.d_later != sp.d_first) dev_free(sp.d_later);
     dev_free(sp.d_first);
+    dev_free(sp.nd_first);
+    dev_free(sp.nd_later);
     dev_free(sp.cls);
     dev_free(sp.diag_pos);
     dev_free(sp.x2);
@@ -371,7 +373,9 @@ void smoother_free(SmootherPlan &sp)
 }
 
 // ---- kernels -------------------------------------------------------------------------------
-// exact GS, one thread per row of the current depth
+// exact GS, one thread per row of the current depth.  NAT: natural-order GS (Solve/SSS_smooth.c:
+// 90-137), x_i = t * d with d the carried reciprocal of the diagonal, written unconditionally.
+template <bool NAT>
 __global__ __launch_bounds__(kBlock) void gs_depth_thread(const int *__restrict__ rows, int cnt,
                                                           const int *__restrict__ rp, const int *__restrict__ ci,
                                                           const double *__restrict__ v, const double *__restrict__ b,
@@ -386,11 +390,13 @@ __global__ __launch_bounds__(kBlock) void gs_depth_thread(const int *__restrict_
         if (j != i) acc -= v[k] * x[j];
     }
     const double d = deff[i];
-    if (fabs(d) > SMALLFLOAT) x[i] = acc / d;
+    if (NAT) x[i] = acc * d;
+    else if (fabs(d) > SMALLFLOAT) x[i] = acc / d;
 }
 
 // exact GS on long rows: four rows of the current depth per workgroup, one per wave; lanes
 // gather the products, lane 0 subtracts them in CSR order (sss_spmv_dev.hpp wave_row_chain).
+template <bool NAT>
 __global__ __launch_bounds__(kBlock) void gs_depth_wave(const int *__restrict__ rows, int cnt,
                                                         const int *__restrict__ rp, const int *__restrict__ ci,
                                                         const double *__restrict__ v, const double *__restrict__ b,
@@ -405,7 +411,8 @@ __global__ __launch_bounds__(kBlock) void gs_depth_wave(const int *__restrict__ 
         rp[i], rp[i + 1], ci, v, [&](int c, double a) { return c == i ? 0.0 : a * x[c]; }, b[i], strips[wave]);
     if ((threadIdx.x & 63) == 0) {
         const double d = deff[i];
-        if (fabs(d) > SMALLFLOAT) x[i] = acc / d;
+        if (NAT) x[i] = acc * d;
+        else if (fabs(d) > SMALLFLOAT) x[i] = acc / d;
     }
 }
 
@@ -829,9 +836,101 @@ __global__ __launch_bounds__(kBlock) void scatter_rows(int m, const int *__restr
     if (r < m) x[map[r]] = y[r];
 }
 
-int smoother_run(const SmootherPlan &sp, const DevCSR &A, const double *b, double *x, int sweeps, hipStream_t s,
-                 const PassHooks *hk, ResidFuse *rf, const double *pre_f, bool x_zero)
+// One launch per DAG depth of an exact pass (the schedule of PassSchedule::h_off).
+static int depth_launches(const PassSchedule &ps, bool long_rows, bool nat, const DevCSR &A, const double *b, double *x,
+                          const double *deff, hipStream_t s)
 {
+    for (int l = 0; l < ps.depth; ++l) {
+        const int off = ps.h_off[l], cnt = ps.h_off[l + 1] - off;
+        if (cnt == 0) continue;
+        if (long_rows)
+            hipLaunchKernelGGL(nat ? gs_depth_wave<true> : gs_depth_wave<false>, dim3((cnt + 3) / 4), dim3(kBlock), 0, s,
+                               ps.rows + off, cnt, A.rp, A.ci, A.v, b, x, deff);
+        else
+            hipLaunchKernelGGL(nat ? gs_depth_thread<true> : gs_depth_thread<false>, dim3((cnt + kBlock - 1) / kBlock),
+                               dim3(kBlock), 0, s, ps.rows + off, cnt, A.rp, A.ci, A.v, b, x, deff);
+    }
+    SSS_HIP(hipGetLastError());
+    return 0;
+}
+
+int smoother_build_natural(SmootherPlan &sp, const SSS_MAT &A, int lo, int hi)
+{
+    const int n = A.num_rows, m = hi - lo;
+    const int *rp = A.row_ptr, *ci = A.col_idx;
+    const double *v = A.val;
+    int rc;
+    sp.kind = SSS_HIP_SMOOTH_EXACT;
+    sp.natural = true;
+    long long nnz = 0;
+    for (int i = lo; i < hi; ++i) nnz += rp[i + 1] - rp[i];
+    sp.long_rows = m > 0 && nnz >= (long long)std::min(32, wave_row_min()) * m;
+    // the carried reciprocal d (Solve/SSS_smooth.c:106-109): per direction, first sweep from
+    // d = 0, later sweeps from the previous sweep's last value
+    std::vector<double> df[2] = {std::vector<double>(n, 0.0), std::vector<double>(n, 0.0)},
+                        dl[2] = {std::vector<double>(n, 0.0), std::vector<double>(n, 0.0)};
+    for (int dir = 0; dir < 2; ++dir) {
+        double d = 0.0;
+        for (int sweep = 0; sweep < 2; ++sweep)
+            for (int q = 0; q < m; ++q) {
+                const int i = dir == 0 ? lo + q : hi - 1 - q;
+                for (int k = rp[i]; k < rp[i + 1]; ++k)
+                    if (ci[k] == i && SSS_ABS(v[k]) > SMALLFLOAT) d = 1.e+0 / v[k];
+                (sweep == 0 ? df : dl)[dir][i] = d;
+            }
+    }
+    // level schedules: ascending (row i reads the new x_j of coupled j < i, the old x_j of j > i,
+    // which must wait for it) and descending (mirrored)
+    for (int dir = 0; dir < 2; ++dir) {
+        PassSchedule &ps = sp.pass[dir];
+        std::vector<int> depth(n, 0), pushed(n, 0);
+        auto in = [&](int j) { return j >= lo && j < hi; };
+        for (int q = 0; q < m; ++q) {
+            const int i = dir == 0 ? lo + q : hi - 1 - q;
+            int dep = pushed[i];
+            for (int k = rp[i]; k < rp[i + 1]; ++k) {
+                const int j = ci[k];
+                if (in(j) && (dir == 0 ? j < i : j > i)) dep = std::max(dep, depth[j] + 1);
+            }
+            depth[i] = dep;
+            for (int k = rp[i]; k < rp[i + 1]; ++k) {
+                const int j = ci[k];
+                if (in(j) && (dir == 0 ? j > i : j < i)) pushed[j] = std::max(pushed[j], dep + 1);
+            }
+        }
+        int maxd = -1;
+        for (int i = lo; i < hi; ++i) maxd = std::max(maxd, depth[i]);
+        ps.depth = maxd + 1;
+        ps.h_off.assign(ps.depth + 1, 0);
+        for (int i = lo; i < hi; ++i) ps.h_off[depth[i] + 1]++;
+        for (int l = 0; l < ps.depth; ++l) ps.h_off[l + 1] += ps.h_off[l];
+        ps.nrows = m;
+        std::vector<int> fill(ps.h_off.begin(), ps.h_off.end()), rows(std::max(m, 1));
+        for (int i = lo; i < hi; ++i) rows[fill[depth[i]]++] = i;
+        if ((rc = upload_ints(&ps.rows, rows))) return rc;
+        if (ps.depth > 1 && (rc = gs_persist_build(ps, A, lo, hi, sp.long_rows, true, dir == 1))) return rc;
+    }
+    if ((rc = upload_doubles(&sp.d_first, df[0])) || (rc = upload_doubles(&sp.d_later, dl[0])) ||
+        (rc = upload_doubles(&sp.nd_first, df[1])) || (rc = upload_doubles(&sp.nd_later, dl[1])))
+        return rc;
+    return 0;
+}
+
+int smoother_run(const SmootherPlan &sp, const DevCSR &A, const double *b, double *x, int sweeps, hipStream_t s,
+                 const PassHooks *hk, ResidFuse *rf, const double *pre_f, bool x_zero, bool post)
+{
+    if (sp.natural) {   // natural-order GS: ascending pre-smoother, descending post-smoother
+        if (hk || pre_f) return ERROR_INPUT_PAR;
+        if (rf) rf->done = false;
+        const PassSchedule &ps = sp.pass[post ? 1 : 0];
+        if (ps.nrows == 0) return 0;
+        for (int sw = 0; sw < sweeps; ++sw) {
+            const double *deff = post ? (sw == 0 ? sp.nd_first : sp.nd_later) : (sw == 0 ? sp.d_first : sp.d_later);
+            int rc = ps.gp.engine ? gs_persist_run(ps, A, b, x, deff, s) : depth_launches(ps, sp.long_rows, true, A, b, x, deff, s);
+            if (rc) return rc;
+        }
+        return 0;
+    }
     if (rf) rf->done = false;
     if (pre_f && (!sp.pend_ok || hk || sweeps < 1)) return ERROR_INPUT_PAR;
     const int n = A.n;
@@ -983,16 +1082,7 @@ int smoother_run(const SmootherPlan &sp, const DevCSR &A, const double *b, doubl
                 if ((rc = gs_persist_run(ps, A, b, x, deff, s))) return rc;
                 continue;
             }
-            for (int l = 0; l < ps.depth; ++l) {
-                const int off = ps.h_off[l], cnt = ps.h_off[l + 1] - off;
-                if (cnt == 0) continue;
-                if (sp.long_rows)
-                    hipLaunchKernelGGL(gs_depth_wave, dim3((cnt + 3) / 4), dim3(kBlock), 0, s, ps.rows + off, cnt, A.rp,
-                                       A.ci, A.v, b, x, deff);
-                else
-                    hipLaunchKernelGGL(gs_depth_thread, dim3((cnt + kBlock - 1) / kBlock), dim3(kBlock), 0, s,
-                                       ps.rows + off, cnt, A.rp, A.ci, A.v, b, x, deff);
-            }
+            if ((rc = depth_launches(ps, sp.long_rows, false, A, b, x, deff, s))) return rc;
         }
     }
     for (int c = 0; c < 2; ++c)   // odd number of writes to a class (odd sweeps x (1 + inner))

@@ -76,7 +76,10 @@ def parse():
                    help="0: stored CSR order everywhere (bitwise kernels); 1: tree-summed long rows "
                         "(default: 1 in throughput mode, 0 in parity mode)")
     p.add_argument("--sorted-tiles", type=int, default=None, help="column-sorted tile staging (default 1)")
-    return p.parse_args()
+    argv = None
+    if "WORLD_SIZE" in os.environ and "SSS_BENCH_ARGV" in os.environ:   # ranks spawned by spawn_ranks()
+        argv = json.loads(os.environ["SSS_BENCH_ARGV"])
+    return p.parse_args(argv)
 
 
 class Dist:
@@ -212,9 +215,12 @@ def spawn_ranks(n: int) -> int:
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
         port = s.getsockname()[1]
+    # the ranks get this command line through the environment: torch.distributed.run would try to
+    # parse options such as --n itself
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
-           "--master-addr=127.0.0.1", f"--master-port={port}", str(Path(__file__).resolve())] + sys.argv[1:]
-    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY=os.environ.get("HSA_ENABLE_IPC_MODE_LEGACY", "0"))
+           "--master-addr=127.0.0.1", f"--master-port={port}", str(Path(__file__).resolve())]
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY=os.environ.get("HSA_ENABLE_IPC_MODE_LEGACY", "0"),
+               SSS_BENCH_ARGV=json.dumps(sys.argv[1:]))
     return subprocess.call(cmd, env=env)
 
 

@@ -142,3 +142,87 @@ def test_repeated_launches_stay_bitwise(p32_h, monkeypatch):
             D.close()
     for eng in ("flow", "cu"):
         assert np.array_equal(out[eng].view(np.uint64), out["launch"].view(np.uint64)), eng
+
+
+# ---------------------------------------------------------------- natural-order GS (row a5)
+def _natural(H):
+    """The hierarchy with the reference's cf_order = 0 (SSS_amg_smoother_pre/post then call
+    SSS_amg_smoother_gs, Solve/SSS_smooth.c:171-176, 256-260)."""
+    H.mg.pars.cf_order = 0
+    return H
+
+
+@pytest.mark.parametrize("hname", ["bus_h", "p32_h", "a27_h"])
+def test_natural_gs_levels_bitwise(request, hname, engine):
+    H = _natural(request.getfixturevalue(hname))
+    ora = oracle.load()
+    D = A.DeviceHierarchy(H, smoother="exact", coarse="krylov")
+    rng = np.random.default_rng(41)
+    try:
+        for l in range(H.num_levels - 1):
+            L = H.level(l)
+            n = L.A.num_rows
+            for post in (False, True):
+                b = rng.standard_normal(n)
+                x0 = rng.standard_normal(n)
+                D.upload(l, "b", b)
+                D.upload(l, "x", x0)
+                D.smooth(l, post)
+                xg = D.download(l, "x")
+                xr = x0.copy()
+                sweeps = H.pars.post_iter if post else H.pars.pre_iter
+                sr = _smtr(L.A, b, xr, L.cfmark.d, sweeps, post)
+                sr.cf_order = 0
+                (ora.ora_smoother_post if post else ora.ora_smoother_pre)(C.byref(sr))
+                assert np.array_equal(xg.view(np.uint64), xr.view(np.uint64)), (hname, l, post, engine)
+            info = D.level_info(l)
+            assert info.gs_stall == 0
+    finally:
+        D.close()
+        H.mg.pars.cf_order = 1
+
+
+@pytest.mark.parametrize("hname", ["bus_h", "p32_h", "a27_h"])
+def test_natural_gs_solve_bitwise(request, hname, engine):
+    H = _natural(request.getfixturevalue(hname))
+    try:
+        n = H.level(0).A.num_rows
+        rtn, rel_r, _ = oracle_solve(H, np.ones(n), x_r := np.ones(n))
+        D = A.DeviceHierarchy(H, smoother="exact", coarse="krylov")
+        try:
+            D.upload(0, "b", np.ones(n))
+            D.upload(0, "x", np.ones(n))
+            rel = []
+            for _ in range(len(rel_r)):
+                D.cycle()
+                rel.append(D.residual_norm() / np.sqrt(n))
+            x_g = D.download(0, "x")
+        finally:
+            D.close()
+        assert np.array_equal(x_g.view(np.uint64), x_r.view(np.uint64))
+        assert np.allclose(rel, rel_r, rtol=1e-13, atol=0)
+    finally:
+        H.mg.pars.cf_order = 1
+
+
+@pytest.mark.parametrize("istart,iend,istep", [(0, -1, 1), (0, -1, -1), (5, 40, 1), (7, 30, -1), (30, 7, 1)])
+def test_natural_gs_host_entry(p32_h, istart, iend, istep):
+    """SSS_amg_smoother_pre/post's device entry with cf_order = 0 (any contiguous row range,
+    either direction; crossed bounds run no row, as the reference's loops)."""
+    ora = oracle.load()
+    L = p32_h.level(1)
+    n = L.A.num_rows
+    iend = n - 1 if iend < 0 else iend
+    rng = np.random.default_rng(istart + 3 * iend)
+    for post in (False, True):
+        b = rng.standard_normal(n)
+        x0 = rng.standard_normal(n)
+        xg, xr = x0.copy(), x0.copy()
+        sg = _smtr(L.A, b, xg, L.cfmark.d, 2, post)
+        sr = _smtr(L.A, b, xr, L.cfmark.d, 2, post)
+        for s_ in (sg, sr):
+            s_.cf_order = 0
+            s_.istart, s_.iend, s_.istep = istart, iend, istep
+        assert A.lib().sss_hip_host_smooth(C.byref(sg), int(post)) == 0
+        (ora.ora_smoother_post if post else ora.ora_smoother_pre)(C.byref(sr))
+        assert np.array_equal(xg.view(np.uint64), xr.view(np.uint64)), (istart, iend, istep, post)
