@@ -226,3 +226,35 @@ def test_natural_gs_host_entry(p32_h, istart, iend, istep):
         assert A.lib().sss_hip_host_smooth(C.byref(sg), int(post)) == 0
         (ora.ora_smoother_post if post else ora.ora_smoother_pre)(C.byref(sr))
         assert np.array_equal(xg.view(np.uint64), xr.view(np.uint64)), (istart, iend, istep, post)
+
+
+@pytest.mark.parametrize("hname", ["bus_h", "p32_h", "a27_h"])
+@pytest.mark.parametrize("smoother,coarse", [("exact", "krylov"), ("exact", "direct")])
+def test_w_cycle_bitwise(request, hname, smoother, coarse):
+    """cycle_type = 2 (the W-cycle branch of SSS_amg_cycle, Solve/SSS_cycle.cu:959-966: a level
+    re-descends until it has been visited cycle_type times) -- x bitwise the oracle's."""
+    H = request.getfixturevalue(hname)
+    H.mg.pars.cycle_type = 2
+    try:
+        n = H.level(0).A.num_rows
+        kw = {} if coarse == "krylov" else {"coarse_mode": 1}
+        rtn, rel_r, _ = oracle_solve(H, np.ones(n), x_r := np.ones(n), **kw)
+        D = A.DeviceHierarchy(H, smoother=smoother, coarse=coarse)
+        try:
+            D.upload(0, "b", np.ones(n))
+            D.upload(0, "x", np.ones(n))
+            rel = []
+            for _ in range(len(rel_r)):
+                D.cycle()
+                rel.append(D.residual_norm() / np.sqrt(n))
+            x_g = D.download(0, "x")
+        finally:
+            D.close()
+        if coarse == "krylov":
+            assert np.array_equal(x_g.view(np.uint64), x_r.view(np.uint64))
+            assert np.allclose(rel, rel_r, rtol=1e-13, atol=0)
+        else:   # explicit inverse vs the oracle's dense LU: same iterates to rounding
+            assert np.linalg.norm(x_g - x_r) <= 1e-9 * np.linalg.norm(x_r)
+            assert np.allclose(rel, rel_r, rtol=1e-6, atol=0)
+    finally:
+        H.mg.pars.cycle_type = 1
