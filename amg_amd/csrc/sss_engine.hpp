@@ -105,6 +105,15 @@ struct DevCSR {
     // col << 4 | segment << 3 | row-in-group (segment: 0, or 1 for [seg, rp+1) of two-segment rows).  One wave sums a group lane-strided with one accumulator per
     // row; neighbouring rows share most columns, so a wave's 64 gathers touch ~G x fewer x lines
     // (the long-row levels are bound by the L2->CU line rate of those gathers, not by HBM).
+    // Dictionary tiles (kEncDict; bitwise-neutral): every entry as a 16-bit code in stored order,
+    // delta index << 8 | value index, into its block's dictionaries of distinct column offsets
+    // col - row (<= 256) and distinct value bit patterns (<= 256): 2 B per entry instead of 12.
+    // dv_pd[block] = {delta offset, delta count, value offset, value count}.  Built only when every
+    // block qualifies (the stencil levels: 7-pt Poisson level 0 has 7 offsets and 2 values per block).
+    unsigned short *dv_code = nullptr;
+    int4 *dv_pd = nullptr;
+    int *dv_dd = nullptr;
+    double *dv_vd = nullptr;
     int mg_G = 0;              // 0: no merged copy
     int mg_ng = 0;             // groups
     int mg_W = 4;              // waves per group (1, 2 or 4): 4 / mg_W groups per workgroup
@@ -121,7 +130,7 @@ constexpr int kTileColBits = 20;         // column offset bits of a packed sorte
 constexpr unsigned kTileDiagMark = (1u << kTileColBits) - 256;
 static_assert((1 << kTileShift) == kTileEntries, "tile packing");
 static_assert(1 + kTileColBits + kTileShift == 32, "tile packing");
-enum { kEncSortedTiles = 1, kEncFreeOrder = 2 };
+enum { kEncSortedTiles = 1, kEncFreeOrder = 2, kEncDict = 4 };
 // split >= 0 forces a row-block boundary at that row (the F|C class boundary of a relabeled level);
 // enc: kEnc* flags; seg (kEncFreeOrder only, optional): per row, the absolute CSR position that
 // splits the row into two independently summed segments (two-stage [N_i | L_i] rows).
@@ -133,6 +142,8 @@ int build_row_blocks(const int *h_rp, int n, std::vector<int> &blk, int split = 
 int upload_block_bounds(int2 **dst, const std::vector<int> &blk, const int *h_rp);
 int wave_row_min();
 int free_row_min();
+struct DevDict;
+DevDict devdict(const DevCSR &A, int blo);   // the matrix's dictionary tiles, block numbers from blo
 
 // ---- hierarchy internals shared with the distributed engine (sss_hier.hip) ------------------
 // A hierarchy over mg->cg[0 .. num_levels); its L[0] is global level `level_base` (smoother

@@ -123,7 +123,11 @@ static int level_inner(const sss_hip_opts &o, int l)
 int sss::level_kind_of(const sss_hip_opts &o, int l) { return level_smoother_kind(o, l); }
 int sss::level_encoding(const sss_hip_opts &o)
 {
-    return (o.sorted_tiles ? kEncSortedTiles : 0) | (o.sum_order == 1 ? kEncFreeOrder : 0);
+    // dictionary tiles (kEncDict) are offered for the level matrices A_l; uploads of P, R and the
+    // two-stage split copies mask them out (their column offsets are not row-relative)
+    const char *dz = getenv("SSS_HIP_DICT");
+    const int dict = (dz && *dz == '0') ? 0 : kEncDict;
+    return (o.sorted_tiles ? kEncSortedTiles : 0) | (o.sum_order == 1 ? kEncFreeOrder : 0) | dict;
 }
 int sss::level_inner_of(const sss_hip_opts &o, int l) { return level_inner(o, l); }
 
@@ -320,10 +324,10 @@ sss_hip_hier *sss::hier_create_impl(const SSS_AMG *mg, const sss_hip_opts *o, in
                 relabel_csr(C.R, pc, inv[l], R);
                 // P's rows follow the level's F|C relabeling: blocks split there too, so a
                 // prolongation can be limited to the C rows (SmootherPlan::f_overwritten)
-                if (devcsr_upload(L.P, P.view(C.P.num_rows, C.P.num_cols), rl ? nF[l] : -1, enc) ||
-                    devcsr_upload(L.R, R.view(C.R.num_rows, C.R.num_cols), -1, enc))
+                if (devcsr_upload(L.P, P.view(C.P.num_rows, C.P.num_cols), rl ? nF[l] : -1, enc & ~kEncDict) ||
+                    devcsr_upload(L.R, R.view(C.R.num_rows, C.R.num_cols), -1, enc & ~kEncDict))
                     return fail("upload P/R");
-            } else if (devcsr_upload(L.P, C.P, -1, enc) || devcsr_upload(L.R, C.R, -1, enc)) {
+            } else if (devcsr_upload(L.P, C.P, -1, enc & ~kEncDict) || devcsr_upload(L.R, C.R, -1, enc & ~kEncDict)) {
                 return fail("upload P/R");
             }
         }
@@ -740,6 +744,8 @@ extern "C" int sss_hip_level_info_get(sss_hip_hier *h, int level, sss_hip_level_
     unsigned ef = 0, ec = 0;
     if (gs_persist_error(L.sm.pass[0], &ef) || gs_persist_error(L.sm.pass[1], &ec)) return ERROR_MISC;
     out->gs_stall = (int)(ef | ec);
+    out->a_format = (L.A.pk ? 1 : 0) | (L.A.dv_code ? 2 : 0) | (L.A.vec_rows ? 4 : 0) | (L.A.mg_G ? 8 : 0) |
+                    (L.A.wave_rows ? 16 : 0);
     return 0;
 }
 
@@ -792,7 +798,7 @@ extern "C" int sss_hip_host_spmv(int op, double alpha, const SSS_MAT *A, const d
     HostCSR M;
     sss_hip_opts o;
     sss_hip_opts_default(&o);   // SSS_HIP_SORTED_TILES; always the reference's summation order here
-    if (devcsr_upload(M.d, *A, -1, level_encoding(o) & kEncSortedTiles)) return ERROR_MISC;
+    if (devcsr_upload(M.d, *A, -1, level_encoding(o) & (kEncSortedTiles | kEncDict))) return ERROR_MISC;
     const size_t ny = (size_t)A->num_rows, nx = (size_t)A->num_cols;
     double *dx = dev_alloc<double>(nx), *dy = dev_alloc<double>(ny), *db = dev_alloc<double>(ny);
     int rc = 0;

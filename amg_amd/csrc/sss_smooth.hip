@@ -277,7 +277,8 @@ int smoother_build(SmootherPlan &sp, const SSS_MAT &A, const int *mark, int kind
             };
             SSS_MAT Mn = mk(nrp, nci, nv), Ml = mk(lrp, lci, lv);
             std::vector<int> seg(split);   // absolute [N_i | L_i] cut of each row of Mn
-            if ((rc = devcsr_upload(ps.ts_nl, Mn, -1, enc, seg.data())) || (rc = devcsr_upload(ps.ts_lo, Ml, -1, enc)))
+            if ((rc = devcsr_upload(ps.ts_nl, Mn, -1, enc & ~kEncDict, seg.data())) ||
+                (rc = devcsr_upload(ps.ts_lo, Ml, -1, enc & ~kEncDict)))
                 return rc;
             if ((rc = upload_ints(&ps.ts_split, split))) return rc;
             ps.ts_P = dev_alloc<double>((size_t)m);
@@ -471,7 +472,7 @@ __global__ __launch_bounds__(kBlock) void relax_wave(int m, const int *__restric
 //           other product of the row changes; per-block sums of squares into partial[bid].
 // t = b_r - sum over off-diagonal entries in stored order (diag_pos skips the diagonal); rows with
 // |d| <= 1e-20 keep their value.
-template <int MODE>
+template <int MODE, bool DICT = false>
 __global__ __launch_bounds__(kBlock) void relax_range(int blo, const int2 *__restrict__ blk, const int *__restrict__ rp,
                                                       const int *__restrict__ ci, const double *__restrict__ v,
                                                       const int *__restrict__ diag_pos, int lo,
@@ -479,9 +480,13 @@ __global__ __launch_bounds__(kBlock) void relax_range(int blo, const int2 *__res
                                                       const double *__restrict__ yp, double *__restrict__ y,
                                                       const double *__restrict__ deff, const unsigned *__restrict__ pk,
                                                       const double *__restrict__ pv, const int2 *__restrict__ pb,
-                                                      double *__restrict__ rr, double *__restrict__ partial, XSrc xs)
+                                                      double *__restrict__ rr, double *__restrict__ partial, XSrc xs,
+                                                      DevDict dt = DevDict())
 {
     __shared__ SpmvSmem sm;
+    __shared__ std::conditional_t<DICT, DictSmem, char> dsm;
+    DictSmem *ds = nullptr;
+    if constexpr (DICT) ds = &dsm;
     const int bid = blo + xcd_bid();
     const int2 ba = blk[bid], be = blk[bid + 1];
     const int r0 = ba.x, r1 = be.x, k0 = ba.y, k1 = be.y;
@@ -501,7 +506,7 @@ __global__ __launch_bounds__(kBlock) void relax_range(int blo, const int2 *__res
         int a = 0, e = 0, dp = -1;
         double acc = 0.0, br = 0.0;
         if (r < r1) a = rp[r] - k0, e = rp[r + 1] - k0, dp = diag_pos[r], br = b[r];   // ahead of the tile
-        stage_any(sm.v, k0, k1, ci, v, pk, pv, pb, bid, r0, deff ? (double *)nullptr : sm.d, fetch);
+        stage_any(sm.v, k0, k1, ci, v, pk, pv, pb, bid, r0, deff ? (double *)nullptr : sm.d, fetch, dt, ds, r1, rp);
         __syncthreads();
         double sq = 0.0;
         if (r < r1) {
@@ -542,7 +547,8 @@ __global__ __launch_bounds__(kBlock) void relax_range(int blo, const int2 *__res
         double acc = b[r];
         for (int base = k0; base < k1; base += kTileEntries) {
             const int m = min(kTileEntries, k1 - base);
-            stage_any(sm.v, base, base + m, ci, v, pk, pv, pb, bid, r0, deff ? (double *)nullptr : sm.d, fetch);
+            stage_any(sm.v, base, base + m, ci, v, pk, pv, pb, bid, r0, deff ? (double *)nullptr : sm.d, fetch, dt, ds,
+                      r1, rp);
             __syncthreads();
             if (threadIdx.x == 0) {
                 if (dp >= base && dp < base + m) {
@@ -821,10 +827,15 @@ int launch_f_residual_pending(const SmootherPlan &sp, const DevCSR &A, const dou
 {
     if (!sp.pend_ok) return ERROR_INPUT_PAR;
     const PassSchedule &F = sp.pass[0];
-    const double *deff = (sp.own_diag && A.pk) ? nullptr : sp.d_first;
-    hipLaunchKernelGGL(relax_range<3>, dim3(F.bhi - F.blo), dim3(kBlock), 0, s, F.blo, A.bk, A.rp, A.ci, A.v,
-                       sp.diag_pos, F.lo, b, const_cast<double *>(x), (const double *)nullptr, pend, deff, A.pk, A.pv,
-                       A.pb, r, partial, xsrc_of(x));
+    const double *deff = (sp.own_diag && (A.pk || A.dv_code)) ? nullptr : sp.d_first;
+    if (A.dv_code)
+        hipLaunchKernelGGL((relax_range<3, true>), dim3(F.bhi - F.blo), dim3(kBlock), 0, s, F.blo, A.bk, A.rp, A.ci, A.v,
+                           sp.diag_pos, F.lo, b, const_cast<double *>(x), (const double *)nullptr, pend, deff, A.pk,
+                           A.pv, A.pb, r, partial, xsrc_of(x), devdict(A, 0));
+    else
+        hipLaunchKernelGGL((relax_range<3, false>), dim3(F.bhi - F.blo), dim3(kBlock), 0, s, F.blo, A.bk, A.rp, A.ci, A.v,
+                           sp.diag_pos, F.lo, b, const_cast<double *>(x), (const double *)nullptr, pend, deff, A.pk,
+                           A.pv, A.pb, r, partial, xsrc_of(x), DevDict());
     SSS_HIP(hipGetLastError());
     return 0;
 }
@@ -964,7 +975,7 @@ int smoother_run(const SmootherPlan &sp, const DevCSR &A, const double *b, doubl
                 XSrc xs = nocopy ? XSrc{cur[0], cur[1], sp.csplit} : xsrc_of(x);
                 if (pre_f && sw == 0) xs = XSrc{pre_f, x, sp.pass[0].hi};   // this sweep's F values
                 // tile passes take each row's divisor from its staged diagonal (no deff stream)
-                const bool tile_d = sp.own_diag && A.pk != nullptr;
+                const bool tile_d = sp.own_diag && (A.pk != nullptr || A.dv_code != nullptr);
                 auto relax = [&](auto mode, const int *cols, const double *yp, double *y) -> int {
                     constexpr int M = decltype(mode)::value;
                     if (wave && A.vec_rows)
@@ -975,9 +986,16 @@ int smoother_run(const SmootherPlan &sp, const DevCSR &A, const double *b, doubl
                                            A.rp, cols, A.v, b, x, yp, y, deff, xs);
                     else {
                         auto go = [&](int b0, int b1) {
-                            hipLaunchKernelGGL(relax_range<M>, dim3(b1 - b0), dim3(kBlock), 0, s, b0, A.bk, A.rp,
-                                               cols, A.v, sp.diag_pos, ps.lo, b, x, yp, y, tile_d ? nullptr : deff,
-                                               A.pk, A.pv, A.pb, (double *)nullptr, (double *)nullptr, xs);
+                            if (A.dv_code)
+                                hipLaunchKernelGGL((relax_range<M, true>), dim3(b1 - b0), dim3(kBlock), 0, s, b0, A.bk,
+                                                   A.rp, cols, A.v, sp.diag_pos, ps.lo, b, x, yp, y,
+                                                   tile_d ? nullptr : deff, A.pk, A.pv, A.pb, (double *)nullptr,
+                                                   (double *)nullptr, xs, devdict(A, 0));
+                            else
+                                hipLaunchKernelGGL((relax_range<M, false>), dim3(b1 - b0), dim3(kBlock), 0, s, b0, A.bk,
+                                                   A.rp, cols, A.v, sp.diag_pos, ps.lo, b, x, yp, y,
+                                                   tile_d ? nullptr : deff, A.pk, A.pv, A.pb, (double *)nullptr,
+                                                   (double *)nullptr, xs, DevDict());
                         };
                         if (split_pass) return hk->split(x, ps.blo, ps.bhi, go);
                         go(ps.blo, ps.bhi);
@@ -1041,9 +1059,16 @@ int smoother_run(const SmootherPlan &sp, const DevCSR &A, const double *b, doubl
                     SSS_HIP(hipMemcpyAsync(x + ps.lo, ps.y, sizeof(double) * (size_t)m, hipMemcpyDeviceToDevice, s));
                 } else if (fused_pass) {
                     auto go = [&](int b0, int b1) {
-                        hipLaunchKernelGGL(relax_range<2>, dim3(b1 - b0), dim3(kBlock), 0, s, b0, A.bk, A.rp, A.ci,
-                                           A.v, sp.diag_pos, ps.lo, b, x, (const double *)nullptr, (double *)nullptr,
-                                           tile_d ? nullptr : deff, A.pk, A.pv, A.pb, rf->r, rf->partial, xs);
+                        if (A.dv_code)
+                            hipLaunchKernelGGL((relax_range<2, true>), dim3(b1 - b0), dim3(kBlock), 0, s, b0, A.bk,
+                                               A.rp, A.ci, A.v, sp.diag_pos, ps.lo, b, x, (const double *)nullptr,
+                                               (double *)nullptr, tile_d ? nullptr : deff, A.pk, A.pv, A.pb, rf->r,
+                                               rf->partial, xs, devdict(A, 0));
+                        else
+                            hipLaunchKernelGGL((relax_range<2, false>), dim3(b1 - b0), dim3(kBlock), 0, s, b0, A.bk,
+                                               A.rp, A.ci, A.v, sp.diag_pos, ps.lo, b, x, (const double *)nullptr,
+                                               (double *)nullptr, tile_d ? nullptr : deff, A.pk, A.pv, A.pb, rf->r,
+                                               rf->partial, xs, DevDict());
                     };
                     if (split_pass) {
                         if ((rc = hk->split(x, ps.blo, ps.bhi, go))) return rc;

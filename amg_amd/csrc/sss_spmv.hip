@@ -20,6 +20,7 @@
 #include "sss_spmv_dev.hpp"
 
 #include <algorithm>
+#include <type_traits>
 #include <cstring>
 #include <mutex>
 
@@ -245,6 +246,76 @@ static void build_merged(const SSS_MAT &h, const int *seg, int G, std::vector<in
     gp[ng] = rp[n];
 }
 
+DevDict devdict(const DevCSR &A, int blo)
+{
+    DevDict t;
+    if (!A.dv_code) return t;
+    t.code = A.dv_code;
+    t.pd = A.dv_pd + blo;
+    t.dd = A.dv_dd;
+    t.vd = A.dv_vd;
+    return t;
+}
+
+// Dictionary tiles of a square matrix (DevCSR::dv_*): per block, the distinct column offsets
+// col - row and the distinct value bit patterns, each at most 256; false when a block has more.
+static bool build_dict_tiles(const SSS_MAT &h, const std::vector<int> &blk, std::vector<unsigned short> &code,
+                             std::vector<int4> &pd, std::vector<int> &dd, std::vector<double> &vd)
+{
+    const int *rp = h.row_ptr, *ci = h.col_idx;
+    const double *v = h.val;
+    const int nb = (int)blk.size() - 1;
+    if (h.num_rows != h.num_cols || nb <= 0) return false;
+    std::vector<std::vector<int>> bd(nb);
+    std::vector<std::vector<unsigned long long>> bv(nb);
+    code.resize((size_t)h.num_nnzs);
+    std::atomic<int> ok{1};
+    parallel_chunks(nb, 256, [&](int qlo, int qhi) {
+        for (int q = qlo; q < qhi && ok; ++q) {
+            auto &D = bd[q];
+            auto &V = bv[q];
+            for (int r = blk[q]; r < blk[q + 1]; ++r)
+                for (int k = rp[r]; k < rp[r + 1]; ++k) {
+                    D.push_back(ci[k] - r);
+                    unsigned long long u;
+                    std::memcpy(&u, &v[k], sizeof(u));
+                    V.push_back(u);
+                }
+            std::sort(D.begin(), D.end());
+            D.erase(std::unique(D.begin(), D.end()), D.end());
+            std::sort(V.begin(), V.end());
+            V.erase(std::unique(V.begin(), V.end()), V.end());
+            if (D.size() > 256 || V.size() > 256) {
+                ok = 0;
+                return;
+            }
+            for (int r = blk[q]; r < blk[q + 1]; ++r)
+                for (int k = rp[r]; k < rp[r + 1]; ++k) {
+                    unsigned long long u;
+                    std::memcpy(&u, &v[k], sizeof(u));
+                    const int di = (int)(std::lower_bound(D.begin(), D.end(), ci[k] - r) - D.begin());
+                    const int vi = (int)(std::lower_bound(V.begin(), V.end(), u) - V.begin());
+                    code[(size_t)k] = (unsigned short)(di << 8 | vi);
+                }
+        }
+    });
+    if (!ok) return false;
+    pd.resize((size_t)nb);
+    size_t nd = 0, nv = 0;
+    for (int q = 0; q < nb; ++q) {
+        pd[q] = make_int4((int)nd, (int)bd[q].size(), (int)nv, (int)bv[q].size());
+        nd += bd[q].size();
+        nv += bv[q].size();
+    }
+    dd.resize(std::max<size_t>(nd, 1));
+    vd.resize(std::max<size_t>(nv, 1));
+    for (int q = 0; q < nb; ++q) {
+        std::copy(bd[q].begin(), bd[q].end(), dd.begin() + pd[q].x);
+        for (size_t t = 0; t < bv[q].size(); ++t) std::memcpy(&vd[(size_t)pd[q].z + t], &bv[q][t], sizeof(double));
+    }
+    return true;
+}
+
 int devcsr_upload(DevCSR &d, const SSS_MAT &h, int split, int enc, const int *seg)
 {
     d.n = h.num_rows;
@@ -306,11 +377,32 @@ int devcsr_upload(DevCSR &d, const SSS_MAT &h, int split, int enc, const int *se
         if (int rc = h2d(d.mg_k, mk.data(), sizeof(unsigned) * mk.size())) return rc;
         if (int rc = h2d(d.mg_v, mv.data(), sizeof(double) * mv.size())) return rc;
     }
+    // dictionary tiles (the tile kernels then stage from them instead of the sorted copy)
+    const char *dz = getenv("SSS_HIP_DICT");   // 0: never (tests compare both ways)
+    if ((enc & kEncDict) && !(dz && *dz == '0') && !d.wave_rows && !d.vec_rows && d.nnz > 0) {
+        std::vector<unsigned short> code;
+        std::vector<int4> pd;
+        std::vector<int> dd;
+        std::vector<double> vd;
+        if (build_dict_tiles(h, blk, code, pd, dd, vd)) {
+            d.dv_code = dev_alloc<unsigned short>(code.size());
+            d.dv_pd = dev_alloc<int4>(pd.size());
+            d.dv_dd = dev_alloc<int>(dd.size());
+            d.dv_vd = dev_alloc<double>(vd.size());
+            if (!d.dv_code || !d.dv_pd || !d.dv_dd || !d.dv_vd)
+                return hip_fail(hipErrorOutOfMemory, "hipMalloc(dictionary tiles)", __FILE__, __LINE__);
+            if (int rc = h2d(d.dv_code, code.data(), sizeof(unsigned short) * code.size())) return rc;
+            if (int rc = h2d(d.dv_pd, pd.data(), sizeof(int4) * pd.size())) return rc;
+            if (int rc = h2d(d.dv_dd, dd.data(), sizeof(int) * dd.size())) return rc;
+            if (int rc = h2d(d.dv_vd, vd.data(), sizeof(double) * vd.size())) return rc;
+        }
+    }
     // the tile kernels of a wave-path matrix never run on the hierarchy; no sorted copy for them
     std::vector<unsigned> pk;
     std::vector<double> pv;
     std::vector<int2> pb;
-    if ((enc & kEncSortedTiles) && !d.wave_rows && !d.vec_rows && d.nnz > 0 && build_sorted_tiles(h, blk, pk, pv, pb)) {
+    if ((enc & kEncSortedTiles) && !d.dv_code && !d.wave_rows && !d.vec_rows && d.nnz > 0 &&
+        build_sorted_tiles(h, blk, pk, pv, pb)) {
         d.pk = dev_alloc<unsigned>((size_t)d.nnz);
         d.pv = dev_alloc<double>((size_t)d.nnz);
         d.pb = dev_alloc<int2>(pb.size());
@@ -335,19 +427,27 @@ void devcsr_free(DevCSR &d)
     dev_free(d.mg_gp);
     dev_free(d.mg_k);
     dev_free(d.mg_v);
+    dev_free(d.dv_code);
+    dev_free(d.dv_pd);
+    dev_free(d.dv_dd);
+    dev_free(d.dv_vd);
     d = DevCSR();
 }
 
 // ---- kernel -------------------------------------------------------------------------------
-template <int OP, bool NORM>
+template <int OP, bool NORM, bool DICT = false>
 __global__ __launch_bounds__(kBlock) void spmv_adaptive(const int2 *__restrict__ blk, const int *__restrict__ rp,
                                                         const int *__restrict__ ci, const double *__restrict__ v,
                                                         const double *__restrict__ x, const double *__restrict__ b,
                                                         double *__restrict__ y, double alpha, int cap,
                                                         double *__restrict__ partial, const unsigned *__restrict__ pk,
-                                                        const double *__restrict__ pv, const int2 *__restrict__ pb)
+                                                        const double *__restrict__ pv, const int2 *__restrict__ pb,
+                                                        DevDict dt = DevDict())
 {
     __shared__ SpmvSmem sm;
+    __shared__ std::conditional_t<DICT, DictSmem, char> dsm;
+    DictSmem *ds = nullptr;
+    if constexpr (DICT) ds = &dsm;
     const double sq = csr_block_rows(blk, rp, ci, v, x, sm, [&](int r, double s) -> double {
         double out;
         if constexpr (OP == SSS_HIP_SPMV_MXY) out = s;
@@ -359,7 +459,7 @@ __global__ __launch_bounds__(kBlock) void spmv_adaptive(const int2 *__restrict__
         }
         y[r] = out;
         return NORM ? out * out : 0.0;
-    }, pk, pv, pb);
+    }, pk, pv, pb, &dt, ds);
     if (NORM) {
         const double t = block_sum(sq, sm.red);
         if (threadIdx.x == 0) partial[xcd_bid()] = t;
@@ -453,9 +553,12 @@ static void launch_op(const DevCSR &A, double alpha, const double *x, const doub
     else if (A.wave_rows)
         hipLaunchKernelGGL((spmv_wave<OP, NORM, false>), dim3(A.ngrid), dim3(kBlock), 0, s, A.n, A.rp, A.ci, A.v, x,
                            b, y, alpha, cap, partial);
+    else if (A.dv_code)
+        hipLaunchKernelGGL((spmv_adaptive<OP, NORM, true>), dim3(A.nblk), dim3(kBlock), 0, s, A.bk, A.rp, A.ci, A.v,
+                           x, b, y, alpha, cap, partial, A.pk, A.pv, A.pb, devdict(A, 0));
     else
         hipLaunchKernelGGL((spmv_adaptive<OP, NORM>), dim3(A.nblk), dim3(kBlock), 0, s, A.bk, A.rp, A.ci, A.v, x,
-                           b, y, alpha, cap, partial, A.pk, A.pv, A.pb);
+                           b, y, alpha, cap, partial, A.pk, A.pv, A.pb, DevDict());
 }
 
 int launch_spmv(const DevCSR &A, int op, double alpha, const double *x, const double *b, double *y, int cap,
@@ -486,18 +589,23 @@ int launch_spmv_range(const DevCSR &A, int blo, int bhi, int op, double alpha, c
     // the kernel indexes blocks from 0: shift the block-indexed arrays
     const int2 *pb = A.pb ? A.pb + blo : nullptr;
     double *pp = partial ? partial + blo : nullptr;
-    if (op == SSS_HIP_SPMV_AMXPY)
-        hipLaunchKernelGGL((spmv_adaptive<SSS_HIP_SPMV_AMXPY, false>), dim3(nb), dim3(kBlock), 0, s, A.bk + blo, A.rp,
-                           A.ci, A.v, x, b, y, alpha, 0, pp, A.pk, A.pv, pb);
-    else if (op == SSS_HIP_SPMV_MXY)
-        hipLaunchKernelGGL((spmv_adaptive<SSS_HIP_SPMV_MXY, false>), dim3(nb), dim3(kBlock), 0, s, A.bk + blo, A.rp,
-                           A.ci, A.v, x, b, y, alpha, 0, pp, A.pk, A.pv, pb);
-    else if (partial)
-        hipLaunchKernelGGL((spmv_adaptive<SSS_HIP_SPMV_RESID, true>), dim3(nb), dim3(kBlock), 0, s, A.bk + blo, A.rp,
-                           A.ci, A.v, x, b, y, alpha, 0, pp, A.pk, A.pv, pb);
-    else
-        hipLaunchKernelGGL((spmv_adaptive<SSS_HIP_SPMV_RESID, false>), dim3(nb), dim3(kBlock), 0, s, A.bk + blo, A.rp,
-                           A.ci, A.v, x, b, y, alpha, 0, pp, A.pk, A.pv, pb);
+    const DevDict dt = devdict(A, blo);
+    auto go = [&](auto op_c, auto norm_c) {
+        constexpr int O = decltype(op_c)::value;
+        constexpr bool NM = decltype(norm_c)::value;
+        if (A.dv_code)
+            hipLaunchKernelGGL((spmv_adaptive<O, NM, true>), dim3(nb), dim3(kBlock), 0, s, A.bk + blo, A.rp, A.ci, A.v,
+                               x, b, y, alpha, 0, pp, A.pk, A.pv, pb, dt);
+        else
+            hipLaunchKernelGGL((spmv_adaptive<O, NM, false>), dim3(nb), dim3(kBlock), 0, s, A.bk + blo, A.rp, A.ci,
+                               A.v, x, b, y, alpha, 0, pp, A.pk, A.pv, pb, dt);
+    };
+    using T = std::true_type;
+    using F = std::false_type;
+    if (op == SSS_HIP_SPMV_AMXPY) go(std::integral_constant<int, SSS_HIP_SPMV_AMXPY>(), F());
+    else if (op == SSS_HIP_SPMV_MXY) go(std::integral_constant<int, SSS_HIP_SPMV_MXY>(), F());
+    else if (partial) go(std::integral_constant<int, SSS_HIP_SPMV_RESID>(), T());
+    else go(std::integral_constant<int, SSS_HIP_SPMV_RESID>(), F());
     SSS_HIP(hipGetLastError());
     return 0;
 }

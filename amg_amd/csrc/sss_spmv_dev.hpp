@@ -36,6 +36,19 @@ struct SpmvSmem {
     double d[kBlock];          // sorted tiles: the raw diagonal value of each row of the block
 };
 
+// Dictionary tiles (DevCSR::dv_*): the block's dictionaries and each staged entry's row in LDS.
+struct DictSmem {
+    int dd[256];
+    double vd[256];
+    unsigned char rowof[kTileEntries];
+};
+struct DevDict {
+    const unsigned short *code = nullptr;
+    const int4 *pd = nullptr;   // indexed by the block number the kernel sees
+    const int *dd = nullptr;
+    const double *vd = nullptr;
+};
+
 // In-order chains over LDS products: 8 reads issued ahead of 8 dependent adds/subtractions,
 // the additions themselves in exactly the stored order.
 __device__ __forceinline__ double chain_add(double s, const double *p, int a, int e)
@@ -178,6 +191,53 @@ __device__ __forceinline__ void stage_sorted(double *__restrict__ sm, int k0, in
     }
 }
 
+// Dictionary tiles: entry k of segment [k0, k1) of block `bid` (rows [r0, r1)) is
+// code = delta index << 8 | value index; col = row + dd[delta index], a = vd[value index]; the
+// product lands at its stored position, as stage_products_f's.  Starts with a workgroup barrier
+// of its own (the block's dictionaries and the entry -> row map go to LDS first).
+template <class Fetch>
+__device__ __forceinline__ void stage_dict(double *__restrict__ sm, int k0, int k1, const DevDict &dt, int bid,
+                                           int r0, int r1, const int *__restrict__ rp, DictSmem &ds, double *diag,
+                                           Fetch fetch)
+{
+    const int4 p = dt.pd[bid];
+    for (int t = threadIdx.x; t < p.y; t += kBlock) ds.dd[t] = dt.dd[p.x + t];
+    for (int t = threadIdx.x; t < p.w; t += kBlock) ds.vd[t] = dt.vd[p.z + t];
+    for (int r = r0 + (int)threadIdx.x; r < r1; r += kBlock) {
+        const int a = max(rp[r], k0), e = min(rp[r + 1], k1);
+        for (int k = a; k < e; ++k) ds.rowof[k - k0] = (unsigned char)(r - r0);
+    }
+    __syncthreads();
+    constexpr int U = 8;
+    for (int kb = k0 + (int)threadIdx.x; kb < k1; kb += U * kBlock) {
+        unsigned q[U];
+        int c[U];
+        double a[U], xv[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int k = kb + u * kBlock;
+            q[u] = k < k1 ? dt.code[k] : 0u;
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int k = kb + u * kBlock;
+            const int row = r0 + (k < k1 ? ds.rowof[k - k0] : 0);
+            c[u] = row + ds.dd[q[u] >> 8];
+            a[u] = ds.vd[q[u] & 255u];
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) xv[u] = kb + u * kBlock < k1 ? fetch(c[u]) : 0.0;
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int k = kb + u * kBlock;
+            if (k < k1) {
+                sm[k - k0] = a[u] * xv[u];
+                if (diag && c[u] == r0 + ds.rowof[k - k0]) diag[ds.rowof[k - k0]] = a[u];
+            }
+        }
+    }
+}
+
 // Stage the products of segment [k0, k1) of block `bid` (first row r0): from the sorted copy when
 // the matrix has one (then diag[row - r0], if given, receives each row's diagonal value).
 template <class Fetch>
@@ -188,6 +248,17 @@ __device__ __forceinline__ void stage_any(double *__restrict__ sm, int k0, int k
 {
     if (pk) stage_sorted(sm, k0, k1, pk, pv, pb[bid], r0, diag, fetch);
     else stage_products_f(sm, k0, k1, ci, v, fetch);
+}
+// ... or from the dictionary tiles when ds is given (kernels instantiated for them)
+template <class Fetch>
+__device__ __forceinline__ void stage_any(double *__restrict__ sm, int k0, int k1, const int *__restrict__ ci,
+                                          const double *__restrict__ v, const unsigned *__restrict__ pk,
+                                          const double *__restrict__ pv, const int2 *__restrict__ pb, int bid, int r0,
+                                          double *diag, Fetch fetch, const DevDict &dt, DictSmem *ds, int r1,
+                                          const int *__restrict__ rp)
+{
+    if (ds) stage_dict(sm, k0, k1, dt, bid, r0, r1, rp, *ds, diag, fetch);
+    else stage_any(sm, k0, k1, ci, v, pk, pv, pb, bid, r0, diag, fetch);
 }
 
 // Returns this thread's summed epilogue contribution (0 for idle threads).
@@ -217,7 +288,8 @@ __device__ __forceinline__ double csr_block_rows(const BlkT *__restrict__ blk, c
                                                  const double *__restrict__ x, SpmvSmem &sm, Epi epi,
                                                  const unsigned *__restrict__ pk = nullptr,
                                                  const double *__restrict__ pv = nullptr,
-                                                 const int2 *__restrict__ pb = nullptr)
+                                                 const int2 *__restrict__ pb = nullptr, const DevDict *dt = nullptr,
+                                                 DictSmem *ds = nullptr)
 {
     auto fetch = [&](int c) -> double { return x[c]; };
     const int bid = xcd_bid();
@@ -229,7 +301,8 @@ __device__ __forceinline__ double csr_block_rows(const BlkT *__restrict__ blk, c
         const int r = r0 + (int)threadIdx.x;
         int ra = 0, re = 0;
         if (r < r1) ra = rp[r], re = rp[r + 1];   // issued ahead of the tile
-        if (pk) stage_sorted(sm.v, k0, k1, pk, pv, pb[bid], r0, (double *)nullptr, fetch);
+        if (ds) stage_dict(sm.v, k0, k1, *dt, bid, r0, r1, rp, *ds, (double *)nullptr, fetch);
+        else if (pk) stage_sorted(sm.v, k0, k1, pk, pv, pb[bid], r0, (double *)nullptr, fetch);
         else stage_products(sm.v, k0, k1, ci, v, x);
         __syncthreads();
         if (r < r1) {
@@ -240,7 +313,8 @@ __device__ __forceinline__ double csr_block_rows(const BlkT *__restrict__ blk, c
         double s = 0.0;
         for (int base = k0; base < k1; base += kTileEntries) {
             const int m = min(kTileEntries, k1 - base);
-            if (pk) stage_sorted(sm.v, base, base + m, pk, pv, pb[bid], r0, (double *)nullptr, fetch);
+            if (ds) stage_dict(sm.v, base, base + m, *dt, bid, r0, r1, rp, *ds, (double *)nullptr, fetch);
+            else if (pk) stage_sorted(sm.v, base, base + m, pk, pv, pb[bid], r0, (double *)nullptr, fetch);
             else stage_products(sm.v, base, base + m, ci, v, x);
             __syncthreads();
             if (threadIdx.x == 0) s = chain_add(s, sm.v, 0, m);

@@ -102,11 +102,13 @@ int sss_hip_smooth(sss_hip_hier *h, int level, int post);
 int sss_hip_sync(sss_hip_hier *h);
 
 /* Per-level statistics for reporting: rows, nnz(A), nnz(P), smoother DAG depths; the exact GS
- * engine of the F / C pass (0: one launch per DAG depth, 1: chip-wide dataflow, 2: single CU) and
- * whether a one-launch pass ever gave up waiting (gs_stall != 0: results invalid). */
+ * engine of the F / C pass (0: one launch per DAG depth, 1: chip-wide dataflow, 2: single CU);
+ * whether a one-launch pass ever gave up waiting (gs_stall != 0: results invalid); the storage of
+ * A_l in HBM (a_format bits: 1 column-sorted tiles, 2 dictionary tiles, 4 free-order rows,
+ * 8 merged row groups, 16 wave-per-row). */
 typedef struct sss_hip_level_info {
     int rows, nnz, nnz_p, dag_f, dag_c, smoother_kind;
-    int gs_engine_f, gs_engine_c, gs_stall;
+    int gs_engine_f, gs_engine_c, gs_stall, a_format;
 } sss_hip_level_info;
 int sss_hip_level_info_get(sss_hip_hier *h, int level, sss_hip_level_info *out);
 int sss_hip_num_levels(sss_hip_hier *h);

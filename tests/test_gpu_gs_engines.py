@@ -258,3 +258,33 @@ def test_w_cycle_bitwise(request, hname, smoother, coarse):
             assert np.allclose(rel, rel_r, rtol=1e-6, atol=0)
     finally:
         H.mg.pars.cycle_type = 1
+
+
+# ---------------------------------------------------------------- dictionary tiles
+@pytest.mark.parametrize("hname", ["p32_h", "a27_h", "p64_h"])
+@pytest.mark.parametrize("smoother,coarse", [("exact", "krylov"), ("hybrid", "direct")])
+def test_dictionary_tiles_bitwise(request, hname, smoother, coarse, monkeypatch):
+    """A_l staged from dictionary tiles (2 B per entry: column offset and value indices into
+    per-block dictionaries) gives the iterates of the column-sorted tiles bit for bit, and the
+    stencil levels do take that storage."""
+    H = request.getfixturevalue(hname)
+    n = H.level(0).A.num_rows
+    out, fmt = {}, {}
+    for dict_on in ("1", "0"):
+        monkeypatch.setenv("SSS_HIP_DICT", dict_on)
+        D = A.DeviceHierarchy(H, smoother=smoother, coarse=coarse)
+        try:
+            D.upload(0, "b", np.ones(n))
+            D.upload(0, "x", np.ones(n))
+            rel = []
+            for _ in range(6):
+                D.cycle()
+                rel.append(D.residual_norm())
+            out[dict_on] = (D.download(0, "x"), rel)
+            fmt[dict_on] = [D.level_info(l).a_format for l in range(H.num_levels - 1)]
+        finally:
+            D.close()
+    assert fmt["1"][0] & 2, fmt   # level 0 of the stencil operators takes dictionary tiles
+    assert not any(f & 2 for f in fmt["0"])
+    assert np.array_equal(out["1"][0].view(np.uint64), out["0"][0].view(np.uint64))
+    assert out["1"][1] == out["0"][1]

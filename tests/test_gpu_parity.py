@@ -48,13 +48,16 @@ def test_device_present():
 
 
 # ---------------------------------------------------------------- SpMV family, bitwise
-@pytest.fixture(params=["tile", "tile-unsorted", "wave"])
+@pytest.fixture(params=["tile", "tile-sorted", "tile-unsorted", "wave"])
 def row_path(request, monkeypatch):
-    """Run a test with the default kernel choice (column-sorted tile staging), with the tiles
-    staged in stored order (SSS_HIP_SORTED_TILES=0), and with every matrix forced onto the
+    """Run a test with the default kernel choice (dictionary tiles where every block qualifies,
+    else column-sorted tiles), with the column-sorted tiles only (SSS_HIP_DICT=0), with the tiles
+    staged in stored order (SSS_HIP_SORTED_TILES=0 too), and with every matrix forced onto the
     wave-per-row kernels (SSS_HIP_WAVE_MIN=1), so every row path is checked bitwise."""
     if request.param == "wave":
         monkeypatch.setenv("SSS_HIP_WAVE_MIN", "1")
+    if request.param in ("tile-sorted", "tile-unsorted"):
+        monkeypatch.setenv("SSS_HIP_DICT", "0")
     if request.param == "tile-unsorted":
         monkeypatch.setenv("SSS_HIP_SORTED_TILES", "0")
     return request.param
