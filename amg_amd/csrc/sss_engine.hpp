@@ -110,6 +110,7 @@ struct DevCSR {
     // col - row (<= 256) and distinct value bit patterns (<= 256): 2 B per entry instead of 12.
     // dv_pd[block] = {delta offset, delta count, value offset, value count}.  Built only when every
     // block qualifies (the stencil levels: 7-pt Poisson level 0 has 7 offsets and 2 values per block).
+    long long stream_bytes = 0;   // bytes of the stored format one tile-path SpMV streams (no vectors)
     unsigned short *dv_code = nullptr;
     int4 *dv_pd = nullptr;
     int *dv_dd = nullptr;

@@ -411,6 +411,19 @@ int devcsr_upload(DevCSR &d, const SSS_MAT &h, int split, int enc, const int *se
         if (int rc = h2d(d.pv, pv.data(), sizeof(double) * (size_t)d.nnz)) return rc;
         if (int rc = h2d(d.pb, pb.data(), sizeof(int2) * pb.size())) return rc;
     }
+    // what one SpMV over the stored format reads besides the vectors (reported for the roofline)
+    const long long nnz = d.nnz, nb = d.nblk, rows = d.n;
+    if (d.dv_code) {
+        long long dict = 0;
+        std::vector<int4> pd((size_t)nb);
+        if (nb > 0) SSS_HIP(hipMemcpy(pd.data(), d.dv_pd, sizeof(int4) * (size_t)nb, hipMemcpyDeviceToHost));
+        for (const auto &p : pd) dict += 4LL * p.y + 8LL * p.w;
+        d.stream_bytes = 2 * nnz + 4 * (rows + 1) + 8 * (nb + 1) + 16 * nb + dict;
+    } else if (d.pk) {
+        d.stream_bytes = 12 * nnz + 4 * (rows + 1) + 8 * (nb + 1) + 8 * nb;
+    } else {
+        d.stream_bytes = 12 * nnz + 4 * (rows + 1) + 8 * (nb + 1);
+    }
     return 0;
 }
 

@@ -72,6 +72,9 @@ def parse():
     p.add_argument("--inner-from", type=int, default=None,
                    help="first level with the two-stage form (default: SSS_HIP_INNER_FROM or 2)")
     p.add_argument("--converge-max", type=int, default=100, help="max V-cycles of the iterations-to-tol run (0: skip)")
+    p.add_argument("--parity-cycles", type=int, default=2,
+                   help="N=1: V-cycles timed on a second mirror in parity mode (the drop-in default: exact GS-CF "
+                        "on every level, reference CG(beta=1)+GMRES coarse solve; 0 skips it)")
     p.add_argument("--sum-order", type=int, default=None,
                    help="0: stored CSR order everywhere (bitwise kernels); 1: tree-summed long rows "
                         "(default: 1 in throughput mode, 0 in parity mode)")
@@ -437,11 +440,18 @@ def main():
     # roofline of the dominant streaming kernel: level-0 fused residual SpMV (wp = b - A0 x);
     # N > 1: rank 0's share (its rows, x with ghosts), no exchange inside the timed launches
     spmv_ms = DH.time_level0_spmv(20)
+    a_format = None
+    csr_bytes = 12 * nnz + 4 * (N + 1) + 8 * N + 8 * N + 8 * N   # val+col, row_ptr, x, b, y
     if D.world == 1:
-        spmv_bytes = 12 * nnz + 4 * (N + 1) + 8 * N + 8 * N + 8 * N   # val+col, row_ptr, x, b, y
+        info0 = DH.DH.level_info(0)
+        a_format = {1: "column-sorted tiles (12 B/entry)", 2: "dictionary tiles (2 B/entry)"}.get(
+            info0.a_format & 3, "CSR (12 B/entry)")
+        # the stored format's own bytes (dictionary tiles: 2 B per entry + block dictionaries)
+        spmv_bytes = info0.a_stream_bytes + 8 * N + 8 * N + 8 * N
     else:
         m, g = DH.rows, DH.ghosts
         spmv_bytes = 12 * DH.nnz + 4 * (m + 1) + 8 * (m + g) + 8 * m + 8 * m
+        csr_bytes = spmv_bytes
     achieved = spmv_bytes / (spmv_ms * 1e-3) / 1e9
 
     # iterations to tol from x0 = 1 (the CLI's problem), and time to solution
@@ -468,17 +478,56 @@ def main():
                "time_to_solution_s": time.perf_counter() - t0}
         print(f"[bench] AMG-PCG: {pits} iterations, relres {pcg['final_relres']:.3e}, "
               f"{pcg['time_to_solution_s']:.3f} s", file=sys.stderr, flush=True)
+    # the drop-in default (parity mode) on the same problem: V-cycles/s of the engine whose x is
+    # bitwise the reference's after every cycle
+    parity = None
+    if D.world == 1 and args.parity_cycles > 0 and args.mode == "throughput":
+        DH.close()   # one mirror at a time
+        t0 = time.perf_counter()
+        PD = A.DeviceHierarchy(H, smoother="exact", coarse="krylov", device=-1, sum_order=0)
+        up = time.perf_counter() - t0
+        PD.upload(0, "b", np.ones(N))
+        PD.upload(0, "x", np.ones(N))
+        PD.cycle()   # warm-up (graph capture)
+        PD.residual_norm()
+        PD.upload(0, "x", np.ones(N))
+        t0 = time.perf_counter()
+        prel = []
+        for _ in range(args.parity_cycles):
+            PD.cycle()
+            prel.append(PD.residual_norm() / float(np.sqrt(N)))
+        pdt = (time.perf_counter() - t0) / args.parity_cycles
+        info = [PD.level_info(l) for l in range(len(table) - 1)]
+        PD.close()
+        parity = {"value": 1.0 / pdt, "unit": "V-cycle iter/s", "ms_per_step": pdt * 1e3, "upload_s": up,
+                  "relres_first_cycles": prel, "gs_engines": [[i.gs_engine_f, i.gs_engine_c] for i in info],
+                  "gs_stall": any(i.gs_stall for i in info)}
+        print(f"[bench] parity mode: {pdt * 1e3:.1f} ms per V-cycle (upload {up:.1f} s)", file=sys.stderr, flush=True)
+    # reference-semantics iteration counts measured with the parity engine (tools/conv_study.py; the
+    # parity engine's printed history equals the reference's, tests/test_gpu_at_size.py)
+    ref_conv = None
+    conv = ROOT / "profiles" / f"r02_conv{n}_parity_vs_throughput.json"
+    if conv.exists() and args.stencil == 7:
+        try:
+            cj = json.loads(conv.read_text())["modes"]
+            ref_conv = {"iterations_to_tol_reference": cj["parity"]["iters"],
+                        "iterations_to_tol_throughput_same_run": cj["throughput"]["iters"],
+                        "parity_ms_per_cycle_same_run": cj["parity"]["ms_per_iter_median"],
+                        "source": f"profiles/{conv.name}"}
+        except Exception:
+            ref_conv = None
+
     levels = [(L["rows"], L["nnz"]) for L in table]
     vbytes = vcycle_bytes(table, pars["pre_iter"] + pars["post_iter"])
     import resource
     rss_gb = D.max(resource.getrusage(resource.RUSAGE_SELF).ru_maxrss / 2**20)   # peak over the ranks
 
     traffic = None
-    pmc = ROOT / "profiles" / "r01_level0_spmv_pmc.json"
+    pmc = ROOT / "profiles" / "r02_level0_spmv_pmc.json"   # tools/gpu/pmc.sh at this format
     if pmc.exists() and D.world == 1:
         try:
             rec = json.loads(pmc.read_text())
-            if rec.get("n") == n:
+            if rec.get("n") == n and rec.get("a_format") == a_format:
                 traffic = rec.get("hbm_bytes_per_launch")
         except Exception:
             traffic = None
@@ -546,6 +595,9 @@ def main():
                    "sorted_tiles": bool(sorted_tiles),
                    "iterations_to_tol": its, "final_relres": relres, "time_to_solution_s": solve_s,
                    "amg_pcg": pcg,
+                   "reference_convergence": ref_conv,
+                   "time_to_solution_reference_semantics_s": (ref_conv["iterations_to_tol_reference"] / parity["value"])
+                   if (ref_conv and parity) else None,
                    "setup_s": setup_s, "hierarchy_source": hier_src, "upload_s": upload_s,
                    "parallelism": f"rowpart{D.world}" if D.world > 1 else "single-gpu",
                    "host_peak_rss_gb_max_over_ranks": rss_gb,
@@ -553,15 +605,22 @@ def main():
         "roofline": {"bound": "hbm", "kernel": "spmv_adaptive<RESID> level 0", "achieved": achieved,
                      "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": achieved / PEAK_HBM_GBS,
                      "frac_of_copy_peak": achieved / COPY_PEAK_GBS, "avg_launch_ms": spmv_ms,
-                     "bytes_per_launch": spmv_bytes, "traffic": traffic},
-        "vcycle_roofline": {
+                     "bytes_per_launch": spmv_bytes, "traffic": traffic, "a_format": a_format,
+                     "csr_equivalent": {"bytes_per_launch": csr_bytes,
+                                        "GBps": csr_bytes / (spmv_ms * 1e-3) / 1e9,
+                                        "note": "SURVEY 8(d) CSR bytes (12 B/entry) over the same time: the rate a "
+                                                "CSR SpMV would need to match this kernel"}},
+        "vcycle_csr_equivalent": {
             "bytes_per_step": vbytes, "achieved": vbytes / (ms_per_step * 1e-3) / 1e9, "peak": PEAK_HBM_GBS,
             "unit": "GB/s", "frac": vbytes / (ms_per_step * 1e-3) / 1e9 / PEAK_HBM_GBS,
-            "definition": "SURVEY.md 8(d) V-cycle algorithmic bytes: per smoothed level 4 GS-CF sweeps, "
-                          "residual, restriction, prolongation, zero-fill; plus the outer residual+norm; "
-                          "coarse solve excluded -- divided by the measured time per outer iteration "
-                          "(whole-job bytes / max-over-ranks time at N > 1)",
+            "definition": "SURVEY.md 8(d) V-cycle algorithmic bytes of CSR storage (12 B/entry): per smoothed "
+                          "level 4 GS-CF sweeps, residual, restriction, prolongation, zero-fill; plus the outer "
+                          "residual+norm; coarse solve excluded -- divided by the measured time per outer "
+                          "iteration (whole-job bytes / max-over-ranks time at N > 1).  The engine stores the "
+                          "stencil levels as dictionary tiles and skips exactly-dead work, so it moves fewer "
+                          "bytes than this: a CSR-equivalent rate, not a roofline fraction",
         },
+        "parity_mode": parity,
         "cpu_baseline": cpu_baseline,
         "cpu_baseline_same_mode": cpu_mt,
     }

@@ -109,6 +109,7 @@ int sss_hip_sync(sss_hip_hier *h);
 typedef struct sss_hip_level_info {
     int rows, nnz, nnz_p, dag_f, dag_c, smoother_kind;
     int gs_engine_f, gs_engine_c, gs_stall, a_format;
+    long long a_stream_bytes;   /* bytes of A_l's stored format one tile-path SpMV reads (no vectors) */
 } sss_hip_level_info;
 int sss_hip_level_info_get(sss_hip_hier *h, int level, sss_hip_level_info *out);
 int sss_hip_num_levels(sss_hip_hier *h);
