@@ -441,11 +441,13 @@ def main():
     # N > 1: rank 0's share (its rows, x with ghosts), no exchange inside the timed launches
     spmv_ms = DH.time_level0_spmv(20)
     a_format = None
+    level_formats = None
     csr_bytes = 12 * nnz + 4 * (N + 1) + 8 * N + 8 * N + 8 * N   # val+col, row_ptr, x, b, y
     if D.world == 1:
         info0 = DH.DH.level_info(0)
         a_format = {1: "column-sorted tiles (12 B/entry)", 2: "dictionary tiles (2 B/entry)"}.get(
             info0.a_format & 3, "CSR (12 B/entry)")
+        level_formats = [DH.DH.level_info(l).a_format for l in range(len(table) - 1)]
         # the stored format's own bytes (dictionary tiles: 2 B per entry + block dictionaries)
         spmv_bytes = info0.a_stream_bytes + 8 * N + 8 * N + 8 * N
     else:
@@ -593,6 +595,7 @@ def main():
                    "inner_from": inner_from if smoother != "exact" else None,
                    "sum_order": "tree (long rows)" if sum_order == 1 else "stored CSR order",
                    "sorted_tiles": bool(sorted_tiles),
+                   "level_storage_bits": level_formats,
                    "iterations_to_tol": its, "final_relres": relres, "time_to_solution_s": solve_s,
                    "amg_pcg": pcg,
                    "reference_convergence": ref_conv,

