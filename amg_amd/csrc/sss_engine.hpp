@@ -105,13 +105,14 @@ struct DevCSR {
     // col << 4 | segment << 3 | row-in-group (segment: 0, or 1 for [seg, rp+1) of two-segment rows).  One wave sums a group lane-strided with one accumulator per
     // row; neighbouring rows share most columns, so a wave's 64 gathers touch ~G x fewer x lines
     // (the long-row levels are bound by the L2->CU line rate of those gathers, not by HBM).
-    // Dictionary tiles (kEncDict; bitwise-neutral): every entry as a 16-bit code in stored order,
-    // delta index << 8 | value index, into its block's dictionaries of distinct column offsets
-    // col - row (<= 256) and distinct value bit patterns (<= 256): 2 B per entry instead of 12.
-    // dv_pd[block] = {delta offset, delta count, value offset, value count}.  Built only when every
-    // block qualifies (the stencil levels: 7-pt Poisson level 0 has 7 offsets and 2 values per block).
+    // Dictionary tiles (kEncDict; bitwise-neutral): every staging segment column-sorted (as the
+    // sorted tiles), each entry a 32-bit code  value index << 19 | offset index << 11 | position
+    // in the segment  into its block's dictionaries of distinct column offsets col - row (<= 256)
+    // and distinct value bit patterns (<= 256): 4 B per entry instead of 12, gathers still in
+    // column order.  dv_pd[block] = {offset base, offset count, value base, value count}.  Built
+    // only when every block qualifies (7-pt Poisson level 0: 7 offsets and 2 values per block).
     long long stream_bytes = 0;   // bytes of the stored format one tile-path SpMV streams (no vectors)
-    unsigned short *dv_code = nullptr;
+    unsigned *dv_code = nullptr;
     int4 *dv_pd = nullptr;
     int *dv_dd = nullptr;
     double *dv_vd = nullptr;

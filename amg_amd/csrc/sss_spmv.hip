@@ -258,8 +258,10 @@ DevDict devdict(const DevCSR &A, int blo)
 }
 
 // Dictionary tiles of a square matrix (DevCSR::dv_*): per block, the distinct column offsets
-// col - row and the distinct value bit patterns, each at most 256; false when a block has more.
-static bool build_dict_tiles(const SSS_MAT &h, const std::vector<int> &blk, std::vector<unsigned short> &code,
+// col - row and the distinct value bit patterns, each at most 256 (false when a block has more);
+// the codes of each staging segment (the block, or a kTileEntries chunk of a longer row) in
+// column order.
+static bool build_dict_tiles(const SSS_MAT &h, const std::vector<int> &blk, std::vector<unsigned> &code,
                              std::vector<int4> &pd, std::vector<int> &dd, std::vector<double> &vd)
 {
     const int *rp = h.row_ptr, *ci = h.col_idx;
@@ -271,11 +273,17 @@ static bool build_dict_tiles(const SSS_MAT &h, const std::vector<int> &blk, std:
     code.resize((size_t)h.num_nnzs);
     std::atomic<int> ok{1};
     parallel_chunks(nb, 256, [&](int qlo, int qhi) {
+        std::vector<int> idx;
+        std::vector<int> rowof, di;
+        std::vector<int> vi;
         for (int q = qlo; q < qhi && ok; ++q) {
             auto &D = bd[q];
             auto &V = bv[q];
+            const int a0 = rp[blk[q]], e0 = rp[blk[q + 1]];
+            rowof.resize((size_t)(e0 - a0));
             for (int r = blk[q]; r < blk[q + 1]; ++r)
                 for (int k = rp[r]; k < rp[r + 1]; ++k) {
+                    rowof[(size_t)(k - a0)] = r;
                     D.push_back(ci[k] - r);
                     unsigned long long u;
                     std::memcpy(&u, &v[k], sizeof(u));
@@ -289,14 +297,20 @@ static bool build_dict_tiles(const SSS_MAT &h, const std::vector<int> &blk, std:
                 ok = 0;
                 return;
             }
-            for (int r = blk[q]; r < blk[q + 1]; ++r)
-                for (int k = rp[r]; k < rp[r + 1]; ++k) {
+            for (int a = a0; a < e0; a += kTileEntries) {   // staging segments, column-sorted
+                const int e = std::min(e0, a + kTileEntries);
+                idx.resize((size_t)(e - a));
+                for (int t = 0; t < e - a; ++t) idx[t] = a + t;
+                std::stable_sort(idx.begin(), idx.end(), [&](int x, int y) { return ci[x] < ci[y]; });
+                for (int t = 0; t < e - a; ++t) {
+                    const int k = idx[t], r = rowof[(size_t)(k - a0)];
                     unsigned long long u;
                     std::memcpy(&u, &v[k], sizeof(u));
-                    const int di = (int)(std::lower_bound(D.begin(), D.end(), ci[k] - r) - D.begin());
-                    const int vi = (int)(std::lower_bound(V.begin(), V.end(), u) - V.begin());
-                    code[(size_t)k] = (unsigned short)(di << 8 | vi);
+                    const unsigned dix = (unsigned)(std::lower_bound(D.begin(), D.end(), ci[k] - r) - D.begin());
+                    const unsigned vix = (unsigned)(std::lower_bound(V.begin(), V.end(), u) - V.begin());
+                    code[(size_t)a + t] = vix << (kTileShift + 8) | dix << kTileShift | (unsigned)(k - a);
                 }
+            }
         }
     });
     if (!ok) return false;
@@ -380,18 +394,18 @@ int devcsr_upload(DevCSR &d, const SSS_MAT &h, int split, int enc, const int *se
     // dictionary tiles (the tile kernels then stage from them instead of the sorted copy)
     const char *dz = getenv("SSS_HIP_DICT");   // 0: never (tests compare both ways)
     if ((enc & kEncDict) && !(dz && *dz == '0') && !d.wave_rows && !d.vec_rows && d.nnz > 0) {
-        std::vector<unsigned short> code;
+        std::vector<unsigned> code;
         std::vector<int4> pd;
         std::vector<int> dd;
         std::vector<double> vd;
         if (build_dict_tiles(h, blk, code, pd, dd, vd)) {
-            d.dv_code = dev_alloc<unsigned short>(code.size());
+            d.dv_code = dev_alloc<unsigned>(code.size());
             d.dv_pd = dev_alloc<int4>(pd.size());
             d.dv_dd = dev_alloc<int>(dd.size());
             d.dv_vd = dev_alloc<double>(vd.size());
             if (!d.dv_code || !d.dv_pd || !d.dv_dd || !d.dv_vd)
                 return hip_fail(hipErrorOutOfMemory, "hipMalloc(dictionary tiles)", __FILE__, __LINE__);
-            if (int rc = h2d(d.dv_code, code.data(), sizeof(unsigned short) * code.size())) return rc;
+            if (int rc = h2d(d.dv_code, code.data(), sizeof(unsigned) * code.size())) return rc;
             if (int rc = h2d(d.dv_pd, pd.data(), sizeof(int4) * pd.size())) return rc;
             if (int rc = h2d(d.dv_dd, dd.data(), sizeof(int) * dd.size())) return rc;
             if (int rc = h2d(d.dv_vd, vd.data(), sizeof(double) * vd.size())) return rc;
@@ -418,7 +432,7 @@ int devcsr_upload(DevCSR &d, const SSS_MAT &h, int split, int enc, const int *se
         std::vector<int4> pd((size_t)nb);
         if (nb > 0) SSS_HIP(hipMemcpy(pd.data(), d.dv_pd, sizeof(int4) * (size_t)nb, hipMemcpyDeviceToHost));
         for (const auto &p : pd) dict += 4LL * p.y + 8LL * p.w;
-        d.stream_bytes = 2 * nnz + 4 * (rows + 1) + 8 * (nb + 1) + 16 * nb + dict;
+        d.stream_bytes = 4 * nnz + 4 * (rows + 1) + 8 * (nb + 1) + 16 * nb + dict;
     } else if (d.pk) {
         d.stream_bytes = 12 * nnz + 4 * (rows + 1) + 8 * (nb + 1) + 8 * nb;
     } else {

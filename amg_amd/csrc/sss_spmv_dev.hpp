@@ -43,7 +43,7 @@ struct DictSmem {
     unsigned char rowof[kTileEntries];
 };
 struct DevDict {
-    const unsigned short *code = nullptr;
+    const unsigned *code = nullptr;
     const int4 *pd = nullptr;   // indexed by the block number the kernel sees
     const int *dd = nullptr;
     const double *vd = nullptr;
@@ -191,10 +191,11 @@ __device__ __forceinline__ void stage_sorted(double *__restrict__ sm, int k0, in
     }
 }
 
-// Dictionary tiles: entry k of segment [k0, k1) of block `bid` (rows [r0, r1)) is
-// code = delta index << 8 | value index; col = row + dd[delta index], a = vd[value index]; the
-// product lands at its stored position, as stage_products_f's.  Starts with a workgroup barrier
-// of its own (the block's dictionaries and the entry -> row map go to LDS first).
+// Dictionary tiles: slot k of segment [k0, k1) of block `bid` (rows [r0, r1)) holds
+// code = value index << 19 | offset index << 11 | pos, pos = the entry's stored-order position in
+// the segment (slots are in column order); col = row(pos) + dd[offset index], a = vd[value index];
+// the product lands at sm[pos], so the LDS image is stage_products_f's.  Starts with a workgroup
+// barrier of its own (the block's dictionaries and the position -> row map go to LDS first).
 template <class Fetch>
 __device__ __forceinline__ void stage_dict(double *__restrict__ sm, int k0, int k1, const DevDict &dt, int bid,
                                            int r0, int r1, const int *__restrict__ rp, DictSmem &ds, double *diag,
@@ -209,9 +210,10 @@ __device__ __forceinline__ void stage_dict(double *__restrict__ sm, int k0, int 
     }
     __syncthreads();
     constexpr int U = 8;
+    constexpr unsigned kMask = kTileEntries - 1;
     for (int kb = k0 + (int)threadIdx.x; kb < k1; kb += U * kBlock) {
         unsigned q[U];
-        int c[U];
+        int c[U], rw[U];
         double a[U], xv[U];
 #pragma unroll
         for (int u = 0; u < U; ++u) {
@@ -220,21 +222,18 @@ __device__ __forceinline__ void stage_dict(double *__restrict__ sm, int k0, int 
         }
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-            const int k = kb + u * kBlock;
-            const int row = r0 + (k < k1 ? ds.rowof[k - k0] : 0);
-            c[u] = row + ds.dd[q[u] >> 8];
-            a[u] = ds.vd[q[u] & 255u];
+            rw[u] = ds.rowof[q[u] & kMask];
+            c[u] = r0 + rw[u] + ds.dd[(q[u] >> kTileShift) & 255u];
+            a[u] = ds.vd[(q[u] >> (kTileShift + 8)) & 255u];
         }
 #pragma unroll
         for (int u = 0; u < U; ++u) xv[u] = kb + u * kBlock < k1 ? fetch(c[u]) : 0.0;
 #pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const int k = kb + u * kBlock;
-            if (k < k1) {
-                sm[k - k0] = a[u] * xv[u];
-                if (diag && c[u] == r0 + ds.rowof[k - k0]) diag[ds.rowof[k - k0]] = a[u];
+        for (int u = 0; u < U; ++u)
+            if (kb + u * kBlock < k1) {
+                sm[q[u] & kMask] = a[u] * xv[u];
+                if (diag && c[u] == r0 + rw[u]) diag[rw[u]] = a[u];
             }
-        }
     }
 }
 
