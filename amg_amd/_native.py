@@ -125,6 +125,15 @@ ALLREDUCE_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, _dp, C.c_int)
 ALLGATHERV_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, _dp, C.c_int, _dp, _ip, _ip)
 
 
+# sss_hip_level_info::a_format & 3 -> storage format of a level operator
+A_FORMATS = {0: "CSR (12 B/entry)", 1: "column-sorted tiles (12 B/entry)", 2: "dictionary tiles (4 B/entry)",
+             3: "value-dictionary sorted tiles (5 B/entry)"}
+
+
+def a_format_name(code: int) -> str:
+    return A_FORMATS.get(code & 3, A_FORMATS[0])
+
+
 class SSS_HIP_HOST_TRANSPORT(C.Structure):
     _fields_ = [("ctx", C.c_void_p), ("exchange", EXCHANGE_FN), ("allreduce_sum", ALLREDUCE_FN),
                 ("allgatherv", ALLGATHERV_FN)]

@@ -111,8 +111,13 @@ struct DevCSR {
     // and distinct value bit patterns (<= 256): 4 B per entry instead of 12, gathers still in
     // column order.  dv_pd[block] = {offset base, offset count, value base, value count}.  Built
     // only when every block qualifies (7-pt Poisson level 0: 7 offsets and 2 values per block).
+    // Value-dictionary sorted tiles (kEncDict, when the offsets do not fit a dictionary but every
+    // block has <= 256 distinct values -- a relabeled Galerkin level): the sorted tiles' pk/pb with
+    // a 1-byte value index dv_vi per slot into the block's value dictionary instead of pv: 5 B per
+    // entry.  dv_code stays null, dv_pd[block].y = 0, pv is not uploaded.
     long long stream_bytes = 0;   // bytes of the stored format one tile-path SpMV streams (no vectors)
     unsigned *dv_code = nullptr;
+    unsigned char *dv_vi = nullptr;
     int4 *dv_pd = nullptr;
     int *dv_dd = nullptr;
     double *dv_vd = nullptr;
@@ -146,6 +151,8 @@ int wave_row_min();
 int free_row_min();
 struct DevDict;
 DevDict devdict(const DevCSR &A, int blo);   // the matrix's dictionary tiles, block numbers from blo
+// the tile kernels stage from a dictionary (either kind): instantiate them with DICT = true
+inline bool has_dict(const DevCSR &A) { return A.dv_code != nullptr || A.dv_vi != nullptr; }
 
 // ---- hierarchy internals shared with the distributed engine (sss_hier.hip) ------------------
 // A hierarchy over mg->cg[0 .. num_levels); its L[0] is global level `level_base` (smoother

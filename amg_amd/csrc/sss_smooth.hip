@@ -827,8 +827,8 @@ int launch_f_residual_pending(const SmootherPlan &sp, const DevCSR &A, const dou
 {
     if (!sp.pend_ok) return ERROR_INPUT_PAR;
     const PassSchedule &F = sp.pass[0];
-    const double *deff = (sp.own_diag && (A.pk || A.dv_code)) ? nullptr : sp.d_first;
-    if (A.dv_code)
+    const double *deff = (sp.own_diag && (A.pk || has_dict(A))) ? nullptr : sp.d_first;
+    if (has_dict(A))
         hipLaunchKernelGGL((relax_range<3, true>), dim3(F.bhi - F.blo), dim3(kBlock), 0, s, F.blo, A.bk, A.rp, A.ci, A.v,
                            sp.diag_pos, F.lo, b, const_cast<double *>(x), (const double *)nullptr, pend, deff, A.pk,
                            A.pv, A.pb, r, partial, xsrc_of(x), devdict(A, 0));
@@ -975,7 +975,7 @@ int smoother_run(const SmootherPlan &sp, const DevCSR &A, const double *b, doubl
                 XSrc xs = nocopy ? XSrc{cur[0], cur[1], sp.csplit} : xsrc_of(x);
                 if (pre_f && sw == 0) xs = XSrc{pre_f, x, sp.pass[0].hi};   // this sweep's F values
                 // tile passes take each row's divisor from its staged diagonal (no deff stream)
-                const bool tile_d = sp.own_diag && (A.pk != nullptr || A.dv_code != nullptr);
+                const bool tile_d = sp.own_diag && (A.pk != nullptr || has_dict(A));
                 auto relax = [&](auto mode, const int *cols, const double *yp, double *y) -> int {
                     constexpr int M = decltype(mode)::value;
                     if (wave && A.vec_rows)
@@ -986,7 +986,7 @@ int smoother_run(const SmootherPlan &sp, const DevCSR &A, const double *b, doubl
                                            A.rp, cols, A.v, b, x, yp, y, deff, xs);
                     else {
                         auto go = [&](int b0, int b1) {
-                            if (A.dv_code)
+                            if (has_dict(A))
                                 hipLaunchKernelGGL((relax_range<M, true>), dim3(b1 - b0), dim3(kBlock), 0, s, b0, A.bk,
                                                    A.rp, cols, A.v, sp.diag_pos, ps.lo, b, x, yp, y,
                                                    tile_d ? nullptr : deff, A.pk, A.pv, A.pb, (double *)nullptr,
@@ -1059,7 +1059,7 @@ int smoother_run(const SmootherPlan &sp, const DevCSR &A, const double *b, doubl
                     SSS_HIP(hipMemcpyAsync(x + ps.lo, ps.y, sizeof(double) * (size_t)m, hipMemcpyDeviceToDevice, s));
                 } else if (fused_pass) {
                     auto go = [&](int b0, int b1) {
-                        if (A.dv_code)
+                        if (has_dict(A))
                             hipLaunchKernelGGL((relax_range<2, true>), dim3(b1 - b0), dim3(kBlock), 0, s, b0, A.bk,
                                                A.rp, A.ci, A.v, sp.diag_pos, ps.lo, b, x, (const double *)nullptr,
                                                (double *)nullptr, tile_d ? nullptr : deff, A.pk, A.pv, A.pb, rf->r,

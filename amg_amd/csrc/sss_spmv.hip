@@ -249,11 +249,16 @@ static void build_merged(const SSS_MAT &h, const int *seg, int G, std::vector<in
 DevDict devdict(const DevCSR &A, int blo)
 {
     DevDict t;
-    if (!A.dv_code) return t;
+    if (!has_dict(A)) return t;
     t.code = A.dv_code;
     t.pd = A.dv_pd + blo;
     t.dd = A.dv_dd;
     t.vd = A.dv_vd;
+    if (A.dv_vi) {
+        t.pk = A.pk;
+        t.vi = A.dv_vi;
+        t.pb = A.pb + blo;
+    }
     return t;
 }
 
@@ -327,6 +332,48 @@ static bool build_dict_tiles(const SSS_MAT &h, const std::vector<int> &blk, std:
         std::copy(bd[q].begin(), bd[q].end(), dd.begin() + pd[q].x);
         for (size_t t = 0; t < bv[q].size(); ++t) std::memcpy(&vd[(size_t)pd[q].z + t], &bv[q][t], sizeof(double));
     }
+    return true;
+}
+
+// Value dictionaries over the sorted tiles' values pv (slot order): per block at most 256 distinct
+// bit patterns (false when a block has more), vi = each slot's index; pd[block] = {0, 0, base, count}.
+static bool build_value_dict(const std::vector<int> &blk, const int *rp, const std::vector<double> &pv,
+                             std::vector<unsigned char> &vi, std::vector<int4> &pd, std::vector<double> &vd)
+{
+    const int nb = (int)blk.size() - 1;
+    if (nb <= 0) return false;
+    std::vector<std::vector<unsigned long long>> bv(nb);
+    vi.resize(pv.size());
+    std::atomic<int> ok{1};
+    parallel_chunks(nb, 256, [&](int qlo, int qhi) {
+        for (int q = qlo; q < qhi && ok; ++q) {
+            auto &V = bv[q];
+            const int a0 = rp[blk[q]], e0 = rp[blk[q + 1]];
+            V.resize((size_t)(e0 - a0));
+            std::memcpy(V.data(), pv.data() + a0, sizeof(double) * (size_t)(e0 - a0));
+            std::sort(V.begin(), V.end());
+            V.erase(std::unique(V.begin(), V.end()), V.end());
+            if (V.size() > 256) {
+                ok = 0;
+                return;
+            }
+            for (int k = a0; k < e0; ++k) {
+                unsigned long long u;
+                std::memcpy(&u, &pv[(size_t)k], sizeof(u));
+                vi[(size_t)k] = (unsigned char)(std::lower_bound(V.begin(), V.end(), u) - V.begin());
+            }
+        }
+    });
+    if (!ok) return false;
+    pd.resize((size_t)nb);
+    size_t nv = 0;
+    for (int q = 0; q < nb; ++q) {
+        pd[q] = make_int4(0, 0, (int)nv, (int)bv[q].size());
+        nv += bv[q].size();
+    }
+    vd.resize(std::max<size_t>(nv, 1));
+    for (int q = 0; q < nb; ++q)
+        for (size_t t = 0; t < bv[q].size(); ++t) std::memcpy(&vd[(size_t)pd[q].z + t], &bv[q][t], sizeof(double));
     return true;
 }
 
@@ -418,21 +465,36 @@ int devcsr_upload(DevCSR &d, const SSS_MAT &h, int split, int enc, const int *se
     if ((enc & kEncSortedTiles) && !d.dv_code && !d.wave_rows && !d.vec_rows && d.nnz > 0 &&
         build_sorted_tiles(h, blk, pk, pv, pb)) {
         d.pk = dev_alloc<unsigned>((size_t)d.nnz);
-        d.pv = dev_alloc<double>((size_t)d.nnz);
         d.pb = dev_alloc<int2>(pb.size());
-        if (!d.pk || !d.pv || !d.pb) return hip_fail(hipErrorOutOfMemory, "hipMalloc(sorted tiles)", __FILE__, __LINE__);
+        if (!d.pk || !d.pb) return hip_fail(hipErrorOutOfMemory, "hipMalloc(sorted tiles)", __FILE__, __LINE__);
         if (int rc = h2d(d.pk, pk.data(), sizeof(unsigned) * (size_t)d.nnz)) return rc;
-        if (int rc = h2d(d.pv, pv.data(), sizeof(double) * (size_t)d.nnz)) return rc;
         if (int rc = h2d(d.pb, pb.data(), sizeof(int2) * pb.size())) return rc;
+        std::vector<unsigned char> vi;
+        std::vector<int4> pd;
+        std::vector<double> vd;
+        if ((enc & kEncDict) && !(dz && *dz == '0') && build_value_dict(blk, h.row_ptr, pv, vi, pd, vd)) {
+            d.dv_vi = dev_alloc<unsigned char>(vi.size());
+            d.dv_pd = dev_alloc<int4>(pd.size());
+            d.dv_vd = dev_alloc<double>(vd.size());
+            if (!d.dv_vi || !d.dv_pd || !d.dv_vd)
+                return hip_fail(hipErrorOutOfMemory, "hipMalloc(value dictionaries)", __FILE__, __LINE__);
+            if (int rc = h2d(d.dv_vi, vi.data(), vi.size())) return rc;
+            if (int rc = h2d(d.dv_pd, pd.data(), sizeof(int4) * pd.size())) return rc;
+            if (int rc = h2d(d.dv_vd, vd.data(), sizeof(double) * vd.size())) return rc;
+        } else {
+            d.pv = dev_alloc<double>((size_t)d.nnz);
+            if (!d.pv) return hip_fail(hipErrorOutOfMemory, "hipMalloc(sorted tiles)", __FILE__, __LINE__);
+            if (int rc = h2d(d.pv, pv.data(), sizeof(double) * (size_t)d.nnz)) return rc;
+        }
     }
     // what one SpMV over the stored format reads besides the vectors (reported for the roofline)
     const long long nnz = d.nnz, nb = d.nblk, rows = d.n;
-    if (d.dv_code) {
+    if (has_dict(d)) {
         long long dict = 0;
         std::vector<int4> pd((size_t)nb);
         if (nb > 0) SSS_HIP(hipMemcpy(pd.data(), d.dv_pd, sizeof(int4) * (size_t)nb, hipMemcpyDeviceToHost));
         for (const auto &p : pd) dict += 4LL * p.y + 8LL * p.w;
-        d.stream_bytes = 4 * nnz + 4 * (rows + 1) + 8 * (nb + 1) + 16 * nb + dict;
+        d.stream_bytes = (d.dv_vi ? 5 * nnz + 8 * nb : 4 * nnz) + 4 * (rows + 1) + 8 * (nb + 1) + 16 * nb + dict;
     } else if (d.pk) {
         d.stream_bytes = 12 * nnz + 4 * (rows + 1) + 8 * (nb + 1) + 8 * nb;
     } else {
@@ -455,6 +517,7 @@ void devcsr_free(DevCSR &d)
     dev_free(d.mg_k);
     dev_free(d.mg_v);
     dev_free(d.dv_code);
+    dev_free(d.dv_vi);
     dev_free(d.dv_pd);
     dev_free(d.dv_dd);
     dev_free(d.dv_vd);
@@ -580,7 +643,7 @@ static void launch_op(const DevCSR &A, double alpha, const double *x, const doub
     else if (A.wave_rows)
         hipLaunchKernelGGL((spmv_wave<OP, NORM, false>), dim3(A.ngrid), dim3(kBlock), 0, s, A.n, A.rp, A.ci, A.v, x,
                            b, y, alpha, cap, partial);
-    else if (A.dv_code)
+    else if (has_dict(A))
         hipLaunchKernelGGL((spmv_adaptive<OP, NORM, true>), dim3(A.nblk), dim3(kBlock), 0, s, A.bk, A.rp, A.ci, A.v,
                            x, b, y, alpha, cap, partial, A.pk, A.pv, A.pb, devdict(A, 0));
     else
@@ -620,7 +683,7 @@ int launch_spmv_range(const DevCSR &A, int blo, int bhi, int op, double alpha, c
     auto go = [&](auto op_c, auto norm_c) {
         constexpr int O = decltype(op_c)::value;
         constexpr bool NM = decltype(norm_c)::value;
-        if (A.dv_code)
+        if (has_dict(A))
             hipLaunchKernelGGL((spmv_adaptive<O, NM, true>), dim3(nb), dim3(kBlock), 0, s, A.bk + blo, A.rp, A.ci, A.v,
                                x, b, y, alpha, 0, pp, A.pk, A.pv, pb, dt);
         else

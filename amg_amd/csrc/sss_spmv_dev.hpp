@@ -47,6 +47,11 @@ struct DevDict {
     const int4 *pd = nullptr;   // indexed by the block number the kernel sees
     const int *dd = nullptr;
     const double *vd = nullptr;
+    // value-dictionary sorted tiles (code null): the sorted tiles' slots and cluster bases (pb
+    // indexed as pd) with a value index per slot
+    const unsigned *pk = nullptr;
+    const unsigned char *vi = nullptr;
+    const int2 *pb = nullptr;
 };
 
 // In-order chains over LDS products: 8 reads issued ahead of 8 dependent adds/subtractions,
@@ -191,6 +196,41 @@ __device__ __forceinline__ void stage_sorted(double *__restrict__ sm, int k0, in
     }
 }
 
+// Value-dictionary sorted tiles: stage_sorted with the value of slot k read from the block's
+// dictionary in LDS (vd[vi[k]], the same bit pattern pv[k] held).
+template <class Fetch>
+__device__ __forceinline__ void stage_vdict(double *__restrict__ sm, int k0, int k1, const unsigned *__restrict__ pk,
+                                            const unsigned char *__restrict__ vi, const double *vd, int2 base, int r0,
+                                            double *diag, Fetch fetch)
+{
+    constexpr int U = 8;
+    constexpr unsigned kMask = kTileEntries - 1;
+    for (int kb = k0 + (int)threadIdx.x; kb < k1; kb += U * kBlock) {
+        unsigned q[U], w[U];
+        double a[U], xv[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int k = kb + u * kBlock;
+            q[u] = k < k1 ? pk[k] : 0u;
+            w[u] = k < k1 ? vi[k] : 0u;
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const unsigned off = (q[u] >> kTileShift) & ((1u << kTileColBits) - 1);
+            const int c = off >= kTileDiagMark ? r0 + (int)(off - kTileDiagMark) : (int)off + ((q[u] >> 31) ? base.y : base.x);
+            xv[u] = kb + u * kBlock < k1 ? fetch(c) : 0.0;
+            a[u] = vd[w[u]];
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            if (kb + u * kBlock < k1) {
+                sm[q[u] & kMask] = a[u] * xv[u];
+                const unsigned off = (q[u] >> kTileShift) & ((1u << kTileColBits) - 1);
+                if (diag && off >= kTileDiagMark) diag[off - kTileDiagMark] = a[u];
+            }
+    }
+}
+
 // Dictionary tiles: slot k of segment [k0, k1) of block `bid` (rows [r0, r1)) holds
 // code = value index << 19 | offset index << 11 | pos, pos = the entry's stored-order position in
 // the segment (slots are in column order); col = row(pos) + dd[offset index], a = vd[value index];
@@ -202,8 +242,13 @@ __device__ __forceinline__ void stage_dict(double *__restrict__ sm, int k0, int 
                                            Fetch fetch)
 {
     const int4 p = dt.pd[bid];
-    for (int t = threadIdx.x; t < p.y; t += kBlock) ds.dd[t] = dt.dd[p.x + t];
     for (int t = threadIdx.x; t < p.w; t += kBlock) ds.vd[t] = dt.vd[p.z + t];
+    if (dt.vi) {   // value-dictionary sorted tiles: stage_sorted with a[k] = vd[vi[k]]
+        __syncthreads();
+        stage_vdict(sm, k0, k1, dt.pk, dt.vi, ds.vd, dt.pb[bid], r0, diag, fetch);
+        return;
+    }
+    for (int t = threadIdx.x; t < p.y; t += kBlock) ds.dd[t] = dt.dd[p.x + t];
     for (int r = r0 + (int)threadIdx.x; r < r1; r += kBlock) {
         const int a = max(rp[r], k0), e = min(rp[r + 1], k1);
         for (int k = a; k < e; ++k) ds.rowof[k - k0] = (unsigned char)(r - r0);

@@ -445,10 +445,9 @@ def main():
     csr_bytes = 12 * nnz + 4 * (N + 1) + 8 * N + 8 * N + 8 * N   # val+col, row_ptr, x, b, y
     if D.world == 1:
         info0 = DH.DH.level_info(0)
-        a_format = {1: "column-sorted tiles (12 B/entry)", 2: "dictionary tiles (4 B/entry)"}.get(
-            info0.a_format & 3, "CSR (12 B/entry)")
+        a_format = A._native.a_format_name(info0.a_format)
         level_formats = [DH.DH.level_info(l).a_format for l in range(len(table) - 1)]
-        # the stored format's own bytes (dictionary tiles: 2 B per entry + block dictionaries)
+        # the stored format's own bytes (dictionary tiles: 4 B per entry + block dictionaries)
         spmv_bytes = info0.a_stream_bytes + 8 * N + 8 * N + 8 * N
     else:
         m, g = DH.rows, DH.ghosts

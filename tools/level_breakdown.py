@@ -38,7 +38,7 @@ def main():
         m = re.search(r"(spmv_\w+)<(\d), (true|false)(?:, \w+)?>", name)
         # the outer residual norm ends a cycle: the fused-norm SpMV, or relax_range<3> (its F half
         # fused with the next cycle's first F pass, SmootherPlan::pend_ok)
-        if (m and m.group(2) == "2" and m.group(3) == "true") or "relax_range<3>" in name:
+        if (m and m.group(2) == "2" and m.group(3) == "true") or "relax_range<3" in name:
             if cur is not None:
                 cur[("out", "resid")] += dur
                 cycles.append(cur)

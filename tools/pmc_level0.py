@@ -36,4 +36,9 @@ N = H.level(0).A.num_rows
 D.upload(0, "b", np.ones(N))
 D.upload(0, "x", np.ones(N))
 ms = D.time_level0_spmv(reps)
+info = D.level_info(0)
 print(f"level0 n={N} nnz={H.level(0).A.num_nnzs} avg_ms={ms:.4f}", flush=True)
+import json  # noqa: E402
+print(json.dumps({"n": n, "rows": N, "nnz": H.level(0).A.num_nnzs, "avg_ms": ms,
+                  "a_format": A._native.a_format_name(info.a_format),
+                  "algorithmic_bytes_per_launch": int(info.a_stream_bytes) + 24 * N}), flush=True)
