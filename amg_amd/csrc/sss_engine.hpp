@@ -100,6 +100,10 @@ struct DevCSR {
     // (or each of its two segments [rp, seg) / [seg, rp+1)) column-sorted for the wave-per-row
     // kernels (64 lane-strided sums, xor-shuffle reduction) ...
     bool vec_rows = false;
+    // ... and on a short-row matrix of a free-order level, the rows longer than one tile (a hub
+    // row of an irregular operator) are tree-summed chunk by chunk by the whole workgroup instead
+    // of chained by one thread (block_tree_sum; the short rows keep the stored order)
+    bool tree_long = false;
     // ... and, for matrices with enough rows to fill the chip in groups (merge_group_size), a
     // merged copy: G consecutive rows' entries merged into one column-sorted list, packed
     // col << 4 | segment << 3 | row-in-group (segment: 0, or 1 for [seg, rp+1) of two-segment rows).  One wave sums a group lane-strided with one accumulator per

@@ -39,6 +39,8 @@ struct sss_hip_hier {
     } L[kMaxLevels];
     std::vector<double> stage;   // host staging for permuted vector transfers
     int level_base = 0;          // global level index of L[0] (a tail of a distributed hierarchy)
+    // hybrid smoother on a level 0 whose classes are not independent sets: two-stage GS-CF there
+    bool hybrid0_two_stage = false;
     bool own_stream = true;
     int coarse_mode = SSS_HIP_COARSE_DIRECT;
     CoarseDirect direct;
@@ -131,11 +133,44 @@ int sss::level_encoding(const sss_hip_opts &o)
 }
 int sss::level_inner_of(const sss_hip_opts &o, int l) { return level_inner(o, l); }
 
+// Are the C and the F points of A each an independent set (no off-diagonal coupling inside a
+// class)?  Then exact GS-CF has no chains: each class pass is one C/F-Jacobi pass (7-pt level 0).
+static bool classes_independent(const SSS_MAT &A, const int *mark)
+{
+    std::atomic<int> ok{1};
+    parallel_chunks(A.num_rows, 1 << 14, [&](int lo, int hi) {
+        for (int i = lo; i < hi && ok; ++i) {
+            const bool ci = mark[i] == 1;
+            for (int k = A.row_ptr[i]; k < A.row_ptr[i + 1]; ++k) {
+                const int j = A.col_idx[k];
+                if (j != i && (mark[j] == 1) == ci) {
+                    ok = 0;
+                    return;
+                }
+            }
+        }
+    });
+    return ok != 0;
+}
+
+// per-level smoother of this hierarchy (level_smoother_kind/level_inner with the hybrid level-0
+// rule applied)
+static int hier_kind(const sss_hip_hier *h, int gl)
+{
+    if (gl == 0 && h->hybrid0_two_stage) return SSS_HIP_SMOOTH_JACOBI;
+    return level_smoother_kind(h->opts, gl);
+}
+static int hier_inner(const sss_hip_hier *h, int gl)
+{
+    if (gl == 0 && h->hybrid0_two_stage) return std::max(1, h->opts.inner);
+    return level_inner(h->opts, gl);
+}
+
 // Natural-order GS (SSS_amg_smoother_pre/post with cf_order = 0, Solve/SSS_smooth.c:171-176,
 // 256-260) on the levels the reference would smooth by GS
 static bool natural_level(const sss_hip_hier *h, int gl)
 {
-    return h->pars.cf_order == 0 && h->pars.smoother == SSS_SM_GS && level_smoother_kind(h->opts, gl) == SSS_HIP_SMOOTH_EXACT;
+    return h->pars.cf_order == 0 && h->pars.smoother == SSS_SM_GS && hier_kind(h, gl) == SSS_HIP_SMOOTH_EXACT;
 }
 
 static void hier_release(sss_hip_hier *h)
@@ -261,6 +296,13 @@ sss_hip_hier *sss::hier_create_impl(const SSS_AMG *mg, const sss_hip_opts *o, in
     }
     if (hipEventCreate(&h->ev0) != hipSuccess || hipEventCreate(&h->ev1) != hipSuccess) return fail("events");
 
+    // hybrid: exact GS-CF on level 0 only where it is chain-free (its cost is then that of
+    // C/F-Jacobi); a level 0 with same-class couplings (27-pt, irregular operators) would run the
+    // level-scheduled chains every sweep -- there the two-stage form takes its place
+    if (h->opts.smoother == SSS_HIP_SMOOTH_HYBRID && level_base == 0 && h->nl > 1 && mg->cg[0].cfmark.d &&
+        mg->cg[0].cfmark.n >= mg->cg[0].A.num_rows && mg->pars.cf_order != 0)
+        h->hybrid0_two_stage = !classes_independent(mg->cg[0].A, mg->cg[0].cfmark.d);
+
     // F|C relabeling of every level but the coarsest (identity there)
     std::vector<std::vector<int>> inv(h->nl);
     std::vector<int> nF(h->nl, -1);
@@ -270,7 +312,7 @@ sss_hip_hier *sss::hier_create_impl(const SSS_AMG *mg, const sss_hip_opts *o, in
             if (!C.cfmark.d || C.cfmark.n < n) continue;
             // two-stage levels need contiguous classes; otherwise follow opts.relabel
             const int gl = h->level_base + l;
-            const bool two_stage = level_inner(h->opts, gl) > 0;
+            const bool two_stage = hier_inner(h, gl) > 0;
             if (natural_level(h, gl)) continue;   // the natural order is the stored row order
             if (!two_stage && !(h->opts.relabel == 1 || (h->opts.relabel == 2 && gl > 0))) continue;
             auto &perm = h->L[l].perm;
@@ -303,15 +345,15 @@ sss_hip_hier *sss::hier_create_impl(const SSS_AMG *mg, const sss_hip_opts *o, in
             t_up = now();
             std::vector<int> mark(n);
             for (int i = 0; i < n; ++i) mark[i] = C.cfmark.d[L.perm[i]];
-            if (smoother_build(L.sm, Av, mark.data(), level_smoother_kind(h->opts, h->level_base + l), &L.A,
-                               level_inner(h->opts, h->level_base + l), nullptr, enc))
+            if (smoother_build(L.sm, Av, mark.data(), hier_kind(h, h->level_base + l), &L.A,
+                               hier_inner(h, h->level_base + l), nullptr, enc))
                 return fail("smoother plan");
             t_sm = now();
         } else {
             if (devcsr_upload(L.A, C.A, -1, enc)) return fail("upload A");
             if (l < h->nl - 1 && natural_level(h, h->level_base + l)) {
                 if (smoother_build_natural(L.sm, C.A, 0, n)) return fail("smoother plan");
-            } else if (l < h->nl - 1 && smoother_build(L.sm, C.A, C.cfmark.d, level_smoother_kind(h->opts, h->level_base + l),
+            } else if (l < h->nl - 1 && smoother_build(L.sm, C.A, C.cfmark.d, hier_kind(h, h->level_base + l),
                                                        nullptr, 0, nullptr, enc)) {
                 return fail("smoother plan");
             }
@@ -739,6 +781,7 @@ extern "C" int sss_hip_level_info_get(sss_hip_hier *h, int level, sss_hip_level_
     out->dag_f = L.sm.pass[0].depth;
     out->dag_c = L.sm.pass[1].depth;
     out->smoother_kind = L.sm.kind;
+    out->inner = L.sm.inner;
     out->gs_engine_f = L.sm.pass[0].gp.engine;
     out->gs_engine_c = L.sm.pass[1].gp.engine;
     unsigned ef = 0, ec = 0;

@@ -550,7 +550,12 @@ __global__ __launch_bounds__(kBlock) void relax_range(int blo, const int2 *__res
             stage_any(sm.v, base, base + m, ci, v, pk, pv, pb, bid, r0, deff ? (double *)nullptr : sm.d, fetch, dt, ds,
                       r1, rp);
             __syncthreads();
-            if (threadIdx.x == 0) {
+            if (dt.tree_long) {   // free order: acc -= tree sum of the chunk's off-diagonal products
+                if (threadIdx.x == 0 && dp >= base && dp < base + m) sm.v[dp - base] = 0.0;
+                __syncthreads();
+                const double c = block_tree_sum(sm.v, 0, m, sm.red);
+                if (threadIdx.x == 0) acc -= c;
+            } else if (threadIdx.x == 0) {
                 if (dp >= base && dp < base + m) {
                     acc = chain_sub(acc, sm.v, 0, dp - base);
                     acc = chain_sub(acc, sm.v, dp - base + 1, m);
@@ -669,7 +674,16 @@ __global__ __launch_bounds__(kBlock) void ts_stage0(int lo, DevCSR M, const int 
                 const int m = min(kTileEntries, k1 - base);
                 stage_any(sm.v, base, base + m, M.ci, M.v, M.pk, M.pv, M.pb, bq, q0, (double *)nullptr, [&](int c) -> double { return x(c); });
                 __syncthreads();
-                if (threadIdx.x == 0) {
+                if (M.tree_long) {   // free order: the N part and the L part of the chunk tree-summed
+                    const int cut = min(max(sp - base, 0), m);
+                    const double c1 = block_tree_sum(sm.v, 0, cut, sm.red);
+                    const double c2 = block_tree_sum(sm.v, cut, m, sm.red);
+                    if (threadIdx.x == 0) {
+                        acc -= c1;
+                        if (sp >= base && sp < base + m) P[q] = acc;
+                        acc -= c2;
+                    }
+                } else if (threadIdx.x == 0) {
                     if (sp >= base && sp < base + m) {
                         acc = chain_sub(acc, sm.v, 0, sp - base);
                         P[q] = acc;
@@ -746,7 +760,12 @@ __global__ __launch_bounds__(kBlock) void ts_inner(int lo, DevCSR M, const doubl
                 const int m = min(kTileEntries, k1 - base);
                 stage_any(sm.v, base, base + m, M.ci, M.v, M.pk, M.pv, M.pb, bq, q0, (double *)nullptr, fetch);
                 __syncthreads();
-                if (threadIdx.x == 0) acc = chain_sub(acc, sm.v, 0, m);
+                if (M.tree_long) {
+                    const double c = block_tree_sum(sm.v, 0, m, sm.red);
+                    if (threadIdx.x == 0) acc -= c;
+                } else if (threadIdx.x == 0) {
+                    acc = chain_sub(acc, sm.v, 0, m);
+                }
                 __syncthreads();
             }
             if (threadIdx.x == 0) finish(q, acc);
@@ -835,7 +854,7 @@ int launch_f_residual_pending(const SmootherPlan &sp, const DevCSR &A, const dou
     else
         hipLaunchKernelGGL((relax_range<3, false>), dim3(F.bhi - F.blo), dim3(kBlock), 0, s, F.blo, A.bk, A.rp, A.ci, A.v,
                            sp.diag_pos, F.lo, b, const_cast<double *>(x), (const double *)nullptr, pend, deff, A.pk,
-                           A.pv, A.pb, r, partial, xsrc_of(x), DevDict());
+                           A.pv, A.pb, r, partial, xsrc_of(x), devdict(A, 0));
     SSS_HIP(hipGetLastError());
     return 0;
 }
@@ -995,7 +1014,7 @@ int smoother_run(const SmootherPlan &sp, const DevCSR &A, const double *b, doubl
                                 hipLaunchKernelGGL((relax_range<M, false>), dim3(b1 - b0), dim3(kBlock), 0, s, b0, A.bk,
                                                    A.rp, cols, A.v, sp.diag_pos, ps.lo, b, x, yp, y,
                                                    tile_d ? nullptr : deff, A.pk, A.pv, A.pb, (double *)nullptr,
-                                                   (double *)nullptr, xs, DevDict());
+                                                   (double *)nullptr, xs, devdict(A, 0));
                         };
                         if (split_pass) return hk->split(x, ps.blo, ps.bhi, go);
                         go(ps.blo, ps.bhi);
@@ -1068,7 +1087,7 @@ int smoother_run(const SmootherPlan &sp, const DevCSR &A, const double *b, doubl
                             hipLaunchKernelGGL((relax_range<2, false>), dim3(b1 - b0), dim3(kBlock), 0, s, b0, A.bk,
                                                A.rp, A.ci, A.v, sp.diag_pos, ps.lo, b, x, (const double *)nullptr,
                                                (double *)nullptr, tile_d ? nullptr : deff, A.pk, A.pv, A.pb, rf->r,
-                                               rf->partial, xs, DevDict());
+                                               rf->partial, xs, devdict(A, 0));
                     };
                     if (split_pass) {
                         if ((rc = hk->split(x, ps.blo, ps.bhi, go))) return rc;

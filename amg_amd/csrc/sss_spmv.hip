@@ -249,6 +249,7 @@ static void build_merged(const SSS_MAT &h, const int *seg, int G, std::vector<in
 DevDict devdict(const DevCSR &A, int blo)
 {
     DevDict t;
+    t.tree_long = A.tree_long ? 1 : 0;
     if (!has_dict(A)) return t;
     t.code = A.dv_code;
     t.pd = A.dv_pd + blo;
@@ -384,6 +385,7 @@ int devcsr_upload(DevCSR &d, const SSS_MAT &h, int split, int enc, const int *se
     d.nnz = h.num_nnzs;
     d.wave_rows = d.n > 0 && (long long)d.nnz >= (long long)wave_row_min() * d.n;
     d.vec_rows = d.n > 0 && (enc & kEncFreeOrder) && (long long)d.nnz >= (long long)free_row_min() * d.n;
+    d.tree_long = (enc & kEncFreeOrder) && !d.vec_rows;
     if (d.vec_rows && (unsigned long long)std::max(d.ncols, 1) < (1ull << (32 - kMergeShift))) {
         d.mg_G = merge_group_size(d.n);
         if (seg && d.mg_G > 4) d.mg_G = 4;   // two segments: 2G accumulators per lane
@@ -648,7 +650,7 @@ static void launch_op(const DevCSR &A, double alpha, const double *x, const doub
                            x, b, y, alpha, cap, partial, A.pk, A.pv, A.pb, devdict(A, 0));
     else
         hipLaunchKernelGGL((spmv_adaptive<OP, NORM>), dim3(A.nblk), dim3(kBlock), 0, s, A.bk, A.rp, A.ci, A.v, x,
-                           b, y, alpha, cap, partial, A.pk, A.pv, A.pb, DevDict());
+                           b, y, alpha, cap, partial, A.pk, A.pv, A.pb, devdict(A, 0));
 }
 
 int launch_spmv(const DevCSR &A, int op, double alpha, const double *x, const double *b, double *y, int cap,

@@ -52,6 +52,7 @@ struct DevDict {
     const unsigned *pk = nullptr;
     const unsigned char *vi = nullptr;
     const int2 *pb = nullptr;
+    int tree_long = 0;   // DevCSR::tree_long (set for every matrix, dictionary or not)
 };
 
 // In-order chains over LDS products: 8 reads issued ahead of 8 dependent adds/subtractions,
@@ -105,6 +106,16 @@ __device__ __forceinline__ double block_max(double v, double *red)
     if (threadIdx.x == 0)
         for (int w = 0; w < (int)(blockDim.x >> 6); ++w) t = fmax(t, red[w]);
     return t;
+}
+
+// Tree sum of the LDS products p[a, e) (thread-strided partial sums, block_sum): the free
+// summation order of a long row's chunk (DevCSR::tree_long).  Result valid in thread 0; every
+// thread of the block must call it.
+__device__ __forceinline__ double block_tree_sum(const double *p, int a, int e, double *red)
+{
+    double t = 0.0;
+    for (int k = a + (int)threadIdx.x; k < e; k += kBlock) t += p[k];
+    return block_sum(t, red);
 }
 
 // Phase 1 of every tile kernel: sm[k - k0] = v[k] * x[ci[k]] for k in [k0, k1).  Each thread
@@ -361,7 +372,12 @@ __device__ __forceinline__ double csr_block_rows(const BlkT *__restrict__ blk, c
             else if (pk) stage_sorted(sm.v, base, base + m, pk, pv, pb[bid], r0, (double *)nullptr, fetch);
             else stage_products(sm.v, base, base + m, ci, v, x);
             __syncthreads();
-            if (threadIdx.x == 0) s = chain_add(s, sm.v, 0, m);
+            if (dt && dt->tree_long) {
+                const double c = block_tree_sum(sm.v, 0, m, sm.red);
+                if (threadIdx.x == 0) s += c;
+            } else if (threadIdx.x == 0) {
+                s = chain_add(s, sm.v, 0, m);
+            }
             __syncthreads();
         }
         if (threadIdx.x == 0) contrib = epi(r0, s);

@@ -57,6 +57,12 @@ def parse():
     p.add_argument("--stencil", type=int, default=None, choices=[7, 27],
                    help="7: 7-pt Poisson (the metric's workload); 27: the 27-pt anisotropic operator of "
                         "BASELINE.json configs[4] (SURVEY.md 8(d)); default 27 at N=4, else 7")
+    p.add_argument("--workload", default="stencil", choices=["stencil", "circuit"],
+                   help="stencil: the --stencil operator on an --n grid; circuit: the G3_circuit stand-in "
+                        "(BASELINE.json configs[3], amg_amd/workloads.py; --n = rows, default 1,585,478; 1 GPU)")
+    p.add_argument("--parity-converge", type=int, default=None,
+                   help="run the parity-mode mirror to tol (reference iteration count measured in this run); "
+                        "default 1 for --workload circuit, else 0 (the 400^3 count comes from profiles/)")
     p.add_argument("--mode", default="throughput", choices=["throughput", "parity"])
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-threads", type=int, default=0,
@@ -324,10 +330,16 @@ def main():
         return
     # the BASELINE.json config of this rank count (configs[2]: 512^3 on 8 GPUs; configs[4]: 27-pt
     # 256^3 on 4 GPUs; the metric's 64M-row 400^3 otherwise)
+    circuit = args.workload == "circuit"
+    if circuit and D.world > 1:
+        raise SystemExit("bench.py: --workload circuit is a single-GPU configuration (BASELINE.json configs[3])")
     if args.stencil is None:
         args.stencil = 27 if D.world == 4 and args.n is None else 7
     if args.n is None:
-        args.n = 256 if args.stencil == 27 else {8: 512}.get(D.world, 400)
+        from amg_amd.workloads import G3_CIRCUIT_ROWS
+        args.n = G3_CIRCUIT_ROWS if circuit else 256 if args.stencil == 27 else {8: 512}.get(D.world, 400)
+    if args.parity_converge is None:
+        args.parity_converge = 1 if circuit else 0
     hb_stop = threading.Event()
     threading.Thread(target=heartbeat, args=(hb_stop, time.perf_counter()), daemon=True).start()
     import amg_amd as A
@@ -351,6 +363,12 @@ def main():
         if cache is not None and cache.exists():
             H = A.Hierarchy.load(cache)
             hier_src = f"loaded from {cache}"
+        elif circuit:
+            from amg_amd.workloads import circuit_csr
+            M = circuit_csr(n)
+            H = quiet_call(A.Hierarchy, M.mat)
+            del M
+            hier_src = "setup"
         else:
             M = A.generate(args.stencil, n)
             H = quiet_call(A.Hierarchy, M)
@@ -442,18 +460,23 @@ def main():
     spmv_ms = DH.time_level0_spmv(20)
     a_format = None
     level_formats = None
+    level_smoothers = None
     csr_bytes = 12 * nnz + 4 * (N + 1) + 8 * N + 8 * N + 8 * N   # val+col, row_ptr, x, b, y
     if D.world == 1:
         info0 = DH.DH.level_info(0)
         a_format = A._native.a_format_name(info0.a_format)
         level_formats = [DH.DH.level_info(l).a_format for l in range(len(table) - 1)]
+        level_smoothers = [(DH.DH.level_info(l).smoother_kind, DH.DH.level_info(l).inner) for l in range(len(table) - 1)]
         # the stored format's own bytes (dictionary tiles: 4 B per entry + block dictionaries)
         spmv_bytes = info0.a_stream_bytes + 8 * N + 8 * N + 8 * N
     else:
         m, g = DH.rows, DH.ghosts
         spmv_bytes = 12 * DH.nnz + 4 * (m + 1) + 8 * (m + g) + 8 * m + 8 * m
         csr_bytes = spmv_bytes
-    achieved = spmv_bytes / (spmv_ms * 1e-3) / 1e9
+    # roofline.achieved uses the algorithmic bytes of the CSR SpMV (12 B per entry +
+    # row pointers + vectors); the bytes the stored format actually streams are reported beside it
+    achieved = csr_bytes / (spmv_ms * 1e-3) / 1e9
+    format_gbps = spmv_bytes / (spmv_ms * 1e-3) / 1e9
 
     # iterations to tol from x0 = 1 (the CLI's problem), and time to solution
     DH.set_x_ones()
@@ -494,21 +517,31 @@ def main():
         PD.upload(0, "x", np.ones(N))
         t0 = time.perf_counter()
         prel = []
-        for _ in range(args.parity_cycles):
+        ncyc = args.converge_max if args.parity_converge else args.parity_cycles
+        for _ in range(ncyc):
             PD.cycle()
             prel.append(PD.residual_norm() / float(np.sqrt(N)))
-        pdt = (time.perf_counter() - t0) / args.parity_cycles
+            if args.parity_converge and prel[-1] < pars["tol"]:
+                break
+        pdt = (time.perf_counter() - t0) / len(prel)
         info = [PD.level_info(l) for l in range(len(table) - 1)]
         PD.close()
         parity = {"value": 1.0 / pdt, "unit": "V-cycle iter/s", "ms_per_step": pdt * 1e3, "upload_s": up,
-                  "relres_first_cycles": prel, "gs_engines": [[i.gs_engine_f, i.gs_engine_c] for i in info],
+                  "relres_first_cycles": prel[:4], "gs_engines": [[i.gs_engine_f, i.gs_engine_c] for i in info],
                   "gs_stall": any(i.gs_stall for i in info)}
+        if args.parity_converge:
+            parity.update(iterations_to_tol=len(prel), final_relres=prel[-1], time_to_solution_s=pdt * len(prel))
         print(f"[bench] parity mode: {pdt * 1e3:.1f} ms per V-cycle (upload {up:.1f} s)", file=sys.stderr, flush=True)
     # reference-semantics iteration counts measured with the parity engine (tools/conv_study.py; the
     # parity engine's printed history equals the reference's, tests/test_gpu_at_size.py)
     ref_conv = None
     conv = ROOT / "profiles" / f"r02_conv{n}_parity_vs_throughput.json"
-    if conv.exists() and args.stencil == 7:
+    if parity and args.parity_converge:
+        ref_conv = {"iterations_to_tol_reference": parity["iterations_to_tol"],
+                    "iterations_to_tol_throughput_same_run": its,
+                    "parity_ms_per_cycle_same_run": parity["ms_per_step"],
+                    "source": "this run (parity-mode mirror to tol)"}
+    elif conv.exists() and args.stencil == 7 and not circuit:
         try:
             cj = json.loads(conv.read_text())["modes"]
             ref_conv = {"iterations_to_tol_reference": cj["parity"]["iters"],
@@ -542,10 +575,11 @@ def main():
         hb_stop = threading.Event()
         threading.Thread(target=heartbeat, args=(hb_stop, time.perf_counter()), daemon=True).start()
         Hc = H
-        if args.cpu_n and args.cpu_n != n:
+        if args.cpu_n and args.cpu_n != n and not circuit:
             Mc = A.generate(args.stencil, args.cpu_n)
             Hc = quiet_call(A.Hierarchy, Mc)
-        cpu_n = args.cpu_n or n
+        cpu_n = n if circuit else (args.cpu_n or n)
+        wname = f"G3_circuit stand-in ({n} rows)" if circuit else f"{args.stencil}-pt {cpu_n}^3"
         hostinfo = host_cpus()
         a0_bytes = 12 * nnz + 4 * (N + 1) + 24 * N
         print("[bench] CPU baseline: reference semantics, 1 thread", file=sys.stderr, flush=True)
@@ -555,7 +589,7 @@ def main():
             "value": 1.0 / cpu["seconds"], "unit": "V-cycle iter/s", "cores": 1, "kind": "port",
             "sample": f"median of {args.cpu_iters} outer iterations after {args.cpu_warmup} warm-up (V-cycle incl. the "
                       f"reference CG(beta=1)+GMRES coarse solve, residual, norm) of oracle/sss_oracle.c with the "
-                      f"reference semantics on the same {args.stencil}-pt {cpu_n}^3 hierarchy, 1 host thread, run "
+                      f"reference semantics on the same {wname} hierarchy, 1 host thread, run "
                       f"after the GPU measurements; coarse solve {cpu['coarse_seconds']:.1f} s of {cpu['seconds']:.1f} s",
             "seconds": cpu["seconds"], "seconds_all": cpu["seconds_all"], "coarse_seconds": cpu["coarse_seconds"],
             "fine_spmv_GBps": a0_bytes / cpu["spmv_seconds"] / 1e9 if cpu_n == n else None,
@@ -567,14 +601,18 @@ def main():
         mt = {}
         mode = {}
         if args.mode == "throughput":
-            mode = dict(smoother=1, jacobi_from=1, coarse_mode=1 if coarse == "direct" else 0,
-                        inner=inner if smoother != "exact" else 0, inner_mask=~((1 << inner_from) - 1))
+            # the device's per-level smoothers (hybrid: level 0 exact only where chain-free)
+            jac = [l for l, (k, _) in enumerate(level_smoothers) if k == 2]   # SSS_HIP_SMOOTH_JACOBI
+            mask = sum(1 << l for l, (_, i) in enumerate(level_smoothers) if i > 0)
+            mode = dict(smoother=1, jacobi_from=jac[0] if jac else len(level_smoothers),
+                        coarse_mode=1 if coarse == "direct" else 0,
+                        inner=max((i for _, i in level_smoothers), default=0), inner_mask=mask if mask else 1 << 30)
         cpu_iterations(Hc, mt, threads=thr, iters=args.cpu_iters, warmup=args.cpu_warmup, **mode)
         cpu_mt = {
             "value": 1.0 / mt["seconds"], "unit": "V-cycle iter/s", "cores": mt["threads"], "kind": "port",
             "sample": f"median of {args.cpu_iters} outer iterations after {args.cpu_warmup} warm-up, "
                       f"oracle/sss_oracle.c in the GPU's mode ({smoother} smoother, {coarse} coarse solve) on the same "
-                      f"{args.stencil}-pt {cpu_n}^3 hierarchy, row loops on {mt['threads']} host threads; coarse solve "
+                      f"{wname} hierarchy, row loops on {mt['threads']} host threads; coarse solve "
                       f"{mt['coarse_seconds']:.2f} s of {mt['seconds']:.2f} s",
             "seconds": mt["seconds"], "seconds_all": mt["seconds_all"], "coarse_seconds": mt["coarse_seconds"],
             "fine_spmv_GBps": a0_bytes / mt["spmv_seconds"] / 1e9 if cpu_n == n else None,
@@ -586,8 +624,10 @@ def main():
         "value": value, "unit": "V-cycle iter/s", "n_gpus": D.world, "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": ms_per_step, "higher_is_better": True,
         "scaling": "strong" if D.world > 1 else None, "vs_baseline": None,
-        "dtype": "f64", "data": f"synthetic ({args.stencil}-pt Poisson generated in memory, b = x0 = 1)",
-        "config": {"workload": f"poisson{args.stencil}_{n}^3", "rows": N, "nnz": nnz, "levels": len(levels),
+        "dtype": "f64",
+        "data": ("synthetic (G3_circuit stand-in: weighted graph Laplacian + shift, amg_amd/workloads.py; b = x0 = 1)"
+                 if circuit else f"synthetic ({args.stencil}-pt Poisson generated in memory, b = x0 = 1)"),
+        "config": {"workload": f"g3_circuit_standin_{n}" if circuit else f"poisson{args.stencil}_{n}^3", "rows": N, "nnz": nnz, "levels": len(levels),
                    "hierarchy": [list(t) for t in levels],
                    "mode": args.mode, "smoother": smoother, "coarse": coarse,
                    "inner": inner if smoother != "exact" else None,
@@ -595,6 +635,8 @@ def main():
                    "sum_order": "tree (long rows)" if sum_order == 1 else "stored CSR order",
                    "sorted_tiles": bool(sorted_tiles),
                    "level_storage_bits": level_formats,
+                   "level_smoothers": [["exact", "hybrid", "jacobi"][k] + (f"+inner{i}" if i else "")
+                                       for k, i in level_smoothers] if level_smoothers else None,
                    "iterations_to_tol": its, "final_relres": relres, "time_to_solution_s": solve_s,
                    "amg_pcg": pcg,
                    "reference_convergence": ref_conv,
@@ -607,11 +649,13 @@ def main():
         "roofline": {"bound": "hbm", "kernel": "spmv_adaptive<RESID> level 0", "achieved": achieved,
                      "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": achieved / PEAK_HBM_GBS,
                      "frac_of_copy_peak": achieved / COPY_PEAK_GBS, "avg_launch_ms": spmv_ms,
-                     "bytes_per_launch": spmv_bytes, "traffic": traffic, "a_format": a_format,
-                     "csr_equivalent": {"bytes_per_launch": csr_bytes,
-                                        "GBps": csr_bytes / (spmv_ms * 1e-3) / 1e9,
-                                        "note": "SURVEY 8(d) CSR bytes (12 B/entry) over the same time: the rate a "
-                                                "CSR SpMV would need to match this kernel"}},
+                     "bytes_per_launch": csr_bytes, "traffic": traffic,
+                     "algorithmic_bytes": "SURVEY.md 8(d): 12 nnz + 4 (n + 1) + 8 n_cols + 16 n (y = b - A x)",
+                     "stored_format": {"a_format": a_format, "bytes_per_launch": spmv_bytes, "GBps": format_gbps,
+                                       "frac": format_gbps / PEAK_HBM_GBS,
+                                       "note": "bytes the stored format of A_0 streams per launch (dictionary "
+                                               "tiles: 4 B per entry + block dictionaries) + the vectors, over "
+                                               "the same time; traffic = HBM bytes from the PMC counters"}},
         "vcycle_csr_equivalent": {
             "bytes_per_step": vbytes, "achieved": vbytes / (ms_per_step * 1e-3) / 1e9, "peak": PEAK_HBM_GBS,
             "unit": "GB/s", "frac": vbytes / (ms_per_step * 1e-3) / 1e9 / PEAK_HBM_GBS,

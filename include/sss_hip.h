@@ -27,7 +27,9 @@ extern "C" {
 /* ---- engine options ------------------------------------------------------------------ */
 enum {
     SSS_HIP_SMOOTH_EXACT = 0,    /* reference GS-CF on every level (level-scheduled, bitwise) */
-    SSS_HIP_SMOOTH_HYBRID = 1,   /* exact GS-CF on level 0, C/F-Jacobi below */
+    SSS_HIP_SMOOTH_HYBRID = 1,   /* exact GS-CF on level 0 when its C and F classes are independent
+                                    sets (red-black: no chains), else two-stage GS-CF there;
+                                    C/F-Jacobi (two-stage from inner_from) below */
     SSS_HIP_SMOOTH_JACOBI = 2    /* C/F-Jacobi on every level */
 };
 enum {
@@ -104,12 +106,15 @@ int sss_hip_sync(sss_hip_hier *h);
 /* Per-level statistics for reporting: rows, nnz(A), nnz(P), smoother DAG depths; the exact GS
  * engine of the F / C pass (0: one launch per DAG depth, 1: chip-wide dataflow, 2: single CU);
  * whether a one-launch pass ever gave up waiting (gs_stall != 0: results invalid); the storage of
- * A_l in HBM (a_format bits: 1 column-sorted tiles, 2 dictionary tiles, 4 free-order rows,
- * 8 merged row groups, 16 wave-per-row). */
+ * A_l in HBM (a_format bits: 1 column-sorted tiles, 2 dictionary tiles (with 1: value
+ * dictionaries over the sorted tiles), 4 free-order rows, 8 merged row groups, 16 wave-per-row);
+ * the two-stage inner steps of a C/F-Jacobi level (0: plain C/F-Jacobi). */
 typedef struct sss_hip_level_info {
     int rows, nnz, nnz_p, dag_f, dag_c, smoother_kind;
     int gs_engine_f, gs_engine_c, gs_stall, a_format;
     long long a_stream_bytes;   /* bytes of A_l's stored format one tile-path SpMV reads (no vectors) */
+    int inner;
+    int pad_;
 } sss_hip_level_info;
 int sss_hip_level_info_get(sss_hip_hier *h, int level, sss_hip_level_info *out);
 int sss_hip_num_levels(sss_hip_hier *h);

@@ -91,3 +91,21 @@ def quiet():
 def build_hierarchy(M, quiet_cls):
     with quiet_cls():
         return A.Hierarchy(M)
+
+
+def device_mode_oracle_opts(H, **device_kw) -> dict:
+    """Oracle options (oracle.opts) of the per-level smoothers a DeviceHierarchy(H, **device_kw)
+    actually runs -- throughput mode's hybrid keeps exact GS-CF on level 0 only when that level is
+    chain-free, else the two-stage form there (sss_hier.hip hybrid0_two_stage).  Needs a GPU."""
+    D = A.DeviceHierarchy(H, **device_kw)
+    try:
+        info = [D.level_info(l) for l in range(H.num_levels - 1)]
+    finally:
+        D.close()
+    jac = [l for l, i in enumerate(info) if i.smoother_kind == 2]   # SSS_HIP_SMOOTH_JACOBI
+    mask = sum(1 << l for l, i in enumerate(info) if i.inner > 0)
+    kw = dict(smoother=1, jacobi_from=jac[0] if jac else len(info),
+              inner=max((i.inner for i in info), default=0), inner_mask=mask if mask else 1 << 30)
+    if device_kw.get("coarse") == "direct":
+        kw["coarse_mode"] = 1
+    return kw

@@ -19,7 +19,7 @@ import pytest
 import amg_amd as A
 import oracle
 from amg_amd._native import SSS_SMTR, dptr, iptr
-from conftest import build_hierarchy, oracle_solve, vec
+from conftest import device_mode_oracle_opts, build_hierarchy, oracle_solve, vec
 
 pytestmark = pytest.mark.gpu
 
@@ -330,7 +330,9 @@ def _mask(inner_from):
 
 @pytest.mark.parametrize("inner,inner_from", [(0, 2), (1, 1), (1, 2)])
 def test_solve_hybrid_jacobi_converges(p32_h, inner, inner_from):
-    rel_o, x_o = _oracle_history(p32_h, smoother=1, coarse_mode=1, inner=inner, inner_mask=_mask(inner_from))
+    kw = device_mode_oracle_opts(p32_h, smoother="hybrid", coarse="direct", inner=inner, inner_from=inner_from)
+    assert kw["inner_mask"] & ~_mask(inner_from) == 0   # 7-pt level 0 is chain-free: exact there
+    rel_o, x_o = _oracle_history(p32_h, **kw)
     rel_g, x_g = _gpu_history(p32_h, smoother="hybrid", coarse="direct", inner=inner, inner_from=inner_from)
     assert len(rel_g) == len(rel_o)
     assert np.allclose(rel_g, rel_o, rtol=1e-6)
@@ -392,7 +394,8 @@ def test_relabeled_level_smoothers_bitwise(request, hname, smoother, inner, row_
 def test_solve_hybrid_krylov_bitwise(request, hname, inner, inner_from, row_path):
     """Throughput smoothers with the reference coarse solver: x bitwise equal to the oracle's."""
     H = request.getfixturevalue(hname)
-    rel_r, x_r = _oracle_history(H, smoother=1, inner=inner, inner_mask=_mask(inner_from))
+    kw = device_mode_oracle_opts(H, smoother="hybrid", coarse="krylov", inner=inner, inner_from=inner_from)
+    rel_r, x_r = _oracle_history(H, **kw)
     rel_g, x_g = _gpu_history(H, smoother="hybrid", coarse="krylov", inner=inner, inner_from=inner_from)
     assert len(rel_g) == len(rel_r)
     assert np.array_equal(x_g.view(np.uint64), x_r.view(np.uint64))

@@ -15,13 +15,12 @@ import pytest
 import amg_amd as A
 import oracle
 from amg_amd._native import SSS_VEC, dptr
-from conftest import build_hierarchy
+from conftest import build_hierarchy, device_mode_oracle_opts
 
 pytestmark = pytest.mark.gpu
 
-MODES = {   # engine mode -> oracle options of the same algorithm
-    "hybrid": (dict(smoother="hybrid", coarse="direct"),
-               dict(smoother=1, jacobi_from=1, coarse_mode=1, inner=1, inner_mask=~3)),
+MODES = {   # engine mode -> oracle options of the same algorithm (None: read from the device's levels)
+    "hybrid": (dict(smoother="hybrid", coarse="direct"), None),
     "exact": (dict(smoother="exact", coarse="krylov"), {}),
 }
 
@@ -50,7 +49,8 @@ def _gpu_pcg(H, mode, tol, maxit=100):
 def _oracle_pcg(H, mode, tol, maxit=100):
     """numpy flexible CG (Polak-Ribiere), M^-1 = one oracle V-cycle on (r, 0)."""
     ora = oracle.load()
-    o = oracle.opts(**MODES[mode][1])
+    kw = MODES[mode][1]
+    o = oracle.opts(**(kw if kw is not None else device_mode_oracle_opts(H, **MODES[mode][0])))
     A0 = H.level(0).A
     n = A0.num_rows
     bvec, xv = np.zeros(n), np.zeros(n)
