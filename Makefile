@@ -14,12 +14,13 @@ ARCH    ?= gfx950
 CC      ?= gcc
 JOBS    ?= 8
 
-BUILD   := build
-LIBDIR  := amg_amd/lib
+BUILD   ?= build
+LIBDIR  ?= amg_amd/lib
+EXTRA   ?=
 BINDIR  := amg_amd/bin
 
 CFLAGS   := -O3 -fPIC -ffp-contract=off -fopenmp -std=gnu11 -Wall -Wno-unused-result
-HIPFLAGS := -O3 -fPIC -std=c++17 --offload-arch=$(ARCH) -ffp-contract=off -Wall -Wno-unused-result
+HIPFLAGS := -O3 -fPIC -std=c++17 --offload-arch=$(ARCH) -ffp-contract=off -Wall -Wno-unused-result $(EXTRA)
            
 
 HOST_SRC := $(wildcard amg_amd/host/sss_*.c)

@@ -164,9 +164,12 @@ static int rs_split(const SSS_MAT *A, SSS_IMAT *S, SSS_IVEC *vertices)
     SSS_IMAT ST;
     measure_buckets B;
 
+    const int timing = getenv("SSS_SETUP_TIMING") != NULL;
+    const double t0 = SSS_get_time();
     ncoarse = drop_weak(S);
     if (ncoarse < 0) return ncoarse;
     ST = SSS_imat_trans(S);
+    const double t1 = SSS_get_time();
 
     memset(&B, 0, sizeof(B));
     B.next = (int *)SSS_calloc((size_t)n, sizeof(int));
@@ -208,6 +211,7 @@ static int rs_split(const SSS_MAT *A, SSS_IMAT *S, SSS_IVEC *vertices)
         }
     }
 
+    const double t2 = SSS_get_time();
     while (undecided > 0) {
         int c = bucket_max_head(&B);
         int mc;
@@ -261,6 +265,7 @@ static int rs_split(const SSS_MAT *A, SSS_IMAT *S, SSS_IVEC *vertices)
         }
     }
 
+    const double t3 = SSS_get_time();
     /* C1 criterion: two strongly coupled F points must share a strong C point. */
     owner = lambda;
     for (int i = 0; i < n; ++i) owner[i] = -1;
@@ -289,6 +294,9 @@ static int rs_split(const SSS_MAT *A, SSS_IMAT *S, SSS_IVEC *vertices)
         }
     }
 
+    if (timing)
+        fprintf(stderr, "[setup]   RS split: drop+transpose %.3f s, lists %.3f s, first pass %.3f s, C1 %.3f s\n",
+                t1 - t0, t2 - t1, t3 - t2, SSS_get_time() - t3);
     SSS_imat_destroy(&ST);
     free(B.first);
     free(B.last);
@@ -378,13 +386,21 @@ static void direct_pattern(SSS_MAT *P, const SSS_IMAT *S, const SSS_IVEC *vertic
 int SSS_amg_coarsen(SSS_MAT *A, SSS_IVEC *vertices, SSS_MAT *P, SSS_IMAT *S, SSS_AMG_PARS *pars)
 {
     int ncoarse = 0;
+    const int timing = getenv("SSS_SETUP_TIMING") != NULL;
+    const double t0 = SSS_get_time();
     strong_couplings(A, S, pars);
+    const double t1 = SSS_get_time();
     if (pars->cs_type == SSS_COARSE_RS) ncoarse = rs_split(A, S, vertices);
     else if (pars->cs_type != SSS_COARSE_RSP) SSS_exit_on_errcode(ERROR_AMG_COARSE_TYPE, __func__);
     if (ncoarse <= 0) return ERROR_UNKNOWN;
+    const double t2 = SSS_get_time();
     if (pars->interp_type == intERP_DIR) {
         ncoarse = cleanup_ff(S, vertices, A->num_rows, ncoarse);
+        const double t3 = SSS_get_time();
         direct_pattern(P, S, vertices, A->num_rows, ncoarse);
+        if (timing)
+            fprintf(stderr, "[setup]   coarsen: strength %.3f s, RS split %.3f s, F-F cleanup %.3f s, P pattern %.3f s\n",
+                    t1 - t0, t2 - t1, t3 - t2, SSS_get_time() - t3);
     } else {
         /* Standard interpolation (form_P_pattern_std / interp_STD) is not part of this
          * engine: the reference's default and every BASELINE config use direct. */
