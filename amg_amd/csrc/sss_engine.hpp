@@ -119,6 +119,14 @@ struct DevCSR {
     // block has <= 256 distinct values -- a relabeled Galerkin level): the sorted tiles' pk/pb with
     // a 1-byte value index dv_vi per slot into the block's value dictionary instead of pv: 5 B per
     // entry.  dv_code stays null, dv_pd[block].y = 0, pv is not uploaded.
+    // Dictionary ELL (kEncDict, tried first; stencil levels: every row <= 32 entries, every block
+    // <= 31 column offsets and <= 8 values -- 7-pt level 0): row r's entries in stored order as
+    // ell_w one-byte codes  value index << 5 | offset index  at dv_ell[r * ell_w] (0xFF pads), into
+    // the block dictionaries dv_pd/dv_dd/dv_vd.  One thread per row, no LDS staging, no row_ptr:
+    // ell_w bytes per row (8 for 7-pt) instead of 12 per entry.  pk and dv_code stay null.
+    unsigned char *dv_ell = nullptr;
+    int ell_w = 0;
+    int ell_remap = 0;   // ELL kernels take their blocks XCD-contiguously (SSS_HIP_ELL_REMAP)
     long long stream_bytes = 0;   // bytes of the stored format one tile-path SpMV streams (no vectors)
     unsigned *dv_code = nullptr;
     unsigned char *dv_vi = nullptr;
@@ -156,7 +164,22 @@ int free_row_min();
 struct DevDict;
 DevDict devdict(const DevCSR &A, int blo);   // the matrix's dictionary tiles, block numbers from blo
 // the tile kernels stage from a dictionary (either kind): instantiate them with DICT = true
-inline bool has_dict(const DevCSR &A) { return A.dv_code != nullptr || A.dv_vi != nullptr; }
+inline bool has_dict(const DevCSR &A) { return A.dv_code != nullptr || A.dv_vi != nullptr || A.dv_ell != nullptr; }
+// f(std::integral_constant<int, K>) with the tile kernels' storage argument K of A: 0 plain or
+// sorted tiles, 1 dictionary tiles (either kind), 8 / 16 / 32 dictionary ELL of that row width
+template <class F>
+inline void with_tile_kind(const DevCSR &A, F f)
+{
+    if (A.dv_ell) {
+        if (A.ell_w == 8) f(std::integral_constant<int, 8>{});
+        else if (A.ell_w == 16) f(std::integral_constant<int, 16>{});
+        else f(std::integral_constant<int, 32>{});
+    } else if (has_dict(A)) {
+        f(std::integral_constant<int, 1>{});
+    } else {
+        f(std::integral_constant<int, 0>{});
+    }
+}
 
 // ---- hierarchy internals shared with the distributed engine (sss_hier.hip) ------------------
 // A hierarchy over mg->cg[0 .. num_levels); its L[0] is global level `level_base` (smoother

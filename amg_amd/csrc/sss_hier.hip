@@ -788,7 +788,7 @@ extern "C" int sss_hip_level_info_get(sss_hip_hier *h, int level, sss_hip_level_
     if (gs_persist_error(L.sm.pass[0], &ef) || gs_persist_error(L.sm.pass[1], &ec)) return ERROR_MISC;
     out->gs_stall = (int)(ef | ec);
     out->a_format = (L.A.pk ? 1 : 0) | (has_dict(L.A) ? 2 : 0) | (L.A.vec_rows ? 4 : 0) | (L.A.mg_G ? 8 : 0) |
-                    (L.A.wave_rows ? 16 : 0);
+                    (L.A.wave_rows ? 16 : 0) | (L.A.dv_ell ? 64 : 0);
     out->a_stream_bytes = L.A.stream_bytes;
     return 0;
 }

@@ -472,7 +472,57 @@ __global__ __launch_bounds__(kBlock) void relax_wave(int m, const int *__restric
 //           other product of the row changes; per-block sums of squares into partial[bid].
 // t = b_r - sum over off-diagonal entries in stored order (diag_pos skips the diagonal); rows with
 // |d| <= 1e-20 keep their value.
-template <int MODE, bool DICT = false>
+// Dictionary ELL rows (DICT == 2): the same per-row arithmetic, the row's products in registers in
+// stored (slot) order instead of staged in LDS.
+template <int MODE, int W>
+__device__ __forceinline__ void relax_range_ell(int blo, const int2 *__restrict__ blk, int lo,
+                                                const double *__restrict__ b, double *x, double *__restrict__ y,
+                                                const double *__restrict__ deff, double *__restrict__ rr,
+                                                double *__restrict__ partial, XSrc xs, const DevDict &dt)
+{
+    __shared__ EllSmem es;
+    const int bid = blo + (dt.remap ? xcd_remap(blockIdx.x, gridDim.x) : (int)blockIdx.x);
+    const int2 ba = blk[bid], be = blk[bid + 1];
+    ell_load_dicts(dt, bid, es);
+    const int r = ba.x + (int)threadIdx.x;
+    double sq = 0.0;
+    if (r < be.x) {
+            double p[W];
+            int dsl;
+            double dv;
+            const int len = ell_row<W>(dt.ell, r, es, [&](int c) -> double { return xs(c); }, p, dsl, dv);
+            const double br = b[r];
+            const double acc = dsl < 0 ? ell_sub(br, p, 0, len) : ell_sub(ell_sub(br, p, 0, dsl), p, dsl + 1, len);
+            const double d = deff ? deff[r] : dv;
+            if constexpr (MODE == 2) {
+                const double xn = fabs(d) > SMALLFLOAT ? acc / d : x[r];
+                if (fabs(d) > SMALLFLOAT) x[r] = xn;
+                double t = ell_add(0.0, p, 0, dsl);
+                t += d * xn;
+                t = ell_add(t, p, dsl + 1, len);
+                const double out = br + t * -1.0;
+                rr[r] = out;
+                sq = out * out;
+            } else if constexpr (MODE == 3) {
+                const double out = br + ell_add(0.0, p, 0, len) * -1.0;
+                rr[r] = out;
+                sq = out * out;
+                y[r - lo] = fabs(d) > SMALLFLOAT ? acc / d : x[r];
+            } else if constexpr (MODE == 1) {
+                y[r - lo] = fabs(d) > SMALLFLOAT ? acc / d : xs(r);
+            } else {
+                if (fabs(d) > SMALLFLOAT) x[r] = acc / d;
+            }
+    }
+    if constexpr (MODE >= 2) {
+        if (partial) {
+            const double t = block_sum(sq, es.red);
+            if (threadIdx.x == 0) partial[bid] = t;
+        }
+    }
+}
+
+template <int MODE, int DICT = 0>   // DICT: with_tile_kind (8/16/32: dictionary ELL, that width)
 __global__ __launch_bounds__(kBlock) void relax_range(int blo, const int2 *__restrict__ blk, const int *__restrict__ rp,
                                                       const int *__restrict__ ci, const double *__restrict__ v,
                                                       const int *__restrict__ diag_pos, int lo,
@@ -483,10 +533,13 @@ __global__ __launch_bounds__(kBlock) void relax_range(int blo, const int2 *__res
                                                       double *__restrict__ rr, double *__restrict__ partial, XSrc xs,
                                                       DevDict dt = DevDict())
 {
+    if constexpr (DICT >= 8) {
+        relax_range_ell<MODE, DICT>(blo, blk, lo, b, x, y, deff, rr, partial, xs, dt);
+    } else {
     __shared__ SpmvSmem sm;
-    __shared__ std::conditional_t<DICT, DictSmem, char> dsm;
+    __shared__ std::conditional_t<DICT != 0, DictSmem, char> dsm;
     DictSmem *ds = nullptr;
-    if constexpr (DICT) ds = &dsm;
+    if constexpr (DICT != 0) ds = &dsm;
     const int bid = blo + xcd_bid();
     const int2 ba = blk[bid], be = blk[bid + 1];
     const int r0 = ba.x, r1 = be.x, k0 = ba.y, k1 = be.y;
@@ -566,6 +619,7 @@ __global__ __launch_bounds__(kBlock) void relax_range(int blo, const int2 *__res
             __syncthreads();
         }
         if (threadIdx.x == 0) finish(r, acc);
+    }
     }
 }
 
@@ -847,14 +901,12 @@ int launch_f_residual_pending(const SmootherPlan &sp, const DevCSR &A, const dou
     if (!sp.pend_ok) return ERROR_INPUT_PAR;
     const PassSchedule &F = sp.pass[0];
     const double *deff = (sp.own_diag && (A.pk || has_dict(A))) ? nullptr : sp.d_first;
-    if (has_dict(A))
-        hipLaunchKernelGGL((relax_range<3, true>), dim3(F.bhi - F.blo), dim3(kBlock), 0, s, F.blo, A.bk, A.rp, A.ci, A.v,
-                           sp.diag_pos, F.lo, b, const_cast<double *>(x), (const double *)nullptr, pend, deff, A.pk,
-                           A.pv, A.pb, r, partial, xsrc_of(x), devdict(A, 0));
-    else
-        hipLaunchKernelGGL((relax_range<3, false>), dim3(F.bhi - F.blo), dim3(kBlock), 0, s, F.blo, A.bk, A.rp, A.ci, A.v,
-                           sp.diag_pos, F.lo, b, const_cast<double *>(x), (const double *)nullptr, pend, deff, A.pk,
-                           A.pv, A.pb, r, partial, xsrc_of(x), devdict(A, 0));
+    with_tile_kind(A, [&](auto K) {
+        hipLaunchKernelGGL((relax_range<3, decltype(K)::value>), dim3(F.bhi - F.blo), dim3(kBlock), 0, s,
+                           F.blo, A.bk, A.rp, A.ci, A.v, sp.diag_pos, F.lo, b, const_cast<double *>(x),
+                           (const double *)nullptr, pend, deff, A.pk, A.pv, A.pb, r, partial, xsrc_of(x),
+                           devdict(A, 0));
+    });
     SSS_HIP(hipGetLastError());
     return 0;
 }
@@ -1005,16 +1057,13 @@ int smoother_run(const SmootherPlan &sp, const DevCSR &A, const double *b, doubl
                                            A.rp, cols, A.v, b, x, yp, y, deff, xs);
                     else {
                         auto go = [&](int b0, int b1) {
-                            if (has_dict(A))
-                                hipLaunchKernelGGL((relax_range<M, true>), dim3(b1 - b0), dim3(kBlock), 0, s, b0, A.bk,
-                                                   A.rp, cols, A.v, sp.diag_pos, ps.lo, b, x, yp, y,
-                                                   tile_d ? nullptr : deff, A.pk, A.pv, A.pb, (double *)nullptr,
-                                                   (double *)nullptr, xs, devdict(A, 0));
-                            else
-                                hipLaunchKernelGGL((relax_range<M, false>), dim3(b1 - b0), dim3(kBlock), 0, s, b0, A.bk,
-                                                   A.rp, cols, A.v, sp.diag_pos, ps.lo, b, x, yp, y,
-                                                   tile_d ? nullptr : deff, A.pk, A.pv, A.pb, (double *)nullptr,
-                                                   (double *)nullptr, xs, devdict(A, 0));
+                            with_tile_kind(A, [&](auto K) {
+                                hipLaunchKernelGGL((relax_range<M, decltype(K)::value>), dim3(b1 - b0),
+                                                   dim3(kBlock), 0, s, b0, A.bk, A.rp, cols, A.v, sp.diag_pos, ps.lo,
+                                                   b, x, yp, y, tile_d ? nullptr : deff, A.pk, A.pv, A.pb,
+                                                   (double *)nullptr, (double *)nullptr, xs,
+                                                   devdict(A, 0));
+                            });
                         };
                         if (split_pass) return hk->split(x, ps.blo, ps.bhi, go);
                         go(ps.blo, ps.bhi);
@@ -1078,16 +1127,13 @@ int smoother_run(const SmootherPlan &sp, const DevCSR &A, const double *b, doubl
                     SSS_HIP(hipMemcpyAsync(x + ps.lo, ps.y, sizeof(double) * (size_t)m, hipMemcpyDeviceToDevice, s));
                 } else if (fused_pass) {
                     auto go = [&](int b0, int b1) {
-                        if (has_dict(A))
-                            hipLaunchKernelGGL((relax_range<2, true>), dim3(b1 - b0), dim3(kBlock), 0, s, b0, A.bk,
-                                               A.rp, A.ci, A.v, sp.diag_pos, ps.lo, b, x, (const double *)nullptr,
-                                               (double *)nullptr, tile_d ? nullptr : deff, A.pk, A.pv, A.pb, rf->r,
-                                               rf->partial, xs, devdict(A, 0));
-                        else
-                            hipLaunchKernelGGL((relax_range<2, false>), dim3(b1 - b0), dim3(kBlock), 0, s, b0, A.bk,
-                                               A.rp, A.ci, A.v, sp.diag_pos, ps.lo, b, x, (const double *)nullptr,
-                                               (double *)nullptr, tile_d ? nullptr : deff, A.pk, A.pv, A.pb, rf->r,
-                                               rf->partial, xs, devdict(A, 0));
+                        with_tile_kind(A, [&](auto K) {
+                            hipLaunchKernelGGL((relax_range<2, decltype(K)::value>), dim3(b1 - b0),
+                                               dim3(kBlock), 0, s, b0, A.bk, A.rp, A.ci, A.v, sp.diag_pos, ps.lo, b, x,
+                                               (const double *)nullptr, (double *)nullptr, tile_d ? nullptr : deff,
+                                               A.pk, A.pv, A.pb, rf->r, rf->partial, xs,
+                                               devdict(A, 0));
+                        });
                     };
                     if (split_pass) {
                         if ((rc = hk->split(x, ps.blo, ps.bhi, go))) return rc;

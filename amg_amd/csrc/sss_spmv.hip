@@ -252,6 +252,9 @@ DevDict devdict(const DevCSR &A, int blo)
     t.tree_long = A.tree_long ? 1 : 0;
     if (!has_dict(A)) return t;
     t.code = A.dv_code;
+    t.ell = A.dv_ell;
+    t.ellw = A.ell_w;
+    t.remap = A.ell_remap;
     t.pd = A.dv_pd + blo;
     t.dd = A.dv_dd;
     t.vd = A.dv_vd;
@@ -378,6 +381,70 @@ static bool build_value_dict(const std::vector<int> &blk, const int *rp, const s
     return true;
 }
 
+// Dictionary ELL of a square matrix (DevCSR::dv_ell): every row at most 32 entries, every block at
+// most 31 distinct column offsets and 8 distinct value bit patterns (false otherwise); width W =
+// 8, 16 or 32 bytes per row, codes in stored order, 0xFF pads.
+static bool build_ell(const SSS_MAT &h, const std::vector<int> &blk, std::vector<unsigned char> &ell, int &W,
+                      std::vector<int4> &pd, std::vector<int> &dd, std::vector<double> &vd)
+{
+    const int *rp = h.row_ptr, *ci = h.col_idx;
+    const double *v = h.val;
+    const int n = h.num_rows, nb = (int)blk.size() - 1;
+    if (n != h.num_cols || nb <= 0 || n <= 0) return false;
+    int L = 0;
+    for (int r = 0; r < n; ++r) L = std::max(L, rp[r + 1] - rp[r]);
+    if (L > 32) return false;
+    W = L <= 8 ? 8 : L <= 16 ? 16 : 32;
+    std::vector<std::vector<int>> bd(nb);
+    std::vector<std::vector<unsigned long long>> bv(nb);
+    ell.assign((size_t)n * W, 0xff);
+    std::atomic<int> ok{1};
+    parallel_chunks(nb, 256, [&](int qlo, int qhi) {
+        for (int q = qlo; q < qhi && ok; ++q) {
+            auto &D = bd[q];
+            auto &V = bv[q];
+            for (int r = blk[q]; r < blk[q + 1]; ++r)
+                for (int k = rp[r]; k < rp[r + 1]; ++k) {
+                    D.push_back(ci[k] - r);
+                    unsigned long long u;
+                    std::memcpy(&u, &v[k], sizeof(u));
+                    V.push_back(u);
+                }
+            std::sort(D.begin(), D.end());
+            D.erase(std::unique(D.begin(), D.end()), D.end());
+            std::sort(V.begin(), V.end());
+            V.erase(std::unique(V.begin(), V.end()), V.end());
+            if (D.size() > 31 || V.size() > 8) {
+                ok = 0;
+                return;
+            }
+            for (int r = blk[q]; r < blk[q + 1]; ++r)
+                for (int k = rp[r]; k < rp[r + 1]; ++k) {
+                    unsigned long long u;
+                    std::memcpy(&u, &v[k], sizeof(u));
+                    const unsigned di = (unsigned)(std::lower_bound(D.begin(), D.end(), ci[k] - r) - D.begin());
+                    const unsigned vi = (unsigned)(std::lower_bound(V.begin(), V.end(), u) - V.begin());
+                    ell[(size_t)r * W + (k - rp[r])] = (unsigned char)(vi << 5 | di);
+                }
+        }
+    });
+    if (!ok) return false;
+    pd.resize((size_t)nb);
+    size_t nd = 0, nv = 0;
+    for (int q = 0; q < nb; ++q) {
+        pd[q] = make_int4((int)nd, (int)bd[q].size(), (int)nv, (int)bv[q].size());
+        nd += bd[q].size();
+        nv += bv[q].size();
+    }
+    dd.resize(std::max<size_t>(nd, 1));
+    vd.resize(std::max<size_t>(nv, 1));
+    for (int q = 0; q < nb; ++q) {
+        std::copy(bd[q].begin(), bd[q].end(), dd.begin() + pd[q].x);
+        for (size_t t = 0; t < bv[q].size(); ++t) std::memcpy(&vd[(size_t)pd[q].z + t], &bv[q][t], sizeof(double));
+    }
+    return true;
+}
+
 int devcsr_upload(DevCSR &d, const SSS_MAT &h, int split, int enc, const int *seg)
 {
     d.n = h.num_rows;
@@ -440,9 +507,33 @@ int devcsr_upload(DevCSR &d, const SSS_MAT &h, int split, int enc, const int *se
         if (int rc = h2d(d.mg_k, mk.data(), sizeof(unsigned) * mk.size())) return rc;
         if (int rc = h2d(d.mg_v, mv.data(), sizeof(double) * mv.size())) return rc;
     }
-    // dictionary tiles (the tile kernels then stage from them instead of the sorted copy)
+    // dictionary ELL first (one thread per row), else dictionary tiles (the tile kernels then stage
+    // from them instead of the sorted copy)
     const char *dz = getenv("SSS_HIP_DICT");   // 0: never (tests compare both ways)
-    if ((enc & kEncDict) && !(dz && *dz == '0') && !d.wave_rows && !d.vec_rows && d.nnz > 0) {
+    const char *ez = getenv("SSS_HIP_ELL");    // 0: no ELL (dictionary tiles where they qualify)
+    if ((enc & kEncDict) && !(dz && *dz == '0') && !(ez && *ez == '0') && !d.wave_rows && !d.vec_rows && d.nnz > 0) {
+        std::vector<unsigned char> ell;
+        std::vector<int4> pd;
+        std::vector<int> dd;
+        std::vector<double> vd;
+        int W = 0;
+        if (build_ell(h, blk, ell, W, pd, dd, vd)) {
+            d.ell_w = W;
+            const char *rz = getenv("SSS_HIP_ELL_REMAP");
+            d.ell_remap = (rz && *rz) ? atoi(rz) : 0;
+            d.dv_ell = dev_alloc<unsigned char>(ell.size());
+            d.dv_pd = dev_alloc<int4>(pd.size());
+            d.dv_dd = dev_alloc<int>(dd.size());
+            d.dv_vd = dev_alloc<double>(vd.size());
+            if (!d.dv_ell || !d.dv_pd || !d.dv_dd || !d.dv_vd)
+                return hip_fail(hipErrorOutOfMemory, "hipMalloc(dictionary ELL)", __FILE__, __LINE__);
+            if (int rc = h2d(d.dv_ell, ell.data(), ell.size())) return rc;
+            if (int rc = h2d(d.dv_pd, pd.data(), sizeof(int4) * pd.size())) return rc;
+            if (int rc = h2d(d.dv_dd, dd.data(), sizeof(int) * dd.size())) return rc;
+            if (int rc = h2d(d.dv_vd, vd.data(), sizeof(double) * vd.size())) return rc;
+        }
+    }
+    if ((enc & kEncDict) && !(dz && *dz == '0') && !d.dv_ell && !d.wave_rows && !d.vec_rows && d.nnz > 0) {
         std::vector<unsigned> code;
         std::vector<int4> pd;
         std::vector<int> dd;
@@ -464,7 +555,7 @@ int devcsr_upload(DevCSR &d, const SSS_MAT &h, int split, int enc, const int *se
     std::vector<unsigned> pk;
     std::vector<double> pv;
     std::vector<int2> pb;
-    if ((enc & kEncSortedTiles) && !d.dv_code && !d.wave_rows && !d.vec_rows && d.nnz > 0 &&
+    if ((enc & kEncSortedTiles) && !d.dv_code && !d.dv_ell && !d.wave_rows && !d.vec_rows && d.nnz > 0 &&
         build_sorted_tiles(h, blk, pk, pv, pb)) {
         d.pk = dev_alloc<unsigned>((size_t)d.nnz);
         d.pb = dev_alloc<int2>(pb.size());
@@ -496,7 +587,8 @@ int devcsr_upload(DevCSR &d, const SSS_MAT &h, int split, int enc, const int *se
         std::vector<int4> pd((size_t)nb);
         if (nb > 0) SSS_HIP(hipMemcpy(pd.data(), d.dv_pd, sizeof(int4) * (size_t)nb, hipMemcpyDeviceToHost));
         for (const auto &p : pd) dict += 4LL * p.y + 8LL * p.w;
-        d.stream_bytes = (d.dv_vi ? 5 * nnz + 8 * nb : 4 * nnz) + 4 * (rows + 1) + 8 * (nb + 1) + 16 * nb + dict;
+        d.stream_bytes = d.dv_ell ? (long long)d.ell_w * rows + 8 * (nb + 1) + 16 * nb + dict
+                                  : (d.dv_vi ? 5 * nnz + 8 * nb : 4 * nnz) + 4 * (rows + 1) + 8 * (nb + 1) + 16 * nb + dict;
     } else if (d.pk) {
         d.stream_bytes = 12 * nnz + 4 * (rows + 1) + 8 * (nb + 1) + 8 * nb;
     } else {
@@ -519,6 +611,7 @@ void devcsr_free(DevCSR &d)
     dev_free(d.mg_k);
     dev_free(d.mg_v);
     dev_free(d.dv_code);
+    dev_free(d.dv_ell);
     dev_free(d.dv_vi);
     dev_free(d.dv_pd);
     dev_free(d.dv_dd);
@@ -527,7 +620,7 @@ void devcsr_free(DevCSR &d)
 }
 
 // ---- kernel -------------------------------------------------------------------------------
-template <int OP, bool NORM, bool DICT = false>
+template <int OP, bool NORM, int DICT = 0>   // DICT: with_tile_kind (8/16/32: dictionary ELL, that width)
 __global__ __launch_bounds__(kBlock) void spmv_adaptive(const int2 *__restrict__ blk, const int *__restrict__ rp,
                                                         const int *__restrict__ ci, const double *__restrict__ v,
                                                         const double *__restrict__ x, const double *__restrict__ b,
@@ -536,11 +629,7 @@ __global__ __launch_bounds__(kBlock) void spmv_adaptive(const int2 *__restrict__
                                                         const double *__restrict__ pv, const int2 *__restrict__ pb,
                                                         DevDict dt = DevDict())
 {
-    __shared__ SpmvSmem sm;
-    __shared__ std::conditional_t<DICT, DictSmem, char> dsm;
-    DictSmem *ds = nullptr;
-    if constexpr (DICT) ds = &dsm;
-    const double sq = csr_block_rows(blk, rp, ci, v, x, sm, [&](int r, double s) -> double {
+    auto epi = [&](int r, double s) -> double {
         double out;
         if constexpr (OP == SSS_HIP_SPMV_MXY) out = s;
         else if constexpr (OP == SSS_HIP_SPMV_AMXPY) out = y[r] + s * alpha;
@@ -551,10 +640,36 @@ __global__ __launch_bounds__(kBlock) void spmv_adaptive(const int2 *__restrict__
         }
         y[r] = out;
         return NORM ? out * out : 0.0;
-    }, pk, pv, pb, &dt, ds);
-    if (NORM) {
-        const double t = block_sum(sq, sm.red);
-        if (threadIdx.x == 0) partial[xcd_bid()] = t;
+    };
+    if constexpr (DICT >= 8) {   // dictionary ELL rows of width DICT: one thread per row, its sum
+        constexpr int W = DICT;   // from 0.0 in stored order; the grid loops over the row blocks
+        __shared__ EllSmem es;
+        const int bid = dt.remap ? xcd_remap(blockIdx.x, gridDim.x) : (int)blockIdx.x;
+        const int2 ba = blk[bid], be = blk[bid + 1];
+        ell_load_dicts(dt, bid, es);
+        const int r = ba.x + (int)threadIdx.x;
+        double sq = 0.0;
+        if (r < be.x) {
+            double p[W];
+            int ds;
+            double dv;
+            const int len = ell_row<W>(dt.ell, r, es, [&](int c) -> double { return x[c]; }, p, ds, dv);
+            sq = epi(r, ell_add(0.0, p, 0, len));
+        }
+        if (NORM) {
+            const double t = block_sum(sq, es.red);
+            if (threadIdx.x == 0) partial[bid] = t;
+        }
+    } else {
+        __shared__ SpmvSmem sm;
+        __shared__ std::conditional_t<DICT != 0, DictSmem, char> dsm;
+        DictSmem *ds = nullptr;
+        if constexpr (DICT != 0) ds = &dsm;
+        const double sq = csr_block_rows(blk, rp, ci, v, x, sm, epi, pk, pv, pb, &dt, ds);
+        if (NORM) {
+            const double t = block_sum(sq, sm.red);
+            if (threadIdx.x == 0) partial[xcd_bid()] = t;
+        }
     }
 }
 
@@ -645,12 +760,11 @@ static void launch_op(const DevCSR &A, double alpha, const double *x, const doub
     else if (A.wave_rows)
         hipLaunchKernelGGL((spmv_wave<OP, NORM, false>), dim3(A.ngrid), dim3(kBlock), 0, s, A.n, A.rp, A.ci, A.v, x,
                            b, y, alpha, cap, partial);
-    else if (has_dict(A))
-        hipLaunchKernelGGL((spmv_adaptive<OP, NORM, true>), dim3(A.nblk), dim3(kBlock), 0, s, A.bk, A.rp, A.ci, A.v,
-                           x, b, y, alpha, cap, partial, A.pk, A.pv, A.pb, devdict(A, 0));
     else
-        hipLaunchKernelGGL((spmv_adaptive<OP, NORM>), dim3(A.nblk), dim3(kBlock), 0, s, A.bk, A.rp, A.ci, A.v, x,
-                           b, y, alpha, cap, partial, A.pk, A.pv, A.pb, devdict(A, 0));
+        with_tile_kind(A, [&](auto K) {
+            hipLaunchKernelGGL((spmv_adaptive<OP, NORM, decltype(K)::value>), dim3(A.nblk), dim3(kBlock), 0, s,
+                               A.bk, A.rp, A.ci, A.v, x, b, y, alpha, cap, partial, A.pk, A.pv, A.pb, devdict(A, 0));
+        });
 }
 
 int launch_spmv(const DevCSR &A, int op, double alpha, const double *x, const double *b, double *y, int cap,
@@ -685,12 +799,10 @@ int launch_spmv_range(const DevCSR &A, int blo, int bhi, int op, double alpha, c
     auto go = [&](auto op_c, auto norm_c) {
         constexpr int O = decltype(op_c)::value;
         constexpr bool NM = decltype(norm_c)::value;
-        if (has_dict(A))
-            hipLaunchKernelGGL((spmv_adaptive<O, NM, true>), dim3(nb), dim3(kBlock), 0, s, A.bk + blo, A.rp, A.ci, A.v,
-                               x, b, y, alpha, 0, pp, A.pk, A.pv, pb, dt);
-        else
-            hipLaunchKernelGGL((spmv_adaptive<O, NM, false>), dim3(nb), dim3(kBlock), 0, s, A.bk + blo, A.rp, A.ci,
-                               A.v, x, b, y, alpha, 0, pp, A.pk, A.pv, pb, dt);
+        with_tile_kind(A, [&](auto K) {
+            hipLaunchKernelGGL((spmv_adaptive<O, NM, decltype(K)::value>), dim3(nb), dim3(kBlock), 0, s, A.bk + blo,
+                               A.rp, A.ci, A.v, x, b, y, alpha, 0, pp, A.pk, A.pv, pb, dt);
+        });
     };
     using T = std::true_type;
     using F = std::false_type;

@@ -22,12 +22,15 @@ namespace sss {
 // the level-1 residual 2.44 vs 1.97 ms and every coarse level slower): the x lines neighbouring
 // blocks share are served from the Infinity Cache either way, and eight XCDs streaming eight
 // distant regions lose more than the L2 reuse gains.
+__device__ __forceinline__ int xcd_remap(int b, int nb)
+{
+    const int per = nb >> 3, rem = nb & 7, xcd = b & 7, idx = b >> 3;
+    return xcd < rem ? xcd * (per + 1) + idx : rem * (per + 1) + (xcd - rem) * per + idx;
+}
 __device__ __forceinline__ int xcd_bid()
 {
-    const int b = blockIdx.x;
-    if (!SSS_XCD_REMAP) return b;
-    const int nb = gridDim.x, per = nb >> 3, rem = nb & 7, xcd = b & 7, idx = b >> 3;
-    return xcd < rem ? xcd * (per + 1) + idx : rem * (per + 1) + (xcd - rem) * per + idx;
+    if (!SSS_XCD_REMAP) return blockIdx.x;
+    return xcd_remap(blockIdx.x, gridDim.x);
 }
 
 struct SpmvSmem {
@@ -53,7 +56,79 @@ struct DevDict {
     const unsigned char *vi = nullptr;
     const int2 *pb = nullptr;
     int tree_long = 0;   // DevCSR::tree_long (set for every matrix, dictionary or not)
+    const unsigned char *ell = nullptr;   // dictionary ELL (DevCSR::dv_ell), ell_w bytes per row
+    int ellw = 0;
+    int remap = 0;   // ELL launches: XCD-contiguous block order (DevCSR::ell_remap)
 };
+
+// ---- dictionary ELL: one thread per row ----------------------------------------------------
+// The block's dictionaries in LDS (small: the kernels instantiated for ELL keep their LDS
+// footprint to this, so occupancy is not bounded by the tile staging arrays).
+struct EllSmem {
+    int dd[32];
+    double vd[8];
+    double red[kBlock / 64];
+};
+__device__ __forceinline__ void ell_load_dicts(const DevDict &dt, int bid, EllSmem &es)
+{
+    const int4 p = dt.pd[bid];
+    if ((int)threadIdx.x < p.y) es.dd[threadIdx.x] = dt.dd[p.x + threadIdx.x];
+    if ((int)threadIdx.x < p.w) es.vd[threadIdx.x] = dt.vd[p.z + threadIdx.x];
+    __syncthreads();
+}
+// Products of row r in stored (slot) order: p[s] = a_s * x(c_s) for s < len; dslot = the row's
+// (last) diagonal slot or -1, dval its value.
+template <int W, class Fetch>
+__device__ __forceinline__ int ell_row(const unsigned char *__restrict__ ell, int r, const EllSmem &es, Fetch fetch,
+                                       double (&p)[W], int &dslot, double &dval)
+{
+    unsigned w[W / 4];
+    if constexpr (W == 8) {
+        const uint2 q = *reinterpret_cast<const uint2 *>(ell + (size_t)r * 8);
+        w[0] = q.x, w[1] = q.y;
+    } else {
+#pragma unroll
+        for (int h = 0; h < W / 16; ++h) {
+            const uint4 q = *reinterpret_cast<const uint4 *>(ell + (size_t)r * W + 16 * h);
+            w[4 * h] = q.x, w[4 * h + 1] = q.y, w[4 * h + 2] = q.z, w[4 * h + 3] = q.w;
+        }
+    }
+    int len = W;
+    dslot = -1;
+    dval = 0.0;
+    int c[W];
+    double a[W];
+#pragma unroll
+    for (int s = 0; s < W; ++s) {
+        const unsigned byte = (w[s >> 2] >> (8 * (s & 3))) & 0xffu;
+        if (byte == 0xffu && len == W) len = s;
+        c[s] = r + es.dd[byte & 31u];
+        a[s] = es.vd[byte >> 5];
+    }
+#pragma unroll
+    for (int s = 0; s < W; ++s) p[s] = s < len ? a[s] * fetch(c[s]) : 0.0;
+#pragma unroll
+    for (int s = 0; s < W; ++s)
+        if (s < len && c[s] == r) dslot = s, dval = a[s];
+    return len;
+}
+// sum of p[a, e) from s0 in slot order
+template <int W>
+__device__ __forceinline__ double ell_add(double s0, const double (&p)[W], int a, int e)
+{
+#pragma unroll
+    for (int s = 0; s < W; ++s)
+        if (s >= a && s < e) s0 += p[s];
+    return s0;
+}
+template <int W>
+__device__ __forceinline__ double ell_sub(double s0, const double (&p)[W], int a, int e)
+{
+#pragma unroll
+    for (int s = 0; s < W; ++s)
+        if (s >= a && s < e) s0 -= p[s];
+    return s0;
+}
 
 // In-order chains over LDS products: 8 reads issued ahead of 8 dependent adds/subtractions,
 // the additions themselves in exactly the stored order.

@@ -77,14 +77,40 @@ static void strong_couplings(const SSS_MAT *A, SSS_IMAT *S, const SSS_AMG_PARS *
 /* Drops entries marked -1; returns -99 when nothing strong is left (reference's ERROR_UNKNOWN). */
 static int drop_weak(SSS_IMAT *S)
 {
-    int out = 0;
-    for (int i = 0; i < S->num_rows; ++i) {
-        int lo = S->row_ptr[i], hi = S->row_ptr[i + 1];
-        S->row_ptr[i] = out;
-        for (int k = lo; k < hi; ++k)
-            if (S->col_idx[k] > -1) S->col_idx[out++] = S->col_idx[k];
+    const int n = S->num_rows;
+    if (S->num_nnzs < (1 << 20)) {
+        int out = 0;
+        for (int i = 0; i < n; ++i) {
+            int lo = S->row_ptr[i], hi = S->row_ptr[i + 1];
+            S->row_ptr[i] = out;
+            for (int k = lo; k < hi; ++k)
+                if (S->col_idx[k] > -1) S->col_idx[out++] = S->col_idx[k];
+        }
+        S->row_ptr[n] = out;
+        S->num_nnzs = out;
+        return out > 0 ? 0 : -99;
     }
-    S->row_ptr[S->num_rows] = out;
+    /* same compaction in parallel: kept counts per row, prefix sum, copy into a new array */
+    int *cnt = (int *)SSS_calloc((size_t)n + 1, sizeof(int));
+#pragma omp parallel for schedule(static)
+    for (int i = 0; i < n; ++i) {
+        int c = 0;
+        for (int k = S->row_ptr[i]; k < S->row_ptr[i + 1]; ++k) c += S->col_idx[k] > -1;
+        cnt[i + 1] = c;
+    }
+    for (int i = 0; i < n; ++i) cnt[i + 1] += cnt[i];
+    const int out = cnt[n];
+    int *ci = (int *)SSS_calloc((size_t)(out > 0 ? out : 1), sizeof(int));
+#pragma omp parallel for schedule(static)
+    for (int i = 0; i < n; ++i) {
+        int o = cnt[i];
+        for (int k = S->row_ptr[i]; k < S->row_ptr[i + 1]; ++k)
+            if (S->col_idx[k] > -1) ci[o++] = S->col_idx[k];
+    }
+    free(S->col_idx);
+    free(S->row_ptr);
+    S->col_idx = ci;
+    S->row_ptr = cnt;
     S->num_nnzs = out;
     return out > 0 ? 0 : -99;
 }

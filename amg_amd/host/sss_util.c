@@ -312,11 +312,71 @@ void SSS_amg_data_destroy(SSS_AMG *mg)
  * The reference's two-slot shifted prefix trick is an implementation detail; what matters is
  * the resulting order, which this reproduces.
  */
+static int cmp_int(const void *a, const void *b)
+{
+    const int x = *(const int *)a, y = *(const int *)b;
+    return (x > y) - (x < y);
+}
+
+/* The same transpose with OpenMP: entries are scattered by atomic slot claims, then each output
+ * row is sorted by source position -- ascending source row, and stored order inside a row -- which
+ * is exactly the order of the sequential fill below, so the result is identical. */
+static void transpose_pattern_par(int nrows, int ncols, int nnz, const int *ia, const int *ja,
+                                  const void *val, size_t vsize, int *tia, int *tja, void *tval)
+{
+    int *fill = (int *)calloc((size_t)ncols + 1, sizeof(int));
+    int *src = (int *)malloc(sizeof(int) * (size_t)nnz);
+    int *rowof = (int *)malloc(sizeof(int) * (size_t)nnz);
+    memset(tia, 0, ((size_t)ncols + 1) * sizeof(int));
+#pragma omp parallel for schedule(static)
+    for (int i = 0; i < nrows; ++i)
+        for (int k = ia[i]; k < ia[i + 1]; ++k) {
+            rowof[k] = i;
+#pragma omp atomic
+            tia[ja[k] + 1]++;
+        }
+    for (int c = 0; c < ncols; ++c) tia[c + 1] += tia[c];
+    memcpy(fill, tia, (size_t)ncols * sizeof(int));
+#pragma omp parallel for schedule(static)
+    for (int k = 0; k < nnz; ++k) {
+        int dst;
+#pragma omp atomic capture
+        dst = fill[ja[k]]++;
+        src[dst] = k;
+    }
+#pragma omp parallel for schedule(dynamic, 4096)
+    for (int c = 0; c < ncols; ++c) {
+        int *a = src + tia[c];
+        const int m = tia[c + 1] - tia[c];
+        if (m > 32) {
+            qsort(a, (size_t)m, sizeof(int), cmp_int);
+        } else {
+            for (int t = 1; t < m; ++t) {
+                const int key = a[t];
+                int u = t - 1;
+                while (u >= 0 && a[u] > key) a[u + 1] = a[u], --u;
+                a[u + 1] = key;
+            }
+        }
+        for (int t = tia[c]; t < tia[c + 1]; ++t) {
+            const int k = src[t];
+            tja[t] = rowof[k];
+            if (val) memcpy((char *)tval + (size_t)t * vsize, (const char *)val + (size_t)k * vsize, vsize);
+        }
+    }
+    free(src);
+    free(rowof);
+    free(fill);
+}
+
 static void transpose_pattern(int nrows, int ncols, int nnz, const int *ia, const int *ja,
                               const void *val, size_t vsize, int *tia, int *tja, void *tval)
 {
+    if (nnz >= (1 << 20)) {
+        transpose_pattern_par(nrows, ncols, nnz, ia, ja, val, vsize, tia, tja, tval);
+        return;
+    }
     int *fill = (int *)calloc((size_t)ncols + 1, sizeof(int));
-    (void)nnz;
     memset(tia, 0, ((size_t)ncols + 1) * sizeof(int));
     for (int i = 0; i < nrows; ++i)
         for (int k = ia[i]; k < ia[i + 1]; ++k) tia[ja[k] + 1]++;

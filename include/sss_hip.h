@@ -107,7 +107,8 @@ int sss_hip_sync(sss_hip_hier *h);
  * engine of the F / C pass (0: one launch per DAG depth, 1: chip-wide dataflow, 2: single CU);
  * whether a one-launch pass ever gave up waiting (gs_stall != 0: results invalid); the storage of
  * A_l in HBM (a_format bits: 1 column-sorted tiles, 2 dictionary tiles (with 1: value
- * dictionaries over the sorted tiles), 4 free-order rows, 8 merged row groups, 16 wave-per-row);
+ * dictionaries over the sorted tiles; alone with 64: dictionary ELL rows), 4 free-order rows,
+ * 8 merged row groups, 16 wave-per-row;
  * the two-stage inner steps of a C/F-Jacobi level (0: plain C/F-Jacobi). */
 typedef struct sss_hip_level_info {
     int rows, nnz, nnz_p, dag_f, dag_c, smoother_kind;

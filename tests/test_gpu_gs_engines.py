@@ -265,16 +265,20 @@ def test_w_cycle_bitwise(request, hname, smoother, coarse):
 @pytest.mark.parametrize("hname", ["p32_h", "a27_h", "p64_h"])
 @pytest.mark.parametrize("smoother,coarse", [("exact", "krylov"), ("hybrid", "direct")])
 def test_dictionary_tiles_bitwise(request, hname, smoother, coarse, monkeypatch):
-    """A_l staged from dictionary tiles (4 B per entry: column offset and value indices into
-    per-block dictionaries) or value-dictionary sorted tiles (5 B: the sorted tile slot plus a value
-    index) gives the iterates of the column-sorted tiles bit for bit, and the stencil levels do
-    take that storage: level 0 of every operator, and the relabeled Galerkin levels of 7-pt 64^3
+    """A_l stored as dictionary ELL rows (1 B per entry: offset and value indices into per-block
+    dictionaries, one thread per row), as dictionary tiles (4 B per entry) or as value-dictionary
+    sorted tiles (5 B: the sorted tile slot plus a value index) gives the iterates of the plain
+    column-sorted tiles bit for bit, and the stencil levels do take that storage: level 0 of 7-pt
+    the ELL rows (dictionary tiles with ELL off), the relabeled Galerkin levels of 7-pt 64^3
     (offsets too many for a dictionary, at most 8 values per block) the value dictionaries."""
     H = request.getfixturevalue(hname)
     n = H.level(0).A.num_rows
     out, fmt = {}, {}
-    for dict_on in ("1", "0"):
-        monkeypatch.setenv("SSS_HIP_DICT", dict_on)
+    for mode, env in (("ell", {"SSS_HIP_DICT": "1", "SSS_HIP_ELL": "1"}),
+                      ("tiles", {"SSS_HIP_DICT": "1", "SSS_HIP_ELL": "0"}),
+                      ("none", {"SSS_HIP_DICT": "0", "SSS_HIP_ELL": "0"})):
+        for k, v in env.items():
+            monkeypatch.setenv(k, v)
         D = A.DeviceHierarchy(H, smoother=smoother, coarse=coarse)
         try:
             D.upload(0, "b", np.ones(n))
@@ -283,13 +287,17 @@ def test_dictionary_tiles_bitwise(request, hname, smoother, coarse, monkeypatch)
             for _ in range(6):
                 D.cycle()
                 rel.append(D.residual_norm())
-            out[dict_on] = (D.download(0, "x"), rel)
-            fmt[dict_on] = [D.level_info(l).a_format for l in range(H.num_levels - 1)]
+            out[mode] = (D.download(0, "x"), rel)
+            fmt[mode] = [D.level_info(l).a_format for l in range(H.num_levels - 1)]
         finally:
             D.close()
-    assert fmt["1"][0] & 2, fmt
+    if hname != "a27_h":
+        assert fmt["ell"][0] & 64, fmt
+        assert fmt["tiles"][0] & 2 and not fmt["tiles"][0] & 64, fmt
+    assert fmt["tiles"][0] & 2 or hname == "a27_h", fmt
     if hname == "p64_h":
-        assert any(f & 3 == 3 for f in fmt["1"][1:]), fmt
-    assert not any(f & 2 for f in fmt["0"])
-    assert np.array_equal(out["1"][0].view(np.uint64), out["0"][0].view(np.uint64))
-    assert out["1"][1] == out["0"][1]
+        assert any(f & 3 == 3 for f in fmt["tiles"][1:]), fmt
+    assert not any(f & 66 for f in fmt["none"])
+    for mode in ("ell", "tiles"):
+        assert np.array_equal(out[mode][0].view(np.uint64), out["none"][0].view(np.uint64)), mode
+        assert out[mode][1] == out["none"][1], mode

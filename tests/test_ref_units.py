@@ -290,3 +290,31 @@ def test_outer_loop_vs_reference_solve(case, quiet):
     mine_lines = [l for l in mine.text.splitlines() if l.strip()]
     ref_rows = [l for l in lines if not l.startswith("###")]
     assert ref_rows == mine_lines
+
+
+@needs_ref
+@pytest.mark.parametrize("gen", ["p7_64", "circuit"])
+def test_parallel_setup_paths_vs_reference(gen, quiet):
+    """Matrices above the parallel threshold (>= 2^20 entries): the OpenMP transpose
+    (transpose_pattern_par) and weak-coupling compaction give the reference's results exactly --
+    SSS_mat_trans of A and the RS C/F marks (SSS_amg_coarsen) against the compiled reference."""
+    from amg_amd import workloads as W
+    keep = None
+    if gen == "p7_64":
+        M = A.generate(7, 64)
+    else:
+        keep = W.circuit_csr(300000)
+        M = keep.mat
+    assert M.num_nnzs >= 1 << 20
+    assert same_csr(A.lib().SSS_mat_trans(C.byref(M)), REF.SSS_mat_trans(C.byref(M)))
+    pars = A.default_pars()
+    v1, v2 = A.lib().SSS_ivec_create(M.num_rows), REF.SSS_ivec_create(M.num_rows)
+    P1, S1, P2, S2 = SSS_MAT(), SSS_IMAT(), SSS_MAT(), SSS_IMAT()
+    with quiet():
+        r1 = A.lib().SSS_amg_coarsen(C.byref(M), C.byref(v1), C.byref(P1), C.byref(S1), C.byref(pars))
+        r2 = REF.SSS_amg_coarsen(C.byref(M), C.byref(v2), C.byref(P2), C.byref(S2), C.cast(C.byref(pars), C.c_void_p))
+    assert r1 == r2
+    assert np.array_equal(np.ctypeslib.as_array(v1.d, shape=(M.num_rows,)),
+                          np.ctypeslib.as_array(v2.d, shape=(M.num_rows,)))
+    assert (P1.num_cols, P1.num_nnzs) == (P2.num_cols, P2.num_nnzs)
+    del keep
