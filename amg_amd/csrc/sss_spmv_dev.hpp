@@ -600,12 +600,17 @@ __device__ __forceinline__ double wave_row_sum(int k0, int k1, const int *__rest
 // entry's (segment, row), then each accumulator's 64 lane sums are xor-reduced.  Fixed order:
 // deterministic.  s0[u] / s1[u] = sum over row u's first- / second-segment entries of
 // prod(col, val), valid in every lane (S = 1: single-segment matrices, s1 untouched).
+#ifndef SSS_MERGE_U
+#define SSS_MERGE_U 8
+#endif
+// (U, the loads in flight per lane, changes no sum: each lane still adds its entries in increasing
+// position into the same accumulators)
 template <int G, int S, class Prod>
 __device__ __forceinline__ void merged_sums(int k0, int k1, const unsigned *__restrict__ mk,
                                             const double *__restrict__ mv, Prod prod, double (&s0)[G],
                                             double (&s1)[G])
 {
-    constexpr int U = 4;
+    constexpr int U = SSS_MERGE_U;
     const int lane = threadIdx.x & 63;
 #pragma unroll
     for (int u = 0; u < G; ++u) s0[u] = 0.0, s1[u] = 0.0;
