@@ -111,6 +111,7 @@ ABI_SYMBOLS = [
     "sss_hip_coarse_solve", "sss_hip_smooth", "sss_hip_sync", "sss_hip_level_info_get", "sss_hip_num_levels",
     "sss_hip_spmv_plan_create", "sss_hip_spmv_plan_destroy", "sss_hip_spmv", "sss_hip_host_spmv",
     "sss_hip_host_smooth", "sss_hip_host_coarse_solve", "sss_hip_time_level0_spmv", "sss_hip_time_iterations",
+    "sss_hip_time_level0_spmv_csr",
     "sss_gen_stencil",
     "sss_hip_rccl_unique_id", "sss_hip_comm_rccl", "sss_hip_comm_host", "sss_hip_comm_destroy",
     "sss_hip_dist_create", "sss_hip_dist_destroy", "sss_hip_dist_info", "sss_hip_dist_level_flags",
@@ -190,6 +191,7 @@ def _declare(lib):
         "sss_hip_host_coarse_solve": (C.c_int, [P(SSS_MAT), P(SSS_VEC), P(SSS_VEC), C.c_double, C.c_int,
                                                 C.c_int]),
         "sss_hip_time_level0_spmv": (C.c_int, [C.c_void_p, C.c_int, _dbl_p]),
+        "sss_hip_time_level0_spmv_csr": (C.c_int, [C.c_void_p, C.c_int, _dbl_p]),
         "sss_hip_time_iterations": (C.c_int, [C.c_void_p, C.c_int, _dbl_p, _dbl_p]),
         "sss_hip_rccl_unique_id": (C.c_int, [C.c_char_p]),
         "sss_hip_comm_rccl": (C.c_void_p, [C.c_int, C.c_int, C.c_char_p, C.c_int]),
@@ -405,6 +407,12 @@ class DeviceHierarchy:
     def time_level0_spmv(self, reps: int) -> float:
         ms = C.c_double()
         self._check(lib().sss_hip_time_level0_spmv(self.h, reps, C.byref(ms)), "time_level0_spmv")
+        return ms.value
+
+    def time_level0_spmv_csr(self, reps: int) -> float:
+        """the same residual SpMV from A_0's plain CSR arrays (the metric's fine-level CSR SpMV)"""
+        ms = C.c_double()
+        self._check(lib().sss_hip_time_level0_spmv_csr(self.h, reps, C.byref(ms)), "time_level0_spmv_csr")
         return ms.value
 
     def time_iterations(self, reps: int):

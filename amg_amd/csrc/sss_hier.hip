@@ -810,6 +810,33 @@ extern "C" int sss_hip_time_level0_spmv(sss_hip_hier *h, int reps, double *avg_m
     return 0;
 }
 
+// The same residual SpMV of level 0 from its plain CSR arrays (row_ptr, col_idx, val; always
+// resident), whatever storage the cycle uses: the fine-level CSR SpMV of the metric.
+extern "C" int sss_hip_time_level0_spmv_csr(sss_hip_hier *h, int reps, double *avg_ms)
+{
+    auto &L = h->L[0];
+    if (L.A.wave_rows || L.A.vec_rows) return sss_hip_time_level0_spmv(h, reps, avg_ms);
+    DevCSR c = L.A;   // a view: the CSR arrays and row blocks only (never freed through c)
+    c.pk = nullptr;
+    c.pv = nullptr;
+    c.pb = nullptr;
+    c.dv_ell = nullptr;
+    c.dv_code = nullptr;
+    c.dv_vi = nullptr;
+    SSS_HIP(hipStreamSynchronize(h->stream));
+    SSS_HIP(hipEventRecord(h->ev0, h->stream));
+    for (int r = 0; r < reps; ++r) {
+        int rc = launch_spmv(c, SSS_HIP_SPMV_RESID, -1.0, L.x, L.b, L.wp, 0, nullptr, h->stream);
+        if (rc) return rc;
+    }
+    SSS_HIP(hipEventRecord(h->ev1, h->stream));
+    SSS_HIP(hipEventSynchronize(h->ev1));
+    float ms = 0.f;
+    SSS_HIP(hipEventElapsedTime(&ms, h->ev0, h->ev1));
+    *avg_ms = (double)ms / reps;
+    return 0;
+}
+
 extern "C" int sss_hip_time_iterations(sss_hip_hier *h, int reps, double *avg_ms, double *absres)
 {
     SSS_HIP(hipStreamSynchronize(h->stream));

@@ -457,7 +457,7 @@ def main():
 
     # roofline of the dominant streaming kernel: level-0 fused residual SpMV (wp = b - A0 x);
     # N > 1: rank 0's share (its rows, x with ghosts), no exchange inside the timed launches
-    spmv_ms = DH.time_level0_spmv(20)
+    spmv_ms = DH.time_level0_spmv(20)   # the cycle's own storage of A_0
     a_format = None
     level_formats = None
     level_smoothers = None
@@ -467,15 +467,18 @@ def main():
         a_format = A._native.a_format_name(info0.a_format)
         level_formats = [DH.DH.level_info(l).a_format for l in range(len(table) - 1)]
         level_smoothers = [(DH.DH.level_info(l).smoother_kind, DH.DH.level_info(l).inner) for l in range(len(table) - 1)]
-        # the stored format's own bytes (dictionary tiles: 4 B per entry + block dictionaries)
+        # the stored format's own bytes (dictionary ELL: 8 B per row + block dictionaries) + vectors
         spmv_bytes = info0.a_stream_bytes + 8 * N + 8 * N + 8 * N
+        # SURVEY.md 8(d)'s kernel: the same residual SpMV from A_0's CSR arrays
+        csr_ms = DH.DH.time_level0_spmv_csr(20)
     else:
         m, g = DH.rows, DH.ghosts
         spmv_bytes = 12 * DH.nnz + 4 * (m + 1) + 8 * (m + g) + 8 * m + 8 * m
         csr_bytes = spmv_bytes
-    # roofline.achieved uses the algorithmic bytes of the CSR SpMV (12 B per entry +
-    # row pointers + vectors); the bytes the stored format actually streams are reported beside it
-    achieved = csr_bytes / (spmv_ms * 1e-3) / 1e9
+        csr_ms = spmv_ms
+    # roofline: SURVEY.md 8(d)'s algorithmic bytes of the CSR SpMV over the CSR kernel's time; the
+    # cycle's own (compressed) storage of A_0 is reported beside it with its own bytes
+    achieved = csr_bytes / (csr_ms * 1e-3) / 1e9
     format_gbps = spmv_bytes / (spmv_ms * 1e-3) / 1e9
 
     # iterations to tol from x0 = 1 (the CLI's problem), and time to solution
@@ -556,13 +559,13 @@ def main():
     import resource
     rss_gb = D.max(resource.getrusage(resource.RUSAGE_SELF).ru_maxrss / 2**20)   # peak over the ranks
 
-    traffic = None
-    pmc = ROOT / "profiles" / "r02_level0_spmv_pmc.json"   # tools/gpu/pmc.sh at this format
-    if pmc.exists() and D.world == 1:
+    traffic = None   # {"csr": bytes, "stored": bytes} per launch, from tools/gpu/pmc.sh at this format
+    pmc = ROOT / "profiles" / "r02_level0_spmv_pmc.json"
+    if pmc.exists() and D.world == 1 and not circuit:
         try:
             rec = json.loads(pmc.read_text())
             if rec.get("n") == n and rec.get("a_format") == a_format:
-                traffic = rec.get("hbm_bytes_per_launch")
+                traffic = {k: rec[k]["hbm_bytes_per_launch"] for k in ("csr", "stored") if k in rec}
         except Exception:
             traffic = None
 
@@ -646,16 +649,20 @@ def main():
                    "parallelism": f"rowpart{D.world}" if D.world > 1 else "single-gpu",
                    "host_peak_rss_gb_max_over_ranks": rss_gb,
                    "transport": transport},
-        "roofline": {"bound": "hbm", "kernel": "spmv_adaptive<RESID> level 0", "achieved": achieved,
-                     "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": achieved / PEAK_HBM_GBS,
-                     "frac_of_copy_peak": achieved / COPY_PEAK_GBS, "avg_launch_ms": spmv_ms,
-                     "bytes_per_launch": csr_bytes, "traffic": traffic,
-                     "algorithmic_bytes": "SURVEY.md 8(d): 12 nnz + 4 (n + 1) + 8 n_cols + 16 n (y = b - A x)",
-                     "stored_format": {"a_format": a_format, "bytes_per_launch": spmv_bytes, "GBps": format_gbps,
-                                       "frac": format_gbps / PEAK_HBM_GBS,
-                                       "note": "bytes the stored format of A_0 streams per launch (dictionary "
-                                               "tiles: 4 B per entry + block dictionaries) + the vectors, over "
-                                               "the same time; traffic = HBM bytes from the PMC counters"}},
+        "roofline": {"bound": "hbm", "kernel": "spmv_adaptive<RESID> level 0 from its CSR arrays (y = b - A0 x)",
+                     "achieved": achieved, "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": achieved / PEAK_HBM_GBS,
+                     "frac_of_copy_peak": achieved / COPY_PEAK_GBS, "avg_launch_ms": csr_ms,
+                     "bytes_per_launch": csr_bytes, "traffic": traffic.get("csr") if traffic else None,
+                     "algorithmic_bytes": "SURVEY.md 8(d): 12 nnz + 4 (n + 1) + 8 n_cols + 16 n",
+                     "cycle_storage": {
+                         "a_format": a_format, "kernel": "the same residual from the storage the V-cycle uses",
+                         "avg_launch_ms": spmv_ms, "bytes_per_launch": spmv_bytes, "GBps": format_gbps,
+                         "frac": format_gbps / PEAK_HBM_GBS,
+                         "traffic": traffic.get("stored") if traffic else None,
+                         "csr_equivalent_GBps": csr_bytes / (spmv_ms * 1e-3) / 1e9,
+                         "note": "bytes = the stored format of A_0 (dictionary ELL: 8 B per row of codes + block "
+                                 "dictionaries) + x, b, y; csr_equivalent = SURVEY 8(d) CSR bytes over this "
+                                 "kernel's time, the rate a CSR SpMV would need to match it"}},
         "vcycle_csr_equivalent": {
             "bytes_per_step": vbytes, "achieved": vbytes / (ms_per_step * 1e-3) / 1e9, "peak": PEAK_HBM_GBS,
             "unit": "GB/s", "frac": vbytes / (ms_per_step * 1e-3) / 1e9 / PEAK_HBM_GBS,

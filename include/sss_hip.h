@@ -146,6 +146,8 @@ int sss_hip_host_coarse_solve(SSS_MAT *A, SSS_VEC *b, SSS_VEC *x, double ctol, i
 /* Engine event timer around `reps` launches of the level-0 residual SpMV on the engine
  * stream: average kernel milliseconds (roofline measurement in bench.py). */
 int sss_hip_time_level0_spmv(sss_hip_hier *h, int reps, double *avg_ms);
+/* The same launch from level 0's plain CSR arrays (whatever storage the cycle uses for A_0). */
+int sss_hip_time_level0_spmv_csr(sss_hip_hier *h, int reps, double *avg_ms);
 /* Average milliseconds of `reps` full iterations (cycle + residual + norm) on the engine
  * stream, timed with HIP events; absres of the last iteration is returned. */
 int sss_hip_time_iterations(sss_hip_hier *h, int reps, double *avg_ms, double *absres);

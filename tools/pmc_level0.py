@@ -35,10 +35,11 @@ D = A.DeviceHierarchy(H, smoother="hybrid", coarse="direct")
 N = H.level(0).A.num_rows
 D.upload(0, "b", np.ones(N))
 D.upload(0, "x", np.ones(N))
-ms = D.time_level0_spmv(reps)
+ms_csr = D.time_level0_spmv_csr(reps)   # spmv_adaptive<2, false, 0>: A_0's CSR arrays
+ms = D.time_level0_spmv(reps)           # the cycle's storage of A_0
 info = D.level_info(0)
 print(f"level0 n={N} nnz={H.level(0).A.num_nnzs} avg_ms={ms:.4f}", flush=True)
 import json  # noqa: E402
-print(json.dumps({"n": n, "rows": N, "nnz": H.level(0).A.num_nnzs, "avg_ms": ms,
+print(json.dumps({"n": n, "rows": N, "nnz": H.level(0).A.num_nnzs, "avg_ms": ms, "avg_ms_csr": ms_csr,
                   "a_format": A._native.a_format_name(info.a_format),
                   "algorithmic_bytes_per_launch": int(info.a_stream_bytes) + 24 * N}), flush=True)

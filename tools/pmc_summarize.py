@@ -19,7 +19,9 @@ from pathlib import Path
 FETCH_CORRECTION = 2.0
 
 
-def counter_avg(d: Path, name: str) -> tuple[float, int]:
+def counter_avg(d: Path, name: str, csr: bool) -> tuple[float, int]:
+    """launches of the level-0 residual: spmv_adaptive<2, false, 0> (CSR arrays) or the other
+    instantiation (the cycle's storage)"""
     vals = []
     for f in d.rglob("*.csv"):
         with open(f) as fh:
@@ -27,10 +29,12 @@ def counter_avg(d: Path, name: str) -> tuple[float, int]:
             if "Counter_Name" not in (rd.fieldnames or []):
                 continue
             for r in rd:
-                if r["Counter_Name"] == name and "spmv_adaptive<2" in r["Kernel_Name"]:
+                kn = r["Kernel_Name"]
+                if r["Counter_Name"] == name and "spmv_adaptive<2, false" in kn and \
+                        ("spmv_adaptive<2, false, 0>" in kn) == csr:
                     vals.append(float(r["Counter_Value"]))
     if not vals:
-        raise SystemExit(f"no {name} rows for spmv_adaptive<2, ...> under {d}")
+        raise SystemExit(f"no {name} rows for the level-0 residual ({'CSR' if csr else 'stored'}) under {d}")
     return sum(vals) / len(vals), len(vals)
 
 
@@ -43,25 +47,28 @@ def main():
             info = json.loads(line)
     if info is None:
         raise SystemExit("pmc_level0.py JSON line not found")
-    fetch, nf = counter_avg(out / "pmc_FETCH_SIZE", "FETCH_SIZE")
-    write, nw = counter_avg(out / "pmc_WRITE_SIZE", "WRITE_SIZE")
-    rd = fetch * 1024 * FETCH_CORRECTION
-    wr = write * 1024
-    alg = info["algorithmic_bytes_per_launch"]
-    rec = {
-        "n": info["n"], "rows": info["rows"], "nnz": info["nnz"], "a_format": info["a_format"],
-        "kernel": "spmv_adaptive<RESID> level 0 (bench roofline kernel)",
-        "avg_ms_unprofiled": info["avg_ms"],
-        "fetch_size_kib_raw": fetch, "write_size_kib_raw": write, "fetch_correction": FETCH_CORRECTION,
+    N, nnz = info["rows"], info["nnz"]
+    survey = 12 * nnz + 4 * (N + 1) + 24 * N   # SURVEY.md 8(d), y = b - A x
+    rec = {"n": info["n"], "rows": N, "nnz": nnz, "a_format": info["a_format"]}
+    for key, csr, alg, ms in (("csr", True, survey, info.get("avg_ms_csr")),
+                              ("stored", False, info["algorithmic_bytes_per_launch"], info["avg_ms"])):
+        fetch, nf = counter_avg(out / "pmc_FETCH_SIZE", "FETCH_SIZE", csr)
+        write, nw = counter_avg(out / "pmc_WRITE_SIZE", "WRITE_SIZE", csr)
+        rd = fetch * 1024 * FETCH_CORRECTION
+        wr = write * 1024
+        rec[key] = {"kernel": "spmv_adaptive<RESID> level 0 from " + ("the CSR arrays" if csr else info["a_format"]),
+                    "avg_ms_unprofiled": ms, "fetch_size_kib_raw": fetch, "write_size_kib_raw": write,
+                    "hbm_read_bytes_per_launch": rd, "hbm_write_bytes_per_launch": wr,
+                    "hbm_bytes_per_launch": rd + wr, "algorithmic_bytes_per_launch": alg,
+                    "traffic_over_algorithmic": (rd + wr) / alg, "launches": min(nf, nw)}
+    rec.update({
+        "fetch_correction": FETCH_CORRECTION,
         "correction_source": "MI355X_MICROARCH.md HBM section; re-measured with tools/pmc_calib.hip "
                              "(profiles/r01_pmc/calibration_fetch_size.csv)",
-        "hbm_read_bytes_per_launch": rd, "hbm_write_bytes_per_launch": wr, "hbm_bytes_per_launch": rd + wr,
-        "algorithmic_bytes_per_launch": alg, "traffic_over_algorithmic": (rd + wr) / alg,
-        "launches": min(nf, nw),
         "method": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes (tools/gpu/pmc.sh running "
                   "tools/pmc_level0.py); Infinity-Cache hits are counted by these counters, so this is an upper "
                   "bound on HBM bytes",
-    }
+    })
     dst.write_text(json.dumps(rec, indent=1))
     print(json.dumps(rec))
 
