@@ -11,7 +11,11 @@
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
+#include <cstdlib>
+#include <string>
 #include <functional>
+#include <memory>
 #include <cstdio>
 #include <thread>
 #include <vector>
@@ -44,29 +48,88 @@ inline void dev_free(void *p)
     if (p) (void)hipFree(p);
 }
 
+// Host array without value-initialisation (the upload builders overwrite every element, and
+// zero-filling gigabyte arrays on one thread was a visible share of the upload time).
+template <class T>
+struct HostBuf {
+    std::unique_ptr<T[]> p;
+    size_t n = 0;
+    void resize(size_t m)
+    {
+        p.reset(m ? new T[m] : nullptr);
+        n = m;
+    }
+    T *data() { return p.get(); }
+    const T *data() const { return p.get(); }
+    size_t size() const { return n; }
+    T &operator[](size_t i) { return p[i]; }
+    const T &operator[](size_t i) const { return p[i]; }
+};
+
+// Persistent host worker pool for the upload-time data preparation (sss_spmv.hip): the workers
+// are started once and reused, so a parallel loop costs a wake-up instead of thread creation
+// (h2d alone issued one loop per 32 MiB chunk).  One job at a time; a loop issued from a worker,
+// or while another thread holds the pool, runs inline on its caller.
+int host_pool_threads();
+bool host_pool_run(const std::function<void()> &work);   // false: pool busy (caller runs inline)
+
 // Host-side data preparation at upload: fn(lo, hi) over [0, n) in chunks of `grain` items taken
-// from a shared counter by up to 32 threads (the .hip units are compiled without OpenMP).
+// from a shared counter by the pool's threads and the caller (the .hip units are compiled
+// without OpenMP).
 template <class Fn>
 void parallel_chunks(int n, int grain, Fn fn)
 {
-    const int nt = (int)std::max(1u, std::min(32u, std::thread::hardware_concurrency()));
-    if (n <= grain || nt == 1) {
-        if (n > 0) fn(0, n);
+    if (n <= 0) return;
+    if (n <= grain || host_pool_threads() <= 1) {
+        fn(0, n);
         return;
     }
     std::atomic<int> next{0};
-    auto work = [&]() {
+    std::function<void()> work = [&]() {
         for (;;) {
             const int lo = next.fetch_add(grain);
             if (lo >= n) return;
             fn(lo, std::min(n, lo + grain));
         }
     };
-    std::vector<std::thread> th;
-    for (int t = 1; t < nt; ++t) th.emplace_back(work);
-    work();
-    for (auto &t : th) t.join();
+    if (!host_pool_run(work)) work();
 }
+
+// Upload phase timer: SSS_HIP_TIMING=2 prints each mark's elapsed time on stderr.
+struct PhaseTimer {
+    const char *what;
+    bool on;
+    double t;
+    std::vector<std::pair<const char *, double>> marks;
+    static double now()
+    {
+        return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+    }
+    explicit PhaseTimer(const char *w) : what(w)
+    {
+        const char *e = getenv("SSS_HIP_TIMING");
+        on = e && atoi(e) >= 2;
+        t = now();
+    }
+    void mark(const char *name)
+    {
+        if (!on) return;
+        const double t1 = now();
+        marks.emplace_back(name, t1 - t);
+        t = t1;
+    }
+    ~PhaseTimer()
+    {
+        if (!on || marks.empty()) return;
+        std::string s;
+        char buf[96];
+        for (auto &m : marks) {
+            snprintf(buf, sizeof(buf), " %s %.3f", m.first, m.second);
+            s += buf;
+        }
+        fprintf(stderr, "[sss_hip]     %s:%s\n", what, s.c_str());
+    }
+};
 
 // Host -> device copy through pinned staging buffers (sss_spmv.hip); returns 0 or an error code.
 int h2d(void *dst, const void *src, size_t bytes);

@@ -216,23 +216,10 @@ static void hier_release(sss_hip_hier *h)
 // keeps its labels, so the iterates are bitwise those of the unrelabeled hierarchy.  What changes
 // is the memory layout: every smoother pass is a contiguous row range of the level matrix, the
 // x values it gathers (the other class) are contiguous too, and it writes a dense half of x.
-template <class Fn>
-static void parallel_rows(int n, Fn fn)
-{
-    const int nt = (int)std::max(1u, std::min(32u, std::thread::hardware_concurrency()));
-    if (n < (1 << 16) || nt == 1) { fn(0, n); return; }
-    std::vector<std::thread> th;
-    const int chunk = (n + nt - 1) / nt;
-    for (int t = 0; t < nt; ++t) {
-        const int lo = t * chunk, hi = std::min(n, lo + chunk);
-        if (lo < hi) th.emplace_back(fn, lo, hi);
-    }
-    for (auto &t : th) t.join();
-}
-
 struct RelabeledCSR {   // owns the arrays an SSS_MAT view points into
-    std::vector<int> rp, ci;
-    std::vector<double> v;
+    std::vector<int> rp;
+    HostBuf<int> ci;
+    HostBuf<double> v;
     SSS_MAT view(int nrows, int ncols)
     {
         SSS_MAT m;
@@ -258,7 +245,7 @@ static void relabel_csr(const SSS_MAT &A, const std::vector<int> &rperm, const s
     }
     B.ci.resize((size_t)B.rp[n]);
     B.v.resize((size_t)B.rp[n]);
-    parallel_rows(n, [&](int lo, int hi) {
+    parallel_chunks(n, 1 << 15, [&](int lo, int hi) {
         for (int i = lo; i < hi; ++i) {
             const int o = rperm.empty() ? i : rperm[i];
             int q = B.rp[i];
@@ -459,7 +446,7 @@ extern "C" int sss_hip_upload_vec(sss_hip_hier *h, int level, int which, const d
         if (n != h->L[level].A.n) return ERROR_INPUT_PAR;   // relabeled levels move whole vectors
         h->stage.resize((size_t)n);
         double *st = h->stage.data();
-        parallel_rows(n, [&](int lo, int hi) {
+        parallel_chunks(n, 1 << 16, [&](int lo, int hi) {
             for (int i = lo; i < hi; ++i) st[i] = src[perm[i]];
         });
         src = st;
@@ -484,7 +471,7 @@ extern "C" int sss_hip_download_vec(sss_hip_hier *h, int level, int which, doubl
     double *st = h->stage.data();
     SSS_HIP(hipMemcpyAsync(st, d, sizeof(double) * (size_t)n, hipMemcpyDeviceToHost, h->stream));
     SSS_HIP(hipStreamSynchronize(h->stream));
-    parallel_rows(n, [&](int lo, int hi) {
+    parallel_chunks(n, 1 << 16, [&](int lo, int hi) {
         for (int i = lo; i < hi; ++i) dst[perm[i]] = st[i];
     });
     return 0;

@@ -112,7 +112,11 @@ int smoother_build(SmootherPlan &sp, const SSS_MAT &A, const int *mark, int kind
                 }
             }
     });
-    if (coupled) {   // red-black levels (no coupling) keep depth 0 everywhere
+    PhaseTimer pt("plan");
+    pt.mark("classes+coupled");
+    // red-black levels (no coupling) keep depth 0 everywhere; so do C/F-Jacobi levels, whose
+    // passes read only the other iterate (their schedule is never walked by depth)
+    if (coupled && kind != SSS_HIP_SMOOTH_JACOBI) {
         for (int i = 0; i < n; ++i) {
             int dep = pushed[i];
             for (int k = rp[i]; k < rp[i + 1]; ++k) {
@@ -126,6 +130,7 @@ int smoother_build(SmootherPlan &sp, const SSS_MAT &A, const int *mark, int kind
             }
         }
     }
+    pt.mark("depth");
     for (int c = 0; c < 2; ++c) {
         PassSchedule &ps = sp.pass[c];
         int maxd = -1;
@@ -245,6 +250,7 @@ int smoother_build(SmootherPlan &sp, const SSS_MAT &A, const int *mark, int kind
                 }
             });
             for (int q = 0; q < m; ++q) nrp[q + 1] += nrp[q], lrp[q + 1] += lrp[q];
+            pt.mark("ts count");
             std::vector<int> nci((size_t)nrp[m]), lci((size_t)lrp[m]);
             std::vector<double> nv((size_t)nrp[m]), lv((size_t)lrp[m]);
             parallel_chunks(m, 1 << 14, [&](int a, int e) {
@@ -275,11 +281,13 @@ int smoother_build(SmootherPlan &sp, const SSS_MAT &A, const int *mark, int kind
                 M.val = w.data();
                 return M;
             };
+            pt.mark("ts fill");
             SSS_MAT Mn = mk(nrp, nci, nv), Ml = mk(lrp, lci, lv);
             std::vector<int> seg(split);   // absolute [N_i | L_i] cut of each row of Mn
             if ((rc = devcsr_upload(ps.ts_nl, Mn, -1, enc & ~kEncDict, seg.data())) ||
                 (rc = devcsr_upload(ps.ts_lo, Ml, -1, enc & ~kEncDict)))
                 return rc;
+            pt.mark("ts upload");
             if ((rc = upload_ints(&ps.ts_split, split))) return rc;
             ps.ts_P = dev_alloc<double>((size_t)m);
             if (!ps.ts_P) return hip_fail(hipErrorOutOfMemory, "hipMalloc(P)", __FILE__, __LINE__);

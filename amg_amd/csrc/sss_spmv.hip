@@ -21,8 +21,10 @@
 
 #include <algorithm>
 #include <type_traits>
+#include <condition_variable>
 #include <cstring>
 #include <mutex>
+#include <sched.h>
 
 namespace sss {
 
@@ -35,6 +37,89 @@ int hip_fail(hipError_t e, const char *what, const char *file, int line)
 // Host -> device copy of a large host array through a ring of pinned staging buffers: host threads
 // copy chunk k + 1 into one buffer while the DMA engine moves chunk k out of another (a pageable
 // hipMemcpy of the 400^3 hierarchy's ~60 GB ran at ~3 GB/s).  Small copies go straight through.
+// ---- host worker pool (sss_engine.hpp) ----------------------------------------------------------
+// Threads: SSS_HOST_THREADS, else the usable CPUs (affinity mask, capped by a cgroup v2 cpu.max
+// quota), at most 32.
+static int usable_cpus()
+{
+    const char *e = getenv("SSS_HOST_THREADS");
+    if (e && *e) return std::max(1, atoi(e));
+    int n = (int)std::max(1u, std::thread::hardware_concurrency());
+    cpu_set_t set;
+    if (sched_getaffinity(0, sizeof(set), &set) == 0) n = std::max(1, CPU_COUNT(&set));
+    if (FILE *f = fopen("/sys/fs/cgroup/cpu.max", "r")) {
+        char q[32] = {0};
+        long long period = 0;
+        if (fscanf(f, "%31s %lld", q, &period) == 2 && strcmp(q, "max") != 0 && period > 0)
+            n = std::min(n, (int)std::max(1LL, (atoll(q) + period - 1) / period));
+        fclose(f);
+    }
+    return std::min(n, 32);
+}
+
+namespace {
+struct HostPool {
+    std::mutex job_mu, mu;
+    std::condition_variable cv, done_cv;
+    const std::function<void()> *job = nullptr;
+    unsigned long long gen = 0;
+    int running = 0;
+    int nt = 1;
+    static thread_local bool in_worker;
+    HostPool()
+    {
+        nt = usable_cpus();
+        for (int t = 1; t < nt; ++t) std::thread([this] { loop(); }).detach();   // lives as long as the process
+    }
+    void loop()
+    {
+        in_worker = true;
+        unsigned long long seen = 0;
+        for (;;) {
+            const std::function<void()> *w;
+            {
+                std::unique_lock<std::mutex> lk(mu);
+                cv.wait(lk, [&] { return gen != seen; });
+                seen = gen;
+                w = job;
+            }
+            (*w)();
+            std::lock_guard<std::mutex> lk(mu);
+            if (--running == 0) done_cv.notify_all();
+        }
+    }
+    bool run(const std::function<void()> &work)
+    {
+        if (in_worker || !job_mu.try_lock()) return false;
+        {
+            std::lock_guard<std::mutex> lk(mu);
+            job = &work;
+            running = nt - 1;
+            ++gen;
+        }
+        cv.notify_all();
+        work();
+        {
+            std::unique_lock<std::mutex> lk(mu);
+            done_cv.wait(lk, [&] { return running == 0; });
+            job = nullptr;
+        }
+        job_mu.unlock();
+        return true;
+    }
+};
+thread_local bool HostPool::in_worker = false;
+
+HostPool &host_pool()
+{
+    static HostPool *p = new HostPool();   // never destroyed: detached workers outlive static teardown
+    return *p;
+}
+}   // namespace
+
+int host_pool_threads() { return host_pool().nt; }
+bool host_pool_run(const std::function<void()> &work) { return host_pool().run(work); }
+
 int h2d(void *dst, const void *src, size_t bytes)
 {
     constexpr size_t kChunk = (size_t)32 << 20;
@@ -133,12 +218,66 @@ int build_row_blocks(const int *h_rp, int n, std::vector<int> &blk, int split)
     return (int)blk.size() - 1;
 }
 
+// Distinct 64-bit patterns of one block (at most 256), collected by open addressing; rank(id)
+// is the pattern's position in ascending order -- what sort + unique + lower_bound gives, at a
+// hash probe per entry instead of a sort of the whole block.
+struct SmallDict {
+    static constexpr int kSlots = 1024;
+    unsigned long long key[kSlots];
+    short slot[kSlots];                 // -1: empty; else local id
+    unsigned long long val[256];        // local id -> pattern (insertion order)
+    unsigned char rk[256];              // local id -> rank
+    int n = 0;
+    void clear()
+    {
+        std::memset(slot, 0xff, sizeof(slot));
+        n = 0;
+    }
+    int insert(unsigned long long u, int cap)   // local id, or -1 past cap distinct patterns
+    {
+        unsigned h = (unsigned)((u * 0x9E3779B97F4A7C15ull) >> 54);
+        for (;; h = (h + 1) & (kSlots - 1)) {
+            if (slot[h] < 0) {
+                if (n >= cap) return -1;
+                slot[h] = (short)n;
+                key[h] = u;
+                val[n] = u;
+                return n++;
+            }
+            if (key[h] == u) return slot[h];
+        }
+    }
+    template <class T>
+    void finish(std::vector<T> &sorted)   // ranks + the patterns in ascending order
+    {
+        int ord[256];
+        for (int t = 0; t < n; ++t) ord[t] = t;
+        std::sort(ord, ord + n, [&](int a, int b) { return (T)val[a] < (T)val[b]; });
+        sorted.resize((size_t)n);
+        for (int t = 0; t < n; ++t) rk[ord[t]] = (unsigned char)t, sorted[t] = (T)val[ord[t]];
+    }
+};
+static inline unsigned long long bits_of(double d)
+{
+    unsigned long long u;
+    std::memcpy(&u, &d, sizeof(u));
+    return u;
+}
+static inline double double_of(unsigned long long u)
+{
+    double d;
+    std::memcpy(&d, &u, sizeof(d));
+    return d;
+}
+
 // Sorted tile segments of a blocking: a block's entries, or kTileEntries chunks of a long row
 // (exactly the segments the tile kernels stage, sss_spmv_dev.hpp csr_block_rows).  Per block the
 // columns are cut into two clusters at their widest gap; returns false when a cluster spans
-// 2^kTileColBits columns or more (the matrix then keeps stored-order staging).
-static bool build_sorted_tiles(const SSS_MAT &h, const std::vector<int> &blk, std::vector<unsigned> &pk,
-                               std::vector<double> &pv, std::vector<int2> &pb)
+// 2^kTileColBits columns or more (the matrix then keeps stored-order staging).  One sort of
+// (column << 32 | position) keys per segment gives both the column order and, on ties, the
+// stored order (a stable sort by column).
+static bool build_sorted_tiles(const SSS_MAT &h, const std::vector<int> &blk, HostBuf<unsigned> &pk,
+                               HostBuf<double> &pv, std::vector<int2> &pb)
 {
     const int *rp = h.row_ptr, *ci = h.col_idx;
     const int nb = (int)blk.size() - 1;
@@ -148,8 +287,9 @@ static bool build_sorted_tiles(const SSS_MAT &h, const std::vector<int> &blk, st
     pb.resize((size_t)std::max(nb, 1));
     std::atomic<int> ok{1};
     parallel_chunks(nb, 512, [&](int qlo, int qhi) {
-        std::vector<int> idx, cols, rowof;
-        for (int q = qlo; q < qhi; ++q) {
+        std::vector<unsigned long long> key, seg;
+        std::vector<int> rowof;
+        for (int q = qlo; q < qhi && ok; ++q) {
             const int a0 = rp[blk[q]], e0 = rp[blk[q + 1]];
             if (a0 == e0) {
                 pb[q] = make_int2(0, 0);
@@ -158,14 +298,17 @@ static bool build_sorted_tiles(const SSS_MAT &h, const std::vector<int> &blk, st
             rowof.resize((size_t)(e0 - a0));   // entry position -> its row (one pass over the block)
             for (int r = blk[q]; r < blk[q + 1]; ++r)
                 for (int k = rp[r]; k < rp[r + 1]; ++k) rowof[(size_t)(k - a0)] = r;
-            cols.assign(ci + a0, ci + e0);
-            std::sort(cols.begin(), cols.end());
-            size_t gap = 0;   // cut after cols[gap]
-            for (size_t t = 1; t < cols.size(); ++t)
-                if (cols[t] - cols[t - 1] > cols[gap + 1] - cols[gap]) gap = t - 1;
-            const int b0 = cols.front(), b1 = cols.size() > 1 ? cols[gap + 1] : cols.front();
+            key.resize((size_t)(e0 - a0));
+            for (int k = a0; k < e0; ++k) key[(size_t)(k - a0)] = (unsigned long long)(unsigned)ci[k] << 32 | (unsigned)(k - a0);
+            std::sort(key.begin(), key.end());
+            auto col = [&](size_t t) { return (int)(key[t] >> 32); };
+            const size_t m = key.size();
+            size_t gap = 0;   // cut after col(gap)
+            for (size_t t = 1; t < m; ++t)
+                if (col(t) - col(t - 1) > col(gap + 1) - col(gap)) gap = t - 1;
+            const int b0 = col(0), b1 = m > 1 ? col(gap + 1) : col(0);
             const int cut = b1;   // columns >= cut go to cluster 1
-            if (cols.size() > 1 && ((long long)cols[gap] - b0 >= kSpan || (long long)cols.back() - b1 >= kSpan)) {
+            if (m > 1 && ((long long)col(gap) - b0 >= kSpan || (long long)col(m - 1) - b1 >= kSpan)) {
                 ok = 0;
                 return;
             }
@@ -173,13 +316,17 @@ static bool build_sorted_tiles(const SSS_MAT &h, const std::vector<int> &blk, st
             const int r0 = blk[q];
             for (int a = a0; a < e0; a += kTileEntries) {
                 const int e = std::min(e0, a + kTileEntries);
-                idx.resize((size_t)(e - a));
-                for (int t = 0; t < e - a; ++t) idx[t] = a + t;
-                std::stable_sort(idx.begin(), idx.end(), [&](int p, int r) { return ci[p] < ci[r]; });
+                const unsigned long long *sk = key.data();
+                if (e - a != e0 - a0) {   // a long row's chunk: its own column order
+                    seg.resize((size_t)(e - a));
+                    for (int k = a; k < e; ++k) seg[(size_t)(k - a)] = (unsigned long long)(unsigned)ci[k] << 32 | (unsigned)(k - a0);
+                    std::sort(seg.begin(), seg.end());
+                    sk = seg.data();
+                }
                 for (int t = 0; t < e - a; ++t) {
-                    const int k = idx[t], c = ci[k];
+                    const int k = a0 + (int)(unsigned)sk[t], c = ci[k];
                     const int r = rowof[(size_t)(k - a0)];   // the entry's row
-                    const unsigned cl = (cols.size() > 1 && c >= cut) ? 1u : 0u;
+                    const unsigned cl = (m > 1 && c >= cut) ? 1u : 0u;
                     const unsigned off = c == r ? kTileDiagMark + (unsigned)(r - r0) : (unsigned)(c - (cl ? b1 : b0));
                     pk[(size_t)a + t] = (cl << 31) | (off << kTileShift) | (unsigned)(k - a);
                     pv[(size_t)a + t] = h.val[k];
@@ -191,22 +338,25 @@ static bool build_sorted_tiles(const SSS_MAT &h, const std::vector<int> &blk, st
 }
 
 // Rows of a free-order (tree-summed) matrix, stored column-sorted within each segment.
-static void sort_row_segments(const SSS_MAT &h, const int *seg, std::vector<int> &ci, std::vector<double> &v)
+static void sort_row_segments(const SSS_MAT &h, const int *seg, HostBuf<int> &ci, HostBuf<double> &v)
 {
     const int n = h.num_rows;
     const int *rp = h.row_ptr;
     ci.resize((size_t)h.num_nnzs);
     v.resize((size_t)h.num_nnzs);
-    parallel_chunks(n, 2048, [&](int rlo, int rhi) {
-        std::vector<int> idx;
+    parallel_chunks(n, 256, [&](int rlo, int rhi) {
+        std::vector<unsigned long long> key;   // column << 32 | position: a stable sort by column
         for (int r = rlo; r < rhi; ++r) {
             const int cut[3] = {rp[r], seg ? seg[r] : rp[r + 1], rp[r + 1]};
             for (int part = 0; part < 2; ++part) {
                 const int a = cut[part], e = cut[part + 1];
-                idx.resize((size_t)std::max(0, e - a));
-                for (int t = 0; t < e - a; ++t) idx[t] = a + t;
-                std::stable_sort(idx.begin(), idx.end(), [&](int p, int q) { return h.col_idx[p] < h.col_idx[q]; });
-                for (int t = 0; t < e - a; ++t) ci[(size_t)a + t] = h.col_idx[idx[t]], v[(size_t)a + t] = h.val[idx[t]];
+                key.resize((size_t)std::max(0, e - a));
+                for (int t = 0; t < e - a; ++t) key[t] = (unsigned long long)(unsigned)h.col_idx[a + t] << 32 | (unsigned)t;
+                std::sort(key.begin(), key.end());
+                for (int t = 0; t < e - a; ++t) {
+                    const int k = a + (int)(unsigned)key[t];
+                    ci[(size_t)a + t] = h.col_idx[k], v[(size_t)a + t] = h.val[k];
+                }
             }
         }
     });
@@ -215,8 +365,8 @@ static void sort_row_segments(const SSS_MAT &h, const int *seg, std::vector<int>
 // Merged row groups of a free-order matrix: group g = rows [gG, gG + G); its entries keep their CSR
 // span [rp[gG], rp[gG + G]), sorted by (column, segment, row); segment 1 = [seg[r], rp[r+1]) of a
 // two-segment row.
-static void build_merged(const SSS_MAT &h, const int *seg, int G, std::vector<int> &gp, std::vector<unsigned> &mk,
-                         std::vector<double> &mv)
+static void build_merged(const SSS_MAT &h, const int *seg, int G, std::vector<int> &gp, HostBuf<unsigned> &mk,
+                         HostBuf<double> &mv)
 {
     const int n = h.num_rows, ng = (n + G - 1) / G;
     const int *rp = h.row_ptr, *ci = h.col_idx;
@@ -270,7 +420,7 @@ DevDict devdict(const DevCSR &A, int blo)
 // col - row and the distinct value bit patterns, each at most 256 (false when a block has more);
 // the codes of each staging segment (the block, or a kTileEntries chunk of a longer row) in
 // column order.
-static bool build_dict_tiles(const SSS_MAT &h, const std::vector<int> &blk, std::vector<unsigned> &code,
+static bool build_dict_tiles(const SSS_MAT &h, const std::vector<int> &blk, HostBuf<unsigned> &code,
                              std::vector<int4> &pd, std::vector<int> &dd, std::vector<double> &vd)
 {
     const int *rp = h.row_ptr, *ci = h.col_idx;
@@ -282,41 +432,41 @@ static bool build_dict_tiles(const SSS_MAT &h, const std::vector<int> &blk, std:
     code.resize((size_t)h.num_nnzs);
     std::atomic<int> ok{1};
     parallel_chunks(nb, 256, [&](int qlo, int qhi) {
-        std::vector<int> idx;
-        std::vector<int> rowof, di;
-        std::vector<int> vi;
+        std::unique_ptr<SmallDict> Dd(new SmallDict()), Vd(new SmallDict());
+        std::vector<unsigned long long> key;
+        std::vector<int> rowof;
+        std::vector<unsigned char> did, vid;   // entry -> local dictionary ids
         for (int q = qlo; q < qhi && ok; ++q) {
-            auto &D = bd[q];
-            auto &V = bv[q];
             const int a0 = rp[blk[q]], e0 = rp[blk[q + 1]];
             rowof.resize((size_t)(e0 - a0));
+            did.resize((size_t)(e0 - a0));
+            vid.resize((size_t)(e0 - a0));
+            Dd->clear();
+            Vd->clear();
             for (int r = blk[q]; r < blk[q + 1]; ++r)
                 for (int k = rp[r]; k < rp[r + 1]; ++k) {
                     rowof[(size_t)(k - a0)] = r;
-                    D.push_back(ci[k] - r);
-                    unsigned long long u;
-                    std::memcpy(&u, &v[k], sizeof(u));
-                    V.push_back(u);
+                    const int di = Dd->insert((unsigned long long)(long long)(ci[k] - r), 256);
+                    const int vi = Vd->insert(bits_of(v[k]), 256);
+                    if (di < 0 || vi < 0) {
+                        ok = 0;
+                        return;
+                    }
+                    did[(size_t)(k - a0)] = (unsigned char)di;
+                    vid[(size_t)(k - a0)] = (unsigned char)vi;
                 }
-            std::sort(D.begin(), D.end());
-            D.erase(std::unique(D.begin(), D.end()), D.end());
-            std::sort(V.begin(), V.end());
-            V.erase(std::unique(V.begin(), V.end()), V.end());
-            if (D.size() > 256 || V.size() > 256) {
-                ok = 0;
-                return;
-            }
+            std::vector<long long> ds;
+            Dd->finish(ds);
+            Vd->finish(bv[q]);
+            bd[q].assign(ds.begin(), ds.end());
             for (int a = a0; a < e0; a += kTileEntries) {   // staging segments, column-sorted
                 const int e = std::min(e0, a + kTileEntries);
-                idx.resize((size_t)(e - a));
-                for (int t = 0; t < e - a; ++t) idx[t] = a + t;
-                std::stable_sort(idx.begin(), idx.end(), [&](int x, int y) { return ci[x] < ci[y]; });
+                key.resize((size_t)(e - a));
+                for (int k = a; k < e; ++k) key[(size_t)(k - a)] = (unsigned long long)(unsigned)ci[k] << 32 | (unsigned)(k - a);
+                std::sort(key.begin(), key.end());
                 for (int t = 0; t < e - a; ++t) {
-                    const int k = idx[t], r = rowof[(size_t)(k - a0)];
-                    unsigned long long u;
-                    std::memcpy(&u, &v[k], sizeof(u));
-                    const unsigned dix = (unsigned)(std::lower_bound(D.begin(), D.end(), ci[k] - r) - D.begin());
-                    const unsigned vix = (unsigned)(std::lower_bound(V.begin(), V.end(), u) - V.begin());
+                    const int k = a + (int)(unsigned)key[t];
+                    const unsigned dix = Dd->rk[did[(size_t)(k - a0)]], vix = Vd->rk[vid[(size_t)(k - a0)]];
                     code[(size_t)a + t] = vix << (kTileShift + 8) | dix << kTileShift | (unsigned)(k - a);
                 }
             }
@@ -334,15 +484,15 @@ static bool build_dict_tiles(const SSS_MAT &h, const std::vector<int> &blk, std:
     vd.resize(std::max<size_t>(nv, 1));
     for (int q = 0; q < nb; ++q) {
         std::copy(bd[q].begin(), bd[q].end(), dd.begin() + pd[q].x);
-        for (size_t t = 0; t < bv[q].size(); ++t) std::memcpy(&vd[(size_t)pd[q].z + t], &bv[q][t], sizeof(double));
+        for (size_t t = 0; t < bv[q].size(); ++t) vd[(size_t)pd[q].z + t] = double_of(bv[q][t]);
     }
     return true;
 }
 
 // Value dictionaries over the sorted tiles' values pv (slot order): per block at most 256 distinct
 // bit patterns (false when a block has more), vi = each slot's index; pd[block] = {0, 0, base, count}.
-static bool build_value_dict(const std::vector<int> &blk, const int *rp, const std::vector<double> &pv,
-                             std::vector<unsigned char> &vi, std::vector<int4> &pd, std::vector<double> &vd)
+static bool build_value_dict(const std::vector<int> &blk, const int *rp, const HostBuf<double> &pv,
+                             HostBuf<unsigned char> &vi, std::vector<int4> &pd, std::vector<double> &vd)
 {
     const int nb = (int)blk.size() - 1;
     if (nb <= 0) return false;
@@ -350,22 +500,20 @@ static bool build_value_dict(const std::vector<int> &blk, const int *rp, const s
     vi.resize(pv.size());
     std::atomic<int> ok{1};
     parallel_chunks(nb, 256, [&](int qlo, int qhi) {
+        std::unique_ptr<SmallDict> Vd(new SmallDict());
         for (int q = qlo; q < qhi && ok; ++q) {
-            auto &V = bv[q];
             const int a0 = rp[blk[q]], e0 = rp[blk[q + 1]];
-            V.resize((size_t)(e0 - a0));
-            std::memcpy(V.data(), pv.data() + a0, sizeof(double) * (size_t)(e0 - a0));
-            std::sort(V.begin(), V.end());
-            V.erase(std::unique(V.begin(), V.end()), V.end());
-            if (V.size() > 256) {
-                ok = 0;
-                return;
-            }
+            Vd->clear();
             for (int k = a0; k < e0; ++k) {
-                unsigned long long u;
-                std::memcpy(&u, &pv[(size_t)k], sizeof(u));
-                vi[(size_t)k] = (unsigned char)(std::lower_bound(V.begin(), V.end(), u) - V.begin());
+                const int id = Vd->insert(bits_of(pv[(size_t)k]), 256);
+                if (id < 0) {
+                    ok = 0;
+                    return;
+                }
+                vi[(size_t)k] = (unsigned char)id;
             }
+            Vd->finish(bv[q]);
+            for (int k = a0; k < e0; ++k) vi[(size_t)k] = Vd->rk[vi[(size_t)k]];
         }
     });
     if (!ok) return false;
@@ -377,54 +525,64 @@ static bool build_value_dict(const std::vector<int> &blk, const int *rp, const s
     }
     vd.resize(std::max<size_t>(nv, 1));
     for (int q = 0; q < nb; ++q)
-        for (size_t t = 0; t < bv[q].size(); ++t) std::memcpy(&vd[(size_t)pd[q].z + t], &bv[q][t], sizeof(double));
+        for (size_t t = 0; t < bv[q].size(); ++t) vd[(size_t)pd[q].z + t] = double_of(bv[q][t]);
     return true;
 }
 
 // Dictionary ELL of a square matrix (DevCSR::dv_ell): every row at most 32 entries, every block at
 // most 31 distinct column offsets and 8 distinct value bit patterns (false otherwise); width W =
 // 8, 16 or 32 bytes per row, codes in stored order, 0xFF pads.
-static bool build_ell(const SSS_MAT &h, const std::vector<int> &blk, std::vector<unsigned char> &ell, int &W,
+static bool build_ell(const SSS_MAT &h, const std::vector<int> &blk, HostBuf<unsigned char> &ell, int &W,
                       std::vector<int4> &pd, std::vector<int> &dd, std::vector<double> &vd)
 {
     const int *rp = h.row_ptr, *ci = h.col_idx;
     const double *v = h.val;
     const int n = h.num_rows, nb = (int)blk.size() - 1;
     if (n != h.num_cols || nb <= 0 || n <= 0) return false;
-    int L = 0;
-    for (int r = 0; r < n; ++r) L = std::max(L, rp[r + 1] - rp[r]);
+    std::atomic<int> Lmax{0};
+    parallel_chunks(n, 1 << 16, [&](int lo, int hi) {
+        int L = 0;
+        for (int r = lo; r < hi; ++r) L = std::max(L, rp[r + 1] - rp[r]);
+        int cur = Lmax.load();
+        while (L > cur && !Lmax.compare_exchange_weak(cur, L)) {}
+    });
+    const int L = Lmax.load();
     if (L > 32) return false;
     W = L <= 8 ? 8 : L <= 16 ? 16 : 32;
-    std::vector<std::vector<int>> bd(nb);
-    std::vector<std::vector<unsigned long long>> bv(nb);
-    ell.assign((size_t)n * W, 0xff);
+    // per block at most 31 offsets and 8 values: fixed slots, compacted afterwards
+    std::vector<int> bdf((size_t)nb * 31), nd_of(nb), nv_of(nb);
+    std::vector<double> bvf((size_t)nb * 8);
+    ell.resize((size_t)n * W);
     std::atomic<int> ok{1};
     parallel_chunks(nb, 256, [&](int qlo, int qhi) {
+        std::unique_ptr<SmallDict> Dd(new SmallDict()), Vd(new SmallDict());
+        std::vector<long long> ds;
+        std::vector<unsigned long long> vs;
         for (int q = qlo; q < qhi && ok; ++q) {
-            auto &D = bd[q];
-            auto &V = bv[q];
+            Dd->clear();
+            Vd->clear();
+            unsigned char *row0 = ell.data() + (size_t)blk[q] * W;
+            std::memset(row0, 0xff, (size_t)(blk[q + 1] - blk[q]) * W);
             for (int r = blk[q]; r < blk[q + 1]; ++r)
                 for (int k = rp[r]; k < rp[r + 1]; ++k) {
-                    D.push_back(ci[k] - r);
-                    unsigned long long u;
-                    std::memcpy(&u, &v[k], sizeof(u));
-                    V.push_back(u);
-                }
-            std::sort(D.begin(), D.end());
-            D.erase(std::unique(D.begin(), D.end()), D.end());
-            std::sort(V.begin(), V.end());
-            V.erase(std::unique(V.begin(), V.end()), V.end());
-            if (D.size() > 31 || V.size() > 8) {
-                ok = 0;
-                return;
-            }
-            for (int r = blk[q]; r < blk[q + 1]; ++r)
-                for (int k = rp[r]; k < rp[r + 1]; ++k) {
-                    unsigned long long u;
-                    std::memcpy(&u, &v[k], sizeof(u));
-                    const unsigned di = (unsigned)(std::lower_bound(D.begin(), D.end(), ci[k] - r) - D.begin());
-                    const unsigned vi = (unsigned)(std::lower_bound(V.begin(), V.end(), u) - V.begin());
+                    const int di = Dd->insert((unsigned long long)(long long)(ci[k] - r), 31);
+                    const int vi = Vd->insert(bits_of(v[k]), 8);
+                    if (di < 0 || vi < 0) {
+                        ok = 0;
+                        return;
+                    }
                     ell[(size_t)r * W + (k - rp[r])] = (unsigned char)(vi << 5 | di);
+                }
+            Dd->finish(ds);
+            Vd->finish(vs);
+            nd_of[q] = (int)ds.size();
+            nv_of[q] = (int)vs.size();
+            std::copy(ds.begin(), ds.end(), bdf.begin() + (size_t)q * 31);
+            for (size_t t = 0; t < vs.size(); ++t) bvf[(size_t)q * 8 + t] = double_of(vs[t]);
+            for (int r = blk[q]; r < blk[q + 1]; ++r)
+                for (int k = 0; k < rp[r + 1] - rp[r]; ++k) {
+                    unsigned char &c = ell[(size_t)r * W + k];
+                    c = (unsigned char)(Vd->rk[c >> 5] << 5 | Dd->rk[c & 31]);
                 }
         }
     });
@@ -432,21 +590,24 @@ static bool build_ell(const SSS_MAT &h, const std::vector<int> &blk, std::vector
     pd.resize((size_t)nb);
     size_t nd = 0, nv = 0;
     for (int q = 0; q < nb; ++q) {
-        pd[q] = make_int4((int)nd, (int)bd[q].size(), (int)nv, (int)bv[q].size());
-        nd += bd[q].size();
-        nv += bv[q].size();
+        pd[q] = make_int4((int)nd, nd_of[q], (int)nv, nv_of[q]);
+        nd += nd_of[q];
+        nv += nv_of[q];
     }
     dd.resize(std::max<size_t>(nd, 1));
     vd.resize(std::max<size_t>(nv, 1));
-    for (int q = 0; q < nb; ++q) {
-        std::copy(bd[q].begin(), bd[q].end(), dd.begin() + pd[q].x);
-        for (size_t t = 0; t < bv[q].size(); ++t) std::memcpy(&vd[(size_t)pd[q].z + t], &bv[q][t], sizeof(double));
-    }
+    parallel_chunks(nb, 4096, [&](int qlo, int qhi) {
+        for (int q = qlo; q < qhi; ++q) {
+            std::copy(bdf.begin() + (size_t)q * 31, bdf.begin() + (size_t)q * 31 + nd_of[q], dd.begin() + pd[q].x);
+            std::copy(bvf.begin() + (size_t)q * 8, bvf.begin() + (size_t)q * 8 + nv_of[q], vd.begin() + pd[q].z);
+        }
+    });
     return true;
 }
 
 int devcsr_upload(DevCSR &d, const SSS_MAT &h, int split, int enc, const int *seg)
 {
+    PhaseTimer pt("devcsr");
     d.n = h.num_rows;
     d.ncols = h.num_cols;
     d.nnz = h.num_nnzs;
@@ -461,11 +622,12 @@ int devcsr_upload(DevCSR &d, const SSS_MAT &h, int split, int enc, const int *se
     d.ci = dev_alloc<int>((size_t)d.nnz);
     d.v = dev_alloc<double>((size_t)d.nnz);
     if (!d.rp || !d.ci || !d.v) return hip_fail(hipErrorOutOfMemory, "hipMalloc(CSR)", __FILE__, __LINE__);
+    pt.mark("alloc");
     if (int rc = h2d(d.rp, h.row_ptr, sizeof(int) * ((size_t)d.n + 1))) return rc;
     if (d.nnz > 0) {
         if (d.vec_rows) {
-            std::vector<int> sci;
-            std::vector<double> sv;
+            HostBuf<int> sci;
+            HostBuf<double> sv;
             sort_row_segments(h, seg, sci, sv);
             if (int rc = h2d(d.ci, sci.data(), sizeof(int) * (size_t)d.nnz)) return rc;
             if (int rc = h2d(d.v, sv.data(), sizeof(double) * (size_t)d.nnz)) return rc;
@@ -474,6 +636,7 @@ int devcsr_upload(DevCSR &d, const SSS_MAT &h, int split, int enc, const int *se
             if (int rc = h2d(d.v, h.val, sizeof(double) * (size_t)d.nnz)) return rc;
         }
     }
+    pt.mark("csr");
     std::vector<int> blk;
     d.nblk = build_row_blocks(h.row_ptr, d.n, blk, split);
     d.split_blk = d.nblk;
@@ -486,10 +649,11 @@ int devcsr_upload(DevCSR &d, const SSS_MAT &h, int split, int enc, const int *se
     if (int rc = h2d(d.blk, blk.data(), sizeof(int) * blk.size())) return rc;
     if (int rc = upload_block_bounds(&d.bk, blk, h.row_ptr)) return rc;
     d.ngrid = (d.wave_rows || d.vec_rows) ? (d.n + 3) / 4 : d.nblk;
+    pt.mark("blocks");
     if (d.mg_G > 0) {
         std::vector<int> gp;
-        std::vector<unsigned> mk;
-        std::vector<double> mv;
+        HostBuf<unsigned> mk;
+        HostBuf<double> mv;
         build_merged(h, seg, d.mg_G, gp, mk, mv);
         d.mg_two = seg != nullptr;
         d.mg_ng = (int)gp.size() - 1;
@@ -507,12 +671,13 @@ int devcsr_upload(DevCSR &d, const SSS_MAT &h, int split, int enc, const int *se
         if (int rc = h2d(d.mg_k, mk.data(), sizeof(unsigned) * mk.size())) return rc;
         if (int rc = h2d(d.mg_v, mv.data(), sizeof(double) * mv.size())) return rc;
     }
+    pt.mark("merged");
     // dictionary ELL first (one thread per row), else dictionary tiles (the tile kernels then stage
     // from them instead of the sorted copy)
     const char *dz = getenv("SSS_HIP_DICT");   // 0: never (tests compare both ways)
     const char *ez = getenv("SSS_HIP_ELL");    // 0: no ELL (dictionary tiles where they qualify)
     if ((enc & kEncDict) && !(dz && *dz == '0') && !(ez && *ez == '0') && !d.wave_rows && !d.vec_rows && d.nnz > 0) {
-        std::vector<unsigned char> ell;
+        HostBuf<unsigned char> ell;
         std::vector<int4> pd;
         std::vector<int> dd;
         std::vector<double> vd;
@@ -533,8 +698,9 @@ int devcsr_upload(DevCSR &d, const SSS_MAT &h, int split, int enc, const int *se
             if (int rc = h2d(d.dv_vd, vd.data(), sizeof(double) * vd.size())) return rc;
         }
     }
+    pt.mark("ell");
     if ((enc & kEncDict) && !(dz && *dz == '0') && !d.dv_ell && !d.wave_rows && !d.vec_rows && d.nnz > 0) {
-        std::vector<unsigned> code;
+        HostBuf<unsigned> code;
         std::vector<int4> pd;
         std::vector<int> dd;
         std::vector<double> vd;
@@ -551,9 +717,10 @@ int devcsr_upload(DevCSR &d, const SSS_MAT &h, int split, int enc, const int *se
             if (int rc = h2d(d.dv_vd, vd.data(), sizeof(double) * vd.size())) return rc;
         }
     }
+    pt.mark("dict");
     // the tile kernels of a wave-path matrix never run on the hierarchy; no sorted copy for them
-    std::vector<unsigned> pk;
-    std::vector<double> pv;
+    HostBuf<unsigned> pk;
+    HostBuf<double> pv;
     std::vector<int2> pb;
     if ((enc & kEncSortedTiles) && !d.dv_code && !d.dv_ell && !d.wave_rows && !d.vec_rows && d.nnz > 0 &&
         build_sorted_tiles(h, blk, pk, pv, pb)) {
@@ -562,7 +729,8 @@ int devcsr_upload(DevCSR &d, const SSS_MAT &h, int split, int enc, const int *se
         if (!d.pk || !d.pb) return hip_fail(hipErrorOutOfMemory, "hipMalloc(sorted tiles)", __FILE__, __LINE__);
         if (int rc = h2d(d.pk, pk.data(), sizeof(unsigned) * (size_t)d.nnz)) return rc;
         if (int rc = h2d(d.pb, pb.data(), sizeof(int2) * pb.size())) return rc;
-        std::vector<unsigned char> vi;
+        pt.mark("sorted");
+        HostBuf<unsigned char> vi;
         std::vector<int4> pd;
         std::vector<double> vd;
         if ((enc & kEncDict) && !(dz && *dz == '0') && build_value_dict(blk, h.row_ptr, pv, vi, pd, vd)) {
@@ -580,6 +748,7 @@ int devcsr_upload(DevCSR &d, const SSS_MAT &h, int split, int enc, const int *se
             if (int rc = h2d(d.pv, pv.data(), sizeof(double) * (size_t)d.nnz)) return rc;
         }
     }
+    pt.mark("tiles");
     // what one SpMV over the stored format reads besides the vectors (reported for the roofline)
     const long long nnz = d.nnz, nb = d.nblk, rows = d.n;
     if (has_dict(d)) {

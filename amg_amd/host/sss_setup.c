@@ -116,68 +116,88 @@ static int drop_weak(SSS_IMAT *S)
 }
 
 /* ======================================================================================
- * Measure buckets.  bucket_first/last[m] play the role of the reference list node with
- * data == m (node->head / node->tail); next/prev are the reference's lists/where arrays.
+ * Measure buckets.  The reference keeps one doubly linked list per measure (SSS_coarsen.c
+ * lists/where + list nodes): inserts append at the tail, the next C point is the head of the
+ * largest non-empty list -- i.e. among the points of maximal measure, the one inserted
+ * earliest.  Here each bucket is an append-only FIFO array of (point, version) entries and a
+ * removal only bumps the point's version (its entry goes stale and is skipped when it reaches
+ * the head).  Same head, same order of picks, but a move is two sequential writes instead of
+ * four dependent pointer updates scattered over the grid (the serial first pass is
+ * memory-latency bound).  Buckets are compacted in place (order kept) when most of their
+ * entries are stale.
  * ====================================================================================== */
 typedef struct {
-    int *first, *last;   /* per measure; first == LIST_TAIL marks an absent bucket */
-    int cap;             /* allocated measures */
-    int top;             /* upper bound on the largest non-empty measure */
-    int *next, *prev;    /* per point: successor / predecessor inside its bucket */
+    int pt;
+    unsigned ver;
+} bucket_entry;
+
+typedef struct {
+    bucket_entry *e;
+    size_t head, tail, cap;
+    int live;                /* live entries = points in this bucket */
+} bucket_fifo;
+
+typedef struct {
+    bucket_fifo *b;          /* per measure */
+    int cap;                 /* allocated measures */
+    int top;                 /* upper bound on the largest non-empty measure */
+    unsigned *ver;           /* per point: current version (an entry is live iff it matches) */
 } measure_buckets;
 
 static void buckets_grow(measure_buckets *B, int m)
 {
     int old = B->cap, cap = B->cap;
     while (cap <= m) cap = cap * 2 + 16;
-    B->first = (int *)realloc(B->first, sizeof(int) * (size_t)cap);
-    B->last = (int *)realloc(B->last, sizeof(int) * (size_t)cap);
-    for (int k = old; k < cap; ++k) B->first[k] = B->last[k] = LIST_TAIL;
+    B->b = (bucket_fifo *)realloc(B->b, sizeof(bucket_fifo) * (size_t)cap);
+    memset(B->b + old, 0, sizeof(bucket_fifo) * (size_t)(cap - old));
     B->cap = cap;
 }
 
-static void bucket_insert(measure_buckets *B, int m, int pt)
+static void bucket_compact(bucket_fifo *q, const unsigned *ver)
+{
+    size_t o = 0;
+    for (size_t k = q->head; k < q->tail; ++k)
+        if (q->e[k].ver == ver[q->e[k].pt]) q->e[o++] = q->e[k];
+    q->head = 0;
+    q->tail = o;
+}
+
+static inline void bucket_insert(measure_buckets *B, int m, int pt)
 {
     if (m >= B->cap) buckets_grow(B, m);
-    if (B->first[m] == LIST_TAIL) {               /* new bucket: point is alone */
-        B->first[m] = B->last[m] = pt;
-        B->next[pt] = LIST_TAIL;
-        B->prev[pt] = LIST_HEAD;
-    } else {                                      /* append at the bucket tail */
-        int t = B->last[m];
-        B->next[t] = pt;
-        B->prev[pt] = t;
-        B->next[pt] = LIST_TAIL;
-        B->last[m] = pt;
+    bucket_fifo *q = &B->b[m];
+    if (q->tail == q->cap) {
+        if (q->tail - q->head > 2 * (size_t)q->live + 64 || q->head > q->cap / 2) bucket_compact(q, B->ver);
+        if (q->tail == q->cap) {
+            q->cap = q->cap * 2 + 256;
+            q->e = (bucket_entry *)realloc(q->e, sizeof(bucket_entry) * q->cap);
+        }
     }
+    q->e[q->tail].pt = pt;
+    q->e[q->tail].ver = ++B->ver[pt];
+    q->tail++;
+    q->live++;
     if (m > B->top) B->top = m;
 }
 
-static void bucket_remove(measure_buckets *B, int m, int pt)
+static inline void bucket_remove(measure_buckets *B, int m, int pt)
 {
-    if (m < 0 || m >= B->cap || B->first[m] == LIST_TAIL) {
+    if (m < 0 || m >= B->cap || B->b[m].live == 0) {
         printf("### ERROR: This list is empty! %s : %d\n", __FILE__, __LINE__);
         return;
     }
-    if (B->first[m] == pt && B->last[m] == pt) {
-        B->first[m] = B->last[m] = LIST_TAIL;
-    } else if (B->first[m] == pt) {
-        B->first[m] = B->next[pt];
-        B->prev[B->next[pt]] = LIST_HEAD;
-    } else if (B->last[m] == pt) {
-        B->last[m] = B->prev[pt];
-        B->next[B->prev[pt]] = LIST_TAIL;
-    } else {
-        B->next[B->prev[pt]] = B->next[pt];
-        B->prev[B->next[pt]] = B->prev[pt];
-    }
+    B->ver[pt]++;
+    if (--B->b[m].live == 0) B->b[m].head = B->b[m].tail = 0;
 }
 
 /* Head point of the largest non-empty bucket, or -1 if every bucket is empty. */
 static int bucket_max_head(measure_buckets *B)
 {
-    while (B->top > 0 && B->first[B->top] == LIST_TAIL) B->top--;
-    return (B->top > 0 && B->first[B->top] != LIST_TAIL) ? B->first[B->top] : -1;
+    while (B->top > 0 && B->b[B->top].live == 0) B->top--;
+    if (B->top <= 0) return -1;
+    bucket_fifo *q = &B->b[B->top];
+    while (q->e[q->head].ver != B->ver[q->e[q->head].pt]) q->head++;
+    return q->e[q->head].pt;
 }
 
 /* Classical Ruge-Stueben first pass + C1 fix-up.  Returns the C-point count (or <0). */
@@ -198,8 +218,7 @@ static int rs_split(const SSS_MAT *A, SSS_IMAT *S, SSS_IVEC *vertices)
     const double t1 = SSS_get_time();
 
     memset(&B, 0, sizeof(B));
-    B.next = (int *)SSS_calloc((size_t)n, sizeof(int));
-    B.prev = (int *)SSS_calloc((size_t)n, sizeof(int));
+    B.ver = (unsigned *)SSS_calloc((size_t)n, sizeof(unsigned));
     lambda = (int *)SSS_calloc((size_t)n, sizeof(int));
     buckets_grow(&B, 64);
 
@@ -324,10 +343,9 @@ static int rs_split(const SSS_MAT *A, SSS_IMAT *S, SSS_IVEC *vertices)
         fprintf(stderr, "[setup]   RS split: drop+transpose %.3f s, lists %.3f s, first pass %.3f s, C1 %.3f s\n",
                 t1 - t0, t2 - t1, t3 - t2, SSS_get_time() - t3);
     SSS_imat_destroy(&ST);
-    free(B.first);
-    free(B.last);
-    free(B.next);
-    free(B.prev);
+    for (int m = 0; m < B.cap; ++m) free(B.b[m].e);
+    free(B.b);
+    free(B.ver);
     free(lambda);
     return ncoarse;
 }
