@@ -106,6 +106,7 @@ ABI_SYMBOLS = [
     "SSS_amg_setup", "SSS_amg_coarsen", "SSS_amg_interp", "SSS_amg_interp_trunc", "interp_DIR", "SSS_mat_read",
     "SSS_amg_pars_init", "SSS_amg_pars_print", "mmio_info", "mmio_data",
     "sss_hip_opts_default", "sss_hip_device_count", "sss_hip_hier_create", "sss_hip_hier_destroy",
+    "sss_hip_setup_create", "sss_amg_setup_hooked",
     "sss_hip_upload_vec", "sss_hip_download_vec", "sss_hip_cycle", "sss_hip_residual_norm", "sss_hip_pcg",
     "SSS_amg_save", "SSS_amg_load",
     "sss_hip_coarse_solve", "sss_hip_smooth", "sss_hip_sync", "sss_hip_level_info_get", "sss_hip_num_levels",
@@ -173,6 +174,8 @@ def _declare(lib):
         "sss_hip_opts_default": (None, [P(SSS_HIP_OPTS)]),
         "sss_hip_device_count": (C.c_int, []),
         "sss_hip_hier_create": (C.c_void_p, [P(SSS_AMG), P(SSS_HIP_OPTS)]),
+        "sss_hip_setup_create": (C.c_void_p, [P(SSS_AMG), P(SSS_MAT), P(SSS_AMG_PARS), P(SSS_HIP_OPTS),
+                                              P(C.c_double)]),
         "sss_hip_hier_destroy": (None, [C.c_void_p]),
         "sss_hip_upload_vec": (C.c_int, [C.c_void_p, C.c_int, C.c_int, _dbl_p, C.c_int]),
         "sss_hip_download_vec": (C.c_int, [C.c_void_p, C.c_int, C.c_int, _dbl_p, C.c_int]),
@@ -336,10 +339,13 @@ class Hierarchy:
 class DeviceHierarchy:
     """HBM mirror of a Hierarchy (sss_hip_hier_create)."""
 
-    def __init__(self, H: Hierarchy, smoother: str = "exact", coarse: str = "krylov", row_cap: int = 0,
+    def __init__(self, H: Hierarchy | None, smoother: str = "exact", coarse: str = "krylov", row_cap: int = 0,
                  device: int = -1, verbose: int = 0, relabel: int | None = None, graph: int | None = None,
                  inner: int | None = None, inner_from: int | None = None, sorted_tiles: int | None = None,
-                 sum_order: int | None = None):
+                 sum_order: int | None = None, setup_from: SSS_MAT | None = None):
+        """setup_from: build the Hierarchy from this operator here, with the levels uploaded while
+        the setup is still running (sss_hip_setup_create); H must then be None and self.H is the
+        new Hierarchy.  self.times = (setup s, mirror s after the setup, of which waiting)."""
         o = SSS_HIP_OPTS()
         lib().sss_hip_opts_default(C.byref(o))
         o.smoother, o.coarse, o.row_cap, o.device, o.verbose = SMOOTH[smoother], COARSE[coarse], row_cap, device, verbose
@@ -355,6 +361,17 @@ class DeviceHierarchy:
             o.inner = inner
         if inner_from is not None:
             o.inner_from = inner_from
+        if setup_from is not None:
+            if H is not None:
+                raise ValueError("setup_from builds its own Hierarchy: pass H=None")
+            H = Hierarchy(None)
+            t = (C.c_double * 3)()
+            self.H = H
+            self.h = lib().sss_hip_setup_create(C.byref(H.mg), C.byref(setup_from), C.byref(H.pars), C.byref(o), t)
+            self.times = tuple(t)
+            if not self.h:
+                raise RuntimeError("sss_hip_setup_create failed (no HIP device or out of memory)")
+            return
         self.H = H
         self.h = lib().sss_hip_hier_create(C.byref(H.mg), C.byref(o))
         if not self.h:

@@ -71,6 +71,7 @@ struct HostBuf {
 // (h2d alone issued one loop per 32 MiB chunk).  One job at a time; a loop issued from a worker,
 // or while another thread holds the pool, runs inline on its caller.
 int host_pool_threads();
+void host_thread_background();   // lower the calling thread's CPU priority (SSS_HOST_NICE)
 bool host_pool_run(const std::function<void()> &work);   // false: pool busy (caller runs inline)
 
 // Host-side data preparation at upload: fn(lo, hi) over [0, n) in chunks of `grain` items taken
@@ -130,6 +131,33 @@ struct PhaseTimer {
         fprintf(stderr, "[sss_hip]     %s:%s\n", what, s.c_str());
     }
 };
+
+// In-place prefix sum of a[1..n] (a[0] given): a[i + 1] += a[i] over chunks on the pool.
+inline void parallel_prefix(int *a, int n)
+{
+    constexpr int kC = 1 << 16;
+    const int nc = (n + kC - 1) / kC;
+    if (nc <= 1) {
+        for (int i = 0; i < n; ++i) a[i + 1] += a[i];
+        return;
+    }
+    std::vector<long long> tot((size_t)nc + 1, 0);
+    parallel_chunks(nc, 1, [&](int c0, int c1) {
+        for (int c = c0; c < c1; ++c) {
+            long long t = 0;
+            for (int i = c * kC; i < std::min(n, (c + 1) * kC); ++i) t += a[i + 1];
+            tot[(size_t)c + 1] = t;
+        }
+    });
+    tot[0] = a[0];
+    for (int c = 0; c < nc; ++c) tot[(size_t)c + 1] += tot[c];
+    parallel_chunks(nc, 1, [&](int c0, int c1) {
+        for (int c = c0; c < c1; ++c) {
+            long long run = tot[c];
+            for (int i = c * kC; i < std::min(n, (c + 1) * kC); ++i) run += a[i + 1], a[i + 1] = (int)run;
+        }
+    });
+}
 
 // Host -> device copy through pinned staging buffers (sss_spmv.hip); returns 0 or an error code.
 int h2d(void *dst, const void *src, size_t bytes);

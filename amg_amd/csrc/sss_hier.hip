@@ -11,6 +11,10 @@
 // norm is the only per-iteration device->host transfer.
 #include "sss_engine.hpp"
 
+#include <condition_variable>
+#include <mutex>
+#include <thread>
+
 #include <chrono>
 
 #include <cmath>
@@ -217,7 +221,7 @@ static void hier_release(sss_hip_hier *h)
 // is the memory layout: every smoother pass is a contiguous row range of the level matrix, the
 // x values it gathers (the other class) are contiguous too, and it writes a dense half of x.
 struct RelabeledCSR {   // owns the arrays an SSS_MAT view points into
-    std::vector<int> rp;
+    HostBuf<int> rp;
     HostBuf<int> ci;
     HostBuf<double> v;
     SSS_MAT view(int nrows, int ncols)
@@ -238,11 +242,15 @@ struct RelabeledCSR {   // owns the arrays an SSS_MAT view points into
 static void relabel_csr(const SSS_MAT &A, const std::vector<int> &rperm, const std::vector<int> &cinv, RelabeledCSR &B)
 {
     const int n = A.num_rows;
-    B.rp.assign((size_t)n + 1, 0);
-    for (int i = 0; i < n; ++i) {
-        const int o = rperm.empty() ? i : rperm[i];
-        B.rp[i + 1] = B.rp[i] + (A.row_ptr[o + 1] - A.row_ptr[o]);
-    }
+    B.rp.resize((size_t)n + 1);
+    B.rp[0] = 0;
+    parallel_chunks(n, 1 << 16, [&](int lo, int hi) {
+        for (int i = lo; i < hi; ++i) {
+            const int o = rperm.empty() ? i : rperm[i];
+            B.rp[(size_t)i + 1] = A.row_ptr[o + 1] - A.row_ptr[o];
+        }
+    });
+    parallel_prefix(B.rp.data(), n);
     B.ci.resize((size_t)B.rp[n]);
     B.v.resize((size_t)B.rp[n]);
     parallel_chunks(n, 1 << 15, [&](int lo, int hi) {
@@ -257,120 +265,174 @@ static void relabel_csr(const SSS_MAT &A, const std::vector<int> &rperm, const s
     });
 }
 
-sss_hip_hier *sss::hier_create_impl(const SSS_AMG *mg, const sss_hip_opts *o, int level_base, hipStream_t stream)
+// ---- construction ---------------------------------------------------------------------------
+// The mirror is built level by level: begin (stream, events), then per level the relabeling, A_l
+// with its smoother plan, and P_l / R_l (which need the next level's relabeling), then finish
+// (coarse solver, graph decision).  hier_create_impl runs the steps back to back;
+// sss_hip_setup_create runs them on a worker thread while SSS_amg_setup is still coarsening the
+// later levels (a level is handed over once the setup has moved past it).
+struct HierBuild {
+    sss_hip_hier *h = nullptr;
+    const SSS_AMG *mg = nullptr;
+    std::vector<std::vector<int>> inv = std::vector<std::vector<int>>(kMaxLevels);
+    std::vector<int> nF = std::vector<int>(kMaxLevels, -1);
+    const char *err = nullptr;
+    bool timing = getenv("SSS_HIP_TIMING") != nullptr;   // per-level upload phases on stderr
+};
+
+static bool hb_fail(HierBuild &b, const char *what)
+{
+    if (!b.err) b.err = what;
+    return false;
+}
+
+static bool hb_begin(HierBuild &b, const SSS_AMG *mg, const sss_hip_opts *o, int level_base, hipStream_t stream)
 {
     if (sss_hip_device_count() <= 0) {
         fprintf(stderr, "### ERROR: no HIP device available for the AMG solve phase\n");
-        return nullptr;
+        return false;
     }
-    auto *h = new sss_hip_hier();
-    h->nl = mg->num_levels;
+    auto *h = b.h = new sss_hip_hier();
+    b.mg = mg;
+    h->nl = 0;
     h->pars = mg->pars;
     if (o) h->opts = *o;
     else sss_hip_opts_default(&h->opts);
-    if (h->opts.device >= 0 && hipSetDevice(h->opts.device) != hipSuccess) { delete h; return nullptr; }
-    auto fail = [&](const char *what) {
-        fprintf(stderr, "### ERROR: sss_hip_hier_create: %s\n", what);
-        hier_release(h);
-        return (sss_hip_hier *)nullptr;
-    };
+    if (h->opts.device >= 0 && hipSetDevice(h->opts.device) != hipSuccess) return hb_fail(b, "device");
     h->level_base = level_base;
     if (stream) {
         h->stream = stream;
         h->own_stream = false;
     } else if (hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess) {
-        return fail("stream");
+        return hb_fail(b, "stream");
     }
-    if (hipEventCreate(&h->ev0) != hipSuccess || hipEventCreate(&h->ev1) != hipSuccess) return fail("events");
+    if (hipEventCreate(&h->ev0) != hipSuccess || hipEventCreate(&h->ev1) != hipSuccess) return hb_fail(b, "events");
+    return true;
+}
 
+// F|C relabeling of a level that is not the coarsest (the coarsest keeps the identity)
+static void hb_perm(HierBuild &b, int l)
+{
+    sss_hip_hier *h = b.h;
+    const SSS_AMG *mg = b.mg;
     // hybrid: exact GS-CF on level 0 only where it is chain-free (its cost is then that of
     // C/F-Jacobi); a level 0 with same-class couplings (27-pt, irregular operators) would run the
     // level-scheduled chains every sweep -- there the two-stage form takes its place
-    if (h->opts.smoother == SSS_HIP_SMOOTH_HYBRID && level_base == 0 && h->nl > 1 && mg->cg[0].cfmark.d &&
+    if (l == 0 && h->opts.smoother == SSS_HIP_SMOOTH_HYBRID && h->level_base == 0 && mg->cg[0].cfmark.d &&
         mg->cg[0].cfmark.n >= mg->cg[0].A.num_rows && mg->pars.cf_order != 0)
         h->hybrid0_two_stage = !classes_independent(mg->cg[0].A, mg->cg[0].cfmark.d);
+    const SSS_AMG_COMP &C = mg->cg[l];
+    const int n = C.A.num_rows;
+    if (!C.cfmark.d || C.cfmark.n < n) return;
+    // two-stage levels need contiguous classes; otherwise follow opts.relabel
+    const int gl = h->level_base + l;
+    const bool two_stage = hier_inner(h, gl) > 0;
+    if (natural_level(h, gl)) return;   // the natural order is the stored row order
+    if (!two_stage && !(h->opts.relabel == 1 || (h->opts.relabel == 2 && gl > 0))) return;
+    auto &perm = h->L[l].perm;
+    perm.reserve(n);
+    for (int i = 0; i < n; ++i)
+        if (C.cfmark.d[i] != 1) perm.push_back(i);
+    b.nF[l] = (int)perm.size();
+    for (int i = 0; i < n; ++i)
+        if (C.cfmark.d[i] == 1) perm.push_back(i);
+    b.inv[l].resize(n);
+    auto &iv = b.inv[l];
+    parallel_chunks(n, 1 << 16, [&](int lo, int hi) {
+        for (int i = lo; i < hi; ++i) iv[perm[i]] = i;
+    });
+}
 
-    // F|C relabeling of every level but the coarsest (identity there)
-    std::vector<std::vector<int>> inv(h->nl);
-    std::vector<int> nF(h->nl, -1);
-    for (int l = 0; l + 1 < h->nl; ++l) {
-            const SSS_AMG_COMP &C = mg->cg[l];
-            const int n = C.A.num_rows;
-            if (!C.cfmark.d || C.cfmark.n < n) continue;
-            // two-stage levels need contiguous classes; otherwise follow opts.relabel
-            const int gl = h->level_base + l;
-            const bool two_stage = hier_inner(h, gl) > 0;
-            if (natural_level(h, gl)) continue;   // the natural order is the stored row order
-            if (!two_stage && !(h->opts.relabel == 1 || (h->opts.relabel == 2 && gl > 0))) continue;
-            auto &perm = h->L[l].perm;
-            perm.reserve(n);
-            for (int i = 0; i < n; ++i)
-                if (C.cfmark.d[i] != 1) perm.push_back(i);
-            nF[l] = (int)perm.size();
-            for (int i = 0; i < n; ++i)
-                if (C.cfmark.d[i] == 1) perm.push_back(i);
-            inv[l].resize(n);
-            for (int i = 0; i < n; ++i) inv[l][perm[i]] = i;
+// A_l (+ its smoother plan unless coarsest) and the level vectors
+static bool hb_level_a(HierBuild &b, int l, bool coarsest)
+{
+    sss_hip_hier *h = b.h;
+    const SSS_AMG_COMP &C = b.mg->cg[l];
+    auto &L = h->L[l];
+    const int n = C.A.num_rows;
+    const bool rl = !L.perm.empty();
+    const double t_a = PhaseTimer::now();
+    double t_rel = t_a, t_up = t_a, t_sm = t_a;
+    // the coarsest operator only feeds the coarse solver: stored order there
+    const int enc = !coarsest ? level_encoding(h->opts) : (level_encoding(h->opts) & kEncSortedTiles);
+    if (rl) {
+        RelabeledCSR B;
+        relabel_csr(C.A, L.perm, b.inv[l], B);
+        SSS_MAT Av = B.view(n, C.A.num_cols);
+        t_rel = PhaseTimer::now();
+        if (devcsr_upload(L.A, Av, b.nF[l], enc)) return hb_fail(b, "upload A");
+        t_up = PhaseTimer::now();
+        std::vector<int> mark(n);
+        for (int i = 0; i < n; ++i) mark[i] = C.cfmark.d[L.perm[i]];
+        if (smoother_build(L.sm, Av, mark.data(), hier_kind(h, h->level_base + l), &L.A,
+                           hier_inner(h, h->level_base + l), nullptr, enc))
+            return hb_fail(b, "smoother plan");
+        t_sm = PhaseTimer::now();
+    } else {
+        if (devcsr_upload(L.A, C.A, -1, enc)) return hb_fail(b, "upload A");
+        if (!coarsest && natural_level(h, h->level_base + l)) {
+            if (smoother_build_natural(L.sm, C.A, 0, n)) return hb_fail(b, "smoother plan");
+        } else if (!coarsest && smoother_build(L.sm, C.A, C.cfmark.d, hier_kind(h, h->level_base + l), nullptr, 0,
+                                               nullptr, enc)) {
+            return hb_fail(b, "smoother plan");
         }
-
-    const bool timing = getenv("SSS_HIP_TIMING") != nullptr;   // per-level upload phases on stderr
-    auto now = [] { return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count(); };
-    for (int l = 0; l < h->nl; ++l) {
-        const SSS_AMG_COMP &C = mg->cg[l];
-        auto &L = h->L[l];
-        const int n = C.A.num_rows;
-        const bool rl = !L.perm.empty();
-        double t_a = now(), t_rel = 0, t_up = 0, t_sm = 0;
-        // the coarsest operator only feeds the coarse solver: stored order there
-        const int enc = l + 1 < h->nl ? level_encoding(h->opts) : (level_encoding(h->opts) & kEncSortedTiles);
-        if (rl) {
-            RelabeledCSR B;
-            relabel_csr(C.A, L.perm, inv[l], B);
-            SSS_MAT Av = B.view(n, C.A.num_cols);
-            t_rel = now();
-            if (devcsr_upload(L.A, Av, nF[l], enc)) return fail("upload A");
-            t_up = now();
-            std::vector<int> mark(n);
-            for (int i = 0; i < n; ++i) mark[i] = C.cfmark.d[L.perm[i]];
-            if (smoother_build(L.sm, Av, mark.data(), hier_kind(h, h->level_base + l), &L.A,
-                               hier_inner(h, h->level_base + l), nullptr, enc))
-                return fail("smoother plan");
-            t_sm = now();
-        } else {
-            if (devcsr_upload(L.A, C.A, -1, enc)) return fail("upload A");
-            if (l < h->nl - 1 && natural_level(h, h->level_base + l)) {
-                if (smoother_build_natural(L.sm, C.A, 0, n)) return fail("smoother plan");
-            } else if (l < h->nl - 1 && smoother_build(L.sm, C.A, C.cfmark.d, hier_kind(h, h->level_base + l),
-                                                       nullptr, 0, nullptr, enc)) {
-                return fail("smoother plan");
-            }
-        }
-        if (l < h->nl - 1) {
-            const auto &pc = h->L[l + 1].perm;   // (filled above for every relabeled level)
-            if (rl || !pc.empty()) {
-                RelabeledCSR P, R;
-                relabel_csr(C.P, L.perm, inv[l + 1], P);
-                relabel_csr(C.R, pc, inv[l], R);
-                // P's rows follow the level's F|C relabeling: blocks split there too, so a
-                // prolongation can be limited to the C rows (SmootherPlan::f_overwritten)
-                if (devcsr_upload(L.P, P.view(C.P.num_rows, C.P.num_cols), rl ? nF[l] : -1, enc & ~kEncDict) ||
-                    devcsr_upload(L.R, R.view(C.R.num_rows, C.R.num_cols), -1, enc & ~kEncDict))
-                    return fail("upload P/R");
-            } else if (devcsr_upload(L.P, C.P, -1, enc & ~kEncDict) || devcsr_upload(L.R, C.R, -1, enc & ~kEncDict)) {
-                return fail("upload P/R");
-            }
-        }
-        if (timing)
-            fprintf(stderr, "[sss_hip] upload level %d: relabel %.2f s, A %.2f s, smoother plan %.2f s, P/R %.2f s\n", l,
-                    rl ? t_rel - t_a : 0.0, rl ? t_up - t_rel : 0.0, rl ? t_sm - t_up : 0.0, now() - (rl ? t_sm : t_a));
-        L.b = dev_alloc<double>((size_t)n);
-        L.x = dev_alloc<double>((size_t)n);
-        L.wp = dev_alloc<double>((size_t)n);
-        if (!L.b || !L.x || !L.wp) return fail("vectors");
-        if (hipMemset(L.b, 0, sizeof(double) * n) != hipSuccess || hipMemset(L.x, 0, sizeof(double) * n) != hipSuccess ||
-            hipMemset(L.wp, 0, sizeof(double) * n) != hipSuccess)
-            return fail("memset");
+        t_rel = t_up = t_a;
+        t_sm = PhaseTimer::now();
     }
+    if (b.timing)
+        fprintf(stderr, "[sss_hip] upload level %d: relabel %.2f s, A %.2f s, smoother plan %.2f s\n", l,
+                rl ? t_rel - t_a : 0.0, rl ? t_up - t_rel : t_sm - t_a, rl ? t_sm - t_up : 0.0);
+    L.b = dev_alloc<double>((size_t)n);
+    L.x = dev_alloc<double>((size_t)n);
+    L.wp = dev_alloc<double>((size_t)n);
+    if (!L.b || !L.x || !L.wp) return hb_fail(b, "vectors");
+    if (hipMemset(L.b, 0, sizeof(double) * n) != hipSuccess || hipMemset(L.x, 0, sizeof(double) * n) != hipSuccess ||
+        hipMemset(L.wp, 0, sizeof(double) * n) != hipSuccess)
+        return hb_fail(b, "memset");
+    return true;
+}
+
+// P_l and R_l: rows / columns follow the relabelings of levels l and l + 1 (hb_perm of l + 1 has
+// run, or l + 1 is the coarsest)
+static bool hb_level_pr(HierBuild &b, int l)
+{
+    sss_hip_hier *h = b.h;
+    const SSS_AMG_COMP &C = b.mg->cg[l];
+    auto &L = h->L[l];
+    const bool rl = !L.perm.empty();
+    const auto &pc = h->L[l + 1].perm;
+    const int enc = level_encoding(h->opts);
+    const double t0 = PhaseTimer::now();
+    if (rl || !pc.empty()) {
+        PhaseTimer pt("P/R");
+        RelabeledCSR P, R;
+        relabel_csr(C.P, L.perm, b.inv[l + 1], P);
+        pt.mark("relabel P");
+        relabel_csr(C.R, pc, b.inv[l], R);
+        pt.mark("relabel R");
+        // P's rows follow the level's F|C relabeling: blocks split there too, so a
+        // prolongation can be limited to the C rows (SmootherPlan::f_overwritten)
+        if (devcsr_upload(L.P, P.view(C.P.num_rows, C.P.num_cols), rl ? b.nF[l] : -1, enc & ~kEncDict) ||
+            devcsr_upload(L.R, R.view(C.R.num_rows, C.R.num_cols), -1, enc & ~kEncDict))
+            return hb_fail(b, "upload P/R");
+    } else if (devcsr_upload(L.P, C.P, -1, enc & ~kEncDict) || devcsr_upload(L.R, C.R, -1, enc & ~kEncDict)) {
+        return hb_fail(b, "upload P/R");
+    }
+    if (b.timing) fprintf(stderr, "[sss_hip] upload level %d: P/R %.2f s\n", l, PhaseTimer::now() - t0);
+    return true;
+}
+
+static sss_hip_hier *hb_finish(HierBuild &b)
+{
+    sss_hip_hier *h = b.h;
+    const SSS_AMG *mg = b.mg;
+    auto fail = [&](const char *what) {
+        fprintf(stderr, "### ERROR: sss_hip_hier_create: %s\n", what);
+        hier_release(h);
+        b.h = nullptr;
+        return (sss_hip_hier *)nullptr;
+    };
+    if (b.err) return fail(b.err);
     h->partial = dev_alloc<double>((size_t)h->L[0].A.ngrid + kFinalScratch);
     if (h->nl > 1 && h->L[0].sm.pend_ok) {
         h->pend_f = dev_alloc<double>((size_t)std::max(h->L[0].sm.pass[0].hi, 1));
@@ -408,6 +470,129 @@ sss_hip_hier *sss::hier_create_impl(const SSS_AMG *mg, const sss_hip_opts *o, in
             fprintf(stderr, "[sss_hip] level %d: n=%d nnz=%d blocks=%d dagF=%d dagC=%d kind=%d gs engine F/C=%d/%d\n", l,
                     h->L[l].A.n, h->L[l].A.nnz, h->L[l].A.nblk, h->L[l].sm.pass[0].depth, h->L[l].sm.pass[1].depth,
                     h->L[l].sm.kind, h->L[l].sm.pass[0].gp.engine, h->L[l].sm.pass[1].gp.engine);
+    }
+    b.h = nullptr;
+    return h;
+}
+
+sss_hip_hier *sss::hier_create_impl(const SSS_AMG *mg, const sss_hip_opts *o, int level_base, hipStream_t stream)
+{
+    HierBuild b;
+    if (!hb_begin(b, mg, o, level_base, stream)) {
+        if (b.h) hier_release(b.h);
+        if (b.err) fprintf(stderr, "### ERROR: sss_hip_hier_create: %s\n", b.err);
+        return nullptr;
+    }
+    const int nl = mg->num_levels;
+    b.h->nl = nl;
+    for (int l = 0; l + 1 < nl; ++l) hb_perm(b, l);
+    for (int l = 0; l < nl && !b.err; ++l)
+        if (hb_level_a(b, l, l + 1 == nl) && l + 1 < nl) hb_level_pr(b, l);
+    return hb_finish(b);
+}
+
+// Setup and mirror construction overlapped: SSS_amg_setup (host, reference semantics) runs on the
+// calling thread; each time it completes a level, a worker thread relabels and uploads the levels
+// whose neighbourhood is final -- A_l and its smoother plan once level l is known not to be the
+// coarsest, P_l / R_l once level l + 1's relabeling is known.  The worker's host loops share the
+// CPUs with the setup's OpenMP regions, and its uploads run while the setup's serial RS passes
+// (Setup/SSS_coarsen.c:294-498) keep one core busy.  Results are those of SSS_amg_setup followed by
+// sss_hip_hier_create.
+namespace {
+struct Pipeline {
+    HierBuild b;
+    std::mutex mu;
+    std::condition_variable cv;
+    int done = 0;         // levels the setup has moved past (final, not the coarsest)
+    bool finished = false;
+    int device = 0;
+    double t_setup_end = 0, t_worker_end = 0;
+    void worker()
+    {
+        (void)hipSetDevice(device);
+        host_thread_background();
+        int a_next = 0, pr_next = 0;
+        for (;;) {
+            int d;
+            bool fin;
+            {
+                std::unique_lock<std::mutex> lk(mu);
+                cv.wait(lk, [&] { return finished || done > a_next; });
+                d = done;
+                fin = finished;
+            }
+            for (; a_next < d && !b.err; ++a_next) {
+                hb_perm(b, a_next);
+                hb_level_a(b, a_next, false);
+            }
+            for (; pr_next + 1 < d && !b.err; ++pr_next) hb_level_pr(b, pr_next);
+            if (fin || b.err) break;
+        }
+        t_worker_end = PhaseTimer::now();
+    }
+};
+}   // namespace
+
+static void pipeline_hook(void *ctx, const SSS_AMG *mg, int done, int final)
+{
+    (void)mg;
+    auto *P = static_cast<Pipeline *>(ctx);
+    {
+        std::lock_guard<std::mutex> lk(P->mu);
+        P->done = done;
+        if (final) P->finished = true;
+    }
+    P->cv.notify_all();
+}
+
+extern "C" sss_hip_hier *sss_hip_setup_create(SSS_AMG *mg, SSS_MAT *A, SSS_AMG_PARS *pars, const sss_hip_opts *o,
+                                              double *times)
+{
+    if (!mg || !A || !pars) return nullptr;
+    const double t0 = PhaseTimer::now();
+    Pipeline P;
+    // the mirror's begin needs mg->pars: the same values SSS_amg_data_create copies from pars
+    SSS_AMG shell;
+    std::memset(&shell, 0, sizeof(shell));
+    shell.pars = *pars;
+    if (!hb_begin(P.b, &shell, o, 0, nullptr)) {
+        if (P.b.h) hier_release(P.b.h);
+        SSS_amg_setup(mg, A, pars);
+        return nullptr;
+    }
+    P.b.mg = mg;
+    (void)hipGetDevice(&P.device);
+    std::thread th([&] { P.worker(); });
+    sss_amg_setup_hooked(mg, A, pars, pipeline_hook, &P);
+    P.t_setup_end = PhaseTimer::now();
+    {   // (a setup that returned without its final hook, e.g. no coarse level at all)
+        std::lock_guard<std::mutex> lk(P.mu);
+        P.finished = true;
+    }
+    P.cv.notify_all();
+    th.join();
+    const double t_join = PhaseTimer::now();
+    HierBuild &b = P.b;
+    const int nl = mg->num_levels;
+    b.h->nl = nl;
+    b.h->pars = mg->pars;
+    if (!b.err) {
+        // the levels the worker has not reached: the last non-coarsest level's P/R (its next level,
+        // the coarsest, keeps the identity) and the coarsest operator
+        int a_done = 0, pr_done = 0;
+        for (int l = 0; l < nl; ++l)
+            if (b.h->L[l].A.rp) a_done = l + 1;
+        for (int l = 0; l + 1 < nl; ++l)
+            if (b.h->L[l].P.rp) pr_done = l + 1;
+        for (int l = a_done; l + 1 < nl && !b.err; ++l) hb_perm(b, l), hb_level_a(b, l, false);
+        for (int l = pr_done; l + 1 < nl && !b.err; ++l) hb_level_pr(b, l);
+        if (!b.err && !b.h->L[nl - 1].A.rp) hb_level_a(b, nl - 1, true);
+    }
+    sss_hip_hier *h = hb_finish(b);
+    if (times) {
+        times[0] = P.t_setup_end - t0;                 // setup (with the overlapped uploads)
+        times[1] = PhaseTimer::now() - P.t_setup_end;  // mirror work left after the setup returned
+        times[2] = t_join - P.t_setup_end;             // of which: waiting for the worker
     }
     return h;
 }

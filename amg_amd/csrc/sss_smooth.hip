@@ -30,18 +30,17 @@
 namespace sss {
 
 // ---- host-side planning ---------------------------------------------------------------------
-static int upload_ints(int **dst, const std::vector<int> &src)
+template <class T>
+static int upload_array(T **dst, const T *src, size_t count)
 {
-    *dst = dev_alloc<int>(src.size());
-    if (!*dst) return hip_fail(hipErrorOutOfMemory, "hipMalloc(ints)", __FILE__, __LINE__);
-    return src.empty() ? 0 : h2d(*dst, src.data(), sizeof(int) * src.size());
+    *dst = dev_alloc<T>(count);
+    if (!*dst) return hip_fail(hipErrorOutOfMemory, "hipMalloc(plan array)", __FILE__, __LINE__);
+    return count == 0 ? 0 : h2d(*dst, src, sizeof(T) * count);
 }
-static int upload_doubles(double **dst, const std::vector<double> &src)
-{
-    *dst = dev_alloc<double>(src.size());
-    if (!*dst) return hip_fail(hipErrorOutOfMemory, "hipMalloc(doubles)", __FILE__, __LINE__);
-    return src.empty() ? 0 : h2d(*dst, src.data(), sizeof(double) * src.size());
-}
+static int upload_ints(int **dst, const std::vector<int> &src) { return upload_array(dst, src.data(), src.size()); }
+static int upload_ints(int **dst, const HostBuf<int> &src) { return upload_array(dst, src.data(), src.size()); }
+static int upload_doubles(double **dst, const HostBuf<double> &src) { return upload_array(dst, src.data(), src.size()); }
+static int upload_doubles(double **dst, const std::vector<double> &src) { return upload_array(dst, src.data(), src.size()); }
 
 int smoother_build(SmootherPlan &sp, const SSS_MAT &A, const int *mark, int kind, const DevCSR *dA, int inner,
                    const int *gcls, int enc)
@@ -49,10 +48,11 @@ int smoother_build(SmootherPlan &sp, const SSS_MAT &A, const int *mark, int kind
     const int n = A.num_rows;
     const int *rp = A.row_ptr, *ci = A.col_idx;
     const double *v = A.val;
-    std::vector<int> cls(n), depth(n, 0), pushed(n, 0);
-    std::vector<double> last_diag(n, 0.0), d_first(n, 0.0), d_later(n, 0.0);
-    std::vector<char> has_diag(n, 0);
-    std::vector<int> diag_pos(n, -1);
+    // per-row arrays filled by the row-parallel pass below (no serial zero-fill of n-length arrays)
+    HostBuf<int> cls, depth, pushed, diag_pos;
+    HostBuf<double> last_diag, d_first_buf, d_later_buf;
+    HostBuf<char> has_diag;
+    cls.resize(n), depth.resize(n), pushed.resize(n), diag_pos.resize(n), last_diag.resize(n), has_diag.resize(n);
     bool all_diag = true, single_diag = true;
     int rc;
     const char *tz = getenv("SSS_HIP_TILE_DIAG");   // 0: divisors from the deff stream (tests)
@@ -67,6 +67,10 @@ int smoother_build(SmootherPlan &sp, const SSS_MAT &A, const int *mark, int kind
             bool a = true, s1 = true;
             for (int i = lo; i < hi; ++i) {
                 cls[i] = mark ? (mark[i] == 1 ? 1 : 0) : 0;
+                depth[i] = pushed[i] = 0;
+                last_diag[i] = 0.0;
+                has_diag[i] = 0;
+                diag_pos[i] = -1;
                 for (int k = rp[i]; k < rp[i + 1]; ++k)
                     if (ci[k] == i) {
                         last_diag[i] = v[k];
@@ -84,17 +88,17 @@ int smoother_build(SmootherPlan &sp, const SSS_MAT &A, const int *mark, int kind
     }
     // stale-d resolution: simulate the divisor register over two sweeps of (F pass, C pass); with
     // a diagonal in every row it is each row's own last diagonal entry
-    if (all_diag) {
-        d_first = last_diag;
-        d_later = last_diag;
-    } else {
+    const double *d_first = last_diag.data(), *d_later = last_diag.data();
+    if (!all_diag) {
+        d_first_buf.resize(n), d_later_buf.resize(n);
+        d_first = d_first_buf.data(), d_later = d_later_buf.data();
         double d = 0.0;
         for (int sweep = 0; sweep < 2; ++sweep)
             for (int c = 0; c < 2; ++c)
                 for (int i = 0; i < n; ++i) {
                     if (cls[i] != c) continue;
                     if (has_diag[i]) d = last_diag[i];
-                    (sweep == 0 ? d_first : d_later)[i] = d;
+                    (sweep == 0 ? d_first_buf : d_later_buf)[i] = d;
                 }
     }
     // level schedule per class
@@ -346,13 +350,12 @@ int smoother_build(SmootherPlan &sp, const SSS_MAT &A, const int *mark, int kind
     if (timing)
         fprintf(stderr, "[sss_hip]   smoother plan n=%d: schedule %.2f s, one-launch GS %.2f s, two-stage %.2f s, rest %.2f s\n",
                 n, t_sched - t0, t_persist - t_sched, t_two - t_persist, now() - t_two);
-    if (kind == SSS_HIP_SMOOTH_JACOBI) {
-        if ((rc = upload_doubles(&sp.d_first, last_diag))) return rc;   // Jacobi: row's own diagonal
+    if (kind == SSS_HIP_SMOOTH_JACOBI || all_diag) {   // Jacobi: row's own diagonal
+        if ((rc = upload_doubles(&sp.d_first, last_diag))) return rc;
         sp.d_later = sp.d_first;
     } else {
-        if ((rc = upload_doubles(&sp.d_first, d_first))) return rc;
-        if (all_diag) sp.d_later = sp.d_first;
-        else if ((rc = upload_doubles(&sp.d_later, d_later))) return rc;
+        if ((rc = upload_doubles(&sp.d_first, d_first_buf))) return rc;
+        if ((rc = upload_doubles(&sp.d_later, d_later_buf))) return rc;
     }
     return 0;
 }
@@ -491,17 +494,24 @@ __device__ __forceinline__ void relax_range_ell(int blo, const int2 *__restrict_
     __shared__ EllSmem es;
     const int bid = blo + (dt.remap ? xcd_remap(blockIdx.x, gridDim.x) : (int)blockIdx.x);
     const int2 ba = blk[bid], be = blk[bid + 1];
-    ell_load_dicts(dt, bid, es);
     const int r = ba.x + (int)threadIdx.x;
+    const bool live = r < be.x;
+    unsigned w[W / 4] = {};
+    double br = 0.0, dr = 0.0;
+    if (live) {   // the row's codes, b and divisor are in flight across the dictionaries' barrier
+        ell_codes<W>(dt.ell, r, w);
+        br = b[r];
+        if (deff) dr = deff[r];
+    }
+    ell_load_dicts(dt, bid, es);
     double sq = 0.0;
-    if (r < be.x) {
+    if (live) {
             double p[W];
             int dsl;
             double dv;
-            const int len = ell_row<W>(dt.ell, r, es, [&](int c) -> double { return xs(c); }, p, dsl, dv);
-            const double br = b[r];
+            const int len = ell_decode<W>(w, r, es, [&](int c) -> double { return xs(c); }, p, dsl, dv);
             const double acc = dsl < 0 ? ell_sub(br, p, 0, len) : ell_sub(ell_sub(br, p, 0, dsl), p, dsl + 1, len);
-            const double d = deff ? deff[r] : dv;
+            const double d = deff ? dr : dv;
             if constexpr (MODE == 2) {
                 const double xn = fabs(d) > SMALLFLOAT ? acc / d : x[r];
                 if (fabs(d) > SMALLFLOAT) x[r] = xn;

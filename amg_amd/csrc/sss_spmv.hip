@@ -25,6 +25,9 @@
 #include <cstring>
 #include <mutex>
 #include <sched.h>
+#include <sys/resource.h>
+#include <sys/syscall.h>
+#include <unistd.h>
 
 namespace sss {
 
@@ -57,6 +60,16 @@ static int usable_cpus()
     return std::min(n, 32);
 }
 
+// Upload helpers run at a lower CPU priority (nice SSS_HOST_NICE, default 10): when the mirror is
+// built while the setup runs (sss_hip_setup_create), the setup's serial RS pass and its OpenMP
+// regions keep their cores and the upload takes what they leave idle.
+void host_thread_background()
+{
+    const char *e = getenv("SSS_HOST_NICE");
+    const int nice = (e && *e) ? atoi(e) : 10;
+    if (nice > 0) (void)setpriority(PRIO_PROCESS, (id_t)syscall(SYS_gettid), nice);
+}
+
 namespace {
 struct HostPool {
     std::mutex job_mu, mu;
@@ -74,6 +87,7 @@ struct HostPool {
     void loop()
     {
         in_worker = true;
+        host_thread_background();
         unsigned long long seen = 0;
         for (;;) {
             const std::function<void()> *w;
@@ -373,10 +387,29 @@ static void build_merged(const SSS_MAT &h, const int *seg, int G, std::vector<in
     gp.resize((size_t)ng + 1);
     mk.resize((size_t)h.num_nnzs);
     mv.resize((size_t)h.num_nnzs);
-    parallel_chunks(ng, 256, [&](int glo, int ghi) {
+    parallel_chunks(ng, 64, [&](int glo, int ghi) {
         std::vector<std::pair<unsigned long long, int>> ent;   // ((col << 4 | seg << 3 | row), position)
+        std::vector<unsigned long long> key;   // the same order as one integer: merged key << 24 | position
         for (int g = glo; g < ghi; ++g) {
             const int r0 = g * G, r1 = std::min(n, r0 + G);
+            const int base = rp[r0], cnt = rp[r1] - base;
+            if (cnt < (1 << 24)) {
+                key.resize((size_t)cnt);
+                for (int r = r0; r < r1; ++r)
+                    for (int k = rp[r]; k < rp[r + 1]; ++k) {
+                        const unsigned long long sg = (seg && k >= seg[r]) ? 1u : 0u;
+                        key[(size_t)(k - base)] =
+                            ((((unsigned long long)ci[k] << kMergeShift) | (sg << 3) | (unsigned)(r - r0)) << 24) |
+                            (unsigned)(k - base);
+                    }
+                std::sort(key.begin(), key.end());
+                gp[g] = base;
+                for (int t = 0; t < cnt; ++t) {
+                    mk[(size_t)base + t] = (unsigned)(key[t] >> 24);
+                    mv[(size_t)base + t] = h.val[base + (int)(key[t] & 0xffffff)];
+                }
+                continue;
+            }
             ent.clear();
             for (int r = r0; r < r1; ++r)
                 for (int k = rp[r]; k < rp[r + 1]; ++k) {
@@ -815,15 +848,27 @@ __global__ __launch_bounds__(kBlock) void spmv_adaptive(const int2 *__restrict__
         __shared__ EllSmem es;
         const int bid = dt.remap ? xcd_remap(blockIdx.x, gridDim.x) : (int)blockIdx.x;
         const int2 ba = blk[bid], be = blk[bid + 1];
-        ell_load_dicts(dt, bid, es);
         const int r = ba.x + (int)threadIdx.x;
+        unsigned w[W / 4] = {};
+        double br = 0.0;
+        if (r < be.x) {   // codes (and b) in flight across the dictionaries' barrier
+            ell_codes<W>(dt.ell, r, w);
+            if constexpr (OP == SSS_HIP_SPMV_RESID) br = b[r];
+        }
+        ell_load_dicts(dt, bid, es);
         double sq = 0.0;
         if (r < be.x) {
             double p[W];
             int ds;
             double dv;
-            const int len = ell_row<W>(dt.ell, r, es, [&](int c) -> double { return x[c]; }, p, ds, dv);
-            sq = epi(r, ell_add(0.0, p, 0, len));
+            const int len = ell_decode<W>(w, r, es, [&](int c) -> double { return x[c]; }, p, ds, dv);
+            if constexpr (OP == SSS_HIP_SPMV_RESID) {
+                const double out = br + ell_add(0.0, p, 0, len) * alpha;
+                y[r] = out;
+                sq = NORM ? out * out : 0.0;
+            } else {
+                sq = epi(r, ell_add(0.0, p, 0, len));
+            }
         }
         if (NORM) {
             const double t = block_sum(sq, es.red);

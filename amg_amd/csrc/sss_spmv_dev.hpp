@@ -76,13 +76,11 @@ __device__ __forceinline__ void ell_load_dicts(const DevDict &dt, int bid, EllSm
     if ((int)threadIdx.x < p.w) es.vd[threadIdx.x] = dt.vd[p.z + threadIdx.x];
     __syncthreads();
 }
-// Products of row r in stored (slot) order: p[s] = a_s * x(c_s) for s < len; dslot = the row's
-// (last) diagonal slot or -1, dval its value.
-template <int W, class Fetch>
-__device__ __forceinline__ int ell_row(const unsigned char *__restrict__ ell, int r, const EllSmem &es, Fetch fetch,
-                                       double (&p)[W], int &dslot, double &dval)
+// Row r's W code bytes (one 8/16/32-byte load).  The kernels issue it before the dictionaries'
+// barrier: it depends only on the block bounds, so it overlaps the dictionary loads.
+template <int W>
+__device__ __forceinline__ void ell_codes(const unsigned char *__restrict__ ell, int r, unsigned (&w)[W / 4])
 {
-    unsigned w[W / 4];
     if constexpr (W == 8) {
         const uint2 q = *reinterpret_cast<const uint2 *>(ell + (size_t)r * 8);
         w[0] = q.x, w[1] = q.y;
@@ -93,6 +91,13 @@ __device__ __forceinline__ int ell_row(const unsigned char *__restrict__ ell, in
             w[4 * h] = q.x, w[4 * h + 1] = q.y, w[4 * h + 2] = q.z, w[4 * h + 3] = q.w;
         }
     }
+}
+// Products of row r in stored (slot) order from its codes: p[s] = a_s * x(c_s) for s < len;
+// dslot = the row's (last) diagonal slot or -1, dval its value.
+template <int W, class Fetch>
+__device__ __forceinline__ int ell_decode(const unsigned (&w)[W / 4], int r, const EllSmem &es, Fetch fetch,
+                                          double (&p)[W], int &dslot, double &dval)
+{
     int len = W;
     dslot = -1;
     dval = 0.0;
@@ -111,6 +116,14 @@ __device__ __forceinline__ int ell_row(const unsigned char *__restrict__ ell, in
     for (int s = 0; s < W; ++s)
         if (s < len && c[s] == r) dslot = s, dval = a[s];
     return len;
+}
+template <int W, class Fetch>
+__device__ __forceinline__ int ell_row(const unsigned char *__restrict__ ell, int r, const EllSmem &es, Fetch fetch,
+                                       double (&p)[W], int &dslot, double &dval)
+{
+    unsigned w[W / 4];
+    ell_codes<W>(ell, r, w);
+    return ell_decode<W>(w, r, es, fetch, p, dslot, dval);
 }
 // sum of p[a, e) from s0 in slot order
 template <int W>

@@ -13,10 +13,10 @@
  *   Galerkin RAP ................ SSS_matvec.c:398-534
  *   level loop .................. Setup/SSS_SETUP.cu:36-178
  *
- * The measure lists are kept as an array of buckets indexed by measure instead of the
- * reference's heap-allocated sorted list of list nodes; the element-level linked lists
- * (lists/where) and the order of every insert/remove are the same, so the head of the
- * maximal bucket — the next C point — is the same.  RAP runs the reference's row-by-row
+ * The measure lists are kept as an array of FIFO buckets indexed by measure instead of the
+ * reference's heap-allocated sorted list of list nodes with element-level linked lists
+ * (lists/where); every insert/remove happens in the same order, so the head of the maximal
+ * bucket — the next C point — is the same.  RAP runs the reference's row-by-row
  * marker algorithm independently per coarse row (OpenMP), which yields identical rows
  * (diagonal first, then discovery order; identical summation order).
  */
@@ -404,6 +404,9 @@ static void direct_pattern(SSS_MAT *P, const SSS_IMAT *S, const SSS_IVEC *vertic
     P->num_rows = n;
     P->num_cols = ncoarse;
     P->row_ptr = (int *)SSS_calloc((size_t)n + 1, sizeof(int));
+    /* row counts in parallel, prefix, then each row fills its own span (same arrays as the
+     * reference's sequential pass) */
+#pragma omp parallel for schedule(static) if (n > 65536)
     for (int i = 0; i < n; ++i) {
         int cnt = 0;
         if (mark[i] == FGPT) {
@@ -412,17 +415,21 @@ static void direct_pattern(SSS_MAT *P, const SSS_IMAT *S, const SSS_IVEC *vertic
         } else if (mark[i] == CGPT) {
             cnt = 1;
         }
-        P->row_ptr[i + 1] = P->row_ptr[i] + cnt;
+        P->row_ptr[i + 1] = cnt;
     }
+    for (int i = 0; i < n; ++i) P->row_ptr[i + 1] += P->row_ptr[i];
     P->num_nnzs = P->row_ptr[n] - P->row_ptr[0];
     P->col_idx = (int *)SSS_calloc((size_t)P->num_nnzs, sizeof(int));
     P->val = (double *)SSS_calloc((size_t)P->num_nnzs, sizeof(double));
+    (void)pos;
+#pragma omp parallel for schedule(static) if (n > 65536)
     for (int i = 0; i < n; ++i) {
+        int o = P->row_ptr[i];
         if (mark[i] == FGPT) {
             for (int q = S->row_ptr[i]; q < S->row_ptr[i + 1]; ++q)
-                if (mark[S->col_idx[q]] == CGPT) P->col_idx[pos++] = S->col_idx[q];
+                if (mark[S->col_idx[q]] == CGPT) P->col_idx[o++] = S->col_idx[q];
         } else if (mark[i] == CGPT) {
-            P->col_idx[pos++] = i;
+            P->col_idx[o] = i;
         }
     }
 }
@@ -456,10 +463,74 @@ int SSS_amg_coarsen(SSS_MAT *A, SSS_IVEC *vertices, SSS_MAT *P, SSS_IMAT *S, SSS
 /* ======================================================================================
  * Interpolation and truncation
  * ====================================================================================== */
+/* Per-row form of the truncation below for large P: the same kept entries and scaled values,
+ * computed row-parallel into new arrays (kept counts, prefix, fill). */
+static void interp_trunc_par(SSS_MAT *P, double eps)
+{
+    const int n = P->num_rows;
+    int *nrp = (int *)SSS_calloc((size_t)n + 1, sizeof(int));
+#pragma omp parallel for schedule(static)
+    for (int i = 0; i < n; ++i) {
+        const int lo = P->row_ptr[i], hi = P->row_ptr[i + 1];
+        double pos_max = 0, neg_min = 0;
+        int c = 0;
+        for (int k = lo; k < hi; ++k) {
+            double v = P->val[k];
+            if (v > 0) pos_max = SSS_max(pos_max, v);
+            else if (v < 0) neg_min = SSS_MIN(neg_min, v);
+        }
+        pos_max *= eps;
+        neg_min *= eps;
+        for (int k = lo; k < hi; ++k) c += (P->val[k] >= pos_max) || (P->val[k] <= neg_min);
+        nrp[i + 1] = c;
+    }
+    for (int i = 0; i < n; ++i) nrp[i + 1] += nrp[i];
+    const int kept = nrp[n];
+    int *nci = (int *)SSS_calloc((size_t)(kept > 0 ? kept : 1), sizeof(int));
+    double *nv = (double *)SSS_calloc((size_t)(kept > 0 ? kept : 1), sizeof(double));
+#pragma omp parallel for schedule(static)
+    for (int i = 0; i < n; ++i) {
+        const int lo = P->row_ptr[i], hi = P->row_ptr[i + 1];
+        double pos_max = 0, neg_min = 0, pos_sum = 0, neg_sum = 0, pos_kept = 0, neg_kept = 0;
+        for (int k = lo; k < hi; ++k) {
+            double v = P->val[k];
+            if (v > 0) { pos_sum += v; pos_max = SSS_max(pos_max, v); }
+            else if (v < 0) { neg_sum += v; neg_min = SSS_MIN(neg_min, v); }
+        }
+        pos_max *= eps;
+        neg_min *= eps;
+        int o = nrp[i];
+        for (int k = lo; k < hi; ++k) {
+            double v = P->val[k];
+            if (v >= pos_max) { nci[o++] = P->col_idx[k]; pos_kept += v; }
+            else if (v <= neg_min) { nci[o++] = P->col_idx[k]; neg_kept += v; }
+        }
+        const double pos_fac = pos_kept > SMALLFLOAT ? pos_sum / pos_kept : 1.0;
+        const double neg_fac = neg_kept < -SMALLFLOAT ? neg_sum / neg_kept : 1.0;
+        o = nrp[i];
+        for (int k = lo; k < hi; ++k) {
+            double v = P->val[k];
+            if (v >= pos_max) nv[o++] = v * pos_fac;
+            else if (v <= neg_min) nv[o++] = v * neg_fac;
+        }
+    }
+    free(P->row_ptr);
+    free(P->col_idx);
+    free(P->val);
+    P->row_ptr = nrp;
+    P->col_idx = nci;
+    P->val = nv;
+    P->num_nnzs = kept;
+}
+
 void SSS_amg_interp_trunc(SSS_MAT *P, SSS_AMG_PARS *pars)
 {
     const double eps = pars->trunc_threshold;
     int kept = 0, wcol = 0, wval = 0;
+    if (P->num_nnzs >= (1 << 20)) {
+        interp_trunc_par(P, eps);
+        return;
+    }
     for (int i = 0; i < P->num_rows; ++i) {
         const int lo = P->row_ptr[i], hi = P->row_ptr[i + 1];
         double pos_max = 0, neg_min = 0, pos_sum = 0, neg_sum = 0, pos_kept = 0, neg_kept = 0;
@@ -710,7 +781,13 @@ void SSS_amg_complexity_print(SSS_AMG *mg)
     fputs(rule, stdout);
 }
 
-void SSS_amg_setup(SSS_AMG *mg, SSS_MAT *A, SSS_AMG_PARS *pars)
+void SSS_amg_setup(SSS_AMG *mg, SSS_MAT *A, SSS_AMG_PARS *pars) { sss_amg_setup_hooked(mg, A, pars, NULL, NULL); }
+
+/* SSS_amg_setup with a progress hook: hook(ctx, mg, done, 0) each time level done - 1 has been
+ * completed (its P, R, C/F marks and the next operator are final and it is not the coarsest
+ * level), hook(ctx, mg, num_levels - 1, 1) at the end.  sss_hip_setup_create uploads the
+ * completed levels to the GPU while the later ones are still being coarsened. */
+void sss_amg_setup_hooked(SSS_AMG *mg, SSS_MAT *A, SSS_AMG_PARS *pars, sss_setup_hook hook, void *ctx)
 {
     const int min_cdof = SSS_max(pars->coarse_dof, MIN_CDOF);
     const int max_lvls = pars->max_levels;
@@ -774,6 +851,7 @@ void SSS_amg_setup(SSS_AMG *mg, SSS_MAT *A, SSS_AMG_PARS *pars)
             break;
         }
         lvl++;
+        if (hook) hook(ctx, mg, lvl, 0);
     }
 
     mg->num_levels = lvl + 1;
@@ -787,4 +865,5 @@ void SSS_amg_setup(SSS_AMG *mg, SSS_MAT *A, SSS_AMG_PARS *pars)
     SSS_ivec_destroy(&vertices);
     SSS_amg_complexity_print(mg);
     printf("AMG setup time: %g s\n", SSS_get_time() - t0);
+    if (hook) hook(ctx, mg, mg->num_levels - 1, 1);
 }

@@ -77,6 +77,21 @@ typedef struct sss_hip_hier sss_hip_hier;
 sss_hip_hier *sss_hip_hier_create(const SSS_AMG *mg, const sss_hip_opts *o);
 void sss_hip_hier_destroy(sss_hip_hier *h);
 
+/* SSS_amg_setup (Setup/SSS_SETUP.cu:36-178 semantics, same printed output, same mg) with the
+ * mirror built while the setup runs: every level is relabeled and uploaded on a worker thread as
+ * soon as the setup has moved past it, so the uploads overlap the setup's serial RS passes.
+ * Equivalent to SSS_amg_setup(mg, A, pars) followed by sss_hip_hier_create(mg, o).  times
+ * (optional, 3 doubles): setup seconds (uploads overlapped), seconds of mirror work after the
+ * setup returned, of which waiting for the worker.  NULL on failure (mg is set up even then). */
+sss_hip_hier *sss_hip_setup_create(SSS_AMG *mg, SSS_MAT *A, SSS_AMG_PARS *pars, const sss_hip_opts *o,
+                                   double *times);
+
+/* Progress hook of the setup (amg_amd/host/sss_setup.c): hook(ctx, mg, done, 0) once levels
+ * 0 .. done-1 are final and none of them is the coarsest; hook(ctx, mg, num_levels - 1, 1) at
+ * the end. */
+typedef void (*sss_setup_hook)(void *ctx, const SSS_AMG *mg, int done, int final);
+void sss_amg_setup_hooked(SSS_AMG *mg, SSS_MAT *A, SSS_AMG_PARS *pars, sss_setup_hook hook, void *ctx);
+
 int sss_hip_upload_vec(sss_hip_hier *h, int level, int which, const double *src, int n);
 int sss_hip_download_vec(sss_hip_hier *h, int level, int which, double *dst, int n);
 
