@@ -362,8 +362,11 @@ static bool hb_level_a(HierBuild &b, int l, bool coarsest)
         t_rel = PhaseTimer::now();
         if (devcsr_upload(L.A, Av, b.nF[l], enc)) return hb_fail(b, "upload A");
         t_up = PhaseTimer::now();
-        std::vector<int> mark(n);
-        for (int i = 0; i < n; ++i) mark[i] = C.cfmark.d[L.perm[i]];
+        HostBuf<int> mark;
+        mark.resize((size_t)n);
+        parallel_chunks(n, 1 << 16, [&](int lo, int hi) {
+            for (int i = lo; i < hi; ++i) mark[i] = C.cfmark.d[L.perm[i]];
+        });
         if (smoother_build(L.sm, Av, mark.data(), hier_kind(h, h->level_base + l), &L.A,
                            hier_inner(h, h->level_base + l), nullptr, enc))
             return hb_fail(b, "smoother plan");

@@ -240,7 +240,7 @@ int smoother_build(SmootherPlan &sp, const SSS_MAT &A, const int *mark, int kind
             // two row-parallel passes: count, then fill at the prefix offsets (same order as a
             // sequential build: N_i entries in stored order, then L_i entries in stored order)
             std::vector<int> nrp((size_t)m + 1, 0), lrp((size_t)m + 1, 0), split(m);
-            parallel_chunks(m, 1 << 14, [&](int a, int e) {
+            parallel_chunks(m, 1 << 12, [&](int a, int e) {
                 for (int q = a; q < e; ++q) {
                     const int i = ps.lo + q;
                     int nn = 0, nl = 0;
@@ -255,9 +255,10 @@ int smoother_build(SmootherPlan &sp, const SSS_MAT &A, const int *mark, int kind
             });
             for (int q = 0; q < m; ++q) nrp[q + 1] += nrp[q], lrp[q + 1] += lrp[q];
             pt.mark("ts count");
-            std::vector<int> nci((size_t)nrp[m]), lci((size_t)lrp[m]);
-            std::vector<double> nv((size_t)nrp[m]), lv((size_t)lrp[m]);
-            parallel_chunks(m, 1 << 14, [&](int a, int e) {
+            HostBuf<int> nci, lci;   // every slot written below (no serial zero-fill)
+            HostBuf<double> nv, lv;
+            nci.resize((size_t)nrp[m]), lci.resize((size_t)lrp[m]), nv.resize((size_t)nrp[m]), lv.resize((size_t)lrp[m]);
+            parallel_chunks(m, 1 << 12, [&](int a, int e) {
                 for (int q = a; q < e; ++q) {
                     const int i = ps.lo + q;
                     int o = nrp[q], ol = lrp[q];
@@ -275,7 +276,7 @@ int smoother_build(SmootherPlan &sp, const SSS_MAT &A, const int *mark, int kind
                     }
                 }
             });
-            auto mk = [&](std::vector<int> &r, std::vector<int> &c, std::vector<double> &w) {
+            auto mk = [&](std::vector<int> &r, HostBuf<int> &c, HostBuf<double> &w) {
                 SSS_MAT M;
                 M.num_rows = m;
                 M.num_cols = A.num_cols;

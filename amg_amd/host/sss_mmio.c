@@ -17,6 +17,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <sys/stat.h>
 
 typedef struct {
     int nrows, ncols, nentries;
@@ -29,6 +30,91 @@ typedef struct {
 static void lower(char *s)
 {
     for (; *s; ++s) *s = (char)tolower((unsigned char)*s);
+}
+
+/* One entry starting at p (the same strtol/strtod sequence as the sequential loop below). */
+static const char *parse_entry(const char *p, char field, int *r, int *c, double *v)
+{
+    char *e;
+    long rr = strtol(p, &e, 10), cc;
+    double val = 1.0;
+    p = e;
+    cc = strtol(p, &e, 10);
+    p = e;
+    if (field == 'R' || field == 'C') {
+        val = strtod(p, &e);
+        p = e;
+        if (field == 'C') { (void)strtod(p, &e); p = e; }
+    } else if (field == 'I') {
+        val = (double)(int)strtol(p, &e, 10);
+        p = e;
+    }
+    *r = (int)rr - 1;
+    *c = (int)cc - 1;
+    *v = val;
+    return p;
+}
+
+/* Large files: the data section is cut into chunks at line ends; each thread counts the entry
+ * lines of its chunk, a prefix sum gives every chunk its first entry index, and the chunks are
+ * parsed in parallel into their slots -- the same triplets in file order as the sequential loop.
+ * Returns 0 (nothing written) when the layout is not one entry per non-blank line with exactly
+ * nentries entries, so the sequential parser handles every other case. */
+static int parse_parallel(const char *buf, size_t len, mtx_triplets *t)
+{
+#ifdef _OPENMP
+    if (len < ((size_t)4 << 20) || t->nentries <= 0) return 0;
+    const int nch = 256;
+    size_t cut[257];
+    long long cnt[257];
+    int ok = 1;
+    cut[0] = 0;
+    for (int c = 1; c < nch; ++c) {
+        size_t q = len / nch * (size_t)c;
+        if (q < cut[c - 1]) q = cut[c - 1];
+        while (q < len && buf[q] != '\n') ++q;
+        cut[c] = q < len ? q + 1 : len;
+    }
+    cut[nch] = len;
+#pragma omp parallel for schedule(dynamic, 1) reduction(&& : ok)
+    for (int c = 0; c < nch; ++c) {
+        long long n = 0;
+        int blank = 1;
+        for (size_t q = cut[c]; q < cut[c + 1]; ++q) {
+            const char ch = buf[q];
+            if (ch == '\n') {
+                n += !blank;
+                blank = 1;
+            } else if (!isspace((unsigned char)ch)) {
+                if (blank && ch == '%') ok = 0;   /* comment in the data section */
+                blank = 0;
+            }
+        }
+        if (!blank) ++n;
+        cnt[c + 1] = n;
+    }
+    if (!ok) return 0;
+    cnt[0] = 0;
+    for (int c = 0; c < nch; ++c) cnt[c + 1] += cnt[c];
+    if (cnt[nch] != t->nentries) return 0;
+#pragma omp parallel for schedule(dynamic, 1) reduction(&& : ok)
+    for (int c = 0; c < nch; ++c) {
+        const char *p = buf + cut[c], *lim = buf + cut[c + 1];
+        for (long long k = cnt[c]; k < cnt[c + 1]; ++k) {
+            const char *q = parse_entry(p, t->field, &t->ri[k], &t->ci[k], &t->v[k]);
+            if (q > lim || q == p) ok = 0;
+            p = q;
+            while (p < lim && *p != '\n') {   /* one entry per line: only blanks may follow */
+                if (!isspace((unsigned char)*p)) ok = 0;
+                ++p;
+            }
+        }
+    }
+    return ok;
+#else
+    (void)buf, (void)len, (void)t;
+    return 0;
+#endif
 }
 
 /* Reads the whole file, returns 0 on success (codes follow mmio_info: -1 open, -2 banner, -4 size). */
@@ -87,6 +173,10 @@ static int read_triplets(const char *path, mtx_triplets *t)
     t->ri = (int *)malloc(sizeof(int) * (size_t)(t->nentries > 0 ? t->nentries : 1));
     t->ci = (int *)malloc(sizeof(int) * (size_t)(t->nentries > 0 ? t->nentries : 1));
     t->v = (double *)malloc(sizeof(double) * (size_t)(t->nentries > 0 ? t->nentries : 1));
+    if (parse_parallel(buf, (size_t)(end - pos), t)) {
+        free(buf);
+        return 0;
+    }
     p = buf;
     for (int k = 0; k < t->nentries; ++k) {
         long r = strtol(p, &e, 10);
@@ -130,6 +220,32 @@ static int build_row_ptr(const mtx_triplets *t, int *rp)
     return rp[t->nrows];
 }
 
+/* mmio_info parses the file and SSS_mat_read then calls mmio_data on the same file: the triplets
+ * of the last mmio_info are kept for it (keyed by path, size and modification time), so a matrix
+ * is parsed once. */
+static struct {
+    char path[4096];
+    off_t size;
+    struct timespec mtime;
+    int valid;
+    mtx_triplets t;
+} last_parse;
+
+static int file_key(const char *path, off_t *size, struct timespec *mtime)
+{
+    struct stat st;
+    if (stat(path, &st) != 0) return 0;
+    *size = st.st_size;
+    *mtime = st.st_mtim;
+    return 1;
+}
+
+static void drop_last_parse(void)
+{
+    if (last_parse.valid) free_triplets(&last_parse.t);
+    last_parse.valid = 0;
+}
+
 int mmio_info(int *m, int *n, int *nnz, int *isSymmetric, char *filename)
 {
     mtx_triplets t;
@@ -142,15 +258,32 @@ int mmio_info(int *m, int *n, int *nnz, int *isSymmetric, char *filename)
     *nnz = build_row_ptr(&t, rp);
     *isSymmetric = t.mirrored;
     free(rp);
-    free_triplets(&t);
+    drop_last_parse();
+    if (strlen(filename) < sizeof(last_parse.path) && file_key(filename, &last_parse.size, &last_parse.mtime)) {
+        strcpy(last_parse.path, filename);
+        last_parse.t = t;
+        last_parse.valid = 1;
+    } else {
+        free_triplets(&t);
+    }
     return 0;
 }
 
 int mmio_data(int *csrRowPtr, int *csrColIdx, double *csrAx, char *filename)
 {
     mtx_triplets t;
-    int rc = read_triplets(filename, &t);
+    int rc = 0;
     int *next;
+    off_t size;
+    struct timespec mt;
+    if (last_parse.valid && !strcmp(last_parse.path, filename) && file_key(filename, &size, &mt) &&
+        size == last_parse.size && mt.tv_sec == last_parse.mtime.tv_sec && mt.tv_nsec == last_parse.mtime.tv_nsec) {
+        t = last_parse.t;
+        last_parse.valid = 0;
+    } else {
+        drop_last_parse();
+        rc = read_triplets(filename, &t);
+    }
     if (rc != 0) return rc;
     build_row_ptr(&t, csrRowPtr);
     next = (int *)malloc(sizeof(int) * ((size_t)t.nrows + 1));

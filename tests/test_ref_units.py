@@ -144,6 +144,48 @@ def test_mtx_variants_vs_reference(tmp_path, field, sym, quiet):
     assert same_csr(M1, M2)
 
 
+def _write_big_mtx(path, n, nent, field, sym, seed, layout="lines"):
+    """A Matrix Market file above the parallel-parse threshold (4 MiB of data)."""
+    rng = np.random.default_rng(seed)
+    i = rng.integers(0, n, nent)
+    j = rng.integers(0, n, nent)
+    if sym != "general":
+        i, j = np.maximum(i, j), np.minimum(i, j)
+    v = (rng.standard_normal(nent) * 10).tolist()
+    i, j = i.tolist(), j.tolist()
+    with open(path, "w") as f:
+        f.write(f"%%MatrixMarket matrix coordinate {field} {sym}\n% generated\n{n} {n} {nent}\n")
+        if field == "pattern":
+            body = "\n".join(f"{a + 1} {b + 1}" for a, b in zip(i, j))
+        elif field == "integer":
+            body = "\n".join(f"{a + 1} {b + 1} {int(c)}" for a, b, c in zip(i, j, v))
+        else:
+            body = "\n".join(f"{a + 1}  {b + 1}\t{c!r}  " for a, b, c in zip(i, j, v))
+        if layout == "split":   # an entry spread over two lines: only the sequential parser reads it
+            body = body.replace("\n", " \n", 1).replace(" \n", "\n\n", 1)
+            k = body.index("\n", 1000)
+            body = body[:k] + body[k:].replace(" ", "\n", 1)
+        f.write(body + "\n\n")
+
+
+@needs_ref
+@pytest.mark.parametrize("field,sym,layout", [("real", "general", "lines"), ("real", "symmetric", "lines"),
+                                              ("pattern", "general", "lines"), ("integer", "symmetric", "lines"),
+                                              ("real", "general", "split")])
+def test_mtx_large_vs_reference(tmp_path, field, sym, layout, quiet):
+    """Files above the parallel-parse threshold (sss_mmio.c parse_parallel, chunked at line ends):
+    the same CSR as the reference's sequential mmio_info/mmio_data, also when the data section is
+    laid out so that only the sequential parser applies (an entry split over two lines)."""
+    p = tmp_path / "big.mtx"
+    _write_big_mtx(p, 20000, 450000, field, sym, seed=7, layout=layout)
+    assert p.stat().st_size > (4 << 20)
+    M1, M2 = SSS_MAT(), SSS_MAT()
+    with quiet():
+        A.lib().SSS_mat_read(str(p).encode(), C.byref(M1))
+        REF.SSS_mat_read(str(p).encode(), C.byref(M2))
+    assert same_csr(M1, M2)
+
+
 @needs_ref
 def test_generator_equals_mtx_ingest(tmp_path, quiet):
     """The in-memory 7-pt generator == reference ingest of the same operator written as .mtx."""
