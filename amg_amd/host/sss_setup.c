@@ -137,11 +137,20 @@ typedef struct {
     int live;                /* live entries = points in this bucket */
 } bucket_fifo;
 
+/* Per-point state of the first pass in one 16-byte record (one cache line holds four points; the
+ * pass touches measure, mark and version of the same neighbours). */
+typedef struct {
+    int lambda;              /* measure */
+    int mark;                /* UNPT / CGPT / FGPT / ISPT */
+    unsigned ver;            /* current version: a bucket entry is live iff it matches */
+    int pad;
+} rs_point;
+
 typedef struct {
     bucket_fifo *b;          /* per measure */
     int cap;                 /* allocated measures */
     int top;                 /* upper bound on the largest non-empty measure */
-    unsigned *ver;           /* per point: current version (an entry is live iff it matches) */
+    rs_point *pts;
 } measure_buckets;
 
 static void buckets_grow(measure_buckets *B, int m)
@@ -153,11 +162,11 @@ static void buckets_grow(measure_buckets *B, int m)
     B->cap = cap;
 }
 
-static void bucket_compact(bucket_fifo *q, const unsigned *ver)
+static void bucket_compact(bucket_fifo *q, const rs_point *pts)
 {
     size_t o = 0;
     for (size_t k = q->head; k < q->tail; ++k)
-        if (q->e[k].ver == ver[q->e[k].pt]) q->e[o++] = q->e[k];
+        if (q->e[k].ver == pts[q->e[k].pt].ver) q->e[o++] = q->e[k];
     q->head = 0;
     q->tail = o;
 }
@@ -167,14 +176,14 @@ static inline void bucket_insert(measure_buckets *B, int m, int pt)
     if (m >= B->cap) buckets_grow(B, m);
     bucket_fifo *q = &B->b[m];
     if (q->tail == q->cap) {
-        if (q->tail - q->head > 2 * (size_t)q->live + 64 || q->head > q->cap / 2) bucket_compact(q, B->ver);
+        if (q->tail - q->head > 2 * (size_t)q->live + 64 || q->head > q->cap / 2) bucket_compact(q, B->pts);
         if (q->tail == q->cap) {
             q->cap = q->cap * 2 + 256;
             q->e = (bucket_entry *)realloc(q->e, sizeof(bucket_entry) * q->cap);
         }
     }
     q->e[q->tail].pt = pt;
-    q->e[q->tail].ver = ++B->ver[pt];
+    q->e[q->tail].ver = ++B->pts[pt].ver;
     q->tail++;
     q->live++;
     if (m > B->top) B->top = m;
@@ -186,7 +195,7 @@ static inline void bucket_remove(measure_buckets *B, int m, int pt)
         printf("### ERROR: This list is empty! %s : %d\n", __FILE__, __LINE__);
         return;
     }
-    B->ver[pt]++;
+    B->pts[pt].ver++;
     if (--B->b[m].live == 0) B->b[m].head = B->b[m].tail = 0;
 }
 
@@ -196,7 +205,7 @@ static int bucket_max_head(measure_buckets *B)
     while (B->top > 0 && B->b[B->top].live == 0) B->top--;
     if (B->top <= 0) return -1;
     bucket_fifo *q = &B->b[B->top];
-    while (q->e[q->head].ver != B->ver[q->e[q->head].pt]) q->head++;
+    while (q->e[q->head].ver != B->pts[q->e[q->head].pt].ver) q->head++;
     return q->e[q->head].pt;
 }
 
@@ -218,40 +227,40 @@ static int rs_split(const SSS_MAT *A, SSS_IMAT *S, SSS_IVEC *vertices)
     const double t1 = SSS_get_time();
 
     memset(&B, 0, sizeof(B));
-    B.ver = (unsigned *)SSS_calloc((size_t)n, sizeof(unsigned));
-    lambda = (int *)SSS_calloc((size_t)n, sizeof(int));
+    B.pts = (rs_point *)SSS_calloc((size_t)n, sizeof(rs_point));
+    rs_point *P = B.pts;
     buckets_grow(&B, 64);
 
-    for (int i = 0; i < n; ++i) lambda[i] = ST.row_ptr[i + 1] - ST.row_ptr[i];
+    for (int i = 0; i < n; ++i) P[i].lambda = ST.row_ptr[i + 1] - ST.row_ptr[i];
     for (int i = 0; i < n; ++i) {
         if (S->row_ptr[i + 1] == S->row_ptr[i]) {
-            mark[i] = ISPT;
-            lambda[i] = 0;
+            P[i].mark = ISPT;
+            P[i].lambda = 0;
         } else {
-            mark[i] = UNPT;
+            P[i].mark = UNPT;
             undecided++;
         }
     }
 
     /* Initial lists; points with no influence become F immediately. */
     for (int i = 0; i < n; ++i) {
-        if (mark[i] == ISPT) continue;
-        if (lambda[i] > 0) {
-            bucket_insert(&B, lambda[i], i);
+        if (P[i].mark == ISPT) continue;
+        if (P[i].lambda > 0) {
+            bucket_insert(&B, P[i].lambda, i);
             continue;
         }
-        if (lambda[i] < 0) printf("### WARNING: Negative lambda[%d]!\n", i);
-        mark[i] = FGPT;
+        if (P[i].lambda < 0) printf("### WARNING: Negative lambda[%d]!\n", i);
+        P[i].mark = FGPT;
         undecided--;
         for (int k = S->row_ptr[i]; k < S->row_ptr[i + 1]; ++k) {
             int j = S->col_idx[k];
-            if (mark[j] == ISPT) continue;
+            if (P[j].mark == ISPT) continue;
             if (j < i) {
-                if (lambda[j] > 0) bucket_remove(&B, lambda[j], j);
-                lambda[j]++;
-                bucket_insert(&B, lambda[j], j);
+                if (P[j].lambda > 0) bucket_remove(&B, P[j].lambda, j);
+                P[j].lambda++;
+                bucket_insert(&B, P[j].lambda, j);
             } else {
-                lambda[j]++;
+                P[j].lambda++;
             }
         }
     }
@@ -264,10 +273,10 @@ static int rs_split(const SSS_MAT *A, SSS_IMAT *S, SSS_IVEC *vertices)
             printf("### ERROR: RS coarsening ran out of candidates (%d undecided)\n", undecided);
             break;
         }
-        mc = lambda[c];
+        mc = P[c].lambda;
         if (mc == 0) printf("### WARNING: Head of the list has measure 0!\n");
-        mark[c] = CGPT;
-        lambda[c] = 0;
+        P[c].mark = CGPT;
+        P[c].lambda = 0;
         undecided--;
         bucket_remove(&B, mc, c);
         ncoarse++;
@@ -275,42 +284,45 @@ static int rs_split(const SSS_MAT *A, SSS_IMAT *S, SSS_IVEC *vertices)
         /* points that c strongly influences become F */
         for (int q = ST.row_ptr[c]; q < ST.row_ptr[c + 1]; ++q) {
             int j = ST.col_idx[q];
-            if (mark[j] != UNPT) continue;
-            mark[j] = FGPT;
-            bucket_remove(&B, lambda[j], j);
+            if (P[j].mark != UNPT) continue;
+            P[j].mark = FGPT;
+            bucket_remove(&B, P[j].lambda, j);
             undecided--;
             for (int r = S->row_ptr[j]; r < S->row_ptr[j + 1]; ++r) {
                 int k = S->col_idx[r];
-                if (mark[k] != UNPT) continue;
-                bucket_remove(&B, lambda[k], k);
-                lambda[k]++;
-                bucket_insert(&B, lambda[k], k);
+                if (P[k].mark != UNPT) continue;
+                bucket_remove(&B, P[k].lambda, k);
+                P[k].lambda++;
+                bucket_insert(&B, P[k].lambda, k);
             }
         }
         /* points that strongly influence c lose one unit of measure */
         for (int q = S->row_ptr[c]; q < S->row_ptr[c + 1]; ++q) {
             int j = S->col_idx[q], m;
-            if (mark[j] != UNPT) continue;
-            m = lambda[j];
+            if (P[j].mark != UNPT) continue;
+            m = P[j].lambda;
             bucket_remove(&B, m, j);
-            lambda[j] = --m;
+            P[j].lambda = --m;
             if (m > 0) {
                 bucket_insert(&B, m, j);
                 continue;
             }
-            mark[j] = FGPT;
+            P[j].mark = FGPT;
             undecided--;
             for (int r = S->row_ptr[j]; r < S->row_ptr[j + 1]; ++r) {
                 int k = S->col_idx[r];
-                if (mark[k] != UNPT) continue;
-                bucket_remove(&B, lambda[k], k);
-                lambda[k]++;
-                bucket_insert(&B, lambda[k], k);
+                if (P[k].mark != UNPT) continue;
+                bucket_remove(&B, P[k].lambda, k);
+                P[k].lambda++;
+                bucket_insert(&B, P[k].lambda, k);
             }
         }
     }
 
     const double t3 = SSS_get_time();
+    lambda = (int *)SSS_calloc((size_t)n, sizeof(int));
+    for (int i = 0; i < n; ++i) mark[i] = P[i].mark;
+    free(B.pts);
     /* C1 criterion: two strongly coupled F points must share a strong C point. */
     owner = lambda;
     for (int i = 0; i < n; ++i) owner[i] = -1;
@@ -345,7 +357,6 @@ static int rs_split(const SSS_MAT *A, SSS_IMAT *S, SSS_IVEC *vertices)
     SSS_imat_destroy(&ST);
     for (int m = 0; m < B.cap; ++m) free(B.b[m].e);
     free(B.b);
-    free(B.ver);
     free(lambda);
     return ncoarse;
 }
