@@ -191,6 +191,7 @@ struct DevCSR {
     // (or each of its two segments [rp, seg) / [seg, rp+1)) column-sorted for the wave-per-row
     // kernels (64 lane-strided sums, xor-shuffle reduction) ...
     bool vec_rows = false;
+    bool rows_sorted = false;  // vec_rows: ci/v hold each row (segment) column-sorted (else stored order)
     // ... and on a short-row matrix of a free-order level, the rows longer than one tile (a hub
     // row of an irregular operator) are tree-summed chunk by chunk by the whole workgroup instead
     // of chained by one thread (block_tree_sum; the short rows keep the stored order)
@@ -240,7 +241,9 @@ constexpr int kTileColBits = 20;         // column offset bits of a packed sorte
 constexpr unsigned kTileDiagMark = (1u << kTileColBits) - 256;
 static_assert((1 << kTileShift) == kTileEntries, "tile packing");
 static_assert(1 + kTileColBits + kTileShift == 32, "tile packing");
-enum { kEncSortedTiles = 1, kEncFreeOrder = 2, kEncDict = 4 };
+// kEncMergedOnly: the matrix is only ever read through its merged copy when it gets one (the
+// two-stage split copies, launch_ts_*), so its CSR arrays need not be column-sorted
+enum { kEncSortedTiles = 1, kEncFreeOrder = 2, kEncDict = 4, kEncMergedOnly = 8 };
 // split >= 0 forces a row-block boundary at that row (the F|C class boundary of a relabeled level);
 // enc: kEnc* flags; seg (kEncFreeOrder only, optional): per row, the absolute CSR position that
 // splits the row into two independently summed segments (two-stage [N_i | L_i] rows).
@@ -252,6 +255,9 @@ int build_row_blocks(const int *h_rp, int n, std::vector<int> &blk, int split = 
 int upload_block_bounds(int2 **dst, const std::vector<int> &blk, const int *h_rp);
 int wave_row_min();
 int free_row_min();
+// Re-upload a free-order matrix's CSR rows column-sorted (one uploaded kEncMergedOnly whose
+// merged copy turned out not to be its only reader).
+int devcsr_sort_rows(DevCSR &d, const SSS_MAT &h, const int *seg = nullptr);
 struct DevDict;
 DevDict devdict(const DevCSR &A, int blo);   // the matrix's dictionary tiles, block numbers from blo
 // the tile kernels stage from a dictionary (either kind): instantiate them with DICT = true

@@ -353,8 +353,12 @@ static bool hb_level_a(HierBuild &b, int l, bool coarsest)
     const bool rl = !L.perm.empty();
     const double t_a = PhaseTimer::now();
     double t_rel = t_a, t_up = t_a, t_sm = t_a;
-    // the coarsest operator only feeds the coarse solver: stored order there
-    const int enc = !coarsest ? level_encoding(h->opts) : (level_encoding(h->opts) & kEncSortedTiles);
+    // the coarsest operator only feeds the coarse solver: stored order there.  On a two-stage level
+    // the relaxation reads the split copies, and the level matrix's own free-order products go
+    // through its merged copy (residual) or are order-free (zero-first pass): no sorted rows needed
+    int enc = !coarsest ? level_encoding(h->opts) : (level_encoding(h->opts) & kEncSortedTiles);
+    if (!coarsest && hier_kind(h, h->level_base + l) == SSS_HIP_SMOOTH_JACOBI && hier_inner(h, h->level_base + l) > 0)
+        enc |= kEncMergedOnly;
     if (rl) {
         RelabeledCSR B;
         relabel_csr(C.A, L.perm, b.inv[l], B);
@@ -370,6 +374,7 @@ static bool hb_level_a(HierBuild &b, int l, bool coarsest)
         if (smoother_build(L.sm, Av, mark.data(), hier_kind(h, h->level_base + l), &L.A,
                            hier_inner(h, h->level_base + l), nullptr, enc))
             return hb_fail(b, "smoother plan");
+        if (L.sm.inner == 0 && devcsr_sort_rows(L.A, Av)) return hb_fail(b, "upload A");   // plain passes read A's rows
         t_sm = PhaseTimer::now();
     } else {
         if (devcsr_upload(L.A, C.A, -1, enc)) return hb_fail(b, "upload A");
@@ -379,6 +384,7 @@ static bool hb_level_a(HierBuild &b, int l, bool coarsest)
                                                nullptr, enc)) {
             return hb_fail(b, "smoother plan");
         }
+        if (devcsr_sort_rows(L.A, C.A)) return hb_fail(b, "upload A");   // (no two-stage plan here)
         t_rel = t_up = t_a;
         t_sm = PhaseTimer::now();
     }

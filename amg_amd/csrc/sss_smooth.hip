@@ -289,8 +289,8 @@ int smoother_build(SmootherPlan &sp, const SSS_MAT &A, const int *mark, int kind
             pt.mark("ts fill");
             SSS_MAT Mn = mk(nrp, nci, nv), Ml = mk(lrp, lci, lv);
             std::vector<int> seg(split);   // absolute [N_i | L_i] cut of each row of Mn
-            if ((rc = devcsr_upload(ps.ts_nl, Mn, -1, enc & ~kEncDict, seg.data())) ||
-                (rc = devcsr_upload(ps.ts_lo, Ml, -1, enc & ~kEncDict)))
+            if ((rc = devcsr_upload(ps.ts_nl, Mn, -1, (enc & ~kEncDict) | kEncMergedOnly, seg.data())) ||
+                (rc = devcsr_upload(ps.ts_lo, Ml, -1, (enc & ~kEncDict) | kEncMergedOnly)))
                 return rc;
             pt.mark("ts upload");
             if ((rc = upload_ints(&ps.ts_split, split))) return rc;

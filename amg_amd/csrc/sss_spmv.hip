@@ -658,12 +658,15 @@ int devcsr_upload(DevCSR &d, const SSS_MAT &h, int split, int enc, const int *se
     pt.mark("alloc");
     if (int rc = h2d(d.rp, h.row_ptr, sizeof(int) * ((size_t)d.n + 1))) return rc;
     if (d.nnz > 0) {
-        if (d.vec_rows) {
+        // free-order rows are read column-sorted by the wave-tree kernels; a two-stage split copy
+        // with a merged copy (kEncMergedOnly) is read only through that (launch_ts_*): stored order
+        if (d.vec_rows && !((enc & kEncMergedOnly) && d.mg_G > 0)) {
             HostBuf<int> sci;
             HostBuf<double> sv;
             sort_row_segments(h, seg, sci, sv);
             if (int rc = h2d(d.ci, sci.data(), sizeof(int) * (size_t)d.nnz)) return rc;
             if (int rc = h2d(d.v, sv.data(), sizeof(double) * (size_t)d.nnz)) return rc;
+            d.rows_sorted = true;
         } else {
             if (int rc = h2d(d.ci, h.col_idx, sizeof(int) * (size_t)d.nnz)) return rc;
             if (int rc = h2d(d.v, h.val, sizeof(double) * (size_t)d.nnz)) return rc;
@@ -796,6 +799,18 @@ int devcsr_upload(DevCSR &d, const SSS_MAT &h, int split, int enc, const int *se
     } else {
         d.stream_bytes = 12 * nnz + 4 * (rows + 1) + 8 * (nb + 1);
     }
+    return 0;
+}
+
+int devcsr_sort_rows(DevCSR &d, const SSS_MAT &h, const int *seg)
+{
+    if (!d.vec_rows || d.rows_sorted || d.nnz == 0) return 0;
+    HostBuf<int> sci;
+    HostBuf<double> sv;
+    sort_row_segments(h, seg, sci, sv);
+    if (int rc = h2d(d.ci, sci.data(), sizeof(int) * (size_t)d.nnz)) return rc;
+    if (int rc = h2d(d.v, sv.data(), sizeof(double) * (size_t)d.nnz)) return rc;
+    d.rows_sorted = true;
     return 0;
 }
 

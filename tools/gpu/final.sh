@@ -13,3 +13,6 @@ rc=$?; tail -2 gpurun_out/smoke.log; [ $rc -eq 0 ] || exit $rc
 timeout -k 10 900 python -u bench.py $BENCH_ARGS > gpurun_out/bench.json 2> gpurun_out/bench.err
 rc=$?; cat gpurun_out/bench.json; [ $rc -eq 0 ] || { tail -20 gpurun_out/bench.err; exit $rc; }
 bash tools/gpu/prof.sh
+# N = 2 on the one-GPU box: two ranks (host transport when RCCL cannot pair two ranks on one GPU)
+timeout -k 10 300 python -u bench.py --gpus 2 --n 64 --steps 3 --warmup 1 --no-cpu-baseline > gpurun_out/bench_g2.json 2> gpurun_out/bench_g2.err
+rc=$?; tail -c 400 gpurun_out/bench_g2.json; exit $rc
