@@ -330,6 +330,11 @@ def main():
         sys.stdout.flush()
         D.close()
         return
+    # stdout carries the JSON record only: library banners (RCCL's version block, gloo's peer
+    # lines) and the C setup tables go to stderr
+    sys.stdout.flush()
+    json_fd = os.dup(1)
+    os.dup2(2, 1)
     # the BASELINE.json config of this rank count (configs[2]: 512^3 on 8 GPUs; configs[4]: 27-pt
     # 256^3 on 4 GPUs; the metric's 64M-row 400^3 otherwise)
     circuit = args.workload == "circuit"
@@ -703,7 +708,8 @@ def main():
     DH.close()
     hb_stop.set()
     if D.rank == 0:
-        print(json.dumps(rec), flush=True)
+        sys.stdout.flush()
+        os.write(json_fd, (json.dumps(rec) + "\n").encode())
     D.close()
 
 
