@@ -243,11 +243,7 @@ static_assert((1 << kTileShift) == kTileEntries, "tile packing");
 static_assert(1 + kTileColBits + kTileShift == 32, "tile packing");
 // kEncMergedOnly: the matrix is only ever read through its merged copy when it gets one (the
 // two-stage split copies, launch_ts_*), so its CSR arrays need not be column-sorted
-// kEncValueDict: value dictionaries over the sorted tiles only (rectangular P and R, whose column
-// offsets are not row-relative, take the value-dictionary form of the dictionary formats)
-enum { kEncSortedTiles = 1, kEncFreeOrder = 2, kEncDict = 4, kEncMergedOnly = 8, kEncValueDict = 16 };
-// encoding of a transfer operator (P, R) from the level encoding
-inline int transfer_encoding(int enc) { return (enc & ~kEncDict) | ((enc & kEncDict) ? kEncValueDict : 0); }
+enum { kEncSortedTiles = 1, kEncFreeOrder = 2, kEncDict = 4, kEncMergedOnly = 8 };
 // split >= 0 forces a row-block boundary at that row (the F|C class boundary of a relabeled level);
 // enc: kEnc* flags; seg (kEncFreeOrder only, optional): per row, the absolute CSR position that
 // splits the row into two independently summed segments (two-stage [N_i | L_i] rows).

@@ -129,9 +129,8 @@ static int level_inner(const sss_hip_opts &o, int l)
 int sss::level_kind_of(const sss_hip_opts &o, int l) { return level_smoother_kind(o, l); }
 int sss::level_encoding(const sss_hip_opts &o)
 {
-    // dictionary tiles (kEncDict) are offered for the level matrices A_l; uploads of P and R take
-    // value dictionaries only (transfer_encoding: their column offsets are not row-relative), the
-    // two-stage split copies none
+    // dictionary tiles (kEncDict) are offered for the level matrices A_l; uploads of P, R and the
+    // two-stage split copies mask them out (their column offsets are not row-relative)
     const char *dz = getenv("SSS_HIP_DICT");
     const int dict = (dz && *dz == '0') ? 0 : kEncDict;
     return (o.sorted_tiles ? kEncSortedTiles : 0) | (o.sum_order == 1 ? kEncFreeOrder : 0) | dict;
@@ -422,10 +421,10 @@ static bool hb_level_pr(HierBuild &b, int l)
         pt.mark("relabel R");
         // P's rows follow the level's F|C relabeling: blocks split there too, so a
         // prolongation can be limited to the C rows (SmootherPlan::f_overwritten)
-        if (devcsr_upload(L.P, P.view(C.P.num_rows, C.P.num_cols), rl ? b.nF[l] : -1, transfer_encoding(enc)) ||
-            devcsr_upload(L.R, R.view(C.R.num_rows, C.R.num_cols), -1, transfer_encoding(enc)))
+        if (devcsr_upload(L.P, P.view(C.P.num_rows, C.P.num_cols), rl ? b.nF[l] : -1, enc & ~kEncDict) ||
+            devcsr_upload(L.R, R.view(C.R.num_rows, C.R.num_cols), -1, enc & ~kEncDict))
             return hb_fail(b, "upload P/R");
-    } else if (devcsr_upload(L.P, C.P, -1, transfer_encoding(enc)) || devcsr_upload(L.R, C.R, -1, transfer_encoding(enc))) {
+    } else if (devcsr_upload(L.P, C.P, -1, enc & ~kEncDict) || devcsr_upload(L.R, C.R, -1, enc & ~kEncDict)) {
         return hb_fail(b, "upload P/R");
     }
     if (b.timing) fprintf(stderr, "[sss_hip] upload level %d: P/R %.2f s\n", l, PhaseTimer::now() - t0);

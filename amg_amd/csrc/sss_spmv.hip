@@ -769,7 +769,7 @@ int devcsr_upload(DevCSR &d, const SSS_MAT &h, int split, int enc, const int *se
         HostBuf<unsigned char> vi;
         std::vector<int4> pd;
         std::vector<double> vd;
-        if ((enc & (kEncDict | kEncValueDict)) && !(dz && *dz == '0') && build_value_dict(blk, h.row_ptr, pv, vi, pd, vd)) {
+        if ((enc & kEncDict) && !(dz && *dz == '0') && build_value_dict(blk, h.row_ptr, pv, vi, pd, vd)) {
             d.dv_vi = dev_alloc<unsigned char>(vi.size());
             d.dv_pd = dev_alloc<int4>(pd.size());
             d.dv_vd = dev_alloc<double>(vd.size());
