@@ -209,6 +209,40 @@ static int bucket_max_head(measure_buckets *B)
     return q->e[q->head].pt;
 }
 
+/* Rows that can change in the C1 and F-F passes below.  Both passes visit the F rows in order and
+ * act only on a row with a strongly coupled F neighbour j that shares no strong C point with it
+ * (an "unshared pair").  Between rows, marks only ever move F -> C (a tentative C point that is
+ * reverted was F before), so the C set only grows: a row with no unshared pair under the marks
+ * before the pass never gets one, and the pass does nothing there but per-row bookkeeping.  This
+ * flags the rows that have an unshared pair under the starting marks, row-parallel; the serial
+ * passes run their exact logic on the flagged rows only.  owner (n ints) is a scratch marker
+ * shared by the threads: a concurrent overwrite can only hide a shared C point, so it can add
+ * rows (checked serially anyway), never drop one.  Returns owner reset to -1. */
+static char *flag_unshared_rows(const SSS_IMAT *S, const int *mark, int *owner)
+{
+    const int n = S->num_rows;
+    char *flag = (char *)SSS_calloc((size_t)(n > 0 ? n : 1), 1);
+#pragma omp parallel for schedule(static)
+    for (int i = 0; i < n; ++i) __atomic_store_n(&owner[i], -1, __ATOMIC_RELAXED);
+#pragma omp parallel for schedule(dynamic, 4096)
+    for (int i = 0; i < n; ++i) {
+        if (mark[i] != FGPT) continue;
+        for (int q = S->row_ptr[i]; q < S->row_ptr[i + 1]; ++q)
+            if (mark[S->col_idx[q]] == CGPT) __atomic_store_n(&owner[S->col_idx[q]], i, __ATOMIC_RELAXED);
+        for (int q = S->row_ptr[i]; q < S->row_ptr[i + 1] && !flag[i]; ++q) {
+            const int j = S->col_idx[q];
+            int shares = 0;
+            if (mark[j] != FGPT) continue;
+            for (int r = S->row_ptr[j]; r < S->row_ptr[j + 1]; ++r)
+                if (__atomic_load_n(&owner[S->col_idx[r]], __ATOMIC_RELAXED) == i) { shares = 1; break; }
+            if (!shares) flag[i] = 1;
+        }
+    }
+#pragma omp parallel for schedule(static)
+    for (int i = 0; i < n; ++i) owner[i] = -1;
+    return flag;
+}
+
 /* Classical Ruge-Stueben first pass + C1 fix-up.  Returns the C-point count (or <0). */
 static int rs_split(const SSS_MAT *A, SSS_IMAT *S, SSS_IVEC *vertices)
 {
@@ -325,10 +359,10 @@ static int rs_split(const SSS_MAT *A, SSS_IMAT *S, SSS_IVEC *vertices)
     free(B.pts);
     /* C1 criterion: two strongly coupled F points must share a strong C point. */
     owner = lambda;
-    for (int i = 0; i < n; ++i) owner[i] = -1;
+    char *maybe = flag_unshared_rows(S, mark, owner);   /* the rows this pass can change */
     for (int i = 0; i < n; ++i) {
         int promoted = -1, have_promoted = 0;
-        if (mark[i] != FGPT) continue;
+        if (!maybe[i] || mark[i] != FGPT) continue;
         for (int q = S->row_ptr[i]; q < S->row_ptr[i + 1]; ++q)
             if (mark[S->col_idx[q]] == CGPT) owner[S->col_idx[q]] = i;
         for (int q = S->row_ptr[i]; q < S->row_ptr[i + 1]; ++q) {
@@ -350,6 +384,7 @@ static int rs_split(const SSS_MAT *A, SSS_IMAT *S, SSS_IVEC *vertices)
             }
         }
     }
+    free(maybe);
 
     if (timing)
         fprintf(stderr, "[setup]   RS split: drop+transpose %.3f s, lists %.3f s, first pass %.3f s, C1 %.3f s\n",
@@ -368,10 +403,14 @@ static int cleanup_ff(const SSS_IMAT *S, SSS_IVEC *vertices, int n, int ncoarse)
     int *mark = vertices->d;
     int *tag = (int *)SSS_calloc((size_t)n, sizeof(int));
     int pending = FALSE, pending_owner = -1, tentative = -1;
+    char *maybe = flag_unshared_rows(S, mark, tag);   /* the rows this pass can change; tag = -1 */
 
-    for (int i = 0; i < n; ++i) tag[i] = -1;
     for (int i = 0; i < n; ++i) {
         if (mark[i] != FGPT) continue;
+        if (!maybe[i]) {   /* no unshared pair: the row only resets the tentative C point */
+            if (pending_owner != i) tentative = -1;
+            continue;
+        }
         for (int q = S->row_ptr[i]; q < S->row_ptr[i + 1]; ++q) {
             int j = S->col_idx[q];
             tag[j] = (mark[j] == CGPT) ? i : -1;
@@ -403,6 +442,7 @@ static int cleanup_ff(const SSS_IMAT *S, SSS_IVEC *vertices, int n, int ncoarse)
             break;
         }
     }
+    free(maybe);
     free(tag);
     return ncoarse;
 }
