@@ -206,6 +206,7 @@ static int bucket_max_head(measure_buckets *B)
     if (B->top <= 0) return -1;
     bucket_fifo *q = &B->b[B->top];
     while (q->e[q->head].ver != B->pts[q->e[q->head].pt].ver) q->head++;
+    for (size_t t = q->head + 1; t < q->tail && t < q->head + 4; ++t) __builtin_prefetch(&B->pts[q->e[t].pt]);
     return q->e[q->head].pt;
 }
 
@@ -306,6 +307,31 @@ static int rs_split(const SSS_MAT *A, SSS_IMAT *S, SSS_IVEC *vertices)
         if (c < 0) {
             printf("### ERROR: RS coarsening ran out of candidates (%d undecided)\n", undecided);
             break;
+        }
+        /* The pass is bound by cache misses on the neighbourhood of each pick (≈35 dependent
+         * record / row accesses per pick, spread over three grid planes): request them all up
+         * front -- the records of c's neighbours, their S rows, and the records of the S rows of
+         * the neighbours that are about to become F. */
+        {   /* and the rows of the next candidates in the top bucket (the likely next picks) */
+            const bucket_fifo *tq = &B.b[B.top];
+            for (size_t t = tq->head + 1; t < tq->tail && t < tq->head + 3; ++t) {
+                const int nx = tq->e[t].pt;
+                __builtin_prefetch(&ST.row_ptr[nx]);
+                __builtin_prefetch(ST.col_idx + ST.row_ptr[nx]);
+                __builtin_prefetch(S->col_idx + S->row_ptr[nx]);
+            }
+        }
+        for (int q = ST.row_ptr[c]; q < ST.row_ptr[c + 1]; ++q) {
+            const int j = ST.col_idx[q];
+            __builtin_prefetch(&P[j], 1);
+            __builtin_prefetch(&S->row_ptr[j]);
+        }
+        for (int q = S->row_ptr[c]; q < S->row_ptr[c + 1]; ++q) __builtin_prefetch(&P[S->col_idx[q]], 1);
+        for (int q = ST.row_ptr[c]; q < ST.row_ptr[c + 1]; ++q) __builtin_prefetch(S->col_idx + S->row_ptr[ST.col_idx[q]]);
+        for (int q = ST.row_ptr[c]; q < ST.row_ptr[c + 1]; ++q) {
+            const int j = ST.col_idx[q];
+            if (P[j].mark != UNPT) continue;
+            for (int r = S->row_ptr[j]; r < S->row_ptr[j + 1]; ++r) __builtin_prefetch(&P[S->col_idx[r]], 1);
         }
         mc = P[c].lambda;
         if (mc == 0) printf("### WARNING: Head of the list has measure 0!\n");
