@@ -744,15 +744,23 @@ SSS_MAT SSS_blas_mat_rap(const SSS_MAT *R, const SSS_MAT *A, const SSS_MAT *P)
     const double *rv = R->val, *av = A->val, *pv = P->val;
     int64_t *start = (int64_t *)calloc((size_t)nc + 1, sizeof(int64_t));
     SSS_MAT C;
+    int too_big = 0;
 
     C.num_rows = nc;
     C.num_cols = nc;
     C.row_ptr = (int *)SSS_calloc((size_t)nc + 1, sizeof(int));
+    C.col_idx = NULL;
+    C.val = NULL;
+    C.num_nnzs = 0;
 
+    /* One parallel region for both passes: each thread's marker arrays are initialised once.
+     * Markers hold the coarse row being built: ic in the counting pass, nc + ic in the filling
+     * pass, so the second pass needs no reset. */
 #pragma omp parallel
     {
         int *seen_f = (int *)malloc(sizeof(int) * (size_t)(nf > 0 ? nf : 1));
         int *seen_c = (int *)malloc(sizeof(int) * (size_t)(nc > 0 ? nc : 1));
+        int *slot = (int *)malloc(sizeof(int) * (size_t)(nc > 0 ? nc : 1));
         for (int i = 0; i < nf; ++i) seen_f[i] = -1;
         for (int i = 0; i < nc; ++i) seen_c[i] = -1;
 #pragma omp for schedule(dynamic, 256)
@@ -771,57 +779,52 @@ SSS_MAT SSS_blas_mat_rap(const SSS_MAT *R, const SSS_MAT *A, const SSS_MAT *P)
             }
             start[ic + 1] = cnt;
         }
-        free(seen_f);
-        free(seen_c);
-    }
-    for (int ic = 0; ic < nc; ++ic) start[ic + 1] += start[ic];
-    if (start[nc] > INT32_MAX) {
-        printf("### ERROR: RAP product has %lld nonzeros (int32 index limit)\n", (long long)start[nc]);
-        SSS_exit_on_errcode(ERROR_MAT_SIZE, __func__);
-    }
-    C.num_nnzs = (int)start[nc];
-    for (int ic = 0; ic <= nc; ++ic) C.row_ptr[ic] = (int)start[ic];
-    C.col_idx = (int *)SSS_calloc((size_t)C.num_nnzs, sizeof(int));
-    C.val = (double *)SSS_calloc((size_t)C.num_nnzs, sizeof(double));
-
-#pragma omp parallel
-    {
-        int *seen_f = (int *)malloc(sizeof(int) * (size_t)(nf > 0 ? nf : 1));
-        int *seen_c = (int *)malloc(sizeof(int) * (size_t)(nc > 0 ? nc : 1));
-        int *slot = (int *)malloc(sizeof(int) * (size_t)(nc > 0 ? nc : 1));
-        for (int i = 0; i < nf; ++i) seen_f[i] = -1;
-        for (int i = 0; i < nc; ++i) seen_c[i] = -1;
+#pragma omp single
+        {
+            for (int ic = 0; ic < nc; ++ic) start[ic + 1] += start[ic];
+            if (start[nc] > INT32_MAX) {
+                too_big = 1;
+            } else {
+                C.num_nnzs = (int)start[nc];
+                for (int ic = 0; ic <= nc; ++ic) C.row_ptr[ic] = (int)start[ic];
+                C.col_idx = (int *)SSS_calloc((size_t)C.num_nnzs, sizeof(int));
+                C.val = (double *)SSS_calloc((size_t)C.num_nnzs, sizeof(double));
+            }
+        }   /* implicit barrier */
+        if (!too_big) {
 #pragma omp for schedule(dynamic, 256)
-        for (int ic = 0; ic < nc; ++ic) {
-            int pos = C.row_ptr[ic];
-            seen_c[ic] = ic;
-            slot[ic] = pos;
-            C.col_idx[pos] = ic;
-            C.val[pos] = 0.0;
-            pos++;
-            for (int q1 = ri[ic]; q1 < ri[ic + 1]; ++q1) {
-                const double r = rv[q1];
-                const int i1 = rj[q1];
-                for (int q2 = ai[i1]; q2 < ai[i1 + 1]; ++q2) {
-                    const double ra = r * av[q2];
-                    const int i2 = aj[q2];
-                    if (seen_f[i2] != ic) {
-                        seen_f[i2] = ic;
-                        for (int q3 = pi[i2]; q3 < pi[i2 + 1]; ++q3) {
-                            const double rap = ra * pv[q3];
-                            const int i3 = pj[q3];
-                            if (seen_c[i3] != ic) {
-                                seen_c[i3] = ic;
-                                slot[i3] = pos;
-                                C.val[pos] = rap;
-                                C.col_idx[pos] = i3;
-                                pos++;
-                            } else {
-                                C.val[slot[i3]] += rap;
+            for (int ic = 0; ic < nc; ++ic) {
+                const int mk = nc + ic;
+                int pos = C.row_ptr[ic];
+                seen_c[ic] = mk;
+                slot[ic] = pos;
+                C.col_idx[pos] = ic;
+                C.val[pos] = 0.0;
+                pos++;
+                for (int q1 = ri[ic]; q1 < ri[ic + 1]; ++q1) {
+                    const double r = rv[q1];
+                    const int i1 = rj[q1];
+                    for (int q2 = ai[i1]; q2 < ai[i1 + 1]; ++q2) {
+                        const double ra = r * av[q2];
+                        const int i2 = aj[q2];
+                        if (seen_f[i2] != mk) {
+                            seen_f[i2] = mk;
+                            for (int q3 = pi[i2]; q3 < pi[i2 + 1]; ++q3) {
+                                const double rap = ra * pv[q3];
+                                const int i3 = pj[q3];
+                                if (seen_c[i3] != mk) {
+                                    seen_c[i3] = mk;
+                                    slot[i3] = pos;
+                                    C.val[pos] = rap;
+                                    C.col_idx[pos] = i3;
+                                    pos++;
+                                } else {
+                                    C.val[slot[i3]] += rap;
+                                }
                             }
+                        } else {
+                            for (int q3 = pi[i2]; q3 < pi[i2 + 1]; ++q3) C.val[slot[pj[q3]]] += ra * pv[q3];
                         }
-                    } else {
-                        for (int q3 = pi[i2]; q3 < pi[i2 + 1]; ++q3) C.val[slot[pj[q3]]] += ra * pv[q3];
                     }
                 }
             }
@@ -829,6 +832,10 @@ SSS_MAT SSS_blas_mat_rap(const SSS_MAT *R, const SSS_MAT *A, const SSS_MAT *P)
         free(seen_f);
         free(seen_c);
         free(slot);
+    }
+    if (too_big) {
+        printf("### ERROR: RAP product has %lld nonzeros (int32 index limit)\n", (long long)start[nc]);
+        SSS_exit_on_errcode(ERROR_MAT_SIZE, __func__);
     }
     free(start);
     return C;
