@@ -15,7 +15,7 @@ import pytest
 
 import amg_amd as A
 from amg_amd import workloads as W
-from conftest import build_hierarchy, quiet_ctx
+from conftest import BUS_MTX, build_hierarchy, quiet_ctx
 
 pytestmark = pytest.mark.gpu
 
@@ -46,11 +46,13 @@ def _iterate(D, n, cycles=4):
     return np.array(rel), D.download(0, "x")
 
 
-@pytest.mark.parametrize("case", ["p7_40", "a27_16", "circ60k"])
+@pytest.mark.parametrize("case", ["p7_40", "a27_16", "circ60k", "bus"])
 @pytest.mark.parametrize("mode", [("exact", "krylov"), ("hybrid", "direct")])
 def test_pipelined_setup_matches_sequential(case, mode):
     keep = None
-    if case.startswith("p7"):
+    if case == "bus":
+        M = A.read_mtx(BUS_MTX)
+    elif case.startswith("p7"):
         M = A.generate(7, 40)
     elif case.startswith("a27"):
         M = A.generate(27, 16)
