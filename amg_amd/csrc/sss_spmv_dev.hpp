@@ -297,21 +297,36 @@ __device__ __forceinline__ void stage_sorted(double *__restrict__ sm, int k0, in
 
 // Value-dictionary sorted tiles: stage_sorted with the value of slot k read from the block's
 // dictionary in LDS (vd[vi[k]], the same bit pattern pv[k] held).
+// The slots of one pass of the loop below (U per thread): stage_dict loads the first pass ahead of
+// the dictionary barrier, so the slot stream is in flight while the dictionary arrives.
+constexpr int kVdictU = 8;
+__device__ __forceinline__ void vdict_load(int kb, int k1, const unsigned *__restrict__ pk,
+                                           const unsigned char *__restrict__ vi, unsigned (&q)[kVdictU],
+                                           unsigned (&w)[kVdictU])
+{
+#pragma unroll
+    for (int u = 0; u < kVdictU; ++u) {
+        const int k = kb + u * kBlock;
+        q[u] = k < k1 ? pk[k] : 0u;
+        w[u] = k < k1 ? vi[k] : 0u;
+    }
+}
 template <class Fetch>
 __device__ __forceinline__ void stage_vdict(double *__restrict__ sm, int k0, int k1, const unsigned *__restrict__ pk,
                                             const unsigned char *__restrict__ vi, const double *vd, int2 base, int r0,
-                                            double *diag, Fetch fetch)
+                                            double *diag, Fetch fetch, const unsigned (*pre_q)[kVdictU] = nullptr,
+                                            const unsigned (*pre_w)[kVdictU] = nullptr)
 {
-    constexpr int U = 8;
+    constexpr int U = kVdictU;
     constexpr unsigned kMask = kTileEntries - 1;
     for (int kb = k0 + (int)threadIdx.x; kb < k1; kb += U * kBlock) {
         unsigned q[U], w[U];
         double a[U], xv[U];
+        if (pre_q && kb == k0 + (int)threadIdx.x) {
 #pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const int k = kb + u * kBlock;
-            q[u] = k < k1 ? pk[k] : 0u;
-            w[u] = k < k1 ? vi[k] : 0u;
+            for (int u = 0; u < U; ++u) q[u] = (*pre_q)[u], w[u] = (*pre_w)[u];
+        } else {
+            vdict_load(kb, k1, pk, vi, q, w);
         }
 #pragma unroll
         for (int u = 0; u < U; ++u) {
@@ -341,12 +356,16 @@ __device__ __forceinline__ void stage_dict(double *__restrict__ sm, int k0, int 
                                            Fetch fetch)
 {
     const int4 p = dt.pd[bid];
-    for (int t = threadIdx.x; t < p.w; t += kBlock) ds.vd[t] = dt.vd[p.z + t];
     if (dt.vi) {   // value-dictionary sorted tiles: stage_sorted with a[k] = vd[vi[k]]
+        unsigned q[kVdictU], w[kVdictU];
+        vdict_load(k0 + (int)threadIdx.x, k1, dt.pk, dt.vi, q, w);   // in flight across the barrier
+        const int2 base = dt.pb[bid];
+        for (int t = threadIdx.x; t < p.w; t += kBlock) ds.vd[t] = dt.vd[p.z + t];
         __syncthreads();
-        stage_vdict(sm, k0, k1, dt.pk, dt.vi, ds.vd, dt.pb[bid], r0, diag, fetch);
+        stage_vdict(sm, k0, k1, dt.pk, dt.vi, ds.vd, base, r0, diag, fetch, &q, &w);
         return;
     }
+    for (int t = threadIdx.x; t < p.w; t += kBlock) ds.vd[t] = dt.vd[p.z + t];
     for (int t = threadIdx.x; t < p.y; t += kBlock) ds.dd[t] = dt.dd[p.x + t];
     for (int r = r0 + (int)threadIdx.x; r < r1; r += kBlock) {
         const int a = max(rp[r], k0), e = min(rp[r + 1], k1);
