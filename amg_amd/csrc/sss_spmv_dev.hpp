@@ -646,21 +646,14 @@ __device__ __forceinline__ void merged_sums(int k0, int k1, const unsigned *__re
     const int lane = threadIdx.x & 63;
 #pragma unroll
     for (int u = 0; u < G; ++u) s0[u] = 0.0, s1[u] = 0.0;
-    // software-pipelined: the next U entries' loads are issued before this pass's gathers and sums
-    unsigned q[U], qn[U];
-    double a[U], an[U];
-#pragma unroll
-    for (int t = 0; t < U; ++t) {
-        const int kk = k0 + lane + 64 * t;
-        q[t] = kk < k1 ? mk[kk] : 0u;
-        a[t] = kk < k1 ? mv[kk] : 0.0;
-    }
     for (int k = k0 + lane; k < k1; k += 64 * U) {
+        unsigned q[U];
+        double a[U];
 #pragma unroll
         for (int t = 0; t < U; ++t) {
-            const int kk = k + 64 * (U + t);
-            qn[t] = kk < k1 ? mk[kk] : 0u;
-            an[t] = kk < k1 ? mv[kk] : 0.0;
+            const int kk = k + 64 * t;
+            q[t] = kk < k1 ? mk[kk] : 0u;
+            a[t] = kk < k1 ? mv[kk] : 0.0;
         }
 #pragma unroll
         for (int t = 0; t < U; ++t) {
@@ -673,8 +666,6 @@ __device__ __forceinline__ void merged_sums(int k0, int k1, const unsigned *__re
                 if (S == 2) s1[u] += key == (unsigned)(8 + u) ? p : 0.0;
             }
         }
-#pragma unroll
-        for (int t = 0; t < U; ++t) q[t] = qn[t], a[t] = an[t];
     }
 #pragma unroll
     for (int u = 0; u < G; ++u)
