@@ -350,19 +350,27 @@ __device__ __forceinline__ void stage_vdict(double *__restrict__ sm, int k0, int
 // the segment (slots are in column order); col = row(pos) + dd[offset index], a = vd[value index];
 // the product lands at sm[pos], so the LDS image is stage_products_f's.  Starts with a workgroup
 // barrier of its own (the block's dictionaries and the position -> row map go to LDS first).
-template <class Fetch>
+// PRE: issue the first pass of value-dictionary slot loads before the dictionary barrier (the
+// relaxation kernels gain from it; measured slower in the SpMV kernels, which keep the plain order)
+template <bool PRE = true, class Fetch>
 __device__ __forceinline__ void stage_dict(double *__restrict__ sm, int k0, int k1, const DevDict &dt, int bid,
                                            int r0, int r1, const int *__restrict__ rp, DictSmem &ds, double *diag,
                                            Fetch fetch)
 {
     const int4 p = dt.pd[bid];
     if (dt.vi) {   // value-dictionary sorted tiles: stage_sorted with a[k] = vd[vi[k]]
-        unsigned q[kVdictU], w[kVdictU];
-        vdict_load(k0 + (int)threadIdx.x, k1, dt.pk, dt.vi, q, w);   // in flight across the barrier
-        const int2 base = dt.pb[bid];
-        for (int t = threadIdx.x; t < p.w; t += kBlock) ds.vd[t] = dt.vd[p.z + t];
-        __syncthreads();
-        stage_vdict(sm, k0, k1, dt.pk, dt.vi, ds.vd, base, r0, diag, fetch, &q, &w);
+        if constexpr (PRE) {
+            unsigned q[kVdictU], w[kVdictU];
+            vdict_load(k0 + (int)threadIdx.x, k1, dt.pk, dt.vi, q, w);   // in flight across the barrier
+            const int2 base = dt.pb[bid];
+            for (int t = threadIdx.x; t < p.w; t += kBlock) ds.vd[t] = dt.vd[p.z + t];
+            __syncthreads();
+            stage_vdict(sm, k0, k1, dt.pk, dt.vi, ds.vd, base, r0, diag, fetch, &q, &w);
+        } else {
+            for (int t = threadIdx.x; t < p.w; t += kBlock) ds.vd[t] = dt.vd[p.z + t];
+            __syncthreads();
+            stage_vdict(sm, k0, k1, dt.pk, dt.vi, ds.vd, dt.pb[bid], r0, diag, fetch);
+        }
         return;
     }
     for (int t = threadIdx.x; t < p.w; t += kBlock) ds.vd[t] = dt.vd[p.z + t];
@@ -463,7 +471,7 @@ __device__ __forceinline__ double csr_block_rows(const BlkT *__restrict__ blk, c
         const int r = r0 + (int)threadIdx.x;
         int ra = 0, re = 0;
         if (r < r1) ra = rp[r], re = rp[r + 1];   // issued ahead of the tile
-        if (ds) stage_dict(sm.v, k0, k1, *dt, bid, r0, r1, rp, *ds, (double *)nullptr, fetch);
+        if (ds) stage_dict<false>(sm.v, k0, k1, *dt, bid, r0, r1, rp, *ds, (double *)nullptr, fetch);
         else if (pk) stage_sorted(sm.v, k0, k1, pk, pv, pb[bid], r0, (double *)nullptr, fetch);
         else stage_products(sm.v, k0, k1, ci, v, x);
         __syncthreads();
@@ -475,7 +483,7 @@ __device__ __forceinline__ double csr_block_rows(const BlkT *__restrict__ blk, c
         double s = 0.0;
         for (int base = k0; base < k1; base += kTileEntries) {
             const int m = min(kTileEntries, k1 - base);
-            if (ds) stage_dict(sm.v, base, base + m, *dt, bid, r0, r1, rp, *ds, (double *)nullptr, fetch);
+            if (ds) stage_dict<false>(sm.v, base, base + m, *dt, bid, r0, r1, rp, *ds, (double *)nullptr, fetch);
             else if (pk) stage_sorted(sm.v, base, base + m, pk, pv, pb[bid], r0, (double *)nullptr, fetch);
             else stage_products(sm.v, base, base + m, ci, v, x);
             __syncthreads();

@@ -321,20 +321,19 @@ def main():
     ws = os.environ.get("WORLD_SIZE")
     if ws is None and args.gpus is not None and args.gpus > 1:
         sys.exit(spawn_ranks(args.gpus))   # before anything touches the GPU
+    # stdout carries the JSON record only: library banners (gloo's peer lines at the process group's
+    # start, RCCL's version block) and the C setup tables go to stderr
+    sys.stdout.flush()
+    json_fd = os.dup(1)
+    os.dup2(2, 1)
     D = Dist()
     if args.gpus is not None and args.gpus != D.world:
         raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={D.world}")
     if args.probe_ranks:
         # one write() per line: the ranks share the launcher's stdout pipe
-        sys.stdout.write(json.dumps({"rank": D.rank, "world": D.world, "local_rank": D.local_rank}) + "\n")
-        sys.stdout.flush()
+        os.write(json_fd, (json.dumps({"rank": D.rank, "world": D.world, "local_rank": D.local_rank}) + "\n").encode())
         D.close()
         return
-    # stdout carries the JSON record only: library banners (RCCL's version block, gloo's peer
-    # lines) and the C setup tables go to stderr
-    sys.stdout.flush()
-    json_fd = os.dup(1)
-    os.dup2(2, 1)
     # the BASELINE.json config of this rank count (configs[2]: 512^3 on 8 GPUs; configs[4]: 27-pt
     # 256^3 on 4 GPUs; the metric's 64M-row 400^3 otherwise)
     circuit = args.workload == "circuit"
