@@ -111,7 +111,7 @@ ABI_SYMBOLS = [
     "SSS_amg_save", "SSS_amg_load",
     "sss_hip_coarse_solve", "sss_hip_smooth", "sss_hip_sync", "sss_hip_level_info_get", "sss_hip_num_levels",
     "sss_hip_spmv_plan_create", "sss_hip_spmv_plan_destroy", "sss_hip_spmv", "sss_hip_host_spmv",
-    "sss_hip_host_smooth", "sss_hip_host_coarse_solve", "sss_hip_time_level0_spmv", "sss_hip_time_iterations",
+    "sss_hip_host_smooth", "sss_hip_host_coarse_solve", "sss_hip_host_cache_clear", "sss_hip_time_level0_spmv", "sss_hip_time_iterations",
     "sss_hip_time_level0_spmv_csr",
     "sss_gen_stencil",
     "sss_hip_rccl_unique_id", "sss_hip_comm_rccl", "sss_hip_comm_host", "sss_hip_comm_destroy",

@@ -1036,21 +1036,146 @@ extern "C" int sss_hip_time_iterations(sss_hip_hier *h, int reps, double *avg_ms
 }
 
 // ---- host-memory convenience wrappers for the exported reference entry points ----------------
+// The reference's spmv_cuda re-copies the whole CSR on every call (Solve/SSS_cuda.cu:124-139).
+// Here the device form of a matrix (and of a smoother plan / coarse solver built on it) is kept in
+// a small cache keyed by the matrix contents: a content hash of row_ptr / col_idx / val (host
+// memory, row-parallel; far cheaper than the upload and the format build) plus the dimensions and
+// the use.  A caller that loops over these entry points with the same operator pays the upload
+// once; a caller that changes the matrix in place gets a fresh upload (the hash changes).
+// sss_hip_host_cache_clear() releases everything.
+extern char **environ;
+
 namespace {
 struct HostCSR {
     DevCSR d;
     ~HostCSR() { devcsr_free(d); }
 };
+struct HostSmooth {
+    DevCSR d;
+    SmootherPlan sp;
+    ~HostSmooth()
+    {
+        smoother_free(sp);
+        devcsr_free(d);
+    }
+};
+struct HostCoarse {
+    DevCSR d;
+    CoarseDirect cd;
+    bool direct = false;
+    CoarseKrylov *k = nullptr;
+    ~HostCoarse()
+    {
+        if (direct) coarse_direct_free(cd);
+        coarse_krylov_destroy(k);
+        devcsr_free(d);
+    }
+};
+
+inline unsigned long long mix64(unsigned long long h, unsigned long long w)
+{
+    h ^= w * 0x9E3779B97F4A7C15ull;
+    h = (h << 31) | (h >> 33);
+    return h * 0xC2B2AE3D27D4EB4Full;
+}
+// content hash of n bytes: fixed chunks hashed in parallel, combined in chunk order
+unsigned long long hash_bytes(const void *p, size_t n, unsigned long long seed)
+{
+    const unsigned char *b = static_cast<const unsigned char *>(p);
+    constexpr size_t kChunk = (size_t)1 << 20;
+    const int nc = (int)((n + kChunk - 1) / kChunk);
+    std::vector<unsigned long long> part((size_t)std::max(nc, 1), 0);
+    parallel_chunks(nc, 1, [&](int c0, int c1) {
+        for (int c = c0; c < c1; ++c) {
+            const size_t lo = (size_t)c * kChunk, hi = std::min(n, lo + kChunk);
+            unsigned long long h = 0x2545F4914F6CDD1Dull ^ (unsigned long long)c;
+            size_t i = lo;
+            for (; i + 8 <= hi; i += 8) {
+                unsigned long long w;
+                std::memcpy(&w, b + i, 8);
+                h = mix64(h, w);
+            }
+            for (; i < hi; ++i) h = mix64(h, b[i]);
+            part[(size_t)c] = h;
+        }
+    });
+    unsigned long long h = mix64(seed, n);
+    for (auto v : part) h = mix64(h, v);
+    return h;
+}
+unsigned long long matrix_key(const SSS_MAT &A, unsigned long long use)
+{
+    int dev = 0;
+    (void)hipGetDevice(&dev);   // device objects belong to the current device
+    unsigned long long h = mix64(mix64(use, (unsigned long long)dev), (unsigned long long)A.num_rows);
+    // the upload and plan builders read SSS_HIP_* switches (formats, kernel paths): part of the key
+    for (char **e = environ; e && *e; ++e)
+        if (std::strncmp(*e, "SSS_HIP_", 8) == 0) h = hash_bytes(*e, std::strlen(*e), h);
+    h = mix64(h, (unsigned long long)A.num_cols);
+    h = mix64(h, (unsigned long long)A.num_nnzs);
+    h = hash_bytes(A.row_ptr, sizeof(int) * ((size_t)A.num_rows + 1), h);
+    h = hash_bytes(A.col_idx, sizeof(int) * (size_t)A.num_nnzs, h);
+    return hash_bytes(A.val, sizeof(double) * (size_t)A.num_nnzs, h);
+}
+
+struct PreparedCache {
+    struct Entry {
+        unsigned long long key;
+        std::shared_ptr<void> obj;
+        unsigned long long tick;
+    };
+    std::mutex mu;
+    std::vector<Entry> e;
+    unsigned long long tick = 0;
+    static constexpr size_t kMax = 4;
+    template <class T, class Build>
+    std::shared_ptr<T> get(unsigned long long key, Build build)
+    {
+        {
+            std::lock_guard<std::mutex> lk(mu);
+            for (auto &x : e)
+                if (x.key == key) {
+                    x.tick = ++tick;
+                    return std::static_pointer_cast<T>(x.obj);
+                }
+        }
+        std::shared_ptr<T> obj = build();
+        if (!obj) return obj;
+        std::lock_guard<std::mutex> lk(mu);
+        if (e.size() >= kMax) {
+            auto old = std::min_element(e.begin(), e.end(), [](const Entry &a, const Entry &b) { return a.tick < b.tick; });
+            e.erase(old);
+        }
+        e.push_back({key, obj, ++tick});
+        return obj;
+    }
+    void clear()
+    {
+        std::lock_guard<std::mutex> lk(mu);
+        e.clear();
+    }
+};
+PreparedCache &prepared()
+{
+    static PreparedCache *c = new PreparedCache();   // objects hold device memory: never torn down at exit
+    return *c;
+}
 }  // namespace
+
+extern "C" void sss_hip_host_cache_clear(void) { prepared().clear(); }
 
 extern "C" int sss_hip_host_spmv(int op, double alpha, const SSS_MAT *A, const double *x, const double *b,
                                  double *y, int cap)
 {
     if (sss_hip_device_count() <= 0) return ERROR_MISC;
-    HostCSR M;
     sss_hip_opts o;
     sss_hip_opts_default(&o);   // SSS_HIP_SORTED_TILES; always the reference's summation order here
-    if (devcsr_upload(M.d, *A, -1, level_encoding(o) & (kEncSortedTiles | kEncDict))) return ERROR_MISC;
+    const int enc = level_encoding(o) & (kEncSortedTiles | kEncDict);
+    auto M = prepared().get<HostCSR>(matrix_key(*A, 0x5350ull ^ ((unsigned long long)enc << 8)), [&] {
+        auto m = std::make_shared<HostCSR>();
+        return devcsr_upload(m->d, *A, -1, enc) ? nullptr : m;
+    });
+    if (!M) return ERROR_MISC;
     const size_t ny = (size_t)A->num_rows, nx = (size_t)A->num_cols;
     double *dx = dev_alloc<double>(nx), *dy = dev_alloc<double>(ny), *db = dev_alloc<double>(ny);
     int rc = 0;
@@ -1058,7 +1183,7 @@ extern "C" int sss_hip_host_spmv(int op, double alpha, const SSS_MAT *A, const d
     if (!rc && hipMemcpy(dx, x, sizeof(double) * nx, hipMemcpyHostToDevice) != hipSuccess) rc = ERROR_MISC;
     if (!rc && hipMemcpy(dy, y, sizeof(double) * ny, hipMemcpyHostToDevice) != hipSuccess) rc = ERROR_MISC;
     if (!rc && b && hipMemcpy(db, b, sizeof(double) * ny, hipMemcpyHostToDevice) != hipSuccess) rc = ERROR_MISC;
-    if (!rc) rc = launch_spmv(M.d, op, alpha, dx, db, dy, cap, nullptr, nullptr);
+    if (!rc) rc = launch_spmv(M->d, op, alpha, dx, db, dy, cap, nullptr, nullptr);
     if (!rc && hipMemcpy(y, dy, sizeof(double) * ny, hipMemcpyDeviceToHost) != hipSuccess) rc = ERROR_MISC;
     dev_free(dx);
     dev_free(dy);
@@ -1083,24 +1208,28 @@ extern "C" int sss_hip_host_smooth(const SSS_SMTR *s, int post)
     const int lo = desc ? in : i1, hi = (desc ? i1 : in) + 1;
     if (natural && (lo < 0 || hi > n)) return ERROR_INPUT_PAR;
     if (natural && lo >= hi) return 0;
-    HostCSR M;
-    SmootherPlan sp;
-    if (devcsr_upload(M.d, *s->A)) return ERROR_MISC;
-    if (natural ? smoother_build_natural(sp, *s->A, lo, hi)
-                : smoother_build(sp, *s->A, use_cf ? s->ordering : nullptr,
-                                 s->smoother == SSS_SM_JACOBI ? SSS_HIP_SMOOTH_JACOBI : SSS_HIP_SMOOTH_EXACT)) {
-        smoother_free(sp);
-        return ERROR_MISC;
-    }
+    const int kind = s->smoother == SSS_SM_JACOBI ? SSS_HIP_SMOOTH_JACOBI : SSS_HIP_SMOOTH_EXACT;
+    unsigned long long use = mix64(0x534Dull, natural ? 1 : 0);
+    use = mix64(use, (unsigned long long)kind);
+    if (natural) use = mix64(mix64(use, (unsigned long long)lo), (unsigned long long)hi);
+    if (use_cf) use = hash_bytes(s->ordering, sizeof(int) * (size_t)n, use);
+    auto M = prepared().get<HostSmooth>(matrix_key(*s->A, use), [&] {
+        auto m = std::make_shared<HostSmooth>();
+        if (devcsr_upload(m->d, *s->A)) return std::shared_ptr<HostSmooth>();
+        if (natural ? smoother_build_natural(m->sp, *s->A, lo, hi)
+                    : smoother_build(m->sp, *s->A, use_cf ? s->ordering : nullptr, kind))
+            return std::shared_ptr<HostSmooth>();
+        return m;
+    });
+    if (!M) return ERROR_MISC;
     double *dx = dev_alloc<double>((size_t)n), *db = dev_alloc<double>((size_t)n);
     int rc = (!dx || !db) ? ERROR_ALLOC_MEM : 0;
     if (!rc && hipMemcpy(dx, s->x->d, sizeof(double) * n, hipMemcpyHostToDevice) != hipSuccess) rc = ERROR_MISC;
     if (!rc && hipMemcpy(db, s->b->d, sizeof(double) * n, hipMemcpyHostToDevice) != hipSuccess) rc = ERROR_MISC;
-    if (!rc) rc = smoother_run(sp, M.d, db, dx, s->nsweeps, nullptr, nullptr, nullptr, nullptr, false, natural && desc);
+    if (!rc) rc = smoother_run(M->sp, M->d, db, dx, s->nsweeps, nullptr, nullptr, nullptr, nullptr, false, natural && desc);
     if (!rc && hipMemcpy(s->x->d, dx, sizeof(double) * n, hipMemcpyDeviceToHost) != hipSuccess) rc = ERROR_MISC;
     dev_free(dx);
     dev_free(db);
-    smoother_free(sp);
     return rc;
 }
 
@@ -1109,23 +1238,31 @@ extern "C" int sss_hip_host_coarse_solve(SSS_MAT *A, SSS_VEC *b, SSS_VEC *x, dou
 {
     if (sss_hip_device_count() <= 0) return ERROR_MISC;
     const int n = A->num_rows;
-    HostCSR M;
-    if (devcsr_upload(M.d, *A)) return ERROR_MISC;
+    const bool direct = coarse_mode == SSS_HIP_COARSE_DIRECT && n <= 20000;
+    auto M = prepared().get<HostCoarse>(
+        matrix_key(*A, mix64(mix64(0x4353ull, direct ? 1 : 0), (unsigned long long)row_cap)), [&] {
+            auto m = std::make_shared<HostCoarse>();
+            if (devcsr_upload(m->d, *A)) return std::shared_ptr<HostCoarse>();
+            if (direct) {
+                if (coarse_direct_build(m->cd, *A, nullptr)) return std::shared_ptr<HostCoarse>();
+                m->direct = true;
+            } else {
+                m->k = coarse_krylov_create(m->d, row_cap, nullptr);
+                if (!m->k) return std::shared_ptr<HostCoarse>();
+            }
+            return m;
+        });
+    if (!M) return ERROR_MISC;
     double *dx = dev_alloc<double>((size_t)n), *db = dev_alloc<double>((size_t)n);
     int rc = (!dx || !db) ? ERROR_ALLOC_MEM : 0;
     if (!rc && hipMemcpy(dx, x->d, sizeof(double) * n, hipMemcpyHostToDevice) != hipSuccess) rc = ERROR_MISC;
     if (!rc && hipMemcpy(db, b->d, sizeof(double) * n, hipMemcpyHostToDevice) != hipSuccess) rc = ERROR_MISC;
     if (!rc) {
-        if (coarse_mode == SSS_HIP_COARSE_DIRECT && n <= 20000) {
-            CoarseDirect cd;
-            rc = coarse_direct_build(cd, *A, nullptr);
-            if (!rc) rc = coarse_direct_apply(cd, db, dx, nullptr);
+        if (direct) {
+            rc = coarse_direct_apply(M->cd, db, dx, nullptr);
             if (!rc && hipDeviceSynchronize() != hipSuccess) rc = ERROR_MISC;
-            coarse_direct_free(cd);
         } else {
-            CoarseKrylov *k = coarse_krylov_create(M.d, row_cap, nullptr);
-            rc = k ? coarse_krylov_solve(k, M.d, db, dx, ctol, nullptr) : ERROR_ALLOC_MEM;
-            coarse_krylov_destroy(k);
+            rc = coarse_krylov_solve(M->k, M->d, db, dx, ctol, nullptr);
         }
     }
     if (!rc && hipMemcpy(x->d, dx, sizeof(double) * n, hipMemcpyDeviceToHost) != hipSuccess) rc = ERROR_MISC;

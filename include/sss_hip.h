@@ -155,6 +155,10 @@ int sss_hip_spmv(const sss_hip_spmv_plan *p, int op, double alpha, const int *d_
 int sss_hip_host_spmv(int op, double alpha, const SSS_MAT *A, const double *x, const double *b,
                       double *y, int cap);
 int sss_hip_host_smooth(const SSS_SMTR *s, int post);
+/* The three host-memory entry points keep the device form of their operator (keyed by a content
+ * hash of the CSR arrays, the use and the device) in a small cache, so a caller that loops over
+ * them with the same matrix uploads it once; this releases the cached device objects. */
+void sss_hip_host_cache_clear(void);
 int sss_hip_host_coarse_solve(SSS_MAT *A, SSS_VEC *b, SSS_VEC *x, double ctol, int coarse_mode,
                               int row_cap);
 

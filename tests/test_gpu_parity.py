@@ -94,6 +94,30 @@ def test_spmv_bitwise_all_levels(request, hname, op, row_path):
             assert np.array_equal(y_gpu.view(np.uint64), y_ref.view(np.uint64)), (hname, l, name, op)
 
 
+def test_host_entry_cache_follows_matrix_contents():
+    """The host-memory entry points keep the device form of their operator between calls (keyed by
+    a content hash): repeated calls give the oracle's result, and a value changed in place is seen
+    by the next call (no stale device copy)."""
+    rng = np.random.default_rng(11)
+    n = 5000
+    lens = rng.integers(1, 30, n)
+    rp = np.concatenate([[0], np.cumsum(lens)]).astype(np.int32)
+    ci = rng.integers(0, n, rp[-1]).astype(np.int32)
+    v = rng.standard_normal(rp[-1])
+    M = A.NumpyCSR(rp, ci, v)
+    ora = oracle.load()
+    x = rng.standard_normal(n)
+    _lib().sss_hip_host_cache_clear()
+    for it in range(3):
+        if it == 2:
+            M.v[17] += 1.0   # in place: same pointers, new contents
+        y_gpu, y_ref = np.zeros(n), np.zeros(n)
+        assert _lib().sss_hip_host_spmv(A.SPMV["mxy"], 1.0, C.byref(M.mat), dptr(x), None, dptr(y_gpu), 0) == 0
+        ora.ora_mv_mxy(C.byref(M.mat), dptr(x), dptr(y_ref))
+        assert np.array_equal(y_gpu.view(np.uint64), y_ref.view(np.uint64)), it
+    _lib().sss_hip_host_cache_clear()
+
+
 def test_spmv_long_rows_bitwise():
     """Rows longer than the LDS tile (2048) take the wave-parallel product path."""
     n = 300
