@@ -9,9 +9,6 @@
  * (amg_amd/host/sss_solve.c).
  */
 #include "sss_internal.h"
-#ifdef _OPENMP
-#include <omp.h>
-#endif
 
 #include <math.h>
 #include <stdio.h>
@@ -324,78 +321,9 @@ static int cmp_int(const void *a, const void *b)
 /* The same transpose with OpenMP: entries are scattered by atomic slot claims, then each output
  * row is sorted by source position -- ascending source row, and stored order inside a row -- which
  * is exactly the order of the sequential fill below, so the result is identical. */
-/* Per-thread column counts: thread t owns a contiguous range of source rows; an entry's slot in
- * its column is the column start + the counts of the lower threads' rows + its rank among this
- * thread's, so every column lists its entries in source-row order (the sequential transpose's
- * result) with no atomics and no sort.  Needs threads x ncols counters; 0 when that is too big. */
-static int transpose_pattern_counts(int nrows, int ncols, int nnz, const int *ia, const int *ja, const void *val,
-                                    size_t vsize, int *tia, int *tja, void *tval)
-{
-#ifdef _OPENMP
-    const int Tmax = omp_get_max_threads();
-    if (Tmax < 2 || (size_t)Tmax * (size_t)ncols > ((size_t)1 << 31)) return 0;
-    int *cnt = (int *)calloc((size_t)Tmax * (size_t)ncols, sizeof(int));
-    int *rlo = (int *)malloc(sizeof(int) * ((size_t)Tmax + 1));
-    int T = 0;
-    if (!cnt || !rlo) { free(cnt); free(rlo); return 0; }
-#pragma omp parallel num_threads(Tmax)
-    {
-#pragma omp single
-        {   /* the team actually granted: row ranges of about nnz / T entries each */
-            T = omp_get_num_threads();
-            rlo[0] = 0;
-            for (int t = 1; t < T; ++t) {
-                const long long target = (long long)nnz * t / T;
-                int lo = rlo[t - 1], hi = nrows;
-                while (lo < hi) { const int mid = lo + (hi - lo) / 2; if (ia[mid] < target) lo = mid + 1; else hi = mid; }
-                rlo[t] = lo;
-            }
-            rlo[T] = nrows;
-        }   /* implicit barrier */
-        const int t = omp_get_thread_num();
-        int *ct = cnt + (size_t)t * ncols;
-        for (int k = ia[rlo[t]]; k < ia[rlo[t + 1]]; ++k) ct[ja[k]]++;
-#pragma omp barrier
-#pragma omp for schedule(static)
-        for (int c = 0; c < ncols; ++c) {
-            int sum = 0;
-            for (int u = 0; u < T; ++u) sum += cnt[(size_t)u * ncols + c];
-            tia[c + 1] = sum;
-        }
-#pragma omp single
-        {
-            tia[0] = 0;
-            for (int c = 0; c < ncols; ++c) tia[c + 1] += tia[c];
-        }
-#pragma omp for schedule(static)
-        for (int c = 0; c < ncols; ++c) {
-            int run = tia[c];
-            for (int u = 0; u < T; ++u) {
-                const int x = cnt[(size_t)u * ncols + c];
-                cnt[(size_t)u * ncols + c] = run;
-                run += x;
-            }
-        }   /* implicit barrier */
-        for (int i = rlo[t]; i < rlo[t + 1]; ++i)
-            for (int k = ia[i]; k < ia[i + 1]; ++k) {
-                const int dst = ct[ja[k]]++;
-                tja[dst] = i;
-                if (val) memcpy((char *)tval + (size_t)dst * vsize, (const char *)val + (size_t)k * vsize, vsize);
-            }
-    }
-    free(cnt);
-    free(rlo);
-    return 1;
-#else
-    (void)nrows, (void)ncols, (void)nnz, (void)ia, (void)ja, (void)val, (void)vsize, (void)tia, (void)tja, (void)tval;
-    return 0;
-#endif
-}
-
 static void transpose_pattern_par(int nrows, int ncols, int nnz, const int *ia, const int *ja,
                                   const void *val, size_t vsize, int *tia, int *tja, void *tval)
 {
-    if (transpose_pattern_counts(nrows, ncols, nnz, ia, ja, val, vsize, tia, tja, tval)) return;
     int *fill = (int *)calloc((size_t)ncols + 1, sizeof(int));
     int *src = (int *)malloc(sizeof(int) * (size_t)nnz);
     int *rowof = (int *)malloc(sizeof(int) * (size_t)nnz);
