@@ -663,20 +663,30 @@ void interp_DIR(SSS_MAT *A, SSS_IVEC *vertices, SSS_MAT *P, SSS_AMG_PARS *pars)
             if (ja[k] == i) { d = k; break; }
         diag_pos[i] = d;
     }
-    /* pass 2 (serial, cheap): resolve the carried aii */
+    /* pass 2: the per-row apN correction (row-parallel; stored in aii_row), then the carried aii
+     * resolved in row order (a row without a diagonal entry takes the previous row's value) */
+#pragma omp parallel for schedule(static)
     for (int i = 0; i < n; ++i) {
-        double aii = diag_pos[i] < ia[i + 1] ? a[diag_pos[i]] : carried;
+        double apN = 0.0;
+        int npos = 0, corr = 0;
         if (mark[i] == FGPT) {
-            double apN = 0.0;
-            int npos = 0;
             for (int k = ia[i]; k < ia[i + 1]; ++k) {
                 if (k == diag_pos[i] || !(a[k] > 0)) continue;
                 apN += a[k];
                 for (int q = P->row_ptr[i]; q < P->row_ptr[i + 1]; ++q)
                     if (P->col_idx[q] == ja[k]) { npos++; break; }
             }
-            if (npos == 0) aii += apN;
+            corr = npos == 0;
         }
+        aii_row[i] = apN;
+        if (!corr) diag_pos[i] = -2 - diag_pos[i];   /* flag "no correction", position kept */
+    }
+    for (int i = 0; i < n; ++i) {
+        const int corr = diag_pos[i] >= 0;
+        const int d = corr ? diag_pos[i] : -2 - diag_pos[i];
+        if (!corr) diag_pos[i] = d;
+        double aii = d < ia[i + 1] ? a[d] : carried;
+        if (corr) aii += aii_row[i];
         aii_row[i] = aii;
         carried = aii;
     }
