@@ -106,7 +106,8 @@ struct sss_hip_dist {
     double *d_cown = nullptr, *d_call = nullptr;
     int *d_tail_perm = nullptr;     // tail level-0 new -> old (null: identity)
     std::vector<double> h_cown, h_call;
-    double *partial = nullptr, *d_norm = nullptr, *h_norm = nullptr;
+    double *partial = nullptr, *d_norm = nullptr, *h_norm = nullptr;   // norm: [0] sum of squares, [1] stall flag
+    unsigned *d_err = nullptr;    // stall word of the one-launch GS passes (this rank's levels and tail)
     std::vector<double> stage;
     bool resid_c_ready = false;   // the last cycle's final C pass left r_C and its partials (level 0)
     SSS_AMG tail_host{};          // the tail levels read from a partition set (file-built engines)
@@ -338,13 +339,21 @@ int allgather_coarse(sss_hip_dist *d)
     return 0;
 }
 
-int allreduce_norm(sss_hip_dist *d)   // d_norm (sum of squares) -> global sum, on the host
+// d_norm = {sum of squares, stall flag} -> global sums, on the host: every rank sees a stall on
+// any rank and fails with it
+int allreduce_norm(sss_hip_dist *d)
 {
     sss_hip_comm *c = d->comm;
-    if (!c->host) SSS_NCCL(ncclAllReduce(d->d_norm, d->d_norm, 1, ncclDouble, ncclSum, c->nccl, d->stream));
-    SSS_HIP(hipMemcpyAsync(d->h_norm, d->d_norm, sizeof(double), hipMemcpyDeviceToHost, d->stream));
+    if (int rc = launch_err_flag(d->d_err, d->d_norm + 1, d->stream)) return rc;
+    if (!c->host) SSS_NCCL(ncclAllReduce(d->d_norm, d->d_norm, 2, ncclDouble, ncclSum, c->nccl, d->stream));
+    SSS_HIP(hipMemcpyAsync(d->h_norm, d->d_norm, 2 * sizeof(double), hipMemcpyDeviceToHost, d->stream));
     SSS_HIP(hipStreamSynchronize(d->stream));
-    if (c->host && c->t.allreduce_sum(c->t.ctx, d->h_norm, 1)) return ERROR_MISC;
+    if (c->host && c->t.allreduce_sum(c->t.ctx, d->h_norm, 2)) return ERROR_MISC;
+    if (d->h_norm[1] != 0.0) {
+        fprintf(stderr, "### ERROR: sss_hip_dist_residual_norm (rank %d): an exact Gauss-Seidel pass stalled on "
+                        "the GPU (spin limit reached); the iterate is invalid\n", c->rank);
+        return ERROR_MISC;
+    }
     return 0;
 }
 
@@ -373,6 +382,7 @@ void release(sss_hip_dist *d)
     dev_free(d->d_tail_perm);
     dev_free(d->partial);
     dev_free(d->d_norm);
+    dev_free(d->d_err);
     if (d->h_norm) (void)hipHostFree(d->h_norm);
     if (d->stream) (void)hipStreamDestroy(d->stream);
     if (d->cstream) (void)hipStreamDestroy(d->cstream);
@@ -435,8 +445,10 @@ extern "C" void sss_hip_comm_destroy(sss_hip_comm *c)
 }
 
 // The engine of one rank from its partition `plan` and the replicated tail hierarchy `tailmg`
-// (its cg[0] is global level plan.nagg).  Takes ownership of d.
-static sss_hip_dist *dist_create_impl(sss_hip_dist *d, PartPlan &plan, const SSS_AMG *tailmg)
+// (its cg[0] is global level plan.nagg).  Takes ownership of d.  pre_err: a failure this rank met
+// before (its partition or tail file unreadable); it still joins the status agreement.
+static sss_hip_dist *dist_create_impl(sss_hip_dist *d, PartPlan &plan, const SSS_AMG *tailmg,
+                                      const char *pre_err = nullptr)
 {
     sss_hip_comm *c = d->comm;
     auto fail = [&](const char *what) {
@@ -444,24 +456,27 @@ static sss_hip_dist *dist_create_impl(sss_hip_dist *d, PartPlan &plan, const SSS
         release(d);
         return (sss_hip_dist *)nullptr;
     };
-    if (d->pars.cycle_type > 1) return fail("only V-cycles are distributed");
-    if (d->opts.device >= 0 && hipSetDevice(d->opts.device) != hipSuccess) return fail("hipSetDevice");
-    if (hipStreamCreateWithFlags(&d->stream, hipStreamNonBlocking) != hipSuccess) return fail("stream");
-    if (plan.nranks != c->nranks || plan.rank != c->rank) return fail("partition made for another rank layout");
-    d->nagg = plan.nagg;
-    if (d->nagg < 1) return fail("hierarchy too shallow to partition");
-    if (tailmg->num_levels != plan.nl - plan.nagg) return fail("tail levels do not match the partition");
-
-    if (hipStreamCreateWithFlags(&d->cstream, hipStreamNonBlocking) != hipSuccess ||
-        hipEventCreateWithFlags(&d->ev_packed, hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&d->ev_halo, hipEventDisableTiming) != hipSuccess)
-        return fail("communication stream");
+    // Every failure on one rank only (an unreadable or mismatched partition, memory, a level this
+    // rank cannot smooth) is recorded, and all ranks agree on the outcome with one collective before
+    // the first collective of the set-up, so no rank is left waiting in it.
+    const char *err = pre_err;
+    if (d->opts.device >= 0 && hipSetDevice(d->opts.device) != hipSuccess && !err) err = "hipSetDevice";
+    if (hipStreamCreateWithFlags(&d->stream, hipStreamNonBlocking) != hipSuccess) {
+        d->stream = nullptr;   // the agreement then runs on the default stream
+        if (!err) err = "stream";
+    }
+    if (!err && d->pars.cycle_type > 1) err = "only V-cycles are distributed";
+    if (!err && (plan.nranks != c->nranks || plan.rank != c->rank)) err = "partition made for another rank layout";
+    if (!err && plan.nagg < 1) err = "hierarchy too shallow to partition";
+    if (!err && tailmg->num_levels != plan.nl - plan.nagg) err = "tail levels do not match the partition";
+    if (!err && (hipStreamCreateWithFlags(&d->cstream, hipStreamNonBlocking) != hipSuccess ||
+                 hipEventCreateWithFlags(&d->ev_packed, hipEventDisableTiming) != hipSuccess ||
+                 hipEventCreateWithFlags(&d->ev_halo, hipEventDisableTiming) != hipSuccess))
+        err = "communication stream";
     if (const char *ov = getenv("SSS_HIP_OVERLAP")) d->overlap = atoi(ov);
+    if (!err) d->nagg = plan.nagg;
 
-    // Everything below can fail on one rank only (memory, a level this rank cannot smooth): each
-    // rank records its failure, and all of them agree on the outcome with one collective before the
-    // first collective of the set-up, so no rank is left waiting in it.
-    const char *err = [&]() -> const char * {
+    if (!err) err = [&]() -> const char * {
         // replicated tail first: its level-0 relabeling fixes the column ids of P_{nagg-1}
         sss_hip_opts to = d->opts;
         to.use_graph = 0;
@@ -541,10 +556,15 @@ static sss_hip_dist *dist_create_impl(sss_hip_dist *d, PartPlan &plan, const SSS
         d->d_cown = dev_alloc<double>(d->nc_own);
         d->d_call = dev_alloc<double>(nt);
         d->partial = dev_alloc<double>((size_t)std::max(d->L[0].A.ngrid, 1) + kFinalScratch);
-        d->d_norm = dev_alloc<double>(1);
-        if (!d->d_cown || !d->d_call || !d->partial || !d->d_norm ||
-            hipHostMalloc((void **)&d->h_norm, sizeof(double)) != hipSuccess)
+        d->d_norm = dev_alloc<double>(2);
+        d->d_err = dev_alloc<unsigned>(1);
+        if (!d->d_cown || !d->d_call || !d->partial || !d->d_norm || !d->d_err ||
+            hipHostMalloc((void **)&d->h_norm, 2 * sizeof(double)) != hipSuccess ||
+            hipMemset(d->d_err, 0, sizeof(unsigned)) != hipSuccess)
             return "buffers";
+        // one stall word for every one-launch GS pass of this rank, the replicated tail's included
+        for (int l = 0; l < d->nagg; ++l) smoother_set_err(d->L[l].sm, d->d_err);
+        hier_set_err_word(d->tail, d->d_err);
         return nullptr;
     }();
     double failed = err ? 1.0 : 0.0;
@@ -576,14 +596,15 @@ extern "C" sss_hip_dist *sss_hip_dist_create(const SSS_AMG *mg, const sss_hip_op
 {
     if (!mg || !c || sss_hip_device_count() <= 0) return nullptr;
     PartPlan plan;
+    const char *err = nullptr;
     if (part_plan_build(plan, mg, c->nranks, c->rank, agg_rows_or_default(agg_rows))) {
-        fprintf(stderr, "### ERROR: sss_hip_dist_create (rank %d): partition\n", c->rank);
-        return nullptr;
+        err = "partition";
+        plan = PartPlan();
     }
     SSS_AMG sub = *mg;
     sub.cg = mg->cg + plan.nagg;
     sub.num_levels = mg->num_levels - plan.nagg;
-    return dist_create_impl(dist_new(mg->pars, o, c), plan, &sub);
+    return dist_create_impl(dist_new(mg->pars, o, c), plan, &sub, err);
 }
 
 extern "C" sss_hip_dist *sss_hip_dist_create_from_files(const char *prefix, const sss_hip_opts *o, sss_hip_comm *c)
@@ -591,19 +612,22 @@ extern "C" sss_hip_dist *sss_hip_dist_create_from_files(const char *prefix, cons
     if (!prefix || !c || sss_hip_device_count() <= 0) return nullptr;
     PartPlan plan;
     SSS_AMG_PARS pars;
+    std::memset(&pars, 0, sizeof(pars));
     const std::string part = part_file_name(prefix, c->rank), tail = part_tail_name(prefix);
+    const char *err = nullptr;
     if (part_plan_read(plan, pars, part.c_str())) {
         fprintf(stderr, "### ERROR: sss_hip_dist_create_from_files (rank %d): cannot read %s\n", c->rank, part.c_str());
-        return nullptr;
+        err = "unreadable partition file";
     }
     sss_hip_dist *d = dist_new(pars, o, c);
-    if (SSS_amg_load(&d->tail_host, tail.c_str())) {
+    if (!err && SSS_amg_load(&d->tail_host, tail.c_str())) {
         fprintf(stderr, "### ERROR: sss_hip_dist_create_from_files (rank %d): cannot read %s\n", c->rank, tail.c_str());
-        release(d);
-        return nullptr;
+        err = "unreadable tail file";
+    } else if (!err) {
+        d->own_tail_host = true;
     }
-    d->own_tail_host = true;
-    return dist_create_impl(d, plan, &d->tail_host);
+    // a rank that failed here still joins the status agreement of the set-up
+    return dist_create_impl(d, plan, &d->tail_host, err);
 }
 
 extern "C" void sss_hip_dist_destroy(sss_hip_dist *d) { release(d); }
@@ -744,7 +768,7 @@ extern "C" int sss_hip_dist_residual_norm(sss_hip_dist *d, double *absres)
     if (rc) return rc;
     if ((rc = launch_final_sum(d->partial, L.A.ngrid, d->d_norm, false, d->stream))) return rc;
     if ((rc = allreduce_norm(d))) return rc;
-    *absres = std::sqrt(*d->h_norm);
+    *absres = std::sqrt(d->h_norm[0]);
     return 0;
 }
 

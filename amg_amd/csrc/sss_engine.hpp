@@ -285,6 +285,11 @@ sss_hip_hier *hier_create_impl(const SSS_AMG *mg, const sss_hip_opts *o, int lev
 double *hier_vec(sss_hip_hier *h, int level, int which);
 const std::vector<int> &hier_perm(sss_hip_hier *h, int level);   // new -> old (empty: identity)
 int level_kind_of(const sss_hip_opts &o, int global_level);
+// The stall word of the hierarchy's one-launch GS passes: read (and cleared) with a sync -- 0 or
+// ERROR_MISC with an "### ERROR" line on stderr; re-pointed to an owner's word (distributed tail).
+int hier_stall_check(sss_hip_hier *h);
+unsigned *hier_err_word(sss_hip_hier *h);
+void hier_set_err_word(sss_hip_hier *h, unsigned *err);
 int level_inner_of(const sss_hip_opts &o, int global_level);
 
 // y <- op(A x) on `stream` (see SSS_HIP_SPMV_*).  `partial` (optional, RESID only): one
@@ -312,6 +317,9 @@ struct GsPersist {
     int *ck = nullptr;                  // flow, short rows: chunk -> first position (nchunks + 1)
     int *h_off = nullptr;               // cu: depth offsets (depth + 1)
     unsigned *ctl = nullptr;            // epoch, ticket, exit count, error
+    unsigned *err = nullptr;            // where a stall is reported: ctl's error word, or the
+                                        // hierarchy's (smoother_set_err)
+    int spin = 0;                       // polls before a waiting wave gives up (< 0: test hook)
     unsigned long long *gran = nullptr; // flow: two {epoch, half of x_i} granules per row
 };
 struct PassSchedule {          // rows of one class (F or C), grouped by DAG depth
@@ -347,6 +355,11 @@ void gs_persist_free(PassSchedule &ps);
 int gs_persist_run(const PassSchedule &ps, const DevCSR &A, const double *b, double *x, const double *deff,
                    hipStream_t s);
 int gs_persist_error(const PassSchedule &ps, unsigned *out);
+struct SmootherPlan;
+// Report the one-launch passes' stalls into *err (a word of the owning hierarchy).
+void smoother_set_err(SmootherPlan &sp, unsigned *err);
+// *out = 1.0 if *err is set else 0.0, and *err cleared (one thread on stream s).
+int launch_err_flag(unsigned *err, double *out, hipStream_t s);
 struct SmootherPlan {
     int kind = SSS_HIP_SMOOTH_EXACT;
     // Natural-order GS (SSS_amg_smoother_gs, Solve/SSS_smooth.c:90-137: cf_order = 0 or no C/F

@@ -28,7 +28,9 @@
 // progress without any residency assumption (tickets are handed out in depth order, a wave only
 // waits for rows whose tickets were handed out earlier).  Every spin is bounded: a pass that
 // stalls for ~0.5 s gives up and sets an error word (the engine reports it; results are then
-// garbage, but no wave spins forever).
+// garbage, but no wave spins forever).  The error word is the hierarchy's (GsPersist::err): the
+// engine reads it back with the residual norm and fails loudly (sss_hier.hip).  SSS_HIP_GS_SPIN
+// sets the spin limit (test hook: a negative limit reports a stall from every launch).
 #include "sss_engine.hpp"
 #include "sss_spmv_dev.hpp"
 
@@ -73,13 +75,13 @@ __device__ __forceinline__ void granule_put(unsigned long long *g, unsigned epoc
     __hip_atomic_store(g, ((unsigned long long)epoch << 32) | (u & 0xffffffffull), RLX_AGENT);
     __hip_atomic_store(g + 1, ((unsigned long long)epoch << 32) | (u >> 32), RLX_AGENT);
 }
-// x_j of a same-class lower neighbour: spin on its granules (bounded)
-__device__ __forceinline__ double granule_wait(const unsigned long long *g, unsigned epoch, unsigned *err)
+// x_j of a same-class lower neighbour: spin on its granules (bounded by `spin` polls)
+__device__ __forceinline__ double granule_wait(const unsigned long long *g, unsigned epoch, unsigned *err, int spin)
 {
     double v = 0.0;
     for (int s = 0; !granule_get(g, epoch, v); ++s) {
         // give up after the limit, or at once when another wave already did (checked every 64 polls)
-        if (s >= kFlowSpinLimit || ((s & 63) == 63 && __hip_atomic_load(err, RLX_AGENT))) {
+        if (s >= spin || ((s & 63) == 63 && __hip_atomic_load(err, RLX_AGENT))) {
             __hip_atomic_store(err, 1u, RLX_AGENT);
             return 0.0;
         }
@@ -89,8 +91,9 @@ __device__ __forceinline__ double granule_wait(const unsigned long long *g, unsi
     return v;
 }
 
-__device__ __forceinline__ void flow_exit(unsigned *ctl, unsigned epoch)
+__device__ __forceinline__ void flow_exit(unsigned *ctl, unsigned epoch, unsigned *err, int spin)
 {
+    if (spin < 0 && (threadIdx.x & 63) == 0) __hip_atomic_store(err, 1u, RLX_AGENT);   // test hook
     // the last wave out resets the ticket and the exit count and publishes the epoch for the next
     // launch (visible to it across the kernel boundary)
     const unsigned total = gridDim.x * (blockDim.x >> 6);
@@ -145,7 +148,7 @@ __global__ __launch_bounds__(kBlock) void gs_flow_group(int nchunks, const int *
                                                         const int *__restrict__ ci, const double *__restrict__ v,
                                                         const double *__restrict__ b, double *x,
                                                         const double *__restrict__ deff, unsigned long long *gran,
-                                                        int lo, int hi, unsigned *ctl)
+                                                        int lo, int hi, unsigned *ctl, unsigned *err, int spin)
 {
     constexpr int R = 64 / G, CAP = kGroupBuf / R, U = 8;
     // a same-pass row this row reads the NEW value of (published by its granules)
@@ -155,7 +158,6 @@ __global__ __launch_bounds__(kBlock) void gs_flow_group(int nchunks, const int *
     const int lane = threadIdx.x & 63, grp = lane / G, gl = lane % G;
     double *mine = buf[threadIdx.x >> 6] + grp * CAP;
     const unsigned epoch = __hip_atomic_load(&ctl[kCtlEpoch], RLX_AGENT) + 1u;
-    unsigned *err = &ctl[kCtlErr];
     for (;;) {
         const int q = flow_ticket(ctl);
         if (q >= nchunks) break;
@@ -211,7 +213,7 @@ __global__ __launch_bounds__(kBlock) void gs_flow_group(int nchunks, const int *
                 pend &= pend - 1;
                 const int t = gl + G * j;
                 const int c = ci[kb + t];
-                mine[t] = v[kb + t] * granule_wait(gran + 2 * (size_t)(c - lo), epoch, err);
+                mine[t] = v[kb + t] * granule_wait(gran + 2 * (size_t)(c - lo), epoch, err, spin);
             }
             wave_sync();
             if (gl == 0 && m > 0) acc = chain_sub_pipe(acc, mine, 0, m);   // (C)
@@ -225,7 +227,7 @@ __global__ __launch_bounds__(kBlock) void gs_flow_group(int nchunks, const int *
             granule_put(gran + 2 * (size_t)(i - lo), epoch, xn);
         }
     }
-    flow_exit(ctl, epoch);
+    flow_exit(ctl, epoch, err, spin);
 }
 
 // ---- single-CU engine --------------------------------------------------------------------------
@@ -234,7 +236,7 @@ __global__ __launch_bounds__(64 * kCuWaves) void gs_cu(int nrows, int ndepth, co
                                                        const int *__restrict__ h_off, const int *__restrict__ rp,
                                                        const int *__restrict__ ci, const double *__restrict__ v,
                                                        const double *__restrict__ b, double *x,
-                                                       const double *__restrict__ deff, unsigned *err)
+                                                       const double *__restrict__ deff, unsigned *err, int spin)
 {
     __shared__ int done[kCuMaxDepth];
     __shared__ int ticket, abort_flag;
@@ -269,7 +271,7 @@ __global__ __launch_bounds__(64 * kCuWaves) void gs_cu(int nrows, int ndepth, co
             const int need = h_off[d] - h_off[d - 1];
             for (int s = 0; __hip_atomic_load(&done[d - 1], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < need; ++s) {
                 // give up after the limit, or at once when another wave of the pass already did
-                if (s >= kSpinLimit || __hip_atomic_load(&abort_flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) {
+                if (s >= spin || __hip_atomic_load(&abort_flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) {
                     if (lane == 0) {
                         __hip_atomic_store(err, 1u, RLX_AGENT);
                         __hip_atomic_store(&abort_flag, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -313,6 +315,7 @@ __global__ __launch_bounds__(64 * kCuWaves) void gs_cu(int nrows, int ndepth, co
             __hip_atomic_fetch_add(&done[d], 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
         }
     }
+    if (spin < 0 && threadIdx.x == 0) __hip_atomic_store(err, 1u, RLX_AGENT);   // test hook
 }
 
 // ---- planning ----------------------------------------------------------------------------------
@@ -377,13 +380,18 @@ int gs_persist_build(PassSchedule &ps, const SSS_MAT &A, int lo, int hi, bool lo
         });
         sym = !bad[0];
         if (!sym) {
-            if (ps.depth <= kCuMaxDepth) engine = 2;
+            // the single-CU engine divides by the stale GS-CF divisor; a natural-order pass
+            // multiplies by the carried reciprocal (Solve/SSS_smooth.c:112), so it keeps the
+            // per-depth launches
+            if (ps.depth <= kCuMaxDepth && !natural && !desc) engine = 2;
             else return 0;
         }
     }
     g.engine = engine;
     g.lo = lo;
     g.hi = hi;
+    g.spin = engine == 2 ? kSpinLimit : kFlowSpinLimit;
+    if (const char *sp = getenv("SSS_HIP_GS_SPIN")) g.spin = atoi(sp);
     if (engine == 2) {
         std::vector<int> off(ps.h_off.begin(), ps.h_off.end());
         g.h_off = dev_alloc<int>(off.size());
@@ -391,6 +399,7 @@ int gs_persist_build(PassSchedule &ps, const SSS_MAT &A, int lo, int hi, bool lo
         if (!g.h_off || !g.ctl) return hip_fail(hipErrorOutOfMemory, "hipMalloc(gs cu)", __FILE__, __LINE__);
         SSS_HIP(hipMemcpy(g.h_off, off.data(), sizeof(int) * off.size(), hipMemcpyHostToDevice));
         SSS_HIP(hipMemset(g.ctl, 0, sizeof(unsigned) * kCtlWords));
+        g.err = g.ctl + kCtlErr;
         return 0;
     }
     // lanes per row from the average row length: about 8 entries per lane and round
@@ -403,6 +412,7 @@ int gs_persist_build(PassSchedule &ps, const SSS_MAT &A, int lo, int hi, bool lo
     if (!g.gran || !g.ctl) return hip_fail(hipErrorOutOfMemory, "hipMalloc(gs flow)", __FILE__, __LINE__);
     SSS_HIP(hipMemset(g.gran, 0, sizeof(unsigned long long) * 2 * (size_t)(hi - lo)));
     SSS_HIP(hipMemset(g.ctl, 0, sizeof(unsigned) * kCtlWords));
+    g.err = g.ctl + kCtlErr;
     {   // chunks: up to 64 / G rows of one depth
         const int R = 64 / g.G;
         std::vector<int> ck;
@@ -447,11 +457,11 @@ int gs_persist_run(const PassSchedule &ps, const DevCSR &A, const double *b, dou
     const GsPersist &g = ps.gp;
     if (g.engine == 2) {
         hipLaunchKernelGGL(gs_cu, dim3(1), dim3(64 * kCuWaves), 0, s, ps.nrows, ps.depth, ps.rows, g.h_off, A.rp, A.ci,
-                           A.v, b, x, deff, g.ctl + kCtlErr);
+                           A.v, b, x, deff, g.err, g.spin);
     } else if (g.engine == 1) {
         auto go = [&](auto kern) {
             hipLaunchKernelGGL(kern, dim3(g.grid), dim3(kBlock), 0, s, g.nchunks, g.ck, ps.rows, A.rp, A.ci, A.v, b, x,
-                               deff, g.gran, g.lo, g.hi, g.ctl);
+                               deff, g.gran, g.lo, g.hi, g.ctl, g.err, g.spin);
         };
         auto by_g = [&](auto nat, auto desc) {
             constexpr bool N = decltype(nat)::value, D = decltype(desc)::value;
@@ -478,10 +488,31 @@ int gs_persist_run(const PassSchedule &ps, const DevCSR &A, const double *b, dou
 int gs_persist_error(const PassSchedule &ps, unsigned *out)
 {
     *out = 0;
-    if (!ps.gp.ctl) return 0;
+    if (!ps.gp.err) return 0;
     unsigned e = 0;
-    SSS_HIP(hipMemcpy(&e, ps.gp.ctl + kCtlErr, sizeof(unsigned), hipMemcpyDeviceToHost));
+    SSS_HIP(hipMemcpy(&e, ps.gp.err, sizeof(unsigned), hipMemcpyDeviceToHost));
     *out = e;
+    return 0;
+}
+
+void smoother_set_err(SmootherPlan &sp, unsigned *err)
+{
+    for (auto &ps : sp.pass)
+        if (ps.gp.engine && err) ps.gp.err = err;
+}
+
+// the error word as a double (1.0 if any pass of the hierarchy stalled since the last read, else
+// 0.0) into *out, and the word cleared: one thread
+__global__ void err_flag_kernel(unsigned *err, double *out)
+{
+    const unsigned e = __hip_atomic_exchange(err, 0u, RLX_AGENT);
+    *out = e ? 1.0 : 0.0;
+}
+
+int launch_err_flag(unsigned *err, double *out, hipStream_t s)
+{
+    hipLaunchKernelGGL(err_flag_kernel, dim3(1), dim3(1), 0, s, err, out);
+    SSS_HIP(hipGetLastError());
     return 0;
 }
 

@@ -50,8 +50,9 @@ struct sss_hip_hier {
     CoarseDirect direct;
     CoarseKrylov *krylov = nullptr;
     double *partial = nullptr;   // per-row-block partial sums for the level-0 norm
-    double *d_norm = nullptr;
-    double *h_norm = nullptr;    // pinned
+    double *d_norm = nullptr;    // [0] ||r||, [1] 1.0 if a one-launch GS pass stalled since the last read
+    double *h_norm = nullptr;    // pinned mirror of d_norm
+    unsigned *d_err = nullptr;   // stall word of every one-launch GS pass of the hierarchy
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     // hipGraph replay of the cycle: segments between host-steered coarse solves (a null exec
     // marks "run the Krylov coarse solve here"); the residual-norm tail has its own graph.
@@ -206,6 +207,7 @@ static void hier_release(sss_hip_hier *h)
     coarse_krylov_destroy(h->krylov);
     dev_free(h->partial);
     dev_free(h->d_norm);
+    dev_free(h->d_err);
     if (h->h_norm) (void)hipHostFree(h->h_norm);
     if (h->ev0) (void)hipEventDestroy(h->ev0);
     if (h->ev1) (void)hipEventDestroy(h->ev1);
@@ -447,9 +449,13 @@ static sss_hip_hier *hb_finish(HierBuild &b)
         h->pend_f = dev_alloc<double>((size_t)std::max(h->L[0].sm.pass[0].hi, 1));
         if (!h->pend_f) return fail("pending F pass buffer");
     }
-    h->d_norm = dev_alloc<double>(1);
-    if (!h->partial || !h->d_norm || hipHostMalloc((void **)&h->h_norm, sizeof(double)) != hipSuccess)
+    h->d_norm = dev_alloc<double>(2);
+    h->d_err = dev_alloc<unsigned>(1);
+    if (!h->partial || !h->d_norm || !h->d_err || hipHostMalloc((void **)&h->h_norm, 2 * sizeof(double)) != hipSuccess)
         return fail("norm buffers");
+    if (hipMemset(h->d_err, 0, sizeof(unsigned)) != hipSuccess || hipMemset(h->d_norm, 0, 2 * sizeof(double)) != hipSuccess)
+        return fail("norm buffers");
+    for (int l = 0; l + 1 < h->nl; ++l) smoother_set_err(h->L[l].sm, h->d_err);
 
     const SSS_MAT &Ac = mg->cg[h->nl - 1].A;
     h->coarse_mode = h->opts.coarse;
@@ -654,6 +660,7 @@ extern "C" int sss_hip_download_vec(sss_hip_hier *h, int level, int which, doubl
 {
     double *d = level_vec(h, level, which);
     if (!d || n < 0 || n > h->L[level].A.n) return ERROR_INPUT_PAR;
+    if (int rc = hier_stall_check(h)) return rc;   // a stalled pass leaves an invalid iterate
     const auto &perm = h->L[level].perm;
     if (perm.empty()) {
         SSS_HIP(hipMemcpyAsync(dst, d, sizeof(double) * (size_t)n, hipMemcpyDeviceToHost, h->stream));
@@ -838,7 +845,32 @@ static int enqueue_residual_norm(sss_hip_hier *h, bool f_only)
                                            h->stream)
                       : launch_spmv(L.A, SSS_HIP_SPMV_RESID, -1.0, L.x, L.b, L.wp, 0, h->partial, h->stream);
     if (rc) return rc;
-    return launch_final_sum(h->partial, L.A.ngrid, h->d_norm, true, h->stream);
+    if ((rc = launch_final_sum(h->partial, L.A.ngrid, h->d_norm, true, h->stream))) return rc;
+    return launch_err_flag(h->d_err, h->d_norm + 1, h->stream);
+}
+
+// A one-launch GS pass gave up waiting (sss_gs_persist.hip): its iterate is garbage.  Fatal for
+// the solve, like the reference's error exits (SSS_utils.c:16-94); the word was cleared on read.
+static int stall_error(const char *where)
+{
+    fprintf(stderr, "### ERROR: %s: an exact Gauss-Seidel pass stalled on the GPU (spin limit reached); "
+                    "the iterate is invalid\n", where);
+    return ERROR_MISC;
+}
+
+int sss::hier_stall_check(sss_hip_hier *h)
+{
+    if (!h || !h->d_err) return 0;
+    if (int rc = launch_err_flag(h->d_err, h->d_norm + 1, h->stream)) return rc;
+    SSS_HIP(hipMemcpyAsync(h->h_norm + 1, h->d_norm + 1, sizeof(double), hipMemcpyDeviceToHost, h->stream));
+    SSS_HIP(hipStreamSynchronize(h->stream));
+    return h->h_norm[1] != 0.0 ? stall_error("sss_hip engine") : 0;
+}
+
+unsigned *sss::hier_err_word(sss_hip_hier *h) { return h ? h->d_err : nullptr; }
+void sss::hier_set_err_word(sss_hip_hier *h, unsigned *err)
+{
+    for (int l = 0; l + 1 < h->nl; ++l) smoother_set_err(h->L[l].sm, err);
 }
 
 extern "C" int sss_hip_residual_norm(sss_hip_hier *h, double *absres)
@@ -861,9 +893,13 @@ extern "C" int sss_hip_residual_norm(sss_hip_hier *h, double *absres)
         if (rc) return rc;
     }
     h->pending_f = f_only && h->pend_f;
-    SSS_HIP(hipMemcpyAsync(h->h_norm, h->d_norm, sizeof(double), hipMemcpyDeviceToHost, h->stream));
+    SSS_HIP(hipMemcpyAsync(h->h_norm, h->d_norm, 2 * sizeof(double), hipMemcpyDeviceToHost, h->stream));
     SSS_HIP(hipStreamSynchronize(h->stream));
-    *absres = *h->h_norm;
+    *absres = h->h_norm[0];
+    if (h->h_norm[1] != 0.0) {
+        h->pending_f = h->resid_c_ready = false;
+        return stall_error("sss_hip_residual_norm");
+    }
     return 0;
 }
 
@@ -941,13 +977,13 @@ extern "C" int sss_hip_pcg(sss_hip_hier *h, double tol, int maxit, int *iters, d
     h->resid_c_ready = false;
     if (iters) *iters = it;
     if (relres) *relres = rel;
-    return 0;
+    return hier_stall_check(h);
 }
 
 extern "C" int sss_hip_sync(sss_hip_hier *h)
 {
     SSS_HIP(hipStreamSynchronize(h->stream));
-    return 0;
+    return hier_stall_check(h);
 }
 
 extern "C" int sss_hip_num_levels(sss_hip_hier *h) { return h ? h->nl : 0; }
@@ -1042,7 +1078,10 @@ extern "C" int sss_hip_time_iterations(sss_hip_hier *h, int reps, double *avg_ms
 // memory, row-parallel; far cheaper than the upload and the format build) plus the dimensions and
 // the use.  A caller that loops over these entry points with the same operator pays the upload
 // once; a caller that changes the matrix in place gets a fresh upload (the hash changes).
-// sss_hip_host_cache_clear() releases everything.
+// sss_hip_host_cache_clear() releases everything.  The smoother and coarse-solver objects hold
+// mutable device state (the one-launch GS engine's tickets and granules, the Krylov scratch), so
+// each call holds its entry's mutex for the whole apply; operators above SSS_HIP_HOST_CACHE_MB
+// (default 1024 MiB of CSR) are built for the call and released after it, not cached.
 extern char **environ;
 
 namespace {
@@ -1051,6 +1090,7 @@ struct HostCSR {
     ~HostCSR() { devcsr_free(d); }
 };
 struct HostSmooth {
+    std::mutex run;   // held for a whole apply (shared mutable device state)
     DevCSR d;
     SmootherPlan sp;
     ~HostSmooth()
@@ -1060,6 +1100,7 @@ struct HostSmooth {
     }
 };
 struct HostCoarse {
+    std::mutex run;   // held for a whole apply (Krylov scratch)
     DevCSR d;
     CoarseDirect cd;
     bool direct = false;
@@ -1128,9 +1169,11 @@ struct PreparedCache {
     std::vector<Entry> e;
     unsigned long long tick = 0;
     static constexpr size_t kMax = 4;
+    // cache: false builds a private object for this call (operators too large to keep resident)
     template <class T, class Build>
-    std::shared_ptr<T> get(unsigned long long key, Build build)
+    std::shared_ptr<T> get(unsigned long long key, Build build, bool cache = true)
     {
+        if (!cache) return build();
         {
             std::lock_guard<std::mutex> lk(mu);
             for (auto &x : e)
@@ -1155,6 +1198,12 @@ struct PreparedCache {
         e.clear();
     }
 };
+bool cacheable(const SSS_MAT &A)
+{
+    const char *e = getenv("SSS_HIP_HOST_CACHE_MB");
+    const double mb = (e && *e) ? atof(e) : 1024.0;
+    return 12.0 * (double)A.num_nnzs + 4.0 * (double)A.num_rows <= mb * 1048576.0;
+}
 PreparedCache &prepared()
 {
     static PreparedCache *c = new PreparedCache();   // objects hold device memory: never torn down at exit
@@ -1174,7 +1223,7 @@ extern "C" int sss_hip_host_spmv(int op, double alpha, const SSS_MAT *A, const d
     auto M = prepared().get<HostCSR>(matrix_key(*A, 0x5350ull ^ ((unsigned long long)enc << 8)), [&] {
         auto m = std::make_shared<HostCSR>();
         return devcsr_upload(m->d, *A, -1, enc) ? nullptr : m;
-    });
+    }, cacheable(*A));
     if (!M) return ERROR_MISC;
     const size_t ny = (size_t)A->num_rows, nx = (size_t)A->num_cols;
     double *dx = dev_alloc<double>(nx), *dy = dev_alloc<double>(ny), *db = dev_alloc<double>(ny);
@@ -1220,14 +1269,23 @@ extern "C" int sss_hip_host_smooth(const SSS_SMTR *s, int post)
                     : smoother_build(m->sp, *s->A, use_cf ? s->ordering : nullptr, kind))
             return std::shared_ptr<HostSmooth>();
         return m;
-    });
+    }, cacheable(*s->A));
     if (!M) return ERROR_MISC;
+    std::lock_guard<std::mutex> run_lock(M->run);
     double *dx = dev_alloc<double>((size_t)n), *db = dev_alloc<double>((size_t)n);
     int rc = (!dx || !db) ? ERROR_ALLOC_MEM : 0;
     if (!rc && hipMemcpy(dx, s->x->d, sizeof(double) * n, hipMemcpyHostToDevice) != hipSuccess) rc = ERROR_MISC;
     if (!rc && hipMemcpy(db, s->b->d, sizeof(double) * n, hipMemcpyHostToDevice) != hipSuccess) rc = ERROR_MISC;
     if (!rc) rc = smoother_run(M->sp, M->d, db, dx, s->nsweeps, nullptr, nullptr, nullptr, nullptr, false, natural && desc);
     if (!rc && hipMemcpy(s->x->d, dx, sizeof(double) * n, hipMemcpyDeviceToHost) != hipSuccess) rc = ERROR_MISC;
+    for (auto &ps : M->sp.pass) {   // a stalled one-launch pass: fail (and clear its word for the next call)
+        unsigned e = 0;
+        if (!rc && gs_persist_error(ps, &e)) rc = ERROR_MISC;
+        if (!rc && e) {
+            (void)hipMemset(ps.gp.err, 0, sizeof(unsigned));
+            rc = stall_error("SSS_amg_smoother_pre/post");
+        }
+    }
     dev_free(dx);
     dev_free(db);
     return rc;
@@ -1251,8 +1309,9 @@ extern "C" int sss_hip_host_coarse_solve(SSS_MAT *A, SSS_VEC *b, SSS_VEC *x, dou
                 if (!m->k) return std::shared_ptr<HostCoarse>();
             }
             return m;
-        });
+        }, cacheable(*A));
     if (!M) return ERROR_MISC;
+    std::lock_guard<std::mutex> run_lock(M->run);
     double *dx = dev_alloc<double>((size_t)n), *db = dev_alloc<double>((size_t)n);
     int rc = (!dx || !db) ? ERROR_ALLOC_MEM : 0;
     if (!rc && hipMemcpy(dx, x->d, sizeof(double) * n, hipMemcpyHostToDevice) != hipSuccess) rc = ERROR_MISC;

@@ -3,6 +3,7 @@
 #include "sss_part.hpp"
 
 #include <algorithm>
+#include <atomic>
 #include <cstdint>
 #include <cstdio>
 #include <cstring>
@@ -69,23 +70,19 @@ void take_rows(const SSS_MAT &M, const std::vector<int> &rows, int ncols, Map cm
 
 }  // namespace
 
-int part_plan_build(PartPlan &p, const SSS_AMG *mg, int nranks, int rank, int agg_rows)
+// Partitioned level count and the cuts of every partitioned level (identical for all ranks).
+static int part_cuts(const SSS_AMG *mg, int N, int agg_rows, int &nagg, std::vector<std::vector<int>> &cut)
 {
-    const int nl = mg->num_levels, N = nranks;
-    if (nl < 1 || N < 1 || rank < 0 || rank >= N) return ERROR_INPUT_PAR;
-    p.nranks = N;
-    p.rank = rank;
-    p.nl = nl;
-    int nagg = nl - 1;
+    const int nl = mg->num_levels;
+    nagg = nl - 1;
     for (int l = 1; l < nl - 1; ++l)
         if (mg->cg[l].A.num_rows <= agg_rows) {
             nagg = l;
             break;
         }
-    p.nagg = nagg;
-    p.cut.assign((size_t)nagg + 1, std::vector<int>((size_t)N + 1, 0));
+    cut.assign((size_t)nagg + 1, std::vector<int>((size_t)N + 1, 0));
     const int n0 = mg->cg[0].A.num_rows;
-    for (int q = 0; q <= N; ++q) p.cut[0][q] = (int)((long long)q * n0 / N);
+    for (int q = 0; q <= N; ++q) cut[0][q] = (int)((long long)q * n0 / N);
     for (int l = 0; l < nagg; ++l) {   // coarse cut = number of C points before the fine cut
         const SSS_AMG_COMP &C = mg->cg[l];
         const int n = C.A.num_rows;
@@ -93,8 +90,61 @@ int part_plan_build(PartPlan &p, const SSS_AMG *mg, int nranks, int rank, int ag
         std::vector<int> cpre((size_t)n + 1, 0);
         for (int i = 0; i < n; ++i) cpre[i + 1] = cpre[i] + (C.cfmark.d[i] == 1);
         if (cpre[n] != mg->cg[l + 1].A.num_rows) return ERROR_INPUT_PAR;   // coarse numbering is not cmap
-        for (int q = 0; q <= N; ++q) p.cut[l + 1][q] = cpre[p.cut[l][q]];
+        for (int q = 0; q <= N; ++q) cut[l + 1][q] = cpre[cut[l][q]];
     }
+    return 0;
+}
+
+// Ghost set (ascending global ids) of rank q on level l: the off-rank columns of its own rows of
+// A_l, of R_l's coarse rows it owns and of P_{l-1}'s fine rows it owns.
+static std::vector<int> ghost_set(const SSS_AMG *mg, const std::vector<std::vector<int>> &cut, int l, int q)
+{
+    std::vector<int> g;
+    const int qlo = cut[l][q], qhi = cut[l][q + 1];
+    auto scan = [&](const SSS_MAT &M, int r0, int r1) {
+        for (int i = r0; i < r1; ++i)
+            for (int k = M.row_ptr[i]; k < M.row_ptr[i + 1]; ++k) {
+                const int j = M.col_idx[k];
+                if (j < qlo || j >= qhi) g.push_back(j);
+            }
+    };
+    scan(mg->cg[l].A, qlo, qhi);
+    scan(mg->cg[l].R, cut[l + 1][q], cut[l + 1][q + 1]);
+    if (l > 0) scan(mg->cg[l - 1].P, cut[l - 1][q], cut[l - 1][q + 1]);
+    std::sort(g.begin(), g.end());
+    g.erase(std::unique(g.begin(), g.end()), g.end());
+    return g;
+}
+
+// Every rank's ghost sets of every partitioned level, computed once (in parallel over ranks and
+// levels) for a partition set: gs[l][q].
+using GhostSets = std::vector<std::vector<std::vector<int>>>;
+static void all_ghost_sets(const SSS_AMG *mg, const std::vector<std::vector<int>> &cut, int nagg, int N, GhostSets &gs)
+{
+    gs.assign((size_t)nagg, std::vector<std::vector<int>>((size_t)N));
+    const int jobs = nagg * N;
+    const int nt = (int)std::max(1u, std::min(32u, std::thread::hardware_concurrency()));
+    std::atomic<int> next{0};
+    auto work = [&]() {
+        for (int t; (t = next.fetch_add(1)) < jobs;) gs[(size_t)(t % nagg)][(size_t)(t / nagg)] = ghost_set(mg, cut, t % nagg, t / nagg);
+    };
+    std::vector<std::thread> th;
+    for (int t = 1; t < std::min(nt, jobs); ++t) th.emplace_back(work);
+    work();
+    for (auto &t : th) t.join();
+}
+
+static int part_plan_build_impl(PartPlan &p, const SSS_AMG *mg, int nranks, int rank, int agg_rows,
+                                const GhostSets *pre)
+{
+    const int nl = mg->num_levels, N = nranks;
+    if (nl < 1 || N < 1 || rank < 0 || rank >= N) return ERROR_INPUT_PAR;
+    p.nranks = N;
+    p.rank = rank;
+    p.nl = nl;
+    int nagg = 0;
+    if (int rc = part_cuts(mg, N, agg_rows, nagg, p.cut)) return rc;
+    p.nagg = nagg;
     p.L.assign((size_t)nagg, PartLevel());
 
     // pass 1: own rows and their F|C relabeling
@@ -122,29 +172,8 @@ int part_plan_build(PartPlan &p, const SSS_AMG *mg, int nranks, int rank, int ag
     // pass 2: ghost sets of every rank (own rows of A_l, R_l, P_{l-1}) -> ghosts + halo plan
     for (int l = 0; l < nagg; ++l) {
         PartLevel &P = p.L[l];
-        const int n = mg->cg[l].A.num_rows;
-        std::vector<int> stamp((size_t)n, -1);
-        auto ghost_set = [&](int q) {
-            std::vector<int> g;
-            const int qlo = p.cut[l][q], qhi = p.cut[l][q + 1];
-            auto scan = [&](const SSS_MAT &M, int r0, int r1) {
-                for (int i = r0; i < r1; ++i)
-                    for (int k = M.row_ptr[i]; k < M.row_ptr[i + 1]; ++k) {
-                        const int j = M.col_idx[k];
-                        if ((j < qlo || j >= qhi) && stamp[j] != q) {
-                            stamp[j] = q;
-                            g.push_back(j);
-                        }
-                    }
-            };
-            scan(mg->cg[l].A, qlo, qhi);
-            scan(mg->cg[l].R, p.cut[l + 1][q], p.cut[l + 1][q + 1]);
-            if (l > 0) scan(mg->cg[l - 1].P, p.cut[l - 1][q], p.cut[l - 1][q + 1]);
-            std::sort(g.begin(), g.end());
-            return g;
-        };
         for (int q = 0; q < N; ++q) {
-            std::vector<int> g = ghost_set(q);
+            std::vector<int> g = pre ? (*pre)[(size_t)l][(size_t)q] : ghost_set(mg, p.cut, l, q);
             if (q == rank) {
                 P.ghosts = std::move(g);
                 continue;
@@ -189,6 +218,27 @@ int part_plan_build(PartPlan &p, const SSS_AMG *mg, int nranks, int rank, int ag
             take_rows(C.P, P.perm, C.P.num_cols, [](int j) { return j; }, P.P);
         }
         take_rows(C.R, crow, P.m + P.g, cm, P.R);
+    }
+    return 0;
+}
+
+int part_plan_build(PartPlan &p, const SSS_AMG *mg, int nranks, int rank, int agg_rows)
+{
+    return part_plan_build_impl(p, mg, nranks, rank, agg_rows, nullptr);
+}
+
+// The partition files of every rank (one plan in memory at a time), the ghost sets computed once.
+int part_save_all(const SSS_AMG *mg, int nranks, int agg_rows, const char *prefix, int &nagg)
+{
+    std::vector<std::vector<int>> cut;
+    if (int rc = part_cuts(mg, nranks, agg_rows, nagg, cut)) return rc;
+    if (nagg < 1) return ERROR_INPUT_PAR;
+    GhostSets gs;
+    all_ghost_sets(mg, cut, nagg, nranks, gs);
+    for (int r = 0; r < nranks; ++r) {
+        PartPlan plan;
+        if (int rc = part_plan_build_impl(plan, mg, nranks, r, agg_rows, &gs)) return rc;
+        if (int rc = part_plan_write(plan, mg->pars, part_file_name(prefix, r).c_str())) return rc;
     }
     return 0;
 }
@@ -259,16 +309,26 @@ struct In {
         v.resize((size_t)n);
         raw(v.data(), sizeof(T) * (size_t)n);
     }
+    // a CSR block read back: dimensions, monotone row pointers from 0 and columns in range, so a
+    // corrupt or mismatched file is ERROR_WRONG_FILE instead of out-of-bounds device reads
     void mat(HostMat &m)
     {
         m.rows = i32();
         m.cols = i32();
+        if (bad || m.rows < 0 || m.cols < 0) {
+            bad = true;
+            return;
+        }
         vec(m.rp);
         vec(m.ci);
         vec(m.v);
-        if (!bad && (m.rp.size() != (size_t)m.rows + 1 || m.ci.size() != m.v.size() ||
-                     (size_t)m.rp.back() != m.ci.size()))
+        if (bad || m.rp.size() != (size_t)m.rows + 1 || m.ci.size() != m.v.size() || m.rp[0] != 0 ||
+            (size_t)m.rp.back() != m.ci.size()) {
             bad = true;
+            return;
+        }
+        for (int i = 0; i < m.rows && !bad; ++i) bad = m.rp[i + 1] < m.rp[i];
+        for (size_t k = 0; k < m.ci.size() && !bad; ++k) bad = m.ci[k] < 0 || m.ci[k] >= m.cols;
     }
 };
 }  // namespace
@@ -295,6 +355,31 @@ int part_plan_write(const PartPlan &p, const SSS_AMG_PARS &pars, const char *pat
     }
     const bool bad = o.bad;
     return (fclose(f) != 0 || bad) ? ERROR_OPEN_FILE : 0;
+}
+
+// The cross-field invariants of one level read back from a file (the halo lists index the level's
+// own values and ghosts, the local matrices have the level's local shapes).
+static bool part_level_consistent(const PartLevel &L, int nranks)
+{
+    if (L.m != L.hi - L.lo || L.m < 0 || L.g < 0 || L.nF < 0 || L.nF > L.m) return false;
+    if (L.gcls.size() != (size_t)L.g || L.gclass.size() != (size_t)L.g) return false;
+    for (int v : L.perm)
+        if (v < L.lo || v >= L.hi) return false;
+    if (L.A.rows != L.m || L.A.cols != L.m + L.g || L.R.cols != L.m + L.g || L.P.rows != L.m) return false;
+    if (L.scount.size() != L.sdst.size() || L.rcount.size() != L.rsrc.size()) return false;
+    long long ns = 0, nr = 0;
+    for (size_t i = 0; i < L.sdst.size(); ++i) {
+        if (L.sdst[i] < 0 || L.sdst[i] >= nranks || L.scount[i] < 0) return false;
+        ns += L.scount[i];
+    }
+    for (size_t i = 0; i < L.rsrc.size(); ++i) {
+        if (L.rsrc[i] < 0 || L.rsrc[i] >= nranks || L.rcount[i] < 0) return false;
+        nr += L.rcount[i];
+    }
+    if (ns != (long long)L.sidx.size() || nr != L.g) return false;
+    for (int v : L.sidx)
+        if (v < 0 || v >= L.m) return false;
+    return true;
 }
 
 int part_plan_read(PartPlan &p, SSS_AMG_PARS &pars, const char *path)
@@ -332,6 +417,7 @@ int part_plan_read(PartPlan &p, SSS_AMG_PARS &pars, const char *path)
         in.vec(L.sdst), in.vec(L.scount), in.vec(L.sidx), in.vec(L.rsrc), in.vec(L.rcount);
         if (!in.bad && (L.perm.size() != (size_t)L.m || L.ghosts.size() != (size_t)L.g || L.mark.size() != (size_t)L.m))
             in.bad = true;
+        if (!in.bad) in.bad = !part_level_consistent(L, p.nranks);
     }
     const bool bad = in.bad;
     fclose(f);
@@ -352,14 +438,7 @@ extern "C" int sss_part_save(const SSS_AMG *mg, int nranks, int agg_rows, const 
     if (!mg || nranks < 1 || !prefix) return ERROR_INPUT_PAR;
     if (agg_rows <= 0) agg_rows = 20000;
     int nagg = -1;
-    for (int r = 0; r < nranks; ++r) {   // one rank's plan in memory at a time
-        sss::PartPlan plan;
-        int rc = sss::part_plan_build(plan, mg, nranks, r, agg_rows);
-        if (rc) return rc;
-        if (plan.nagg < 1) return ERROR_INPUT_PAR;
-        nagg = plan.nagg;
-        if ((rc = sss::part_plan_write(plan, mg->pars, sss::part_file_name(prefix, r).c_str()))) return rc;
-    }
+    if (int rc = sss::part_save_all(mg, nranks, agg_rows, prefix, nagg)) return rc;
     SSS_AMG tail = *mg;   // the replicated levels, as their own hierarchy
     tail.cg = mg->cg + nagg;
     tail.num_levels = mg->num_levels - nagg;

@@ -16,6 +16,7 @@ import json
 import os
 import resource
 import sys
+import threading
 import time
 from pathlib import Path
 
@@ -30,14 +31,41 @@ def level_table(H) -> list:
     return out
 
 
-def build(stencil: int, n: int, ranks: int, prefix: Path, agg_rows: int = 0) -> dict:
+def rank_summary(prefix: Path, ranks: int) -> list:
+    """Per rank: its partition file's size and, per partitioned level, own rows, ghosts and the
+    peers it receives from / sends to (read back from the files, one at a time)."""
+    from . import _native as N
+    out = []
+    for r in range(ranks):
+        f = Path(f"{prefix}.r{r}")
+        P = N.PartPlan.load(f)
+        lv = []
+        for l in range(P.nagg):
+            _, _, m, g = P.level(l)
+            h = P.halo(l)
+            lv.append({"m": m, "g": g, "recv_peers": h["rsrc"].tolist(), "send_peers": h["sdst"].tolist()})
+        out.append({"rank": r, "file_bytes": f.stat().st_size, "nagg": P.nagg, "levels": lv})
+        P.close()
+    return out
+
+
+def _heartbeat(stop: threading.Event, t0: float, what: list):
+    while not stop.wait(30.0):
+        print(f"[partition] {what[0]} ({time.perf_counter() - t0:.0f} s)", file=sys.stderr, flush=True)
+
+
+def build(stencil: int, n: int, ranks: int, prefix: Path, agg_rows: int = 0, summary: bool = True) -> dict:
     from . import _native as N
     t0 = time.perf_counter()
+    phase = ["generating the operator"]
+    stop = threading.Event()
+    threading.Thread(target=_heartbeat, args=(stop, t0, phase), daemon=True).start()
     M = N.generate(stencil, n)
     sys.stdout.flush()
     saved = os.dup(1)
     os.dup2(2, 1)   # the setup's level table goes to stderr
     try:
+        phase[0] = "setup"
         H = N.Hierarchy(M)
     finally:
         C.CDLL(None).fflush(None)
@@ -46,6 +74,7 @@ def build(stencil: int, n: int, ranks: int, prefix: Path, agg_rows: int = 0) -> 
     N.lib().SSS_mat_destroy(C.byref(M))
     t1 = time.perf_counter()
     prefix.parent.mkdir(parents=True, exist_ok=True)
+    phase[0] = "writing the partition set"
     N.part_save(H, ranks, prefix, agg_rows)
     t2 = time.perf_counter()
     man = {"stencil": stencil, "n": n, "ranks": ranks, "agg_rows": agg_rows, "levels": level_table(H),
@@ -53,6 +82,11 @@ def build(stencil: int, n: int, ranks: int, prefix: Path, agg_rows: int = 0) -> 
            "setup_s": t1 - t0, "partition_s": t2 - t1,
            "peak_rss_gb": resource.getrusage(resource.RUSAGE_SELF).ru_maxrss / 2**20}
     H.close()
+    if summary:
+        phase[0] = "reading the partition files back"
+        man["ranks_detail"] = rank_summary(prefix, ranks)
+        man["tail_file_bytes"] = Path(f"{prefix}.tail").stat().st_size
+    stop.set()
     Path(str(prefix) + ".json").write_text(json.dumps(man))
     return man
 
@@ -66,7 +100,7 @@ def main():
     p.add_argument("--agg-rows", type=int, default=0)
     a = p.parse_args()
     man = build(a.stencil, a.n, a.ranks, Path(a.prefix), a.agg_rows)
-    print(json.dumps({k: v for k, v in man.items() if k != "levels"}), flush=True)
+    print(json.dumps({k: v for k, v in man.items() if k not in ("levels", "ranks_detail")}), flush=True)
 
 
 if __name__ == "__main__":

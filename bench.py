@@ -61,8 +61,8 @@ def parse():
                    help="stencil: the --stencil operator on an --n grid; circuit: the G3_circuit stand-in "
                         "(BASELINE.json configs[3], amg_amd/workloads.py; --n = rows, default 1,585,478; 1 GPU)")
     p.add_argument("--parity-converge", type=int, default=None,
-                   help="run the parity-mode mirror to tol (reference iteration count measured in this run); "
-                        "default 1 for --workload circuit, else 0 (the 400^3 count comes from profiles/)")
+                   help="run the parity-mode mirror to tol (the reference-semantics iteration count measured in "
+                        "this run, beside the throughput count); default 1 at N = 1")
     p.add_argument("--mode", default="throughput", choices=["throughput", "parity"])
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--sequential-upload", action="store_true",
@@ -345,7 +345,7 @@ def main():
         from amg_amd.workloads import G3_CIRCUIT_ROWS
         args.n = G3_CIRCUIT_ROWS if circuit else 256 if args.stencil == 27 else {8: 512}.get(D.world, 400)
     if args.parity_converge is None:
-        args.parity_converge = 1 if circuit else 0
+        args.parity_converge = 1 if D.world == 1 else 0
     hb_stop = threading.Event()
     threading.Thread(target=heartbeat, args=(hb_stop, time.perf_counter()), daemon=True).start()
     import amg_amd as A
@@ -565,6 +565,9 @@ def main():
                     "iterations_to_tol_throughput_same_run": its,
                     "parity_ms_per_cycle_same_run": parity["ms_per_step"],
                     "source": "this run (parity-mode mirror to tol)"}
+        # throughput mode must converge within the reference's count + 2
+        ref_conv["ladder"] = ("ok" if parity["final_relres"] < pars["tol"] and relres < pars["tol"]
+                              and its <= parity["iterations_to_tol"] + 2 else "violated")
     elif conv.exists() and args.stencil == 7 and not circuit:
         try:
             cj = json.loads(conv.read_text())["modes"]
@@ -580,13 +583,17 @@ def main():
     import resource
     rss_gb = D.max(resource.getrusage(resource.RUSAGE_SELF).ru_maxrss / 2**20)   # peak over the ranks
 
-    traffic = None   # {"csr": bytes, "stored": bytes} per launch, from tools/gpu/pmc.sh at this format
-    pmc = ROOT / "profiles" / "r02_level0_spmv_pmc.json"
-    if pmc.exists() and D.world == 1 and not circuit:
+    # {"csr": bytes, "stored": bytes} per launch: the newest committed PMC record of this workload and
+    # format (tools/gpu/pmc.sh: separate rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes cannot run
+    # inside this process), with the commit it was measured at
+    traffic, traffic_src = None, None
+    pmcs = sorted((ROOT / "profiles").glob("r*_level0_spmv_pmc.json"))
+    if pmcs and D.world == 1 and not circuit:
         try:
-            rec = json.loads(pmc.read_text())
+            rec = json.loads(pmcs[-1].read_text())
             if rec.get("n") == n and rec.get("a_format") == a_format:
                 traffic = {k: rec[k]["hbm_bytes_per_launch"] for k in ("csr", "stored") if k in rec}
+                traffic_src = f"profiles/{pmcs[-1].name} (commit {rec.get('commit', 'unknown')})"
         except Exception:
             traffic = None
 
@@ -676,6 +683,7 @@ def main():
                      "achieved": achieved, "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": achieved / PEAK_HBM_GBS,
                      "frac_of_copy_peak": achieved / COPY_PEAK_GBS, "avg_launch_ms": csr_ms,
                      "bytes_per_launch": csr_bytes, "traffic": traffic.get("csr") if traffic else None,
+                     "traffic_source": traffic_src,
                      "algorithmic_bytes": "SURVEY.md 8(d): 12 nnz + 4 (n + 1) + 8 n_cols + 16 n",
                      "cycle_storage": {
                          "a_format": a_format, "kernel": "the same residual from the storage the V-cycle uses",

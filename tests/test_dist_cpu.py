@@ -1,9 +1,12 @@
-"""CPU, world_size 2 over gloo: the row partition of the distributed engine (sss_part_plan_*).
+"""CPU, world sizes 2, 4 and 8 over gloo: the row partition of the distributed engine
+(sss_part_plan_*).
 
 Each rank builds the same global hierarchy, takes its partition, moves ghost values with the
 plan's halo lists over torch.distributed (gloo) point-to-point, and checks that its local A, R
 and P products equal the global products on its rows bitwise (same entries, same order): the
-host-side contract the multi-GPU engine (amg_amd/csrc/sss_dist.hip) runs on.
+host-side contract the multi-GPU engine (amg_amd/csrc/sss_dist.hip) runs on.  At world 4 and 8
+the interior ranks have two level-0 peers and the coarse levels (wider Galerkin stencils) couple
+to non-adjacent ranks: ghosts arrive from up to seven peers.
 """
 from __future__ import annotations
 
@@ -73,6 +76,17 @@ def _worker(rank, world, port, kind, n, agg_rows, errq, prefix=None):
                     assert all(np.array_equal(x.view(np.uint8), y.view(np.uint8)) for x, y in zip(a, b)), (l, w)
         ora = oracle.load()
         assert plan.nagg >= 2, plan.nagg
+        # peers per level, gathered: slab interior ranks have two on level 0, and at world >= 4 some
+        # coarse level couples a rank to a non-adjacent one
+        peers = [len(plan.halo(l)["rsrc"]) for l in range(plan.nagg)]
+        far = any(abs(int(q) - rank) > 1 for l in range(plan.nagg) for q in plan.halo(l)["rsrc"])
+        allp = [None] * world
+        dist.all_gather_object(allp, (peers, far))
+        if 0 < rank < world - 1:
+            assert peers[0] == 2, peers
+        if world >= 8:
+            assert any(f for _, f in allp), allp
+            assert max(max(p) for p, _ in allp) >= 3, allp
         # ranges tile every partitioned level
         for l in range(plan.nagg + 1):
             lo, hi, _, _ = plan.level(l)
@@ -135,13 +149,13 @@ def _worker(rank, world, port, kind, n, agg_rows, errq, prefix=None):
         errq.put(f"rank {rank}: {e!r}\n{traceback.format_exc()}")
 
 
-def _run_world2(kind, n, agg, prefix=None):
+def _run_world(world, kind, n, agg, prefix=None):
     import torch.multiprocessing as mp
 
     ctx = mp.get_context("spawn")
     errq = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, kind, n, agg, errq, prefix)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, kind, n, agg, errq, prefix)) for r in range(world)]
     for p in procs:
         p.start()
     for p in procs:
@@ -155,26 +169,33 @@ def _run_world2(kind, n, agg, prefix=None):
 
 @pytest.mark.parametrize("kind,n,agg", [(7, 20, 60), (27, 12, 40)])
 def test_partition_products_world2(kind, n, agg):
-    _run_world2(kind, n, agg)
+    _run_world(2, kind, n, agg)
 
 
-@pytest.mark.parametrize("kind,n,agg", [(7, 20, 60), (27, 12, 40)])
-def test_partition_files_world2(kind, n, agg, tmp_path):
+@pytest.mark.parametrize("world,kind,n,agg", [(4, 7, 32, 60), (4, 27, 16, 40), (8, 7, 32, 60), (8, 27, 16, 40)])
+def test_partition_products_multi_peer(world, kind, n, agg):
+    """World 4 and 8: several peers per level, ghosts gathered from two or more neighbours, coarse
+    levels coupled to non-adjacent ranks -- every local product still bitwise the global one."""
+    _run_world(world, kind, n, agg)
+
+
+@pytest.mark.parametrize("world,kind,n,agg", [(2, 7, 20, 60), (2, 27, 12, 40), (8, 7, 32, 60)])
+def test_partition_files(world, kind, n, agg, tmp_path):
     """The same contract with each rank reading only its partition file (sss_part_save /
     sss_part_plan_load): the file round-trips the plan bitwise, and the products match."""
     import amg_amd as A
     from conftest import build_hierarchy, quiet_ctx
     H = build_hierarchy(A.generate(kind, n), quiet_ctx)
     prefix = tmp_path / "part"
-    A.part_save(H, 2, prefix, agg)
-    assert (tmp_path / "part.r0").exists() and (tmp_path / "part.r1").exists() and (tmp_path / "part.tail").exists()
+    A.part_save(H, world, prefix, agg)
+    assert all((tmp_path / f"part.r{r}").exists() for r in range(world)) and (tmp_path / "part.tail").exists()
     T = A.Hierarchy.load(tmp_path / "part.tail")
     plan0 = A.PartPlan.load(tmp_path / "part.r0")
     assert T.num_levels == H.num_levels - plan0.nagg
     for l in range(T.num_levels):   # the replicated tail is the global hierarchy's levels >= nagg
         a, b = A.csr_arrays(T.level(l).A), A.csr_arrays(H.level(plan0.nagg + l).A)
         assert all(np.array_equal(x.view(np.uint8), y.view(np.uint8)) for x, y in zip(a, b))
-    _run_world2(kind, n, agg, str(prefix))
+    _run_world(world, kind, n, agg, str(prefix))
 
 
 def test_bench_gpus_n_launches_n_ranks():

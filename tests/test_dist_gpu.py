@@ -1,4 +1,4 @@
-"""GPU, world_size 2 on one device: the row-partitioned engine (sss_hip_dist_*) over the host
+"""GPU, world sizes 2, 4 and 8 on one device: the row-partitioned engine (sss_hip_dist_*) over the host
 transport (torch.distributed gloo; RCCL refuses two ranks on one GPU).  Each rank's rows are
 computed exactly as on one GPU, so after every V-cycle the gathered x equals the single-GPU
 engine's x bitwise; the residual norm is reduced in another order (rtol 1e-12)."""
@@ -142,6 +142,28 @@ def test_dist_from_partition_files(kind, n, smoother, sum_order, tmp_path):
     A.part_save(H, 2, tmp_path / "part", 100)
     H.close()
     _run(2, "host", kind, n, smoother, 2, 100, sum_order=sum_order, parts=str(tmp_path / "part"))
+
+
+@pytest.mark.parametrize("world,kind,n,smoother,agg", [
+    (4, 7, 32, "hybrid", 60), (8, 7, 32, "hybrid", 60), (4, 27, 16, "jacobi", 40), (8, 27, 16, "jacobi", 40)])
+def test_dist_multi_peer(world, kind, n, smoother, agg, monkeypatch):
+    """4 and 8 ranks sharing the one GPU over the host transport: interior ranks exchange halos with
+    two level-0 neighbours, and at 8 ranks the coarse levels gather ghosts from up to six peers,
+    several of them non-adjacent; the replicated tail is all-gathered from every rank.  The halo
+    overlap split is on (SSS_HIP_OVERLAP=2).  After 4 V-cycles x is bitwise the single-GPU engine's."""
+    monkeypatch.setenv("SSS_HIP_OVERLAP", "2")
+    _run(world, "host", kind, n, smoother, 2, agg)
+
+
+@pytest.mark.parametrize("world,kind,n,smoother,agg,sum_order", [(4, 7, 32, "hybrid", 60, 1), (8, 27, 16, "jacobi", 40, 0)])
+def test_dist_multi_peer_from_files(world, kind, n, smoother, agg, sum_order, tmp_path):
+    """The bench's N > 1 path (partition set, each rank reading only its file) at 4 and 8 ranks."""
+    import amg_amd as A
+    from conftest import build_hierarchy, quiet_ctx
+    H = build_hierarchy(A.generate(kind, n), quiet_ctx)
+    A.part_save(H, world, tmp_path / "part", agg)
+    H.close()
+    _run(world, "host", kind, n, smoother, 2, agg, sum_order=sum_order, parts=str(tmp_path / "part"))
 
 
 def _run(world, transport, kind, n, smoother, inner_from, agg, sum_order=0, parts=None):

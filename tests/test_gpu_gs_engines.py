@@ -228,6 +228,57 @@ def test_natural_gs_host_entry(p32_h, istart, iend, istep):
         assert np.array_equal(xg.view(np.uint64), xr.view(np.uint64)), (istart, iend, istep, post)
 
 
+def _nonsym_upwind(nx: int, seed: int):
+    """Structurally nonsymmetric 2-D operator: 5-point upwind convection-diffusion on an nx*nx
+    grid, with the east coupling dropped on a random third of the rows (so the same-pass coupling
+    of the one-launch engines is not symmetric and they must not take the pass)."""
+    rng = np.random.default_rng(seed)
+    rp, ci, v = [0], [], []
+    for j in range(nx):
+        for i in range(nx):
+            r = i + nx * j
+            ent = []
+            if j > 0:
+                ent.append((r - nx, -1.5))
+            if i > 0:
+                ent.append((r - 1, -1.25))
+            ent.append((r, 4.5 + 0.1 * rng.random()))
+            if i + 1 < nx and rng.random() > 1 / 3:
+                ent.append((r + 1, -0.5))
+            if j + 1 < nx:
+                ent.append((r + nx, -0.75))
+            for c, a in ent:
+                ci.append(c)
+                v.append(a)
+            rp.append(len(ci))
+    return A.NumpyCSR(np.array(rp), np.array(ci), np.array(v))
+
+
+@pytest.mark.parametrize("istart,iend,istep", [(0, -1, 1), (0, -1, -1), (17, 900, 1)])
+def test_natural_gs_nonsymmetric_bitwise(istart, iend, istep, engine):
+    """Natural-order GS (x_i = t * d with the carried reciprocal, Solve/SSS_smooth.c:90-137) on a
+    structurally nonsymmetric matrix: whichever engine is asked for, the pass falls back to a form
+    that multiplies by the reciprocal -- bitwise the oracle in both directions."""
+    ora = oracle.load()
+    M = _nonsym_upwind(40, 5)
+    n = M.mat.num_rows
+    iend = n - 1 if iend < 0 else iend
+    mark = np.zeros(n, np.int32)
+    rng = np.random.default_rng(istart + iend)
+    for post in (False, True):
+        b = rng.standard_normal(n)
+        x0 = rng.standard_normal(n)
+        xg, xr = x0.copy(), x0.copy()
+        sg = _smtr(M.mat, b, xg, mark.ctypes.data_as(C.POINTER(C.c_int)), 2, post)
+        sr = _smtr(M.mat, b, xr, mark.ctypes.data_as(C.POINTER(C.c_int)), 2, post)
+        for s_ in (sg, sr):
+            s_.cf_order = 0
+            s_.istart, s_.iend, s_.istep = istart, iend, istep
+        assert A.lib().sss_hip_host_smooth(C.byref(sg), int(post)) == 0
+        (ora.ora_smoother_post if post else ora.ora_smoother_pre)(C.byref(sr))
+        assert np.array_equal(xg.view(np.uint64), xr.view(np.uint64)), (istart, iend, istep, post, engine)
+
+
 @pytest.mark.parametrize("hname", ["bus_h", "p32_h", "a27_h"])
 @pytest.mark.parametrize("smoother,coarse", [("exact", "krylov"), ("exact", "direct")])
 def test_w_cycle_bitwise(request, hname, smoother, coarse):
@@ -301,3 +352,75 @@ def test_dictionary_tiles_bitwise(request, hname, smoother, coarse, monkeypatch)
     for mode in ("ell", "tiles"):
         assert np.array_equal(out[mode][0].view(np.uint64), out["none"][0].view(np.uint64)), mode
         assert out[mode][1] == out["none"][1], mode
+
+
+# ---------------------------------------------------------------- a stalled pass fails loudly
+def _flow_levels(D, H):
+    return [l for l in range(H.num_levels - 1)
+            if D.level_info(l).gs_engine_f or D.level_info(l).gs_engine_c]
+
+
+def test_stall_fails_loudly(p32_h, monkeypatch):
+    """A one-launch pass that gives up waiting (forced here: SSS_HIP_GS_SPIN < 0 makes every launch
+    report a stall) invalidates the iterate: the residual norm that follows, the sync and the
+    download all fail instead of returning a plausible residual over a wrong x -- and the error
+    word is cleared on read, so the next check reports only new stalls."""
+    monkeypatch.setenv("SSS_HIP_GS_SPIN", "-1")
+    n = p32_h.level(0).A.num_rows
+    D = A.DeviceHierarchy(p32_h, smoother="exact", coarse="krylov")
+    try:
+        assert _flow_levels(D, p32_h), "no one-launch pass on this hierarchy"
+        D.upload(0, "b", np.ones(n))
+        D.upload(0, "x", np.ones(n))
+        D.cycle()
+        with pytest.raises(RuntimeError, match="residual_norm"):
+            D.residual_norm()
+        D.sync()   # cleared by the read above, nothing new since
+        D.cycle()
+        with pytest.raises(RuntimeError, match="sync"):
+            D.sync()
+        D.cycle()
+        with pytest.raises(RuntimeError, match="download"):
+            D.download(0, "x")
+    finally:
+        D.close()
+
+
+def test_tiny_spin_limit_never_silent(p32_h, monkeypatch):
+    """With a spin limit of zero polls a pass gives up whenever a row's lower neighbour is not yet
+    published: every outcome is either the reference's x bit for bit or a loud failure."""
+    monkeypatch.setenv("SSS_HIP_GS_SPIN", "0")
+    n = p32_h.level(0).A.num_rows
+    _, rel_r, _ = oracle_solve(p32_h, np.ones(n), x_r := np.ones(n))
+    D = A.DeviceHierarchy(p32_h, smoother="exact", coarse="krylov")
+    stalled = False
+    try:
+        D.upload(0, "b", np.ones(n))
+        D.upload(0, "x", np.ones(n))
+        try:
+            for _ in range(len(rel_r)):
+                D.cycle()
+                D.residual_norm()
+            x_g = D.download(0, "x")
+        except RuntimeError:
+            stalled = True
+    finally:
+        D.close()
+    if not stalled:
+        assert np.array_equal(x_g.view(np.uint64), x_r.view(np.uint64))
+
+
+def test_stall_exits_drop_in_cli(tmp_path):
+    """The drop-in CLI (amg file.mtx) on a stalled pass: exit(ERROR_MISC) with a '### ERROR' line,
+    no iteration row after the failure, as the reference's fatal paths (SSS_utils.c:16-94)."""
+    import os
+    import subprocess
+    from conftest import BUS_MTX, ROOT
+    exe = ROOT / "amg_amd" / "bin" / "amg"
+    env = dict(os.environ, SSS_HIP_GS_SPIN="-1")
+    r = subprocess.run([str(exe), str(BUS_MTX)], capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == (-14 & 0xFF), (r.returncode, r.stderr[-2000:])
+    assert "### ERROR" in r.stdout and "stalled" in r.stderr
+    rows = [l for l in r.stdout.splitlines() if l[:6].strip().isdigit() and "|" in l]
+    assert len(rows) <= 1, rows   # only the iteration-0 row
+    assert "AMG solve time" not in r.stdout

@@ -27,9 +27,13 @@ REFG = json.loads((HERE / "golden" / "golden.json").read_text())["ref_units"]
 
 class _LazyRef:
     """oracle/_ref/libsss_ref.so, loaded on first use only (so a `-m gpu` run, which deselects
-    these CPU tests, never maps the compiled reference)."""
+    these CPU tests, never maps the compiled reference).  Only the reference's own symbols (SSS_*)
+    load it: pytest's collection probes module attributes (`__test__`, `_pytestfixturefunction`,
+    ...), and those must not map the library."""
 
     def __getattr__(self, name):
+        if not name.startswith("SSS_"):
+            raise AttributeError(name)
         return getattr(oracle.load_ref(), name)
 
 

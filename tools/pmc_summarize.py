@@ -1,6 +1,6 @@
 """Level-0 SpMV HBM traffic from the two rocprofv3 --pmc passes of tools/gpu/pmc.sh.
 
-    python tools/pmc_summarize.py gpurun_out profiles/r02_level0_spmv_pmc.json
+    python tools/pmc_summarize.py gpurun_out profiles/r03_level0_spmv_pmc.json [commit]
 
 Reads gpurun_out/pmc_FETCH_SIZE/**.csv and gpurun_out/pmc_WRITE_SIZE/**.csv (one row per launch),
 keeps the level-0 residual SpMV launches (spmv_adaptive<2, ...>, the kernel tools/pmc_level0.py
@@ -13,6 +13,7 @@ from __future__ import annotations
 
 import csv
 import json
+import subprocess
 import sys
 from pathlib import Path
 
@@ -41,6 +42,13 @@ def counter_avg(d: Path, name: str, csr: bool) -> tuple[float, int]:
 def main():
     out = Path(sys.argv[1])
     dst = Path(sys.argv[2])
+    commit = sys.argv[3] if len(sys.argv) > 3 else None
+    if commit is None:   # the tree that was sent to the box: this checkout's HEAD (+ "-dirty")
+        try:
+            commit = subprocess.run(["git", "describe", "--always", "--dirty"], capture_output=True, text=True,
+                                    check=True).stdout.strip()
+        except (OSError, subprocess.CalledProcessError):
+            commit = "unknown"
     info = None
     for line in (out / "pmc_FETCH_SIZE.log").read_text().splitlines():
         if line.startswith("{"):
@@ -49,7 +57,7 @@ def main():
         raise SystemExit("pmc_level0.py JSON line not found")
     N, nnz = info["rows"], info["nnz"]
     survey = 12 * nnz + 4 * (N + 1) + 24 * N   # SURVEY.md 8(d), y = b - A x
-    rec = {"n": info["n"], "rows": N, "nnz": nnz, "a_format": info["a_format"]}
+    rec = {"n": info["n"], "rows": N, "nnz": nnz, "a_format": info["a_format"], "commit": commit}
     for key, csr, alg, ms in (("csr", True, survey, info.get("avg_ms_csr")),
                               ("stored", False, info["algorithmic_bytes_per_launch"], info["avg_ms"])):
         fetch, nf = counter_avg(out / "pmc_FETCH_SIZE", "FETCH_SIZE", csr)
@@ -57,7 +65,7 @@ def main():
         rd = fetch * 1024 * FETCH_CORRECTION
         wr = write * 1024
         rec[key] = {"kernel": "spmv_adaptive<RESID> level 0 from " + ("the CSR arrays" if csr else info["a_format"]),
-                    "avg_ms_unprofiled": ms, "fetch_size_kib_raw": fetch, "write_size_kib_raw": write,
+                    "avg_ms_under_pmc_pass": ms, "fetch_size_kib_raw": fetch, "write_size_kib_raw": write,
                     "hbm_read_bytes_per_launch": rd, "hbm_write_bytes_per_launch": wr,
                     "hbm_bytes_per_launch": rd + wr, "algorithmic_bytes_per_launch": alg,
                     "traffic_over_algorithmic": (rd + wr) / alg, "launches": min(nf, nw)}
