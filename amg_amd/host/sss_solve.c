@@ -50,6 +50,18 @@ sss_hip_hier *sss_dev_mirror_for(SSS_AMG *mg)
     return g_mirrors[free_slot].h;
 }
 
+/* a mirror built elsewhere (sss_hip_setup_create) becomes this hierarchy's */
+static void sss_dev_adopt_mirror(SSS_AMG *mg, sss_hip_hier *h)
+{
+    for (int s = 0; s < MIRROR_SLOTS; ++s)
+        if (!g_mirrors[s].h) {
+            g_mirrors[s].h = h;
+            g_mirrors[s].key = mg->cg;
+            return;
+        }
+    sss_hip_hier_destroy(h);   /* no slot: the first solve builds it again */
+}
+
 void sss_dev_release_mirror(const void *cg_key)
 {
     for (int s = 0; s < MIRROR_SLOTS; ++s) {
@@ -136,7 +148,25 @@ SSS_RTN SSS_solver_amg(SSS_MAT *A, SSS_VEC *x, SSS_VEC *b, SSS_AMG_PARS *pars)
     t0 = SSS_get_time();
     if (A->num_rows != A->num_cols) printf("### ERROR: A is not a square matrix!\n");
     if (A->num_nnzs <= 0) printf("### ERROR: A has no nonzero entries!\n");
-    SSS_amg_setup(&mg, A, pars);
+    {
+        /* SSS_amg_setup with the HBM mirror built level by level while it runs (same hierarchy,
+         * same stdout); SSS_amg_solve then finds the mirror ready.  SSS_HIP_OVERLAP_SETUP=0: the
+         * reference's sequence (setup, then the mirror at the first solve). */
+        const char *ov = getenv("SSS_HIP_OVERLAP_SETUP");
+        if (ov && ov[0] == '0') {
+            SSS_amg_setup(&mg, A, pars);
+        } else {
+            sss_hip_opts o;
+            sss_hip_hier *h;
+            double times[3];
+            sss_hip_opts_default(&o);
+            h = sss_hip_setup_create(&mg, A, pars, &o, times);
+            if (h) {
+                sss_dev_adopt_mirror(&mg, h);
+                fprintf(stderr, "AMG device mirror: %g s after the setup returned\n", times[1]);
+            }
+        }
+    }
     rtn = SSS_amg_solve(&mg, x, b);
     SSS_amg_data_destroy(&mg);
     printf("AMG totally time: %g s\n", SSS_get_time() - t0);

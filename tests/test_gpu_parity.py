@@ -482,8 +482,12 @@ def test_solve_bus_known_answer(bus_h):
     assert ["%.6e" % r for r in rel] == ["%.6e" % r for r in expect]
 
 
-def test_drop_in_solver_amg(bus_matrix, capfd):
-    """SSS_solver_amg through the C ABI prints the reference's table and fills the caller's x."""
+@pytest.mark.parametrize("overlap", ["1", "0"])
+def test_drop_in_solver_amg(bus_matrix, capfd, overlap, monkeypatch):
+    """SSS_solver_amg through the C ABI prints the reference's table and fills the caller's x --
+    with the HBM mirror built while the setup runs (default) and in the reference's sequence
+    (setup, then the mirror at the first solve: SSS_HIP_OVERLAP_SETUP=0)."""
+    monkeypatch.setenv("SSS_HIP_OVERLAP_SETUP", overlap)
     n = bus_matrix.num_rows
     b, x = np.ones(n), np.ones(n)
     pars = A.default_pars()
