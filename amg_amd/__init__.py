@@ -7,5 +7,6 @@ from ._native import (  # noqa: F401
     ABI_SYMBOLS, COARSE, SMOOTH, SPMV, Comm, DeviceHierarchy, DistHierarchy, Hierarchy, NumpyCSR, PartPlan,
     SSS_AMG, SSS_AMG_COMP,
     SSS_AMG_PARS, SSS_HIP_OPTS, SSS_MAT, SSS_RTN, SSS_SMTR, SSS_VEC, csr_arrays, default_pars, device_count,
+    hbm_used_bytes,
     generate, lib, part_save, read_mtx,
 )

@@ -105,7 +105,7 @@ ABI_SYMBOLS = [
     "SSS_imat_destroy", "SSS_mat_trans", "SSS_blas_mat_rap", "SSS_realloc", "SSS_amg_complexity_print",
     "SSS_amg_setup", "SSS_amg_coarsen", "SSS_amg_interp", "SSS_amg_interp_trunc", "interp_DIR", "SSS_mat_read",
     "SSS_amg_pars_init", "SSS_amg_pars_print", "mmio_info", "mmio_data",
-    "sss_hip_opts_default", "sss_hip_device_count", "sss_hip_hier_create", "sss_hip_hier_destroy",
+    "sss_hip_opts_default", "sss_hip_device_count", "sss_hip_mem_info", "sss_hip_hier_create", "sss_hip_hier_destroy",
     "sss_hip_setup_create", "sss_amg_setup_hooked",
     "sss_hip_upload_vec", "sss_hip_download_vec", "sss_hip_cycle", "sss_hip_residual_norm", "sss_hip_pcg",
     "SSS_amg_save", "SSS_amg_load",
@@ -173,6 +173,7 @@ def _declare(lib):
         "sss_gen_stencil": (C.c_int, [C.c_int] * 6 + [P(SSS_MAT)]),
         "sss_hip_opts_default": (None, [P(SSS_HIP_OPTS)]),
         "sss_hip_device_count": (C.c_int, []),
+        "sss_hip_mem_info": (C.c_int, [P(C.c_size_t), P(C.c_size_t)]),
         "sss_hip_hier_create": (C.c_void_p, [P(SSS_AMG), P(SSS_HIP_OPTS)]),
         "sss_hip_setup_create": (C.c_void_p, [P(SSS_AMG), P(SSS_MAT), P(SSS_AMG_PARS), P(SSS_HIP_OPTS),
                                               P(C.c_double)]),
@@ -447,6 +448,15 @@ class DeviceHierarchy:
             self.close()
         except Exception:
             pass
+
+
+def hbm_used_bytes() -> int:
+    """HBM in use on the current device (total - free, hipMemGetInfo): this process's mirrors plus
+    the runtime's own allocations."""
+    f, t = C.c_size_t(), C.c_size_t()
+    if lib().sss_hip_mem_info(C.byref(f), C.byref(t)) != 0:
+        raise RuntimeError("sss_hip_mem_info failed")
+    return t.value - f.value
 
 
 def device_count() -> int:

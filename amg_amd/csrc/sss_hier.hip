@@ -115,6 +115,15 @@ extern "C" int sss_hip_device_count(void)
     return n;
 }
 
+extern "C" int sss_hip_mem_info(size_t *free_bytes, size_t *total_bytes)
+{
+    size_t f = 0, t = 0;
+    SSS_HIP(hipMemGetInfo(&f, &t));
+    *free_bytes = f;
+    *total_bytes = t;
+    return 0;
+}
+
 static int level_smoother_kind(const sss_hip_opts &o, int l)
 {
     if (o.smoother == SSS_HIP_SMOOTH_JACOBI) return SSS_HIP_SMOOTH_JACOBI;

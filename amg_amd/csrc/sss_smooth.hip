@@ -542,7 +542,7 @@ __device__ __forceinline__ void relax_range_ell(int blo, const int2 *__restrict_
 }
 
 template <int MODE, int DICT = 0>   // DICT: with_tile_kind (8/16/32: dictionary ELL, that width)
-__global__ __launch_bounds__(kBlock) void relax_range(int blo, const int2 *__restrict__ blk, const int *__restrict__ rp,
+__device__ __forceinline__ void relax_range_body(int blo, const int2 *__restrict__ blk, const int *__restrict__ rp,
                                                       const int *__restrict__ ci, const double *__restrict__ v,
                                                       const int *__restrict__ diag_pos, int lo,
                                                       const double *__restrict__ b, double *x,
@@ -640,6 +640,52 @@ __global__ __launch_bounds__(kBlock) void relax_range(int blo, const int2 *__res
         if (threadIdx.x == 0) finish(r, acc);
     }
     }
+}
+
+#define SSS_RELAX_ARGS                                                                                          \
+    int blo, const int2 *__restrict__ blk, const int *__restrict__ rp, const int *__restrict__ ci,                 \
+        const double *__restrict__ v, const int *__restrict__ diag_pos, int lo, const double *__restrict__ b,      \
+        double *x, const double *__restrict__ yp, double *__restrict__ y, const double *__restrict__ deff,          \
+        const unsigned *__restrict__ pk, const double *__restrict__ pv, const int2 *__restrict__ pb,               \
+        double *__restrict__ rr, double *__restrict__ partial, XSrc xs, DevDict dt
+#define SSS_RELAX_PASS blo, blk, rp, ci, v, diag_pos, lo, b, x, yp, y, deff, pk, pv, pb, rr, partial, xs, dt
+template <int MODE, int DICT = 0>
+__global__ __launch_bounds__(kBlock) void relax_range(SSS_RELAX_ARGS)
+{
+    relax_range_body<MODE, DICT>(SSS_RELAX_PASS);
+}
+// The tile paths (plain / sorted / dictionary tiles, K < 8) held to 5 waves per SIMD: the value-
+// dictionary tiles of level 1 otherwise take 107 VGPRs (4 waves per SIMD, 14 resident per CU in
+// profiles/r03_kernels_sq_pmc_400.txt) and wait on memory 70 % of their cycles.  Measured at
+// 400^3 (tools/gpu/ab.sh): level-1 smoothing 4.61 -> 4.23 ms per V-cycle at 5 waves (96 VGPRs);
+// 6 waves (the LDS limit) spill to scratch and take 6.90 ms.
+#ifndef SSS_RELAX_WPE
+#define SSS_RELAX_WPE 5
+#endif
+template <int MODE, int DICT = 0>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(SSS_RELAX_WPE, 8))) void relax_range_occ(SSS_RELAX_ARGS)
+{
+    relax_range_body<MODE, DICT>(SSS_RELAX_PASS);
+}
+static bool relax_occ_on()
+{
+    static const bool on = [] {
+        const char *e = getenv("SSS_HIP_RELAX_OCC");
+        return !(e && *e == '0');
+    }();
+    return on;
+}
+// relax_range / relax_range_occ on dim3(nb) workgroups
+template <int M, int K, class... Args>
+static void launch_relax_range(int nb, hipStream_t s, Args... args)
+{
+    if constexpr (K < 8) {
+        if (relax_occ_on()) {
+            hipLaunchKernelGGL((relax_range_occ<M, K>), dim3(nb), dim3(kBlock), 0, s, args...);
+            return;
+        }
+    }
+    hipLaunchKernelGGL((relax_range<M, K>), dim3(nb), dim3(kBlock), 0, s, args...);
 }
 
 // relax_range for long-row levels: one wave per row (rows lo + 4 * blockIdx.x + wave).  The
@@ -921,10 +967,9 @@ int launch_f_residual_pending(const SmootherPlan &sp, const DevCSR &A, const dou
     const PassSchedule &F = sp.pass[0];
     const double *deff = (sp.own_diag && (A.pk || has_dict(A))) ? nullptr : sp.d_first;
     with_tile_kind(A, [&](auto K) {
-        hipLaunchKernelGGL((relax_range<3, decltype(K)::value>), dim3(F.bhi - F.blo), dim3(kBlock), 0, s,
-                           F.blo, A.bk, A.rp, A.ci, A.v, sp.diag_pos, F.lo, b, const_cast<double *>(x),
-                           (const double *)nullptr, pend, deff, A.pk, A.pv, A.pb, r, partial, xsrc_of(x),
-                           devdict(A, 0));
+        launch_relax_range<3, decltype(K)::value>(F.bhi - F.blo, s, F.blo, A.bk, A.rp, A.ci, A.v, sp.diag_pos, F.lo,
+                                                  b, const_cast<double *>(x), (const double *)nullptr, pend, deff,
+                                                  A.pk, A.pv, A.pb, r, partial, xsrc_of(x), devdict(A, 0));
     });
     SSS_HIP(hipGetLastError());
     return 0;
@@ -1077,11 +1122,10 @@ int smoother_run(const SmootherPlan &sp, const DevCSR &A, const double *b, doubl
                     else {
                         auto go = [&](int b0, int b1) {
                             with_tile_kind(A, [&](auto K) {
-                                hipLaunchKernelGGL((relax_range<M, decltype(K)::value>), dim3(b1 - b0),
-                                                   dim3(kBlock), 0, s, b0, A.bk, A.rp, cols, A.v, sp.diag_pos, ps.lo,
-                                                   b, x, yp, y, tile_d ? nullptr : deff, A.pk, A.pv, A.pb,
-                                                   (double *)nullptr, (double *)nullptr, xs,
-                                                   devdict(A, 0));
+                                launch_relax_range<M, decltype(K)::value>(
+                                    b1 - b0, s, b0, A.bk, A.rp, cols, A.v, sp.diag_pos, ps.lo, b, x, yp, y,
+                                    tile_d ? nullptr : deff, A.pk, A.pv, A.pb, (double *)nullptr, (double *)nullptr, xs,
+                                    devdict(A, 0));
                             });
                         };
                         if (split_pass) return hk->split(x, ps.blo, ps.bhi, go);
@@ -1147,11 +1191,10 @@ int smoother_run(const SmootherPlan &sp, const DevCSR &A, const double *b, doubl
                 } else if (fused_pass) {
                     auto go = [&](int b0, int b1) {
                         with_tile_kind(A, [&](auto K) {
-                            hipLaunchKernelGGL((relax_range<2, decltype(K)::value>), dim3(b1 - b0),
-                                               dim3(kBlock), 0, s, b0, A.bk, A.rp, A.ci, A.v, sp.diag_pos, ps.lo, b, x,
-                                               (const double *)nullptr, (double *)nullptr, tile_d ? nullptr : deff,
-                                               A.pk, A.pv, A.pb, rf->r, rf->partial, xs,
-                                               devdict(A, 0));
+                            launch_relax_range<2, decltype(K)::value>(
+                                b1 - b0, s, b0, A.bk, A.rp, A.ci, A.v, sp.diag_pos, ps.lo, b, x, (const double *)nullptr,
+                                (double *)nullptr, tile_d ? nullptr : deff, A.pk, A.pv, A.pb, rf->r, rf->partial, xs,
+                                devdict(A, 0));
                         });
                     };
                     if (split_pass) {

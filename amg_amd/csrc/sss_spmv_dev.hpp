@@ -299,7 +299,10 @@ __device__ __forceinline__ void stage_sorted(double *__restrict__ sm, int k0, in
 // dictionary in LDS (vd[vi[k]], the same bit pattern pv[k] held).
 // The slots of one pass of the loop below (U per thread): stage_dict loads the first pass ahead of
 // the dictionary barrier, so the slot stream is in flight while the dictionary arrives.
-constexpr int kVdictU = 8;
+#ifndef SSS_VDICT_U
+#define SSS_VDICT_U 8
+#endif
+constexpr int kVdictU = SSS_VDICT_U;
 __device__ __forceinline__ void vdict_load(int kb, int k1, const unsigned *__restrict__ pk,
                                            const unsigned char *__restrict__ vi, unsigned (&q)[kVdictU],
                                            unsigned (&w)[kVdictU])

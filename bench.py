@@ -449,6 +449,7 @@ def main():
                              inner_from=args.inner_from, sum_order=sum_order, sorted_tiles=sorted_tiles, parts=prefix)
         eng = Distributed(DD)
     upload_s = time.perf_counter() - t0
+    hbm_gb = D.max(A.hbm_used_bytes() / 1e9)   # the mirror resident in HBM (max over ranks)
     overlapped = D.world == 1 and getattr(DH, "times", None) is not None
     if overlapped:   # levels were uploaded during the setup: what is left after it returned
         upload_s = DH.times[1]
@@ -678,6 +679,7 @@ def main():
                    "setup_plus_upload_s": setup_s + upload_s,
                    "parallelism": f"rowpart{D.world}" if D.world > 1 else "single-gpu",
                    "host_peak_rss_gb_max_over_ranks": rss_gb,
+                   "hbm_used_gb_max_over_ranks": hbm_gb,
                    "transport": transport},
         "roofline": {"bound": "hbm", "kernel": "spmv_adaptive<RESID> level 0 from its CSR arrays (y = b - A0 x)",
                      "achieved": achieved, "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": achieved / PEAK_HBM_GBS,

@@ -68,6 +68,8 @@ void sss_hip_opts_default(sss_hip_opts *o);
 
 /* Number of usable HIP devices (0 when none; never exits). */
 int sss_hip_device_count(void);
+/* Free and total HBM of the current device, in bytes (hipMemGetInfo). */
+int sss_hip_mem_info(size_t *free_bytes, size_t *total_bytes);
 
 /* ---- hierarchy mirror -------------------------------------------------------------- */
 typedef struct sss_hip_hier sss_hip_hier;
