@@ -106,7 +106,7 @@ ABI_SYMBOLS = [
     "SSS_amg_setup", "SSS_amg_coarsen", "SSS_amg_interp", "SSS_amg_interp_trunc", "interp_DIR", "SSS_mat_read",
     "SSS_amg_pars_init", "SSS_amg_pars_print", "mmio_info", "mmio_data",
     "sss_hip_opts_default", "sss_hip_device_count", "sss_hip_mem_info", "sss_hip_hier_create", "sss_hip_hier_destroy",
-    "sss_hip_setup_create", "sss_amg_setup_hooked",
+    "sss_hip_setup_create", "sss_amg_setup_hooked", "sss_hip_rap",
     "sss_hip_upload_vec", "sss_hip_download_vec", "sss_hip_cycle", "sss_hip_residual_norm", "sss_hip_pcg",
     "SSS_amg_save", "SSS_amg_load",
     "sss_hip_coarse_solve", "sss_hip_smooth", "sss_hip_sync", "sss_hip_level_info_get", "sss_hip_num_levels",
@@ -178,6 +178,7 @@ def _declare(lib):
         "sss_hip_setup_create": (C.c_void_p, [P(SSS_AMG), P(SSS_MAT), P(SSS_AMG_PARS), P(SSS_HIP_OPTS),
                                               P(C.c_double)]),
         "sss_hip_hier_destroy": (None, [C.c_void_p]),
+        "sss_hip_rap": (C.c_int, [P(SSS_MAT), P(SSS_MAT), P(SSS_MAT), P(SSS_MAT)]),
         "sss_hip_upload_vec": (C.c_int, [C.c_void_p, C.c_int, C.c_int, _dbl_p, C.c_int]),
         "sss_hip_download_vec": (C.c_int, [C.c_void_p, C.c_int, C.c_int, _dbl_p, C.c_int]),
         "sss_hip_cycle": (C.c_int, [C.c_void_p]),

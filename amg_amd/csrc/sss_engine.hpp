@@ -258,6 +258,12 @@ int free_row_min();
 // Re-upload a free-order matrix's CSR rows column-sorted (one uploaded kEncMergedOnly whose
 // merged copy turned out not to be its only reader).
 int devcsr_sort_rows(DevCSR &d, const SSS_MAT &h, const int *seg = nullptr);
+// Device-side builders of the free-order formats (sss_build.hip; SSS_HIP_GPU_BUILD=0 keeps the
+// host builders): merged row groups from the resident stored-order CSR, and the in-place column
+// sort of each row (segment).  Results are the host builders' bit for bit.
+bool device_builders_on();
+int merged_build_device(DevCSR &d, const int *h_seg);
+int sort_rows_device(DevCSR &d, const int *h_seg);
 struct DevDict;
 DevDict devdict(const DevCSR &A, int blo);   // the matrix's dictionary tiles, block numbers from blo
 // the tile kernels stage from a dictionary (either kind): instantiate them with DICT = true

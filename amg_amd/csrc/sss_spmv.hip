@@ -660,7 +660,7 @@ int devcsr_upload(DevCSR &d, const SSS_MAT &h, int split, int enc, const int *se
     if (d.nnz > 0) {
         // free-order rows are read column-sorted by the wave-tree kernels; a two-stage split copy
         // with a merged copy (kEncMergedOnly) is read only through that (launch_ts_*): stored order
-        if (d.vec_rows && !((enc & kEncMergedOnly) && d.mg_G > 0)) {
+        if (d.vec_rows && !((enc & kEncMergedOnly) && d.mg_G > 0) && !device_builders_on()) {
             HostBuf<int> sci;
             HostBuf<double> sv;
             sort_row_segments(h, seg, sci, sv);
@@ -686,7 +686,14 @@ int devcsr_upload(DevCSR &d, const SSS_MAT &h, int split, int enc, const int *se
     if (int rc = upload_block_bounds(&d.bk, blk, h.row_ptr)) return rc;
     d.ngrid = (d.wave_rows || d.vec_rows) ? (d.n + 3) / 4 : d.nblk;
     pt.mark("blocks");
-    if (d.mg_G > 0) {
+    if (d.mg_G > 0 && device_builders_on()) {   // from the stored-order CSR just uploaded
+        d.mg_two = seg != nullptr;
+        const char *wz = getenv("SSS_HIP_MERGE_W");
+        d.mg_W = (wz && *wz) ? atoi(wz) : 4;
+        d.mg_W = d.mg_W >= 4 ? 4 : d.mg_W >= 2 ? 2 : 1;
+        if (int rc = merged_build_device(d, seg)) return rc;
+        d.ngrid = (d.mg_ng + 4 / d.mg_W - 1) / (4 / d.mg_W);
+    } else if (d.mg_G > 0) {
         std::vector<int> gp;
         HostBuf<unsigned> mk;
         HostBuf<double> mv;
@@ -707,6 +714,8 @@ int devcsr_upload(DevCSR &d, const SSS_MAT &h, int split, int enc, const int *se
         if (int rc = h2d(d.mg_k, mk.data(), sizeof(unsigned) * mk.size())) return rc;
         if (int rc = h2d(d.mg_v, mv.data(), sizeof(double) * mv.size())) return rc;
     }
+    if (d.vec_rows && !((enc & kEncMergedOnly) && d.mg_G > 0) && device_builders_on() && d.nnz > 0)
+        if (int rc = sort_rows_device(d, seg)) return rc;   // after the merged build (stored order)
     pt.mark("merged");
     // dictionary ELL first (one thread per row), else dictionary tiles (the tile kernels then stage
     // from them instead of the sorted copy)
@@ -805,6 +814,7 @@ int devcsr_upload(DevCSR &d, const SSS_MAT &h, int split, int enc, const int *se
 int devcsr_sort_rows(DevCSR &d, const SSS_MAT &h, const int *seg)
 {
     if (!d.vec_rows || d.rows_sorted || d.nnz == 0) return 0;
+    if (device_builders_on()) return sort_rows_device(d, seg);
     HostBuf<int> sci;
     HostBuf<double> sv;
     sort_row_segments(h, seg, sci, sv);

@@ -889,6 +889,12 @@ void sss_amg_setup_hooked(SSS_AMG *mg, SSS_MAT *A, SSS_AMG_PARS *pars, sss_setup
     const double t0 = SSS_get_time();
     SSS_IVEC vertices;
     int lvl = 0;
+    /* the Galerkin products of the large levels on the GPU when one is present (same result) */
+    const char *gr = getenv("SSS_SETUP_GPU_RAP"), *grm = getenv("SSS_SETUP_GPU_RAP_MIN");
+    const int use_gpu_rap = !(gr && gr[0] == '0') && sss_hip_device_count() > 0;
+    const int gpu_rap_min = (grm && *grm) ? atoi(grm) : 1000000;
+    const char *grx = getenv("SSS_SETUP_GPU_RAP_MAXROW");   /* average A row length up to which */
+    const int gpu_rap_maxrow = (grx && *grx) ? atoi(grx) : 48;
 
     *mg = SSS_amg_data_create(pars);
     vertices = SSS_ivec_create(n0);
@@ -930,7 +936,13 @@ void sss_amg_setup_hooked(SSS_AMG *mg, SSS_MAT *A, SSS_AMG_PARS *pars, sss_setup
         const double tc2 = SSS_get_time();
         L->R = SSS_mat_trans(&L->P);
         const double tc3 = SSS_get_time();
-        mg->cg[lvl + 1].A = SSS_blas_mat_rap(&L->R, &L->A, &L->P);
+        /* the device walks each coarse row's (R entry, A entry) steps in order, so it wins on the
+         * wide levels of short rows (7-pt 400^3 levels 0-2: 3.1 -> 1.1, 2.0 -> 0.75, 0.59 -> 0.37 s)
+         * and loses on the narrow levels of long rows (level 3 and below: 0.75 -> 1.2 s) */
+        const int gpu_here = use_gpu_rap && L->A.num_nnzs >= gpu_rap_min &&
+                             (double)L->A.num_nnzs <= (double)gpu_rap_maxrow * L->A.num_rows;
+        if (!(gpu_here && sss_hip_rap(&L->R, &L->A, &L->P, &mg->cg[lvl + 1].A) == 0))
+            mg->cg[lvl + 1].A = SSS_blas_mat_rap(&L->R, &L->A, &L->P);
         if (getenv("SSS_SETUP_TIMING"))   /* phase times on stderr (stdout stays the reference's) */
             fprintf(stderr, "[setup] level %d: coarsen %.3f s, interp %.3f s, transpose %.3f s, RAP %.3f s\n", lvl,
                     tc1 - tc0, tc2 - tc1, tc3 - tc2, SSS_get_time() - tc3);

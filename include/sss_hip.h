@@ -88,6 +88,14 @@ void sss_hip_hier_destroy(sss_hip_hier *h);
 sss_hip_hier *sss_hip_setup_create(SSS_AMG *mg, SSS_MAT *A, SSS_AMG_PARS *pars, const sss_hip_opts *o,
                                    double *times);
 
+/* The setup's Galerkin product A_c = R A P (SSS_blas_mat_rap, SSS_matvec.c:398-534) on the GPU,
+ * bit for bit the host product (same entries, same column order, same summation order).  C gets
+ * SSS_calloc'd arrays.  Returns 0, or an error code with C untouched (no device, no memory).
+ * The setup uses it, when a device is present, for levels with at least SSS_SETUP_GPU_RAP_MIN
+ * nonzeros in A (default 10^6) and at most SSS_SETUP_GPU_RAP_MAXROW of them per row on average
+ * (default 48); SSS_SETUP_GPU_RAP=0 keeps every product on the host. */
+int sss_hip_rap(const SSS_MAT *R, const SSS_MAT *A, const SSS_MAT *P, SSS_MAT *C);
+
 /* Progress hook of the setup (amg_amd/host/sss_setup.c): hook(ctx, mg, done, 0) once levels
  * 0 .. done-1 are final and none of them is the coarsest; hook(ctx, mg, num_levels - 1, 1) at
  * the end. */

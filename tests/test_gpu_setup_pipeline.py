@@ -76,3 +76,35 @@ def test_pipelined_setup_matches_sequential(case, mode):
     assert np.array_equal(rel_p.view(np.uint64), rel_s.view(np.uint64))
     assert np.array_equal(x_p.view(np.uint64), x_s.view(np.uint64))
     del keep
+
+
+@pytest.mark.parametrize("case", ["p7_32", "a27_16", "circ60k"])
+@pytest.mark.parametrize("merge_g", ["4", "8"])
+def test_device_builders_match_host(case, merge_g, monkeypatch):
+    """The free-order formats built on the GPU (sss_build.hip: merged row groups and column-sorted
+    rows by a segmented radix sort of the resident CSR) are the host builders' bit for bit: with
+    every level on the free-order kernels (SSS_HIP_FREE_MIN=1) and merged groups wherever possible,
+    the throughput-mode iterates (tree-order sums over those formats) are identical either way."""
+    keep = None
+    if case.startswith("p7"):
+        M = A.generate(7, 32)
+    elif case.startswith("a27"):
+        M = A.generate(27, 16)
+    else:
+        keep = W.circuit_csr(60000)
+        M = keep.mat
+    H = build_hierarchy(M, quiet_ctx)
+    n = H.level(0).A.num_rows
+    monkeypatch.setenv("SSS_HIP_FREE_MIN", "1")
+    monkeypatch.setenv("SSS_HIP_MERGE_MIN_ROWS", "1")
+    monkeypatch.setenv("SSS_HIP_MERGE_G", merge_g)
+    out = {}
+    for build in ("1", "0"):
+        monkeypatch.setenv("SSS_HIP_GPU_BUILD", build)
+        D = A.DeviceHierarchy(H, smoother="hybrid", coarse="direct", sum_order=1)
+        assert any(D.level_info(l).a_format & 8 for l in range(H.num_levels - 1))   # merged copies exist
+        out[build] = _iterate(D, n, cycles=6)
+        D.close()
+    assert np.array_equal(out["1"][0].view(np.uint64), out["0"][0].view(np.uint64))
+    assert np.array_equal(out["1"][1].view(np.uint64), out["0"][1].view(np.uint64))
+    del keep
