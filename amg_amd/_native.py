@@ -668,7 +668,8 @@ class DistHierarchy:
         f = lib().sss_hip_dist_level_flags(self.d, l)
         if f < 0:
             raise ValueError(f"no partitioned level {l}")
-        return {"zero_first": bool(f & 1), "fused_residual": bool(f & 2), "dead_prolong": bool(f & 4)}
+        return {"zero_first": bool(f & 1), "fused_residual": bool(f & 2), "dead_prolong": bool(f & 4),
+                "cycle_graph": bool(f & 8)}
 
     def _check(self, rc, what):
         if rc != 0:

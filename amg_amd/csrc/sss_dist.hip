@@ -116,6 +116,12 @@ struct sss_hip_dist {
     hipStream_t cstream = nullptr;
     hipEvent_t ev_packed = nullptr, ev_halo = nullptr;
     int overlap = 1;   // 0 off, 1 on (RCCL), 2 also split the launches over the host transport (tests)
+    // hipGraph of the whole cycle (SSS_HIP_DIST_GRAPH=1, RCCL transport, device-side coarse solve):
+    // kernels, halo packs, the grouped RCCL send/recv on the communication stream (joined back by
+    // events), the coarse all-gather and the replicated tail, captured once and replayed
+    int use_graph = 0;
+    hipGraphExec_t cycle_exec = nullptr;
+    bool graph_resid_ready = false;   // resid_c_ready as the captured cycle leaves it
 };
 
 namespace {
@@ -361,6 +367,7 @@ void release(sss_hip_dist *d)
 {
     if (!d) return;
     if (d->stream) (void)hipStreamSynchronize(d->stream);
+    if (d->cycle_exec) (void)hipGraphExecDestroy(d->cycle_exec);
     for (int l = 0; l < d->nagg; ++l) {
         DLevel &L = d->L[l];
         devcsr_free(L.A);
@@ -474,6 +481,7 @@ static sss_hip_dist *dist_create_impl(sss_hip_dist *d, PartPlan &plan, const SSS
                  hipEventCreateWithFlags(&d->ev_halo, hipEventDisableTiming) != hipSuccess))
         err = "communication stream";
     if (const char *ov = getenv("SSS_HIP_OVERLAP")) d->overlap = atoi(ov);
+    if (const char *gz = getenv("SSS_HIP_DIST_GRAPH")) d->use_graph = atoi(gz) != 0 && !c->host;
     if (!err) d->nagg = plan.nagg;
 
     if (!err) err = [&]() -> const char * {
@@ -572,6 +580,7 @@ static sss_hip_dist *dist_create_impl(sss_hip_dist *d, PartPlan &plan, const SSS
     if (failed > 0.0) return fail(err ? err : "another rank failed its set-up");
     if (agree_eliminations(d, plan)) return fail("agreeing the exact eliminations");
     if (hipStreamSynchronize(d->stream) != hipSuccess) return fail("sync");
+    if (!hier_coarse_on_device(d->tail)) d->use_graph = 0;   // a host-steered Krylov coarse solve
     return d;
 }
 
@@ -661,7 +670,7 @@ extern "C" int sss_hip_dist_level_flags(sss_hip_dist *d, int l)
 {
     if (!d || l < 0 || l >= d->nagg) return ERROR_INPUT_PAR;
     const SmootherPlan &sp = d->L[l].sm;
-    return (sp.finite ? 1 : 0) | (sp.fuse_resid ? 2 : 0) | (sp.f_overwritten ? 4 : 0);
+    return (sp.finite ? 1 : 0) | (sp.fuse_resid ? 2 : 0) | (sp.f_overwritten ? 4 : 0) | (d->cycle_exec ? 8 : 0);
 }
 
 extern "C" int sss_hip_dist_upload_vec(sss_hip_dist *d, int which, const double *own, int n)
@@ -689,7 +698,44 @@ extern "C" int sss_hip_dist_download_vec(sss_hip_dist *d, int which, double *own
     return 0;
 }
 
+static int dist_cycle_enqueue(sss_hip_dist *d);
+
 extern "C" int sss_hip_dist_cycle(sss_hip_dist *d)
+{
+    d->resid_c_ready = false;
+    if (d->use_graph && !d->cycle_exec) {
+        // capture once; any failure (a call the capture cannot take) falls back to eager launches
+        const hipStream_t s = d->stream;
+        SSS_HIP(hipStreamSynchronize(s));
+        hipGraph_t g = nullptr;
+        int rc = hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal) == hipSuccess ? 0 : ERROR_MISC;
+        if (!rc) {
+            rc = dist_cycle_enqueue(d);
+            d->graph_resid_ready = d->resid_c_ready;
+            const hipError_t e = hipStreamEndCapture(s, &g);
+            if (!rc && e != hipSuccess) rc = ERROR_MISC;
+        }
+        hipGraphExec_t ex = nullptr;
+        if (!rc && g && hipGraphInstantiate(&ex, g, nullptr, nullptr, 0) != hipSuccess) rc = ERROR_MISC;
+        if (g) (void)hipGraphDestroy(g);
+        (void)hipGetLastError();
+        if (rc || !ex) {
+            fprintf(stderr, "[sss_hip] rank %d: the distributed cycle could not be captured; eager launches\n",
+                    d->comm->rank);
+            d->use_graph = 0;
+            return dist_cycle_enqueue(d);
+        }
+        d->cycle_exec = ex;
+    }
+    if (d->cycle_exec) {
+        SSS_HIP(hipGraphLaunch(d->cycle_exec, d->stream));
+        d->resid_c_ready = d->graph_resid_ready;
+        return 0;
+    }
+    return dist_cycle_enqueue(d);
+}
+
+static int dist_cycle_enqueue(sss_hip_dist *d)
 {
     const hipStream_t s = d->stream;
     const int nagg = d->nagg;

@@ -295,6 +295,7 @@ int level_kind_of(const sss_hip_opts &o, int global_level);
 // ERROR_MISC with an "### ERROR" line on stderr; re-pointed to an owner's word (distributed tail).
 int hier_stall_check(sss_hip_hier *h);
 unsigned *hier_err_word(sss_hip_hier *h);
+bool hier_coarse_on_device(sss_hip_hier *h);   // the coarsest solve is device-only (explicit inverse)
 void hier_set_err_word(sss_hip_hier *h, unsigned *err);
 int level_inner_of(const sss_hip_opts &o, int global_level);
 

@@ -877,6 +877,7 @@ int sss::hier_stall_check(sss_hip_hier *h)
 }
 
 unsigned *sss::hier_err_word(sss_hip_hier *h) { return h ? h->d_err : nullptr; }
+bool sss::hier_coarse_on_device(sss_hip_hier *h) { return h && h->coarse_mode == SSS_HIP_COARSE_DIRECT; }
 void sss::hier_set_err_word(sss_hip_hier *h, unsigned *err)
 {
     for (int l = 0; l + 1 < h->nl; ++l) smoother_set_err(h->L[l].sm, err);

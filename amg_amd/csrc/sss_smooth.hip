@@ -492,51 +492,71 @@ __device__ __forceinline__ void relax_range_ell(int blo, const int2 *__restrict_
                                                 const double *__restrict__ deff, double *__restrict__ rr,
                                                 double *__restrict__ partial, XSrc xs, const DevDict &dt)
 {
-    __shared__ EllSmem es;
-    const int bid = blo + (dt.remap ? xcd_remap(blockIdx.x, gridDim.x) : (int)blockIdx.x);
-    const int2 ba = blk[bid], be = blk[bid + 1];
-    const int r = ba.x + (int)threadIdx.x;
-    const bool live = r < be.x;
-    unsigned w[W / 4] = {};
-    double br = 0.0, dr = 0.0;
-    if (live) {   // the row's codes, b and divisor are in flight across the dictionaries' barrier
-        ell_codes<W>(dt.ell, r, w);
-        br = b[r];
-        if (deff) dr = deff[r];
+    constexpr int RPT = kEllRpt;
+    __shared__ EllSmem es[RPT];
+    const int g = (RPT == 1 && dt.remap) ? xcd_remap(blockIdx.x, gridDim.x) : (int)blockIdx.x;
+    unsigned w[RPT][W / 4];
+    double br[RPT], dr[RPT];
+    int r[RPT];
+    bool live[RPT], valid[RPT];
+#pragma unroll
+    for (int j = 0; j < RPT; ++j) {   // every row's codes, b and divisor in flight across the barrier
+        const int bid = blo + g * RPT + j;
+        valid[j] = bid < dt.bend;
+        live[j] = false;
+        br[j] = dr[j] = 0.0;
+        r[j] = 0;
+#pragma unroll
+        for (int t = 0; t < W / 4; ++t) w[j][t] = 0u;
+        if (valid[j]) {
+            const int2 ba = blk[bid], be = blk[bid + 1];
+            r[j] = ba.x + (int)threadIdx.x;
+            live[j] = r[j] < be.x;
+            if (live[j]) {
+                ell_codes<W>(dt.ell, r[j], w[j]);
+                br[j] = b[r[j]];
+                if (deff) dr[j] = deff[r[j]];
+            }
+            ell_load_dicts_nosync(dt, bid, es[j]);
+        }
     }
-    ell_load_dicts(dt, bid, es);
-    double sq = 0.0;
-    if (live) {
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < RPT; ++j) {
+        double sq = 0.0;
+        if (live[j]) {
+            const int rj = r[j];
             double p[W];
             int dsl;
             double dv;
-            const int len = ell_decode<W>(w, r, es, [&](int c) -> double { return xs(c); }, p, dsl, dv);
-            const double acc = dsl < 0 ? ell_sub(br, p, 0, len) : ell_sub(ell_sub(br, p, 0, dsl), p, dsl + 1, len);
-            const double d = deff ? dr : dv;
+            const int len = ell_decode<W>(w[j], rj, es[j], [&](int c) -> double { return xs(c); }, p, dsl, dv);
+            const double acc = dsl < 0 ? ell_sub(br[j], p, 0, len) : ell_sub(ell_sub(br[j], p, 0, dsl), p, dsl + 1, len);
+            const double d = deff ? dr[j] : dv;
             if constexpr (MODE == 2) {
-                const double xn = fabs(d) > SMALLFLOAT ? acc / d : x[r];
-                if (fabs(d) > SMALLFLOAT) x[r] = xn;
+                const double xn = fabs(d) > SMALLFLOAT ? acc / d : x[rj];
+                if (fabs(d) > SMALLFLOAT) x[rj] = xn;
                 double t = ell_add(0.0, p, 0, dsl);
                 t += d * xn;
                 t = ell_add(t, p, dsl + 1, len);
-                const double out = br + t * -1.0;
-                rr[r] = out;
+                const double out = br[j] + t * -1.0;
+                rr[rj] = out;
                 sq = out * out;
             } else if constexpr (MODE == 3) {
-                const double out = br + ell_add(0.0, p, 0, len) * -1.0;
-                rr[r] = out;
+                const double out = br[j] + ell_add(0.0, p, 0, len) * -1.0;
+                rr[rj] = out;
                 sq = out * out;
-                y[r - lo] = fabs(d) > SMALLFLOAT ? acc / d : x[r];
+                y[rj - lo] = fabs(d) > SMALLFLOAT ? acc / d : x[rj];
             } else if constexpr (MODE == 1) {
-                y[r - lo] = fabs(d) > SMALLFLOAT ? acc / d : xs(r);
+                y[rj - lo] = fabs(d) > SMALLFLOAT ? acc / d : xs(rj);
             } else {
-                if (fabs(d) > SMALLFLOAT) x[r] = acc / d;
+                if (fabs(d) > SMALLFLOAT) x[rj] = acc / d;
             }
-    }
-    if constexpr (MODE >= 2) {
-        if (partial) {
-            const double t = block_sum(sq, es.red);
-            if (threadIdx.x == 0) partial[bid] = t;
+        }
+        if constexpr (MODE >= 2) {
+            if (partial && valid[j]) {   // (valid is uniform over the workgroup)
+                const double t = block_sum(sq, es[j].red);
+                if (threadIdx.x == 0) partial[blo + g * RPT + j] = t;
+            }
         }
     }
 }
@@ -675,17 +695,21 @@ static bool relax_occ_on()
     }();
     return on;
 }
-// relax_range / relax_range_occ on dim3(nb) workgroups
+// relax_range / relax_range_occ over the row blocks [blo, blo + nb): one workgroup per block, or
+// per kEllRpt blocks on dictionary ELL (K >= 8)
 template <int M, int K, class... Args>
-static void launch_relax_range(int nb, hipStream_t s, Args... args)
+static void launch_relax_range(int blo, int nb, hipStream_t s, DevDict dt, Args... args)
 {
     if constexpr (K < 8) {
         if (relax_occ_on()) {
-            hipLaunchKernelGGL((relax_range_occ<M, K>), dim3(nb), dim3(kBlock), 0, s, args...);
+            hipLaunchKernelGGL((relax_range_occ<M, K>), dim3(nb), dim3(kBlock), 0, s, blo, args..., dt);
             return;
         }
+        hipLaunchKernelGGL((relax_range<M, K>), dim3(nb), dim3(kBlock), 0, s, blo, args..., dt);
+    } else {
+        dt.bend = blo + nb;
+        hipLaunchKernelGGL((relax_range<M, K>), dim3((nb + kEllRpt - 1) / kEllRpt), dim3(kBlock), 0, s, blo, args..., dt);
     }
-    hipLaunchKernelGGL((relax_range<M, K>), dim3(nb), dim3(kBlock), 0, s, args...);
 }
 
 // relax_range for long-row levels: one wave per row (rows lo + 4 * blockIdx.x + wave).  The
@@ -967,9 +991,9 @@ int launch_f_residual_pending(const SmootherPlan &sp, const DevCSR &A, const dou
     const PassSchedule &F = sp.pass[0];
     const double *deff = (sp.own_diag && (A.pk || has_dict(A))) ? nullptr : sp.d_first;
     with_tile_kind(A, [&](auto K) {
-        launch_relax_range<3, decltype(K)::value>(F.bhi - F.blo, s, F.blo, A.bk, A.rp, A.ci, A.v, sp.diag_pos, F.lo,
-                                                  b, const_cast<double *>(x), (const double *)nullptr, pend, deff,
-                                                  A.pk, A.pv, A.pb, r, partial, xsrc_of(x), devdict(A, 0));
+        launch_relax_range<3, decltype(K)::value>(F.blo, F.bhi - F.blo, s, devdict(A, 0), A.bk, A.rp, A.ci, A.v,
+                                                  sp.diag_pos, F.lo, b, const_cast<double *>(x), (const double *)nullptr,
+                                                  pend, deff, A.pk, A.pv, A.pb, r, partial, xsrc_of(x));
     });
     SSS_HIP(hipGetLastError());
     return 0;
@@ -1123,9 +1147,9 @@ int smoother_run(const SmootherPlan &sp, const DevCSR &A, const double *b, doubl
                         auto go = [&](int b0, int b1) {
                             with_tile_kind(A, [&](auto K) {
                                 launch_relax_range<M, decltype(K)::value>(
-                                    b1 - b0, s, b0, A.bk, A.rp, cols, A.v, sp.diag_pos, ps.lo, b, x, yp, y,
-                                    tile_d ? nullptr : deff, A.pk, A.pv, A.pb, (double *)nullptr, (double *)nullptr, xs,
-                                    devdict(A, 0));
+                                    b0, b1 - b0, s, devdict(A, 0), A.bk, A.rp, cols, A.v, sp.diag_pos, ps.lo, b, x, yp,
+                                    y, tile_d ? nullptr : deff, A.pk, A.pv, A.pb, (double *)nullptr, (double *)nullptr,
+                                    xs);
                             });
                         };
                         if (split_pass) return hk->split(x, ps.blo, ps.bhi, go);
@@ -1192,9 +1216,9 @@ int smoother_run(const SmootherPlan &sp, const DevCSR &A, const double *b, doubl
                     auto go = [&](int b0, int b1) {
                         with_tile_kind(A, [&](auto K) {
                             launch_relax_range<2, decltype(K)::value>(
-                                b1 - b0, s, b0, A.bk, A.rp, A.ci, A.v, sp.diag_pos, ps.lo, b, x, (const double *)nullptr,
-                                (double *)nullptr, tile_d ? nullptr : deff, A.pk, A.pv, A.pb, rf->r, rf->partial, xs,
-                                devdict(A, 0));
+                                b0, b1 - b0, s, devdict(A, 0), A.bk, A.rp, A.ci, A.v, sp.diag_pos, ps.lo, b, x,
+                                (const double *)nullptr, (double *)nullptr, tile_d ? nullptr : deff, A.pk, A.pv, A.pb,
+                                rf->r, rf->partial, xs);
                         });
                     };
                     if (split_pass) {

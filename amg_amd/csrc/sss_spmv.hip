@@ -869,35 +869,55 @@ __global__ __launch_bounds__(kBlock) void spmv_adaptive(const int2 *__restrict__
         return NORM ? out * out : 0.0;
     };
     if constexpr (DICT >= 8) {   // dictionary ELL rows of width DICT: one thread per row, its sum
-        constexpr int W = DICT;   // from 0.0 in stored order; the grid loops over the row blocks
-        __shared__ EllSmem es;
-        const int bid = dt.remap ? xcd_remap(blockIdx.x, gridDim.x) : (int)blockIdx.x;
-        const int2 ba = blk[bid], be = blk[bid + 1];
-        const int r = ba.x + (int)threadIdx.x;
-        unsigned w[W / 4] = {};
-        double br = 0.0;
-        if (r < be.x) {   // codes (and b) in flight across the dictionaries' barrier
-            ell_codes<W>(dt.ell, r, w);
-            if constexpr (OP == SSS_HIP_SPMV_RESID) br = b[r];
-        }
-        ell_load_dicts(dt, bid, es);
-        double sq = 0.0;
-        if (r < be.x) {
-            double p[W];
-            int ds;
-            double dv;
-            const int len = ell_decode<W>(w, r, es, [&](int c) -> double { return x[c]; }, p, ds, dv);
-            if constexpr (OP == SSS_HIP_SPMV_RESID) {
-                const double out = br + ell_add(0.0, p, 0, len) * alpha;
-                y[r] = out;
-                sq = NORM ? out * out : 0.0;
-            } else {
-                sq = epi(r, ell_add(0.0, p, 0, len));
+        constexpr int W = DICT;   // from 0.0 in stored order; kEllRpt row blocks per workgroup
+        constexpr int RPT = kEllRpt;
+        __shared__ EllSmem es[RPT];
+        const int g = (RPT == 1 && dt.remap) ? xcd_remap(blockIdx.x, gridDim.x) : (int)blockIdx.x;
+        unsigned w[RPT][W / 4];
+        double br[RPT];
+        int r[RPT];
+        bool live[RPT], valid[RPT];
+#pragma unroll
+        for (int j = 0; j < RPT; ++j) {   // codes (and b) in flight across the dictionaries' barrier
+            const int bid = g * RPT + j;
+            valid[j] = bid < dt.bend;
+            live[j] = false;
+            br[j] = 0.0;
+            r[j] = 0;
+#pragma unroll
+            for (int t = 0; t < W / 4; ++t) w[j][t] = 0u;
+            if (valid[j]) {
+                const int2 ba = blk[bid], be = blk[bid + 1];
+                r[j] = ba.x + (int)threadIdx.x;
+                live[j] = r[j] < be.x;
+                if (live[j]) {
+                    ell_codes<W>(dt.ell, r[j], w[j]);
+                    if constexpr (OP == SSS_HIP_SPMV_RESID) br[j] = b[r[j]];
+                }
+                ell_load_dicts_nosync(dt, bid, es[j]);
             }
         }
-        if (NORM) {
-            const double t = block_sum(sq, es.red);
-            if (threadIdx.x == 0) partial[bid] = t;
+        __syncthreads();
+#pragma unroll
+        for (int j = 0; j < RPT; ++j) {
+            double sq = 0.0;
+            if (live[j]) {
+                double p[W];
+                int ds;
+                double dv;
+                const int len = ell_decode<W>(w[j], r[j], es[j], [&](int c) -> double { return x[c]; }, p, ds, dv);
+                if constexpr (OP == SSS_HIP_SPMV_RESID) {
+                    const double out = br[j] + ell_add(0.0, p, 0, len) * alpha;
+                    y[r[j]] = out;
+                    sq = NORM ? out * out : 0.0;
+                } else {
+                    sq = epi(r[j], ell_add(0.0, p, 0, len));
+                }
+            }
+            if (NORM && valid[j]) {
+                const double t = block_sum(sq, es[j].red);
+                if (threadIdx.x == 0) partial[g * RPT + j] = t;
+            }
         }
     } else {
         __shared__ SpmvSmem sm;
@@ -1001,8 +1021,12 @@ static void launch_op(const DevCSR &A, double alpha, const double *x, const doub
                            b, y, alpha, cap, partial);
     else
         with_tile_kind(A, [&](auto K) {
-            hipLaunchKernelGGL((spmv_adaptive<OP, NORM, decltype(K)::value>), dim3(A.nblk), dim3(kBlock), 0, s,
-                               A.bk, A.rp, A.ci, A.v, x, b, y, alpha, cap, partial, A.pk, A.pv, A.pb, devdict(A, 0));
+            constexpr int KK = decltype(K)::value;
+            DevDict dt = devdict(A, 0);
+            dt.bend = A.nblk;
+            const int grid = KK >= 8 ? (A.nblk + kEllRpt - 1) / kEllRpt : A.nblk;
+            hipLaunchKernelGGL((spmv_adaptive<OP, NORM, KK>), dim3(grid), dim3(kBlock), 0, s, A.bk, A.rp, A.ci, A.v, x,
+                               b, y, alpha, cap, partial, A.pk, A.pv, A.pb, dt);
         });
 }
 
@@ -1034,13 +1058,16 @@ int launch_spmv_range(const DevCSR &A, int blo, int bhi, int op, double alpha, c
     // the kernel indexes blocks from 0: shift the block-indexed arrays
     const int2 *pb = A.pb ? A.pb + blo : nullptr;
     double *pp = partial ? partial + blo : nullptr;
-    const DevDict dt = devdict(A, blo);
+    DevDict dt = devdict(A, blo);
+    dt.bend = nb;   // the kernel sees blocks [0, nb)
     auto go = [&](auto op_c, auto norm_c) {
         constexpr int O = decltype(op_c)::value;
         constexpr bool NM = decltype(norm_c)::value;
         with_tile_kind(A, [&](auto K) {
-            hipLaunchKernelGGL((spmv_adaptive<O, NM, decltype(K)::value>), dim3(nb), dim3(kBlock), 0, s, A.bk + blo,
-                               A.rp, A.ci, A.v, x, b, y, alpha, 0, pp, A.pk, A.pv, pb, dt);
+            constexpr int KK = decltype(K)::value;
+            const int grid = KK >= 8 ? (nb + kEllRpt - 1) / kEllRpt : nb;
+            hipLaunchKernelGGL((spmv_adaptive<O, NM, KK>), dim3(grid), dim3(kBlock), 0, s, A.bk + blo, A.rp, A.ci, A.v,
+                               x, b, y, alpha, 0, pp, A.pk, A.pv, pb, dt);
         });
     };
     using T = std::true_type;

@@ -59,7 +59,16 @@ struct DevDict {
     const unsigned char *ell = nullptr;   // dictionary ELL (DevCSR::dv_ell), ell_w bytes per row
     int ellw = 0;
     int remap = 0;   // ELL launches: XCD-contiguous block order (DevCSR::ell_remap)
+    int bend = 0x7fffffff;   // ELL launches: first block past the launch's range (kEllRpt blocks per workgroup)
 };
+// Dictionary ELL: row blocks per workgroup (each thread takes one row of each; more independent
+// loads in flight per thread, one dictionary barrier for all of them).  Measured at 400^3
+// (tools/gpu/ab.sh): 2 blocks took level 0's smoothing 3.12 -> 3.02 ms and its residual 389 ->
+// 374 us per V-cycle; 4 blocks (70 VGPRs) were slower than 1 (3.36 ms).
+#ifndef SSS_ELL_RPT
+#define SSS_ELL_RPT 2
+#endif
+constexpr int kEllRpt = SSS_ELL_RPT;
 
 // ---- dictionary ELL: one thread per row ----------------------------------------------------
 // The block's dictionaries in LDS (small: the kernels instantiated for ELL keep their LDS
@@ -69,11 +78,15 @@ struct EllSmem {
     double vd[8];
     double red[kBlock / 64];
 };
-__device__ __forceinline__ void ell_load_dicts(const DevDict &dt, int bid, EllSmem &es)
+__device__ __forceinline__ void ell_load_dicts_nosync(const DevDict &dt, int bid, EllSmem &es)
 {
     const int4 p = dt.pd[bid];
     if ((int)threadIdx.x < p.y) es.dd[threadIdx.x] = dt.dd[p.x + threadIdx.x];
     if ((int)threadIdx.x < p.w) es.vd[threadIdx.x] = dt.vd[p.z + threadIdx.x];
+}
+__device__ __forceinline__ void ell_load_dicts(const DevDict &dt, int bid, EllSmem &es)
+{
+    ell_load_dicts_nosync(dt, bid, es);
     __syncthreads();
 }
 // Row r's W code bytes (one 8/16/32-byte load).  The kernels issue it before the dictionaries'

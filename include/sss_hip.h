@@ -221,7 +221,8 @@ int sss_hip_dist_info(sss_hip_dist *d, int *lo, int *hi, int *nagg, int *nghost0
 /* Own rows, ghosts and nonzeros of this rank's partitioned level l. */
 int sss_hip_dist_level_size(sss_hip_dist *d, int l, int *m, int *g, long long *nnz);
 /* exact eliminations in force on partitioned level l (agreed over the ranks), a bit mask:
- * 1 zero-first pass, 2 fused C-row residual, 4 dead F-row prolongation.  <0: bad level. */
+ * 1 zero-first pass, 2 fused C-row residual, 4 dead F-row prolongation, 8 the cycle runs as one
+ * captured hipGraph (SSS_HIP_DIST_GRAPH=1 over RCCL with a device-side coarse solve).  <0: bad level. */
 int sss_hip_dist_level_flags(sss_hip_dist *d, int l);
 /* level-0 vectors, the rank's own rows in the original order (n = hi - lo) */
 int sss_hip_dist_upload_vec(sss_hip_dist *d, int which, const double *own, int n);

@@ -63,6 +63,8 @@ def _worker(rank, world, port, kind, n, smoother, inner_from, agg_rows, cycles, 
         for _ in range(cycles):
             D.cycle()
             rel.append(D.residual_norm() / np.sqrt(N))
+        if os.environ.get("SSS_HIP_DIST_GRAPH") == "1" and transport == "rccl":
+            assert D.level_flags(0)["cycle_graph"], "the distributed cycle was not captured"
         x_own = D.download("x")
         parts = [None] * world
         dist.all_gather_object(parts, (D.lo, x_own))
@@ -111,6 +113,14 @@ def test_dist_rccl_single_rank(smoother):
     the grouped send/recv of the coarse all-gather (no peers) and the ncclAllReduce of ||r||^2 --
     bitwise the single-GPU engine.  (Two ranks cannot share a GPU under RCCL; the halo send/recv
     pattern itself is covered by the host-transport tests above, which run the same plan.)"""
+    _run(1, "rccl", 7, 24, smoother, 2, 100)
+
+
+@pytest.mark.parametrize("smoother", ["hybrid", "jacobi"])
+def test_dist_rccl_graph(smoother, monkeypatch):
+    """The distributed cycle captured into one hipGraph (SSS_HIP_DIST_GRAPH=1) over RCCL on the one
+    GPU: the captured and replayed cycles are bitwise the single-GPU engine's."""
+    monkeypatch.setenv("SSS_HIP_DIST_GRAPH", "1")
     _run(1, "rccl", 7, 24, smoother, 2, 100)
 
 
