@@ -10,6 +10,7 @@
 // writing per-block sums of squares plus a one-block deterministic reduction; the 8-byte
 // norm is the only per-iteration device->host transfer.
 #include "sss_engine.hpp"
+#include "sss_tail.hpp"
 
 #include <condition_variable>
 #include <mutex>
@@ -75,6 +76,7 @@ struct sss_hip_hier {
     double *pcg_part = nullptr;
     double *pcg_s = nullptr;     // device scalars
     double *pcg_h = nullptr;     // pinned host mirror
+    TailPlan tail;               // the small coarse levels as one single-workgroup launch (sss_tail.hip)
 };
 
 static int env_int(const char *name, int dflt)
@@ -207,6 +209,7 @@ static void hier_release(sss_hip_hier *h)
     if (h->resid_f_exec) (void)hipGraphExecDestroy(h->resid_f_exec);
     for (hipGraphExec_t g : h->cycle_steps_p)
         if (g) (void)hipGraphExecDestroy(g);
+    tail_free(h->tail);
     dev_free(h->pend_f);
     dev_free(h->pcg_v);
     dev_free(h->pcg_part);
@@ -442,6 +445,80 @@ static bool hb_level_pr(HierBuild &b, int l)
     return true;
 }
 
+// The V-cycle's tail (sss_tail.hip): the coarsest levels whose passes are all tiny, run as one
+// single-workgroup launch.  A level qualifies when it is smoothed by the no-copy two-stage
+// C/F-Jacobi form on the tile paths (rows of at most one tile, so every row sum is a stored-order
+// chain) and is small (<= 8,192 rows, <= 256K nonzeros in A); the coarsest level needs the explicit
+// inverse and <= 256 rows.  The tail is the longest such run above the coarsest level (level 0
+// never: its residual and smoothers have their own fused forms).  SSS_HIP_TAIL=0: no tail.
+static int max_row(const SSS_MAT &M)
+{
+    int mx = 0;
+    for (int i = 0; i < M.num_rows; ++i) mx = std::max(mx, M.row_ptr[i + 1] - M.row_ptr[i]);
+    return mx;
+}
+static int tail_build(sss_hip_hier *h, const SSS_AMG *mg)
+{
+    h->tail = TailPlan();
+    const char *tz = getenv("SSS_HIP_TAIL");
+    const int nl = h->nl;
+    if ((tz && *tz == '0') || nl < 3 || h->level_base != 0 || h->coarse_mode != SSS_HIP_COARSE_DIRECT ||
+        h->direct.n > 256 || (h->pars.cycle_type > 1))
+        return 0;
+    const char *tn = getenv("SSS_HIP_TAIL_NNZ");
+    const int tail_nnz = (tn && *tn) ? atoi(tn) : 16384;
+    auto ok = [&](int l) {
+        const auto &L = h->L[l];
+        const SmootherPlan &sp = L.sm;
+        if (sp.kind != SSS_HIP_SMOOTH_JACOBI || sp.inner < 1 || !sp.x2 || sp.natural) return false;
+        // one workgroup streams ~8K entries per microsecond: past ~16K nonzeros a pass is slower
+        // in it than as its own launch across the chip (the stand-in's level 7, 169K nonzeros,
+        // took 4.5 ms in the tail against 0.18 ms per V-cycle as launches)
+        if (L.A.n > 4096 || L.A.nnz > tail_nnz) return false;
+        if (L.A.wave_rows || L.A.vec_rows || L.P.wave_rows || L.P.vec_rows || L.R.wave_rows || L.R.vec_rows) return false;
+        for (const auto &ps : sp.pass)
+            if (ps.nrows > 0 && (!ps.range || ps.ts_nl.vec_rows || ps.ts_nl.wave_rows || ps.ts_lo.vec_rows || ps.ts_lo.wave_rows))
+                return false;
+        const SSS_AMG_COMP &C = mg->cg[l];
+        return max_row(C.A) <= kTileEntries && max_row(C.P) <= kTileEntries && max_row(C.R) <= kTileEntries;
+    };
+    int from = nl - 1;
+    while (from - 1 >= 1 && ok(from - 1)) --from;
+    if (from >= nl - 1) return 0;
+    std::vector<TailLevel> lv;
+    for (int l = from; l + 1 < nl; ++l) {
+        const auto &L = h->L[l];
+        const SmootherPlan &sp = L.sm;
+        TailLevel t;
+        t.n = L.A.n;
+        t.nc = h->L[l + 1].A.n;
+        t.b = L.b, t.x = L.x, t.x2 = sp.x2, t.wp = L.wp;
+        t.deff = sp.d_first;
+        t.csplit = sp.csplit, t.inner = sp.inner, t.pre = h->pars.pre_iter, t.post = h->pars.post_iter;
+        t.finite = sp.finite ? 1 : 0;
+        for (int c = 0; c < 2; ++c) {
+            const PassSchedule &ps = sp.pass[c];
+            TailPass &tp = t.pass[c];
+            tp.lo = ps.nrows > 0 ? ps.lo : 0;
+            tp.hi = ps.nrows > 0 ? ps.hi : 0;
+            tp.nrp = ps.ts_nl.rp, tp.nci = ps.ts_nl.ci, tp.nv = ps.ts_nl.v, tp.split = ps.ts_split;
+            tp.lrp = ps.ts_lo.rp, tp.lci = ps.ts_lo.ci, tp.lv = ps.ts_lo.v, tp.P = ps.ts_P;
+        }
+        t.arp = L.A.rp, t.aci = L.A.ci, t.av = L.A.v;
+        t.rrp = L.R.rp, t.rci = L.R.ci, t.rv = L.R.v;
+        t.prp = L.P.rp, t.pci = L.P.ci, t.pv = L.P.v;
+        lv.push_back(t);
+    }
+    const auto &Cl = h->L[nl - 1];
+    h->tail.inv = h->direct.inv;
+    h->tail.nc = h->direct.n;
+    h->tail.cb = Cl.b;
+    h->tail.cx = Cl.x;
+    if (int rc = tail_upload(h->tail, lv)) return rc;
+    h->tail.from = from;
+    return 0;
+}
+
 static sss_hip_hier *hb_finish(HierBuild &b)
 {
     sss_hip_hier *h = b.h;
@@ -475,6 +552,7 @@ static sss_hip_hier *hb_finish(HierBuild &b)
         h->krylov = coarse_krylov_create(h->L[h->nl - 1].A, h->opts.row_cap, h->stream);
         if (!h->krylov) return fail("coarse Krylov workspace");
     }
+    if (tail_build(h, mg)) return fail("tail levels");
     if (hipStreamSynchronize(h->stream) != hipSuccess) return fail("sync");
     // Graph replay only pays for, and is only robust with, a modest node count: the exact
     // smoother on deep coarse levels issues one launch per DAG depth (~10^5 per cycle).
@@ -741,6 +819,11 @@ static int walk_cycle(sss_hip_hier *h, CoarseFn coarse, bool pend = false)
     hipStream_t s = h->stream;
     for (;;) {
         while (l < nl - 1) {
+            if (h->tail.from > 0 && l == h->tail.from && cycle_type == 1) {
+                // levels tail.from .. nl-1: descent, coarsest solve and ascent in one launch
+                if ((rc = tail_launch(h->tail, s))) return rc;
+                goto ascent;
+            }
             auto &L = h->L[l];
             visits[l]++;
             const bool first = l == 0 && visits[0] == 1;
@@ -751,6 +834,7 @@ static int walk_cycle(sss_hip_hier *h, CoarseFn coarse, bool pend = false)
             SSS_HIP(hipMemsetAsync(h->L[l].x, 0, sizeof(double) * (size_t)h->L[l].A.n, s));
         }
         if ((rc = coarse(h))) return rc;
+    ascent:
         while (l > 0) {
             l--;
             auto &L = h->L[l];
@@ -997,6 +1081,8 @@ extern "C" int sss_hip_sync(sss_hip_hier *h)
 }
 
 extern "C" int sss_hip_num_levels(sss_hip_hier *h) { return h ? h->nl : 0; }
+
+extern "C" int sss_hip_tail_from(sss_hip_hier *h) { return h ? h->tail.from : -1; }
 
 extern "C" int sss_hip_level_info_get(sss_hip_hier *h, int level, sss_hip_level_info *out)
 {

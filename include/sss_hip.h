@@ -144,6 +144,9 @@ typedef struct sss_hip_level_info {
 } sss_hip_level_info;
 int sss_hip_level_info_get(sss_hip_hier *h, int level, sss_hip_level_info *out);
 int sss_hip_num_levels(sss_hip_hier *h);
+/* First level of the V-cycle's single-workgroup tail (sss_tail.hip: the small coarse levels,
+ * descent, coarsest solve and ascent in one launch), or -1 when the cycle has none. */
+int sss_hip_tail_from(sss_hip_hier *h);
 
 /* ---- kernel-level entry points on device memory (tests, bench, roofline) ------------- */
 enum {
