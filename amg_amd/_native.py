@@ -110,6 +110,7 @@ ABI_SYMBOLS = [
     "sss_hip_upload_vec", "sss_hip_download_vec", "sss_hip_cycle", "sss_hip_residual_norm", "sss_hip_pcg",
     "SSS_amg_save", "SSS_amg_load",
     "sss_hip_coarse_solve", "sss_hip_smooth", "sss_hip_sync", "sss_hip_level_info_get", "sss_hip_num_levels", "sss_hip_tail_from",
+    "sss_hip_cycle_launches",
     "sss_hip_spmv_plan_create", "sss_hip_spmv_plan_destroy", "sss_hip_spmv", "sss_hip_host_spmv",
     "sss_hip_host_smooth", "sss_hip_host_coarse_solve", "sss_hip_host_cache_clear", "sss_hip_time_level0_spmv", "sss_hip_time_iterations",
     "sss_hip_time_level0_spmv_csr",
@@ -192,6 +193,7 @@ def _declare(lib):
         "sss_hip_level_info_get": (C.c_int, [C.c_void_p, C.c_int, P(SSS_HIP_LEVEL_INFO)]),
         "sss_hip_num_levels": (C.c_int, [C.c_void_p]),
         "sss_hip_tail_from": (C.c_int, [C.c_void_p]),
+        "sss_hip_cycle_launches": (C.c_int, [C.c_void_p]),
         "sss_hip_host_spmv": (C.c_int, [C.c_int, C.c_double, P(SSS_MAT), _dbl_p, _dbl_p, _dbl_p, C.c_int]),
         "sss_hip_host_smooth": (C.c_int, [P(SSS_SMTR), C.c_int]),
         "sss_hip_host_coarse_solve": (C.c_int, [P(SSS_MAT), P(SSS_VEC), P(SSS_VEC), C.c_double, C.c_int,

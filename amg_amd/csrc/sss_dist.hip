@@ -516,7 +516,8 @@ static sss_hip_dist *dist_create_impl(sss_hip_dist *d, PartPlan &plan, const SSS
             if (l + 1 == d->nagg && !tinv.empty())
                 for (int &j : P.P.ci) j = tinv[j];
             SSS_MAT Pv = P.P.view(), Rv = P.R.view();
-            if (devcsr_upload(L.P, Pv, P.nF, enc & ~kEncDict) || devcsr_upload(L.R, Rv, -1, enc & ~kEncDict))
+            if (devcsr_upload(L.P, Pv, P.nF, transfer_encoding(d->opts)) ||
+                devcsr_upload(L.R, Rv, -1, transfer_encoding(d->opts)))
                 return "upload P/R";
             {   // which row blocks read ghosts (the same blockings the uploads made)
                 std::vector<int> blk;

@@ -248,8 +248,10 @@ enum { kEncSortedTiles = 1, kEncFreeOrder = 2, kEncDict = 4, kEncMergedOnly = 8 
 // enc: kEnc* flags; seg (kEncFreeOrder only, optional): per row, the absolute CSR position that
 // splits the row into two independently summed segments (two-stage [N_i | L_i] rows).
 int devcsr_upload(DevCSR &d, const SSS_MAT &h, int split = -1, int enc = 0, const int *seg = nullptr);
-// encoding flags a hierarchy level uses for its matrices under the options o
+// encoding flags a hierarchy level uses for its matrices under the options o, and for its
+// transfer operators P_l, R_l
 int level_encoding(const sss_hip_opts &o);
+int transfer_encoding(const sss_hip_opts &o);
 void devcsr_free(DevCSR &d);
 int build_row_blocks(const int *h_rp, int n, std::vector<int> &blk, int split = -1);
 int upload_block_bounds(int2 **dst, const std::vector<int> &blk, const int *h_rp);

@@ -71,6 +71,7 @@ struct sss_hip_hier {
     double *pend_f = nullptr;
     std::vector<hipGraphExec_t> cycle_steps_p;   // cycle graph variant that consumes pend_f
     bool cycle_graph_ready_p = false;
+    int cycle_kernels = 0, cycle_kernels_p = 0;   // kernel launches per cycle in the captured graphs
     // AMG-preconditioned CG (sss_hip_pcg): level-0 work vectors, dot partials, device scalars
     double *pcg_v = nullptr;     // 7 vectors of n0: b, x, r, z, p, q, r_old
     double *pcg_part = nullptr;
@@ -148,6 +149,12 @@ int sss::level_encoding(const sss_hip_opts &o)
     return (o.sorted_tiles ? kEncSortedTiles : 0) | (o.sum_order == 1 ? kEncFreeOrder : 0) | dict;
 }
 int sss::level_inner_of(const sss_hip_opts &o, int l) { return level_inner(o, l); }
+// P_l and R_l: the level matrices' encodings; dictionary forms only with SSS_HIP_DICT_PR=1
+int sss::transfer_encoding(const sss_hip_opts &o)
+{
+    const char *e = getenv("SSS_HIP_DICT_PR");
+    return (e && *e == '1') ? level_encoding(o) : (level_encoding(o) & ~kEncDict);
+}
 
 // Are the C and the F points of A each an independent set (no off-diagonal coupling inside a
 // class)?  Then exact GS-CF has no chains: each class pass is one C/F-Jacobi pass (7-pt level 0).
@@ -424,7 +431,7 @@ static bool hb_level_pr(HierBuild &b, int l)
     auto &L = h->L[l];
     const bool rl = !L.perm.empty();
     const auto &pc = h->L[l + 1].perm;
-    const int enc = level_encoding(h->opts);
+    const int tenc = transfer_encoding(h->opts);
     const double t0 = PhaseTimer::now();
     if (rl || !pc.empty()) {
         PhaseTimer pt("P/R");
@@ -435,10 +442,10 @@ static bool hb_level_pr(HierBuild &b, int l)
         pt.mark("relabel R");
         // P's rows follow the level's F|C relabeling: blocks split there too, so a
         // prolongation can be limited to the C rows (SmootherPlan::f_overwritten)
-        if (devcsr_upload(L.P, P.view(C.P.num_rows, C.P.num_cols), rl ? b.nF[l] : -1, enc & ~kEncDict) ||
-            devcsr_upload(L.R, R.view(C.R.num_rows, C.R.num_cols), -1, enc & ~kEncDict))
+        if (devcsr_upload(L.P, P.view(C.P.num_rows, C.P.num_cols), rl ? b.nF[l] : -1, tenc) ||
+            devcsr_upload(L.R, R.view(C.R.num_rows, C.R.num_cols), -1, tenc))
             return hb_fail(b, "upload P/R");
-    } else if (devcsr_upload(L.P, C.P, -1, enc & ~kEncDict) || devcsr_upload(L.R, C.R, -1, enc & ~kEncDict)) {
+    } else if (devcsr_upload(L.P, C.P, -1, tenc) || devcsr_upload(L.R, C.R, -1, tenc)) {
         return hb_fail(b, "upload P/R");
     }
     if (b.timing) fprintf(stderr, "[sss_hip] upload level %d: P/R %.2f s\n", l, PhaseTimer::now() - t0);
@@ -866,10 +873,26 @@ static int walk_cycle(sss_hip_hier *h, CoarseFn coarse, bool pend = false)
     return 0;
 }
 
-static int end_capture(sss_hip_hier *h, hipGraphExec_t *exec)
+// kernel nodes of a captured graph (the cycle's launch count, reported by bench.py)
+static int kernel_nodes(hipGraph_t g)
+{
+    size_t n = 0;
+    if (hipGraphGetNodes(g, nullptr, &n) != hipSuccess || n == 0) return 0;
+    std::vector<hipGraphNode_t> nodes(n);
+    if (hipGraphGetNodes(g, nodes.data(), &n) != hipSuccess) return 0;
+    int k = 0;
+    for (size_t i = 0; i < n; ++i) {
+        hipGraphNodeType t;
+        if (hipGraphNodeGetType(nodes[i], &t) == hipSuccess && t == hipGraphNodeTypeKernel) ++k;
+    }
+    return k;
+}
+
+static int end_capture(sss_hip_hier *h, hipGraphExec_t *exec, int *kernels = nullptr)
 {
     hipGraph_t g = nullptr;
     SSS_HIP(hipStreamEndCapture(h->stream, &g));
+    if (kernels) *kernels += kernel_nodes(g);
     hipError_t e = hipGraphInstantiate(exec, g, nullptr, nullptr, 0);
     (void)hipGraphDestroy(g);
     SSS_HIP(e);
@@ -879,11 +902,13 @@ static int end_capture(sss_hip_hier *h, hipGraphExec_t *exec)
 static int build_cycle_graph(sss_hip_hier *h, bool pend)
 {
     std::vector<hipGraphExec_t> &steps = pend ? h->cycle_steps_p : h->cycle_steps;
+    int &kern = pend ? h->cycle_kernels_p : h->cycle_kernels;
+    kern = 0;
     SSS_HIP(hipStreamBeginCapture(h->stream, hipStreamCaptureModeThreadLocal));
-    int rc = walk_cycle(h, [&steps](sss_hip_hier *hh) -> int {
+    int rc = walk_cycle(h, [&steps, &kern](sss_hip_hier *hh) -> int {
         if (hh->coarse_mode == SSS_HIP_COARSE_DIRECT) return sss_hip_coarse_solve(hh);
         hipGraphExec_t seg = nullptr;
-        int r = end_capture(hh, &seg);
+        int r = end_capture(hh, &seg, &kern);
         if (r) return r;
         steps.push_back(seg);
         steps.push_back(nullptr);
@@ -891,7 +916,7 @@ static int build_cycle_graph(sss_hip_hier *h, bool pend)
         return 0;
     }, pend);
     hipGraphExec_t last = nullptr;
-    int rc2 = end_capture(h, &last);
+    int rc2 = end_capture(h, &last, &kern);
     if (rc) return rc;
     if (rc2) return rc2;
     steps.push_back(last);
@@ -1083,6 +1108,12 @@ extern "C" int sss_hip_sync(sss_hip_hier *h)
 extern "C" int sss_hip_num_levels(sss_hip_hier *h) { return h ? h->nl : 0; }
 
 extern "C" int sss_hip_tail_from(sss_hip_hier *h) { return h ? h->tail.from : -1; }
+
+extern "C" int sss_hip_cycle_launches(sss_hip_hier *h)
+{
+    if (!h || !(h->cycle_graph_ready || h->cycle_graph_ready_p)) return -1;
+    return h->cycle_graph_ready_p ? h->cycle_kernels_p : h->cycle_kernels;
+}
 
 extern "C" int sss_hip_level_info_get(sss_hip_hier *h, int level, sss_hip_level_info *out)
 {

@@ -481,6 +481,7 @@ def main():
     # N > 1: rank 0's share (its rows, x with ghosts), no exchange inside the timed launches
     spmv_ms = DH.time_level0_spmv(20)   # the cycle's own storage of A_0
     a_format = None
+    launches, tail_from = None, None
     level_formats = None
     level_smoothers = None
     csr_bytes = 12 * nnz + 4 * (N + 1) + 8 * N + 8 * N + 8 * N   # val+col, row_ptr, x, b, y
@@ -493,6 +494,8 @@ def main():
         spmv_bytes = info0.a_stream_bytes + 8 * N + 8 * N + 8 * N
         # SURVEY.md 8(d)'s kernel: the same residual SpMV from A_0's CSR arrays
         csr_ms = DH.DH.time_level0_spmv_csr(20)
+        launches = A.lib().sss_hip_cycle_launches(DH.DH.h)   # kernels per V-cycle (captured graph)
+        tail_from = A.lib().sss_hip_tail_from(DH.DH.h)
     else:
         m, g = DH.rows, DH.ghosts
         spmv_bytes = 12 * DH.nnz + 4 * (m + 1) + 8 * (m + g) + 8 * m + 8 * m
@@ -667,6 +670,8 @@ def main():
                    "sum_order": "tree (long rows)" if sum_order == 1 else "stored CSR order",
                    "sorted_tiles": bool(sorted_tiles),
                    "level_storage_bits": level_formats,
+                   "kernel_launches_per_cycle": launches,
+                   "single_workgroup_tail_from_level": tail_from if tail_from is not None and tail_from >= 0 else None,
                    "level_smoothers": [["exact", "hybrid", "jacobi"][k] + (f"+inner{i}" if i else "")
                                        for k, i in level_smoothers] if level_smoothers else None,
                    "iterations_to_tol": its, "final_relres": relres, "time_to_solution_s": solve_s,

@@ -147,6 +147,9 @@ int sss_hip_num_levels(sss_hip_hier *h);
 /* First level of the V-cycle's single-workgroup tail (sss_tail.hip: the small coarse levels,
  * descent, coarsest solve and ascent in one launch), or -1 when the cycle has none. */
 int sss_hip_tail_from(sss_hip_hier *h);
+/* Kernel launches of one V-cycle as captured in its hipGraph (host-steered Krylov coarse solves
+ * excluded), or -1 before the first captured cycle / without graphs. */
+int sss_hip_cycle_launches(sss_hip_hier *h);
 
 /* ---- kernel-level entry points on device memory (tests, bench, roofline) ------------- */
 enum {
