@@ -304,10 +304,31 @@ def vcycle_bytes(levels: list, sweeps: int) -> int:
 
 
 def part_prefix(stencil: int, n: int, world: int) -> Path:
-    """Where the partition set of a multi-rank run lives (SSS_PART_DIR, default /tmp); reused by
-    later runs of the same configuration."""
-    base = Path(os.environ.get("SSS_PART_DIR", "/tmp")) / f"sss_parts_{stencil}pt_{n}_{world}r"
-    return base / "part"
+    """Where the partition set of a multi-rank run lives (reused by later runs of the same
+    configuration): SSS_PART_DIR if set, else the first of /tmp, /dev/shm, the home directory and the
+    repository's parent with room for it -- the set takes ~490 B per row for the 7-point operator
+    and ~870 B per row for the 27-point one (profiles/r03_partition_*.json: 65 GB at 512^3)."""
+    import shutil
+    name = f"sss_parts_{stencil}pt_{n}_{world}r"
+    if os.environ.get("SSS_PART_DIR"):
+        return Path(os.environ["SSS_PART_DIR"]) / name / "part"
+    need = 1.25 * (870 if stencil == 27 else 490) * float(n) ** 3
+    cands = [Path("/tmp"), Path("/dev/shm"), Path.home(), ROOT.parent]
+    best, room = None, -1.0
+    for c in cands:
+        if (c / name / "part.json").exists():   # an existing set of this configuration
+            return c / name / "part"
+        try:
+            free = float(shutil.disk_usage(c).free)
+        except OSError:
+            continue
+        if free >= need:
+            return c / name / "part"
+        if free > room:
+            best, room = c, free
+    print(f"[bench] no scratch directory has {need / 1e9:.0f} GB free; using {best} ({room / 1e9:.0f} GB free)",
+          file=sys.stderr, flush=True)
+    return (best or Path("/tmp")) / name / "part"
 
 
 def heartbeat(stop: threading.Event, t0: float):
@@ -401,7 +422,10 @@ def main():
         # rows partitioned over the ranks: a separate host process builds the global hierarchy and
         # writes one partition file per rank (amg_amd/partition.py); each rank then reads only its
         # rows, ghosts and the replicated coarse tail -- no rank ever holds the global hierarchy
-        prefix = part_prefix(args.stencil, n, D.world)
+        # rank 0 chooses the directory (free space changes once the set is being written)
+        box = [str(part_prefix(args.stencil, n, D.world)) if D.rank == 0 else None]
+        D.dist.broadcast_object_list(box, src=0)
+        prefix = Path(box[0])
         manifest = Path(str(prefix) + ".json")
         if D.rank == 0 and not manifest.exists():
             import subprocess
