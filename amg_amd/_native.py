@@ -139,6 +139,8 @@ A_FORMATS = {0: "CSR (12 B/entry)", 1: "column-sorted tiles (12 B/entry)", 2: "d
 def a_format_name(code: int) -> str:
     if code & 64:
         return "dictionary ELL (1 B/entry, padded rows)"
+    if code & 128:
+        return "column ELL (4 B/entry, padded rows)"
     return A_FORMATS.get(code & 3, A_FORMATS[0])
 
 

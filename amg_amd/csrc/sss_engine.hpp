@@ -218,6 +218,15 @@ struct DevCSR {
     // ell_w bytes per row (8 for 7-pt) instead of 12 per entry.  pk and dv_code stay null.
     unsigned char *dv_ell = nullptr;
     int ell_w = 0;
+    // Column ELL (kEncDict, when the offsets do not fit a 1-byte dictionary but every row has at
+    // most 32 entries, every 256-row block at most 128 distinct values and n < 2^25 -- the Galerkin
+    // level of a stencil, 7-pt level 1: 19 entries per row): row r's entries in stored order as
+    // xell_w 32-bit codes  value index << 25 | column  at dv_xell[r * xell_w] (0xFFFFFFFF pads) into
+    // the block value dictionaries dv_pd[block].z/.w -> dv_vd.  One thread per row, no LDS staging:
+    // 4 B per entry (as the value-dictionary tiles' 5) without the tile's staging barrier and its
+    // 2048-entry blocks (~108 rows of a 19-entry level): blocks are 256 rows.
+    unsigned *dv_xell = nullptr;
+    int xell_w = 0;
     int ell_remap = 0;   // ELL kernels take their blocks XCD-contiguously (SSS_HIP_ELL_REMAP)
     long long stream_bytes = 0;   // bytes of the stored format one tile-path SpMV streams (no vectors)
     unsigned *dv_code = nullptr;
@@ -269,13 +278,28 @@ int sort_rows_device(DevCSR &d, const int *h_seg);
 struct DevDict;
 DevDict devdict(const DevCSR &A, int blo);   // the matrix's dictionary tiles, block numbers from blo
 // the tile kernels stage from a dictionary (either kind): instantiate them with DICT = true
-inline bool has_dict(const DevCSR &A) { return A.dv_code != nullptr || A.dv_vi != nullptr || A.dv_ell != nullptr; }
-// f(std::integral_constant<int, K>) with the tile kernels' storage argument K of A: 0 plain or
-// sorted tiles, 1 dictionary tiles (either kind), 8 / 16 / 32 dictionary ELL of that row width
+inline bool has_dict(const DevCSR &A)
+{
+    return A.dv_code != nullptr || A.dv_vi != nullptr || A.dv_ell != nullptr || A.dv_xell != nullptr;
+}
+// Storage argument K of the tile kernels: 0 plain or sorted tiles, 1 dictionary tiles (either kind),
+// 8 / 16 / 32 dictionary ELL of that row width, kXell + W column ELL of row width W (16/20/24/32).
+constexpr int kXell = 256;
+#ifndef SSS_ELL_RPT
+#define SSS_ELL_RPT 2
+#endif
+// row blocks per workgroup of a launch over storage K
+constexpr int rows_per_wg(int K) { return K >= kXell ? 1 : K >= 8 ? SSS_ELL_RPT : 1; }
+// f(std::integral_constant<int, K>) with the storage argument K of A
 template <class F>
 inline void with_tile_kind(const DevCSR &A, F f)
 {
-    if (A.dv_ell) {
+    if (A.dv_xell) {
+        if (A.xell_w == 16) f(std::integral_constant<int, kXell + 16>{});
+        else if (A.xell_w == 20) f(std::integral_constant<int, kXell + 20>{});
+        else if (A.xell_w == 24) f(std::integral_constant<int, kXell + 24>{});
+        else f(std::integral_constant<int, kXell + 32>{});
+    } else if (A.dv_ell) {
         if (A.ell_w == 8) f(std::integral_constant<int, 8>{});
         else if (A.ell_w == 16) f(std::integral_constant<int, 16>{});
         else f(std::integral_constant<int, 32>{});

@@ -1135,7 +1135,7 @@ extern "C" int sss_hip_level_info_get(sss_hip_hier *h, int level, sss_hip_level_
     if (gs_persist_error(L.sm.pass[0], &ef) || gs_persist_error(L.sm.pass[1], &ec)) return ERROR_MISC;
     out->gs_stall = (int)(ef | ec);
     out->a_format = (L.A.pk ? 1 : 0) | (has_dict(L.A) ? 2 : 0) | (L.A.vec_rows ? 4 : 0) | (L.A.mg_G ? 8 : 0) |
-                    (L.A.wave_rows ? 16 : 0) | (L.A.dv_ell ? 64 : 0);
+                    (L.A.wave_rows ? 16 : 0) | (L.A.dv_ell ? 64 : 0) | (L.A.dv_xell ? 128 : 0);
     out->a_stream_bytes = L.A.stream_bytes;
     return 0;
 }
@@ -1162,7 +1162,8 @@ extern "C" int sss_hip_time_level0_spmv(sss_hip_hier *h, int reps, double *avg_m
 extern "C" int sss_hip_time_level0_spmv_csr(sss_hip_hier *h, int reps, double *avg_ms)
 {
     auto &L = h->L[0];
-    if (L.A.wave_rows || L.A.vec_rows) return sss_hip_time_level0_spmv(h, reps, avg_ms);
+    // (column ELL blocks are not tile-sized: the stored format is timed instead)
+    if (L.A.wave_rows || L.A.vec_rows || L.A.dv_xell) return sss_hip_time_level0_spmv(h, reps, avg_ms);
     DevCSR c = L.A;   // a view: the CSR arrays and row blocks only (never freed through c)
     c.pk = nullptr;
     c.pv = nullptr;

@@ -338,14 +338,17 @@ int smoother_build(SmootherPlan &sp, const SSS_MAT &A, const int *mark, int kind
         dA->split_row > 0 &&
         dA->split_row < n && sp.pass[0].range && sp.pass[1].range && sp.pass[0].lo == 0 &&
         sp.pass[0].hi == dA->split_row && sp.pass[1].lo == dA->split_row && sp.pass[1].hi == n) {
+        // the MODE 2 / 3 passes have no long-row path: every block of the pass within one tile (the
+        // ELL formats take one row per thread and rows of at most 32 entries)
         std::vector<int> blk;
-        build_row_blocks(rp, n, blk, dA->split_row);
+        const bool ell = dA->dv_ell || dA->dv_xell;
+        if (!ell) build_row_blocks(rp, n, blk, dA->split_row);
         bool short_blocks = true;
-        for (int q = dA->split_blk; q < dA->nblk && short_blocks; ++q)
+        for (int q = dA->split_blk; !ell && q < dA->nblk && short_blocks; ++q)
             short_blocks = rp[blk[q + 1]] - rp[blk[q]] <= kTileEntries;
         sp.fuse_resid = short_blocks;
         bool f_short = true;
-        for (int q = 0; q < dA->split_blk && f_short; ++q) f_short = rp[blk[q + 1]] - rp[blk[q]] <= kTileEntries;
+        for (int q = 0; !ell && q < dA->split_blk && f_short; ++q) f_short = rp[blk[q + 1]] - rp[blk[q]] <= kTileEntries;
         sp.pend_ok = short_blocks && f_short && sp.f_overwritten && !(pz && *pz == '0');
     }
     if (timing)
@@ -561,7 +564,73 @@ __device__ __forceinline__ void relax_range_ell(int blo, const int2 *__restrict_
     }
 }
 
-template <int MODE, int DICT = 0>   // DICT: with_tile_kind (8/16/32: dictionary ELL, that width)
+// Column ELL rows (DICT = kXell + W): relax_range_ell's per-row arithmetic, one row block per
+// workgroup, the row's products in registers from its explicit-column codes.
+template <int MODE, int W>
+__device__ __forceinline__ void relax_range_xell(int blo, const int2 *__restrict__ blk, int lo,
+                                                 const double *__restrict__ b, double *x, double *__restrict__ y,
+                                                 const double *__restrict__ deff, double *__restrict__ rr,
+                                                 double *__restrict__ partial, XSrc xs, const DevDict &dt)
+{
+    __shared__ XellSmem es;
+    const int bid = blo + (int)blockIdx.x;
+    const bool valid = bid < dt.bend;
+    unsigned w[W];
+    double br = 0.0, dr = 0.0;
+    int r = 0;
+    bool live = false;
+#pragma unroll
+    for (int t = 0; t < W; ++t) w[t] = 0xffffffffu;
+    if (valid) {   // the row's codes, b and divisor in flight across the barrier
+        const int2 ba = blk[bid], be = blk[bid + 1];
+        r = ba.x + (int)threadIdx.x;
+        live = r < be.x;
+        if (live) {
+            xell_codes<W>(dt.xell, r, w);
+            br = b[r];
+            if (deff) dr = deff[r];
+        }
+        xell_load_dict_nosync(dt, bid, es);
+    }
+    __syncthreads();
+    double sq = 0.0;
+    if (live) {
+        double xv[W];
+        int dsl;
+        const int len = xell_gather<W>(w, r, [&](int c) -> double { return xs(c); }, xv, dsl);
+        const double acc = dsl < 0 ? xell_sub(br, w, xv, es, 0, len)
+                                   : xell_sub(xell_sub(br, w, xv, es, 0, dsl), w, xv, es, dsl + 1, len);
+        const double dv = dsl < 0 ? 0.0 : es.vd[(w[dsl] >> kXellColBits) & (kXellValues - 1)];
+        const double d = deff ? dr : dv;
+        if constexpr (MODE == 2) {
+            const double xn = fabs(d) > SMALLFLOAT ? acc / d : x[r];
+            if (fabs(d) > SMALLFLOAT) x[r] = xn;
+            double t = xell_add(0.0, w, xv, es, 0, dsl);
+            t += d * xn;
+            t = xell_add(t, w, xv, es, dsl + 1, len);
+            const double out = br + t * -1.0;
+            rr[r] = out;
+            sq = out * out;
+        } else if constexpr (MODE == 3) {
+            const double out = br + xell_add(0.0, w, xv, es, 0, len) * -1.0;
+            rr[r] = out;
+            sq = out * out;
+            y[r - lo] = fabs(d) > SMALLFLOAT ? acc / d : x[r];
+        } else if constexpr (MODE == 1) {
+            y[r - lo] = fabs(d) > SMALLFLOAT ? acc / d : xs(r);
+        } else {
+            if (fabs(d) > SMALLFLOAT) x[r] = acc / d;
+        }
+    }
+    if constexpr (MODE >= 2) {
+        if (partial && valid) {   // (valid is uniform over the workgroup)
+            const double t = block_sum(sq, es.red);
+            if (threadIdx.x == 0) partial[bid] = t;
+        }
+    }
+}
+
+template <int MODE, int DICT = 0>   // DICT: with_tile_kind (8/16/32: dictionary ELL, kXell + W: column ELL)
 __device__ __forceinline__ void relax_range_body(int blo, const int2 *__restrict__ blk, const int *__restrict__ rp,
                                                       const int *__restrict__ ci, const double *__restrict__ v,
                                                       const int *__restrict__ diag_pos, int lo,
@@ -572,7 +641,9 @@ __device__ __forceinline__ void relax_range_body(int blo, const int2 *__restrict
                                                       double *__restrict__ rr, double *__restrict__ partial, XSrc xs,
                                                       DevDict dt = DevDict())
 {
-    if constexpr (DICT >= 8) {
+    if constexpr (DICT >= kXell) {
+        relax_range_xell<MODE, DICT - kXell>(blo, blk, lo, b, x, y, deff, rr, partial, xs, dt);
+    } else if constexpr (DICT >= 8) {
         relax_range_ell<MODE, DICT>(blo, blk, lo, b, x, y, deff, rr, partial, xs, dt);
     } else {
     __shared__ SpmvSmem sm;
@@ -708,7 +779,8 @@ static void launch_relax_range(int blo, int nb, hipStream_t s, DevDict dt, Args.
         hipLaunchKernelGGL((relax_range<M, K>), dim3(nb), dim3(kBlock), 0, s, blo, args..., dt);
     } else {
         dt.bend = blo + nb;
-        hipLaunchKernelGGL((relax_range<M, K>), dim3((nb + kEllRpt - 1) / kEllRpt), dim3(kBlock), 0, s, blo, args..., dt);
+        hipLaunchKernelGGL((relax_range<M, K>), dim3((nb + rows_per_wg(K) - 1) / rows_per_wg(K)), dim3(kBlock), 0, s, blo,
+                           args..., dt);
     }
 }
 

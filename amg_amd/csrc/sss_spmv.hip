@@ -437,6 +437,7 @@ DevDict devdict(const DevCSR &A, int blo)
     t.code = A.dv_code;
     t.ell = A.dv_ell;
     t.ellw = A.ell_w;
+    t.xell = A.dv_xell;
     t.remap = A.ell_remap;
     t.pd = A.dv_pd + blo;
     t.dd = A.dv_dd;
@@ -638,6 +639,81 @@ static bool build_ell(const SSS_MAT &h, const std::vector<int> &blk, HostBuf<uns
     return true;
 }
 
+// Column ELL of a square matrix (DevCSR::dv_xell) over blocks of 256 rows: W 32-bit codes per row
+// (stored order, 0xFFFFFFFF pads), each block's distinct values (<= 128, ascending) in vd at
+// pd[q].z / .w (false when a block has more).  W = the longest row rounded up to 16, 20, 24 or 32.
+static int xell_width(int L) { return L <= 16 ? 16 : L <= 20 ? 20 : L <= 24 ? 24 : L <= 32 ? 32 : 0; }
+static bool build_xell(const SSS_MAT &h, const std::vector<int> &blk, int W, HostBuf<unsigned> &codes,
+                       std::vector<int4> &pd, std::vector<double> &vd)
+{
+    const int *rp = h.row_ptr, *ci = h.col_idx;
+    const double *v = h.val;
+    const int nb = (int)blk.size() - 1;
+    codes.resize((size_t)h.num_rows * W);
+    std::vector<int> nv_of(nb);
+    std::vector<double> bvf((size_t)nb * kXellValues);
+    std::atomic<int> ok{1};
+    parallel_chunks(nb, 64, [&](int qlo, int qhi) {
+        std::unique_ptr<SmallDict> Vd(new SmallDict());
+        std::vector<unsigned long long> vs;
+        for (int q = qlo; q < qhi && ok; ++q) {
+            Vd->clear();
+            for (int r = blk[q]; r < blk[q + 1]; ++r) {
+                unsigned *row = codes.data() + (size_t)r * W;
+                int s = 0;
+                for (int k = rp[r]; k < rp[r + 1]; ++k, ++s) {
+                    const int vi = Vd->insert(bits_of(v[k]), kXellValues);
+                    if (vi < 0) {
+                        ok = 0;
+                        return;
+                    }
+                    row[s] = (unsigned)vi << kXellColBits | (unsigned)ci[k];
+                }
+                for (; s < W; ++s) row[s] = 0xffffffffu;
+            }
+            Vd->finish(vs);
+            nv_of[q] = (int)vs.size();
+            for (size_t t = 0; t < vs.size(); ++t) bvf[(size_t)q * kXellValues + t] = double_of(vs[t]);
+            for (int r = blk[q]; r < blk[q + 1]; ++r) {
+                unsigned *row = codes.data() + (size_t)r * W;
+                for (int s = 0; s < rp[r + 1] - rp[r]; ++s)
+                    row[s] = (unsigned)Vd->rk[row[s] >> kXellColBits] << kXellColBits | (row[s] & kXellColMask);
+            }
+        }
+    });
+    if (!ok) return false;
+    pd.resize((size_t)nb);
+    size_t nv = 0;
+    for (int q = 0; q < nb; ++q) {
+        pd[q] = make_int4(0, 0, (int)nv, nv_of[q]);
+        nv += nv_of[q];
+    }
+    vd.resize(std::max<size_t>(nv, 1));
+    parallel_chunks(nb, 4096, [&](int qlo, int qhi) {
+        for (int q = qlo; q < qhi; ++q)
+            std::copy(bvf.begin() + (size_t)q * kXellValues, bvf.begin() + (size_t)q * kXellValues + nv_of[q],
+                      vd.begin() + pd[q].z);
+    });
+    return true;
+}
+// 256-row blocks (cut at the class split): the column ELL's blocking
+static int build_rows_blocks(int n, std::vector<int> &blk, int split)
+{
+    blk.clear();
+    for (int r = 0; r < n;) {
+        blk.push_back(r);
+        const int lim = (split > r && split < n) ? split : n;
+        r = std::min(lim, r + kBlock);
+    }
+    blk.push_back(n);
+    return (int)blk.size() - 1;
+}
+static bool xell_on()
+{
+    const char *e = getenv("SSS_HIP_XELL");   // 0: no column ELL (read per upload: tests compare both ways)
+    return !(e && *e == '0');
+}
+
 int devcsr_upload(DevCSR &d, const SSS_MAT &h, int split, int enc, const int *seg)
 {
     PhaseTimer pt("devcsr");
@@ -744,7 +820,52 @@ int devcsr_upload(DevCSR &d, const SSS_MAT &h, int split, int enc, const int *se
         }
     }
     pt.mark("ell");
-    if ((enc & kEncDict) && !(dz && *dz == '0') && !d.dv_ell && !d.wave_rows && !d.vec_rows && d.nnz > 0) {
+    // column ELL where the 1-byte dictionary did not fit: its own 256-row blocking replaces the
+    // CSR-adaptive one (no tile staging, so no entry limit per block)
+    if ((enc & kEncDict) && !(dz && *dz == '0') && xell_on() && !d.dv_ell && !d.wave_rows && !d.vec_rows &&
+        d.nnz > 0 && d.n == d.ncols && (long long)d.ncols <= (1LL << kXellColBits)) {
+        std::atomic<int> Lmax{0};
+        parallel_chunks(d.n, 1 << 16, [&](int lo, int hi) {
+            int L = 0;
+            for (int r = lo; r < hi; ++r) L = std::max(L, h.row_ptr[r + 1] - h.row_ptr[r]);
+            int cur = Lmax.load();
+            while (L > cur && !Lmax.compare_exchange_weak(cur, L)) {}
+        });
+        const int W = xell_width(Lmax.load());
+        std::vector<int> xb;
+        HostBuf<unsigned> codes;
+        std::vector<int4> pd;
+        std::vector<double> vd;
+        if (W > 0) build_rows_blocks(d.n, xb, split);
+        if (W > 0 && build_xell(h, xb, W, codes, pd, vd)) {
+            dev_free(d.blk);
+            dev_free(d.bk);
+            d.blk = nullptr;
+            d.bk = nullptr;
+            blk.swap(xb);
+            d.nblk = (int)blk.size() - 1;
+            d.split_blk = d.nblk;
+            if (split >= 0)
+                for (int q = 0; q <= d.nblk; ++q)
+                    if (blk[q] >= split) { d.split_blk = q; break; }
+            d.ngrid = d.nblk;
+            d.blk = dev_alloc<int>(blk.size());
+            if (!d.blk) return hip_fail(hipErrorOutOfMemory, "hipMalloc(blk)", __FILE__, __LINE__);
+            if (int rc = h2d(d.blk, blk.data(), sizeof(int) * blk.size())) return rc;
+            if (int rc = upload_block_bounds(&d.bk, blk, h.row_ptr)) return rc;
+            d.xell_w = W;
+            d.dv_xell = dev_alloc<unsigned>(codes.size());
+            d.dv_pd = dev_alloc<int4>(pd.size());
+            d.dv_vd = dev_alloc<double>(vd.size());
+            if (!d.dv_xell || !d.dv_pd || !d.dv_vd)
+                return hip_fail(hipErrorOutOfMemory, "hipMalloc(column ELL)", __FILE__, __LINE__);
+            if (int rc = h2d(d.dv_xell, codes.data(), sizeof(unsigned) * codes.size())) return rc;
+            if (int rc = h2d(d.dv_pd, pd.data(), sizeof(int4) * pd.size())) return rc;
+            if (int rc = h2d(d.dv_vd, vd.data(), sizeof(double) * vd.size())) return rc;
+        }
+    }
+    pt.mark("xell");
+    if ((enc & kEncDict) && !(dz && *dz == '0') && !d.dv_ell && !d.dv_xell && !d.wave_rows && !d.vec_rows && d.nnz > 0) {
         HostBuf<unsigned> code;
         std::vector<int4> pd;
         std::vector<int> dd;
@@ -767,7 +888,7 @@ int devcsr_upload(DevCSR &d, const SSS_MAT &h, int split, int enc, const int *se
     HostBuf<unsigned> pk;
     HostBuf<double> pv;
     std::vector<int2> pb;
-    if ((enc & kEncSortedTiles) && !d.dv_code && !d.dv_ell && !d.wave_rows && !d.vec_rows && d.nnz > 0 &&
+    if ((enc & kEncSortedTiles) && !d.dv_code && !d.dv_ell && !d.dv_xell && !d.wave_rows && !d.vec_rows && d.nnz > 0 &&
         build_sorted_tiles(h, blk, pk, pv, pb)) {
         d.pk = dev_alloc<unsigned>((size_t)d.nnz);
         d.pb = dev_alloc<int2>(pb.size());
@@ -801,7 +922,8 @@ int devcsr_upload(DevCSR &d, const SSS_MAT &h, int split, int enc, const int *se
         std::vector<int4> pd((size_t)nb);
         if (nb > 0) SSS_HIP(hipMemcpy(pd.data(), d.dv_pd, sizeof(int4) * (size_t)nb, hipMemcpyDeviceToHost));
         for (const auto &p : pd) dict += 4LL * p.y + 8LL * p.w;
-        d.stream_bytes = d.dv_ell ? (long long)d.ell_w * rows + 8 * (nb + 1) + 16 * nb + dict
+        d.stream_bytes = d.dv_xell ? 4LL * d.xell_w * rows + 8 * (nb + 1) + 16 * nb + dict
+                         : d.dv_ell ? (long long)d.ell_w * rows + 8 * (nb + 1) + 16 * nb + dict
                                   : (d.dv_vi ? 5 * nnz + 8 * nb : 4 * nnz) + 4 * (rows + 1) + 8 * (nb + 1) + 16 * nb + dict;
     } else if (d.pk) {
         d.stream_bytes = 12 * nnz + 4 * (rows + 1) + 8 * (nb + 1) + 8 * nb;
@@ -839,6 +961,7 @@ void devcsr_free(DevCSR &d)
     dev_free(d.mg_v);
     dev_free(d.dv_code);
     dev_free(d.dv_ell);
+    dev_free(d.dv_xell);
     dev_free(d.dv_vi);
     dev_free(d.dv_pd);
     dev_free(d.dv_dd);
@@ -868,7 +991,47 @@ __global__ __launch_bounds__(kBlock) void spmv_adaptive(const int2 *__restrict__
         y[r] = out;
         return NORM ? out * out : 0.0;
     };
-    if constexpr (DICT >= 8) {   // dictionary ELL rows of width DICT: one thread per row, its sum
+    if constexpr (DICT >= kXell) {   // column ELL rows of width DICT - kXell: one thread per row
+        constexpr int W = DICT - kXell;
+        __shared__ XellSmem es;
+        const int bid = blockIdx.x;
+        unsigned w[W];
+        double br = 0.0;
+        int r = 0;
+        bool live = false;
+        const bool valid = bid < dt.bend;
+#pragma unroll
+        for (int t = 0; t < W; ++t) w[t] = 0xffffffffu;
+        if (valid) {   // codes (and b) in flight across the dictionary's barrier
+            const int2 ba = blk[bid], be = blk[bid + 1];
+            r = ba.x + (int)threadIdx.x;
+            live = r < be.x;
+            if (live) {
+                xell_codes<W>(dt.xell, r, w);
+                if constexpr (OP == SSS_HIP_SPMV_RESID) br = b[r];
+            }
+            xell_load_dict_nosync(dt, bid, es);
+        }
+        __syncthreads();
+        double sq = 0.0;
+        if (live) {
+            double xv[W];
+            int ds;
+            const int len = xell_gather<W>(w, r, [&](int c) -> double { return x[c]; }, xv, ds);
+            const double sum = xell_add(0.0, w, xv, es, 0, len);
+            if constexpr (OP == SSS_HIP_SPMV_RESID) {
+                const double out = br + sum * alpha;
+                y[r] = out;
+                sq = NORM ? out * out : 0.0;
+            } else {
+                sq = epi(r, sum);
+            }
+        }
+        if (NORM && valid) {
+            const double t = block_sum(sq, es.red);
+            if (threadIdx.x == 0) partial[bid] = t;
+        }
+    } else if constexpr (DICT >= 8) {   // dictionary ELL rows of width DICT: one thread per row, its sum
         constexpr int W = DICT;   // from 0.0 in stored order; kEllRpt row blocks per workgroup
         constexpr int RPT = kEllRpt;
         __shared__ EllSmem es[RPT];
@@ -1024,7 +1187,7 @@ static void launch_op(const DevCSR &A, double alpha, const double *x, const doub
             constexpr int KK = decltype(K)::value;
             DevDict dt = devdict(A, 0);
             dt.bend = A.nblk;
-            const int grid = KK >= 8 ? (A.nblk + kEllRpt - 1) / kEllRpt : A.nblk;
+            const int grid = (A.nblk + rows_per_wg(KK) - 1) / rows_per_wg(KK);
             hipLaunchKernelGGL((spmv_adaptive<OP, NORM, KK>), dim3(grid), dim3(kBlock), 0, s, A.bk, A.rp, A.ci, A.v, x,
                                b, y, alpha, cap, partial, A.pk, A.pv, A.pb, dt);
         });
@@ -1065,7 +1228,7 @@ int launch_spmv_range(const DevCSR &A, int blo, int bhi, int op, double alpha, c
         constexpr bool NM = decltype(norm_c)::value;
         with_tile_kind(A, [&](auto K) {
             constexpr int KK = decltype(K)::value;
-            const int grid = KK >= 8 ? (nb + kEllRpt - 1) / kEllRpt : nb;
+            const int grid = (nb + rows_per_wg(KK) - 1) / rows_per_wg(KK);
             hipLaunchKernelGGL((spmv_adaptive<O, NM, KK>), dim3(grid), dim3(kBlock), 0, s, A.bk + blo, A.rp, A.ci, A.v,
                                x, b, y, alpha, 0, pp, A.pk, A.pv, pb, dt);
         });

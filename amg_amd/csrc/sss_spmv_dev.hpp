@@ -60,6 +60,7 @@ struct DevDict {
     int ellw = 0;
     int remap = 0;   // ELL launches: XCD-contiguous block order (DevCSR::ell_remap)
     int bend = 0x7fffffff;   // ELL launches: first block past the launch's range (kEllRpt blocks per workgroup)
+    const unsigned *xell = nullptr;   // column ELL (DevCSR::dv_xell), W 32-bit codes per row
 };
 // Dictionary ELL: row blocks per workgroup (each thread takes one row of each; more independent
 // loads in flight per thread, one dictionary barrier for all of them).  Measured at 400^3
@@ -138,6 +139,76 @@ __device__ __forceinline__ int ell_row(const unsigned char *__restrict__ ell, in
     ell_codes<W>(ell, r, w);
     return ell_decode<W>(w, r, es, fetch, p, dslot, dval);
 }
+// ---- column ELL: one thread per row, explicit 25-bit columns ----------------------------------
+// Row r's W codes  value index << 25 | column  (0xFFFFFFFF pads) at xell[r * W], into the block's
+// value dictionary (<= 128 values) in LDS.
+constexpr int kXellColBits = 25;
+constexpr unsigned kXellColMask = (1u << kXellColBits) - 1;
+constexpr int kXellValues = 128;
+struct XellSmem {
+    double vd[kXellValues];
+    double red[kBlock / 64];
+};
+__device__ __forceinline__ void xell_load_dict_nosync(const DevDict &dt, int bid, XellSmem &es)
+{
+    const int4 p = dt.pd[bid];
+    if ((int)threadIdx.x < p.w) es.vd[threadIdx.x] = dt.vd[p.z + threadIdx.x];
+}
+template <int W>
+__device__ __forceinline__ void xell_codes(const unsigned *__restrict__ xell, int r, unsigned (&w)[W])
+{
+    static_assert(W % 4 == 0, "column ELL rows are whole 16-byte loads");
+    const uint4 *q = reinterpret_cast<const uint4 *>(xell + (size_t)r * W);
+#pragma unroll
+    for (int h = 0; h < W / 4; ++h) {
+        const uint4 u = q[h];
+        w[4 * h] = u.x, w[4 * h + 1] = u.y, w[4 * h + 2] = u.z, w[4 * h + 3] = u.w;
+    }
+}
+// Row r's x values in slot order, xv[s] = x(c_s) for s < len (0.0 past it); dslot = the row's
+// (last) diagonal slot or -1.  The products a_s * xv[s] are formed where they are summed
+// (xell_prod: the value from the LDS dictionary), so only the codes and the gathered x values
+// stay in registers.
+template <int W, class Fetch>
+__device__ __forceinline__ int xell_gather(const unsigned (&w)[W], int r, Fetch fetch, double (&xv)[W], int &dslot)
+{
+    int len = W;
+    dslot = -1;
+#pragma unroll
+    for (int s = 0; s < W; ++s)
+        if (w[s] == 0xffffffffu && len == W) len = s;
+#pragma unroll
+    for (int s = 0; s < W; ++s) xv[s] = s < len ? fetch((int)(w[s] & kXellColMask)) : 0.0;
+#pragma unroll
+    for (int s = 0; s < W; ++s)
+        if (s < len && (int)(w[s] & kXellColMask) == r) dslot = s;
+    return len;
+}
+template <int W>
+__device__ __forceinline__ double xell_prod(const unsigned (&w)[W], const double (&xv)[W], const XellSmem &es, int s)
+{
+    return es.vd[(w[s] >> kXellColBits) & (kXellValues - 1)] * xv[s];
+}
+// s0 + (or -) the products of slots [a, e) in slot order
+template <int W>
+__device__ __forceinline__ double xell_add(double s0, const unsigned (&w)[W], const double (&xv)[W], const XellSmem &es,
+                                           int a, int e)
+{
+#pragma unroll
+    for (int s = 0; s < W; ++s)
+        if (s >= a && s < e) s0 += xell_prod(w, xv, es, s);
+    return s0;
+}
+template <int W>
+__device__ __forceinline__ double xell_sub(double s0, const unsigned (&w)[W], const double (&xv)[W], const XellSmem &es,
+                                           int a, int e)
+{
+#pragma unroll
+    for (int s = 0; s < W; ++s)
+        if (s >= a && s < e) s0 -= xell_prod(w, xv, es, s);
+    return s0;
+}
+
 // sum of p[a, e) from s0 in slot order
 template <int W>
 __device__ __forceinline__ double ell_add(double s0, const double (&p)[W], int a, int e)

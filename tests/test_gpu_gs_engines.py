@@ -317,17 +317,21 @@ def test_w_cycle_bitwise(request, hname, smoother, coarse):
 @pytest.mark.parametrize("smoother,coarse", [("exact", "krylov"), ("hybrid", "direct")])
 def test_dictionary_tiles_bitwise(request, hname, smoother, coarse, monkeypatch):
     """A_l stored as dictionary ELL rows (1 B per entry: offset and value indices into per-block
-    dictionaries, one thread per row), as dictionary tiles (4 B per entry) or as value-dictionary
+    dictionaries, one thread per row), as column ELL rows (4 B per entry: explicit column and a
+    value index, one thread per row), as dictionary tiles (4 B per entry) or as value-dictionary
     sorted tiles (5 B: the sorted tile slot plus a value index) gives the iterates of the plain
     column-sorted tiles bit for bit, and the stencil levels do take that storage: level 0 of 7-pt
-    the ELL rows (dictionary tiles with ELL off), the relabeled Galerkin levels of 7-pt 64^3
-    (offsets too many for a dictionary, at most 8 values per block) the value dictionaries."""
+    the dictionary ELL rows (dictionary tiles with both ELLs off, column ELL with only the
+    dictionary ELL off -- every relaxation mode of the exact level-0 passes), the relabeled Galerkin
+    levels of 7-pt (offsets too many for a 1-byte dictionary, at most 8 values per block) the column
+    ELL, or the value dictionaries with it off."""
     H = request.getfixturevalue(hname)
     n = H.level(0).A.num_rows
     out, fmt = {}, {}
-    for mode, env in (("ell", {"SSS_HIP_DICT": "1", "SSS_HIP_ELL": "1"}),
-                      ("tiles", {"SSS_HIP_DICT": "1", "SSS_HIP_ELL": "0"}),
-                      ("none", {"SSS_HIP_DICT": "0", "SSS_HIP_ELL": "0"})):
+    for mode, env in (("ell", {"SSS_HIP_DICT": "1", "SSS_HIP_ELL": "1", "SSS_HIP_XELL": "1"}),
+                      ("xell", {"SSS_HIP_DICT": "1", "SSS_HIP_ELL": "0", "SSS_HIP_XELL": "1"}),
+                      ("tiles", {"SSS_HIP_DICT": "1", "SSS_HIP_ELL": "0", "SSS_HIP_XELL": "0"}),
+                      ("none", {"SSS_HIP_DICT": "0", "SSS_HIP_ELL": "0", "SSS_HIP_XELL": "1"})):
         for k, v in env.items():
             monkeypatch.setenv(k, v)
         D = A.DeviceHierarchy(H, smoother=smoother, coarse=coarse)
@@ -344,14 +348,18 @@ def test_dictionary_tiles_bitwise(request, hname, smoother, coarse, monkeypatch)
             D.close()
     if hname != "a27_h":
         assert fmt["ell"][0] & 64, fmt
-        assert fmt["tiles"][0] & 2 and not fmt["tiles"][0] & 64, fmt
+        assert fmt["xell"][0] & 128, fmt
+        assert fmt["ell"][1] & 128, fmt
+        assert fmt["tiles"][0] & 2 and not fmt["tiles"][0] & 192, fmt
     assert fmt["tiles"][0] & 2 or hname == "a27_h", fmt
     if hname == "p64_h":
         assert any(f & 3 == 3 for f in fmt["tiles"][1:]), fmt
-    assert not any(f & 66 for f in fmt["none"])
-    for mode in ("ell", "tiles"):
+    assert not any(f & 194 for f in fmt["none"])
+    for mode in ("ell", "xell", "tiles"):
         assert np.array_equal(out[mode][0].view(np.uint64), out["none"][0].view(np.uint64)), mode
-        assert out[mode][1] == out["none"][1], mode
+        # the norm's partial sums follow the row blocking, which the column ELL sets to 256 rows:
+        # the same squares, summed in another fixed order
+        assert np.allclose(out[mode][1], out["none"][1], rtol=1e-14, atol=0), mode
 
 
 # ---------------------------------------------------------------- a stalled pass fails loudly
