@@ -57,6 +57,15 @@ struct DLevel {
 };
 
 // Per row block of a local matrix: 1 if any entry reads a column >= own (a ghost).
+// the row blocking a DevCSR was uploaded with (first row of each block, nblk + 1 entries)
+int device_blocks(const DevCSR &M, std::vector<int> &blk)
+{
+    blk.assign((size_t)M.nblk + 1, 0);
+    if (M.nblk <= 0 || !M.blk) return 0;
+    SSS_HIP(hipMemcpy(blk.data(), M.blk, sizeof(int) * blk.size(), hipMemcpyDeviceToHost));
+    return 0;
+}
+
 std::vector<char> block_ghost_flags(const HostMat &M, int own, const std::vector<int> &blk)
 {
     std::vector<char> f(blk.empty() ? 0 : blk.size() - 1, 0);
@@ -519,13 +528,14 @@ static sss_hip_dist *dist_create_impl(sss_hip_dist *d, PartPlan &plan, const SSS
             if (devcsr_upload(L.P, Pv, P.nF, transfer_encoding(d->opts)) ||
                 devcsr_upload(L.R, Rv, -1, transfer_encoding(d->opts)))
                 return "upload P/R";
-            {   // which row blocks read ghosts (the same blockings the uploads made)
+            {   // which row blocks read ghosts (the blockings the uploads made, read back: the
+                // column ELL replaces the CSR-adaptive blocking where it is chosen)
                 std::vector<int> blk;
-                build_row_blocks(P.A.rp.data(), P.A.rows, blk, P.nF);
+                if (device_blocks(L.A, blk)) return "block bounds";
                 L.ghostA = block_ghost_flags(P.A, L.m, blk);
-                build_row_blocks(P.R.rp.data(), P.R.rows, blk, -1);
+                if (device_blocks(L.R, blk)) return "block bounds";
                 L.ghostR = block_ghost_flags(P.R, L.m, blk);
-                build_row_blocks(P.P.rp.data(), P.P.rows, blk, P.nF);
+                if (device_blocks(L.P, blk)) return "block bounds";
                 L.ghostP = block_ghost_flags(P.P, l + 1 < d->nagg ? plan.L[l + 1].m : P.P.cols, blk);
             }
             const size_t nv = (size_t)(L.m + L.g);

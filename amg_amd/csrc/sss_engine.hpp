@@ -219,14 +219,15 @@ struct DevCSR {
     unsigned char *dv_ell = nullptr;
     int ell_w = 0;
     // Column ELL (kEncDict, when the offsets do not fit a 1-byte dictionary but every row has at
-    // most 32 entries, every 256-row block at most 128 distinct values and n < 2^25 -- the Galerkin
+    // most 32 entries, every 256-row block few enough distinct values and the columns fit the code -- the Galerkin
     // level of a stencil, 7-pt level 1: 19 entries per row): row r's entries in stored order as
-    // xell_w 32-bit codes  value index << 25 | column  at dv_xell[r * xell_w] (0xFFFFFFFF pads) into
+    // xell_w 32-bit codes  value index << xell_shift | column  at dv_xell[r * xell_w] (0xFFFFFFFF pads) into
     // the block value dictionaries dv_pd[block].z/.w -> dv_vd.  One thread per row, no LDS staging:
     // 4 B per entry (as the value-dictionary tiles' 5) without the tile's staging barrier and its
     // 2048-entry blocks (~108 rows of a 19-entry level): blocks are 256 rows.
     unsigned *dv_xell = nullptr;
     int xell_w = 0;
+    int xell_shift = 0;   // column bits S of a code (value index << S | column); >= 25
     int ell_remap = 0;   // ELL kernels take their blocks XCD-contiguously (SSS_HIP_ELL_REMAP)
     long long stream_bytes = 0;   // bytes of the stored format one tile-path SpMV streams (no vectors)
     unsigned *dv_code = nullptr;
@@ -252,7 +253,8 @@ static_assert((1 << kTileShift) == kTileEntries, "tile packing");
 static_assert(1 + kTileColBits + kTileShift == 32, "tile packing");
 // kEncMergedOnly: the matrix is only ever read through its merged copy when it gets one (the
 // two-stage split copies, launch_ts_*), so its CSR arrays need not be column-sorted
-enum { kEncSortedTiles = 1, kEncFreeOrder = 2, kEncDict = 4, kEncMergedOnly = 8 };
+// kEncXell: the column ELL may replace the tile storage (its own 256-row blocking)
+enum { kEncSortedTiles = 1, kEncFreeOrder = 2, kEncDict = 4, kEncMergedOnly = 8, kEncXell = 16 };
 // split >= 0 forces a row-block boundary at that row (the F|C class boundary of a relabeled level);
 // enc: kEnc* flags; seg (kEncFreeOrder only, optional): per row, the absolute CSR position that
 // splits the row into two independently summed segments (two-stage [N_i | L_i] rows).
@@ -283,7 +285,7 @@ inline bool has_dict(const DevCSR &A)
     return A.dv_code != nullptr || A.dv_vi != nullptr || A.dv_ell != nullptr || A.dv_xell != nullptr;
 }
 // Storage argument K of the tile kernels: 0 plain or sorted tiles, 1 dictionary tiles (either kind),
-// 8 / 16 / 32 dictionary ELL of that row width, kXell + W column ELL of row width W (16/20/24/32).
+// 8 / 16 / 32 dictionary ELL of that row width, kXell + W column ELL of row width W (8/16/20/24/32).
 constexpr int kXell = 256;
 #ifndef SSS_ELL_RPT
 #define SSS_ELL_RPT 2
@@ -295,7 +297,8 @@ template <class F>
 inline void with_tile_kind(const DevCSR &A, F f)
 {
     if (A.dv_xell) {
-        if (A.xell_w == 16) f(std::integral_constant<int, kXell + 16>{});
+        if (A.xell_w == 8) f(std::integral_constant<int, kXell + 8>{});
+        else if (A.xell_w == 16) f(std::integral_constant<int, kXell + 16>{});
         else if (A.xell_w == 20) f(std::integral_constant<int, kXell + 20>{});
         else if (A.xell_w == 24) f(std::integral_constant<int, kXell + 24>{});
         else f(std::integral_constant<int, kXell + 32>{});

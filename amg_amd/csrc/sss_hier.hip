@@ -146,17 +146,20 @@ int sss::level_encoding(const sss_hip_opts &o)
     // two-stage split copies mask them out (their column offsets are not row-relative)
     const char *dz = getenv("SSS_HIP_DICT");
     const int dict = (dz && *dz == '0') ? 0 : kEncDict;
-    return (o.sorted_tiles ? kEncSortedTiles : 0) | (o.sum_order == 1 ? kEncFreeOrder : 0) | dict;
+    return (o.sorted_tiles ? kEncSortedTiles : 0) | (o.sum_order == 1 ? kEncFreeOrder : 0) | dict | (dict ? kEncXell : 0);
 }
 int sss::level_inner_of(const sss_hip_opts &o, int l) { return level_inner(o, l); }
 // P_l and R_l: the level matrices' encodings; dictionary forms only with SSS_HIP_DICT_PR=1.
 // Measured at 7-pt 400^3 (tools/gpu/ab.sh): 22.15 -> 22.25 ms per V-cycle, level-0 prolongation
 // 255 -> 325 us (P's F rows have 1-8 irregular columns, so the per-tile dictionaries rarely
 // shrink a row and the extra indirection costs more than the 3 bytes saved per entry).
+// The column ELL (kEncXell) is offered to them unless SSS_HIP_XELL_PR=0.
 int sss::transfer_encoding(const sss_hip_opts &o)
 {
     const char *e = getenv("SSS_HIP_DICT_PR");
-    return (e && *e == '1') ? level_encoding(o) : (level_encoding(o) & ~kEncDict);
+    const char *x = getenv("SSS_HIP_XELL_PR");
+    const int enc = (e && *e == '1') ? level_encoding(o) : (level_encoding(o) & ~kEncDict);
+    return (x && *x == '0') ? (enc & ~kEncXell) : enc;
 }
 
 // Are the C and the F points of A each an independent set (no off-diagonal coupling inside a

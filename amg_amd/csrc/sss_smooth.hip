@@ -289,8 +289,8 @@ int smoother_build(SmootherPlan &sp, const SSS_MAT &A, const int *mark, int kind
             pt.mark("ts fill");
             SSS_MAT Mn = mk(nrp, nci, nv), Ml = mk(lrp, lci, lv);
             std::vector<int> seg(split);   // absolute [N_i | L_i] cut of each row of Mn
-            if ((rc = devcsr_upload(ps.ts_nl, Mn, -1, (enc & ~kEncDict) | kEncMergedOnly, seg.data())) ||
-                (rc = devcsr_upload(ps.ts_lo, Ml, -1, (enc & ~kEncDict) | kEncMergedOnly)))
+            const int tenc = (enc & ~(kEncDict | kEncXell)) | kEncMergedOnly;   // read by the ts_* kernels only
+            if ((rc = devcsr_upload(ps.ts_nl, Mn, -1, tenc, seg.data())) || (rc = devcsr_upload(ps.ts_lo, Ml, -1, tenc)))
                 return rc;
             pt.mark("ts upload");
             if ((rc = upload_ints(&ps.ts_split, split))) return rc;
@@ -597,22 +597,22 @@ __device__ __forceinline__ void relax_range_xell(int blo, const int2 *__restrict
     if (live) {
         double xv[W];
         int dsl;
-        const int len = xell_gather<W>(w, r, [&](int c) -> double { return xs(c); }, xv, dsl);
-        const double acc = dsl < 0 ? xell_sub(br, w, xv, es, 0, len)
-                                   : xell_sub(xell_sub(br, w, xv, es, 0, dsl), w, xv, es, dsl + 1, len);
-        const double dv = dsl < 0 ? 0.0 : es.vd[(w[dsl] >> kXellColBits) & (kXellValues - 1)];
+        const int len = xell_gather<W>(w, r, dt.xshift, [&](int c) -> double { return xs(c); }, xv, dsl);
+        const double acc = dsl < 0 ? xell_sub(br, w, xv, es, dt.xshift, 0, len)
+                                   : xell_sub(xell_sub(br, w, xv, es, dt.xshift, 0, dsl), w, xv, es, dt.xshift, dsl + 1, len);
+        const double dv = dsl < 0 ? 0.0 : es.vd[w[dsl] >> dt.xshift];
         const double d = deff ? dr : dv;
         if constexpr (MODE == 2) {
             const double xn = fabs(d) > SMALLFLOAT ? acc / d : x[r];
             if (fabs(d) > SMALLFLOAT) x[r] = xn;
-            double t = xell_add(0.0, w, xv, es, 0, dsl);
+            double t = xell_add(0.0, w, xv, es, dt.xshift, 0, dsl);
             t += d * xn;
-            t = xell_add(t, w, xv, es, dsl + 1, len);
+            t = xell_add(t, w, xv, es, dt.xshift, dsl + 1, len);
             const double out = br + t * -1.0;
             rr[r] = out;
             sq = out * out;
         } else if constexpr (MODE == 3) {
-            const double out = br + xell_add(0.0, w, xv, es, 0, len) * -1.0;
+            const double out = br + xell_add(0.0, w, xv, es, dt.xshift, 0, len) * -1.0;
             rr[r] = out;
             sq = out * out;
             y[r - lo] = fabs(d) > SMALLFLOAT ? acc / d : x[r];

@@ -438,6 +438,7 @@ DevDict devdict(const DevCSR &A, int blo)
     t.ell = A.dv_ell;
     t.ellw = A.ell_w;
     t.xell = A.dv_xell;
+    t.xshift = A.xell_shift;
     t.remap = A.ell_remap;
     t.pd = A.dv_pd + blo;
     t.dd = A.dv_dd;
@@ -642,10 +643,20 @@ static bool build_ell(const SSS_MAT &h, const std::vector<int> &blk, HostBuf<uns
 // Column ELL of a square matrix (DevCSR::dv_xell) over blocks of 256 rows: W 32-bit codes per row
 // (stored order, 0xFFFFFFFF pads), each block's distinct values (<= 128, ascending) in vd at
 // pd[q].z / .w (false when a block has more).  W = the longest row rounded up to 16, 20, 24 or 32.
-static int xell_width(int L) { return L <= 16 ? 16 : L <= 20 ? 20 : L <= 24 ? 24 : L <= 32 ? 32 : 0; }
-static bool build_xell(const SSS_MAT &h, const std::vector<int> &blk, int W, HostBuf<unsigned> &codes,
+static int xell_width(int L) { return L <= 8 ? 8 : L <= 16 ? 16 : L <= 20 ? 20 : L <= 24 ? 24 : L <= 32 ? 32 : 0; }
+// column bits of a code: the smallest S >= 25 with ncols < 2^S (so the all-ones pad is never a
+// column), 0 past 28 (fewer than 16 value slots)
+static int xell_shift_for(int ncols)
+{
+    for (int S = 25; S <= 28; ++S)
+        if ((long long)ncols < (1LL << S)) return S;
+    return 0;
+}
+static bool build_xell(const SSS_MAT &h, const std::vector<int> &blk, int W, int S, HostBuf<unsigned> &codes,
                        std::vector<int4> &pd, std::vector<double> &vd)
 {
+    const int vcap = std::min(kXellValues, 1 << (32 - S));
+    const unsigned cmask = (1u << S) - 1;
     const int *rp = h.row_ptr, *ci = h.col_idx;
     const double *v = h.val;
     const int nb = (int)blk.size() - 1;
@@ -662,12 +673,12 @@ static bool build_xell(const SSS_MAT &h, const std::vector<int> &blk, int W, Hos
                 unsigned *row = codes.data() + (size_t)r * W;
                 int s = 0;
                 for (int k = rp[r]; k < rp[r + 1]; ++k, ++s) {
-                    const int vi = Vd->insert(bits_of(v[k]), kXellValues);
+                    const int vi = Vd->insert(bits_of(v[k]), vcap);
                     if (vi < 0) {
                         ok = 0;
                         return;
                     }
-                    row[s] = (unsigned)vi << kXellColBits | (unsigned)ci[k];
+                    row[s] = (unsigned)vi << S | (unsigned)ci[k];
                 }
                 for (; s < W; ++s) row[s] = 0xffffffffu;
             }
@@ -677,7 +688,7 @@ static bool build_xell(const SSS_MAT &h, const std::vector<int> &blk, int W, Hos
             for (int r = blk[q]; r < blk[q + 1]; ++r) {
                 unsigned *row = codes.data() + (size_t)r * W;
                 for (int s = 0; s < rp[r + 1] - rp[r]; ++s)
-                    row[s] = (unsigned)Vd->rk[row[s] >> kXellColBits] << kXellColBits | (row[s] & kXellColMask);
+                    row[s] = (unsigned)Vd->rk[row[s] >> S] << S | (row[s] & cmask);
             }
         }
     });
@@ -822,8 +833,9 @@ int devcsr_upload(DevCSR &d, const SSS_MAT &h, int split, int enc, const int *se
     pt.mark("ell");
     // column ELL where the 1-byte dictionary did not fit: its own 256-row blocking replaces the
     // CSR-adaptive one (no tile staging, so no entry limit per block)
-    if ((enc & kEncDict) && !(dz && *dz == '0') && xell_on() && !d.dv_ell && !d.wave_rows && !d.vec_rows &&
-        d.nnz > 0 && d.n == d.ncols && (long long)d.ncols <= (1LL << kXellColBits)) {
+    const int xshift = xell_shift_for(d.ncols);
+    if ((enc & kEncXell) && !(dz && *dz == '0') && xell_on() && !d.dv_ell && !d.wave_rows && !d.vec_rows &&
+        d.nnz > 0 && xshift > 0) {
         std::atomic<int> Lmax{0};
         parallel_chunks(d.n, 1 << 16, [&](int lo, int hi) {
             int L = 0;
@@ -831,13 +843,16 @@ int devcsr_upload(DevCSR &d, const SSS_MAT &h, int split, int enc, const int *se
             int cur = Lmax.load();
             while (L > cur && !Lmax.compare_exchange_weak(cur, L)) {}
         });
-        const int W = xell_width(Lmax.load());
+        // rows padded to W: not where that more than doubles the codes (level-0 prolongation of 7-pt:
+        // 3.5 entries per row on average, 8 slots -- measured 258 -> 289 us with the column ELL)
+        int W = xell_width(Lmax.load());
+        if ((long long)d.nnz * 2 < (long long)W * d.n) W = 0;
         std::vector<int> xb;
         HostBuf<unsigned> codes;
         std::vector<int4> pd;
         std::vector<double> vd;
         if (W > 0) build_rows_blocks(d.n, xb, split);
-        if (W > 0 && build_xell(h, xb, W, codes, pd, vd)) {
+        if (W > 0 && build_xell(h, xb, W, xshift, codes, pd, vd)) {
             dev_free(d.blk);
             dev_free(d.bk);
             d.blk = nullptr;
@@ -854,6 +869,7 @@ int devcsr_upload(DevCSR &d, const SSS_MAT &h, int split, int enc, const int *se
             if (int rc = h2d(d.blk, blk.data(), sizeof(int) * blk.size())) return rc;
             if (int rc = upload_block_bounds(&d.bk, blk, h.row_ptr)) return rc;
             d.xell_w = W;
+            d.xell_shift = xshift;
             d.dv_xell = dev_alloc<unsigned>(codes.size());
             d.dv_pd = dev_alloc<int4>(pd.size());
             d.dv_vd = dev_alloc<double>(vd.size());
@@ -1017,8 +1033,8 @@ __global__ __launch_bounds__(kBlock) void spmv_adaptive(const int2 *__restrict__
         if (live) {
             double xv[W];
             int ds;
-            const int len = xell_gather<W>(w, r, [&](int c) -> double { return x[c]; }, xv, ds);
-            const double sum = xell_add(0.0, w, xv, es, 0, len);
+            const int len = xell_gather<W>(w, r, dt.xshift, [&](int c) -> double { return x[c]; }, xv, ds);
+            const double sum = xell_add(0.0, w, xv, es, dt.xshift, 0, len);
             if constexpr (OP == SSS_HIP_SPMV_RESID) {
                 const double out = br + sum * alpha;
                 y[r] = out;

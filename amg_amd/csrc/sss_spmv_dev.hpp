@@ -61,6 +61,7 @@ struct DevDict {
     int remap = 0;   // ELL launches: XCD-contiguous block order (DevCSR::ell_remap)
     int bend = 0x7fffffff;   // ELL launches: first block past the launch's range (kEllRpt blocks per workgroup)
     const unsigned *xell = nullptr;   // column ELL (DevCSR::dv_xell), W 32-bit codes per row
+    int xshift = 0;                   // its column bits (DevCSR::xell_shift)
 };
 // Dictionary ELL: row blocks per workgroup (each thread takes one row of each; more independent
 // loads in flight per thread, one dictionary barrier for all of them).  Measured at 400^3
@@ -139,11 +140,10 @@ __device__ __forceinline__ int ell_row(const unsigned char *__restrict__ ell, in
     ell_codes<W>(ell, r, w);
     return ell_decode<W>(w, r, es, fetch, p, dslot, dval);
 }
-// ---- column ELL: one thread per row, explicit 25-bit columns ----------------------------------
-// Row r's W codes  value index << 25 | column  (0xFFFFFFFF pads) at xell[r * W], into the block's
-// value dictionary (<= 128 values) in LDS.
-constexpr int kXellColBits = 25;
-constexpr unsigned kXellColMask = (1u << kXellColBits) - 1;
+// ---- column ELL: one thread per row, explicit columns ------------------------------------------
+// Row r's W codes  value index << S | column  (0xFFFFFFFF pads) at xell[r * W], S = DevDict::xshift
+// (the column bits of the matrix, >= 25), into the block's value dictionary (<= 2^(32 - S), at most
+// 128 values) in LDS.
 constexpr int kXellValues = 128;
 struct XellSmem {
     double vd[kXellValues];
@@ -170,42 +170,45 @@ __device__ __forceinline__ void xell_codes(const unsigned *__restrict__ xell, in
 // (xell_prod: the value from the LDS dictionary), so only the codes and the gathered x values
 // stay in registers.
 template <int W, class Fetch>
-__device__ __forceinline__ int xell_gather(const unsigned (&w)[W], int r, Fetch fetch, double (&xv)[W], int &dslot)
+__device__ __forceinline__ int xell_gather(const unsigned (&w)[W], int r, int shift, Fetch fetch, double (&xv)[W],
+                                           int &dslot)
 {
+    const unsigned mask = (1u << shift) - 1;
     int len = W;
     dslot = -1;
 #pragma unroll
     for (int s = 0; s < W; ++s)
         if (w[s] == 0xffffffffu && len == W) len = s;
 #pragma unroll
-    for (int s = 0; s < W; ++s) xv[s] = s < len ? fetch((int)(w[s] & kXellColMask)) : 0.0;
+    for (int s = 0; s < W; ++s) xv[s] = s < len ? fetch((int)(w[s] & mask)) : 0.0;
 #pragma unroll
     for (int s = 0; s < W; ++s)
-        if (s < len && (int)(w[s] & kXellColMask) == r) dslot = s;
+        if (s < len && (int)(w[s] & mask) == r) dslot = s;
     return len;
 }
 template <int W>
-__device__ __forceinline__ double xell_prod(const unsigned (&w)[W], const double (&xv)[W], const XellSmem &es, int s)
+__device__ __forceinline__ double xell_prod(const unsigned (&w)[W], const double (&xv)[W], const XellSmem &es, int shift,
+                                            int s)
 {
-    return es.vd[(w[s] >> kXellColBits) & (kXellValues - 1)] * xv[s];
+    return es.vd[w[s] >> shift] * xv[s];
 }
 // s0 + (or -) the products of slots [a, e) in slot order
 template <int W>
 __device__ __forceinline__ double xell_add(double s0, const unsigned (&w)[W], const double (&xv)[W], const XellSmem &es,
-                                           int a, int e)
+                                           int shift, int a, int e)
 {
 #pragma unroll
     for (int s = 0; s < W; ++s)
-        if (s >= a && s < e) s0 += xell_prod(w, xv, es, s);
+        if (s >= a && s < e) s0 += xell_prod(w, xv, es, shift, s);
     return s0;
 }
 template <int W>
 __device__ __forceinline__ double xell_sub(double s0, const unsigned (&w)[W], const double (&xv)[W], const XellSmem &es,
-                                           int a, int e)
+                                           int shift, int a, int e)
 {
 #pragma unroll
     for (int s = 0; s < W; ++s)
-        if (s >= a && s < e) s0 -= xell_prod(w, xv, es, s);
+        if (s >= a && s < e) s0 -= xell_prod(w, xv, es, shift, s);
     return s0;
 }
 
