@@ -227,7 +227,7 @@ struct DevCSR {
     // 2048-entry blocks (~108 rows of a 19-entry level): blocks are 256 rows.
     unsigned *dv_xell = nullptr;
     int xell_w = 0;
-    int xell_shift = 0;   // column bits S of a code (value index << S | column); >= 25
+    int xell_shift = 0;   // column bits S of a code (value index << S | column); >= 23
     int ell_remap = 0;   // ELL kernels take their blocks XCD-contiguously (SSS_HIP_ELL_REMAP)
     long long stream_bytes = 0;   // bytes of the stored format one tile-path SpMV streams (no vectors)
     unsigned *dv_code = nullptr;
@@ -285,7 +285,7 @@ inline bool has_dict(const DevCSR &A)
     return A.dv_code != nullptr || A.dv_vi != nullptr || A.dv_ell != nullptr || A.dv_xell != nullptr;
 }
 // Storage argument K of the tile kernels: 0 plain or sorted tiles, 1 dictionary tiles (either kind),
-// 8 / 16 / 32 dictionary ELL of that row width, kXell + W column ELL of row width W (8/16/20/24/32).
+// 8 / 16 / 32 dictionary ELL of that row width, kXell + W column ELL of row width W (8/16/20/24/32/40).
 constexpr int kXell = 256;
 #ifndef SSS_ELL_RPT
 #define SSS_ELL_RPT 2
@@ -301,7 +301,8 @@ inline void with_tile_kind(const DevCSR &A, F f)
         else if (A.xell_w == 16) f(std::integral_constant<int, kXell + 16>{});
         else if (A.xell_w == 20) f(std::integral_constant<int, kXell + 20>{});
         else if (A.xell_w == 24) f(std::integral_constant<int, kXell + 24>{});
-        else f(std::integral_constant<int, kXell + 32>{});
+        else if (A.xell_w == 32) f(std::integral_constant<int, kXell + 32>{});
+        else f(std::integral_constant<int, kXell + 40>{});
     } else if (A.dv_ell) {
         if (A.ell_w == 8) f(std::integral_constant<int, 8>{});
         else if (A.ell_w == 16) f(std::integral_constant<int, 16>{});

@@ -289,7 +289,9 @@ int smoother_build(SmootherPlan &sp, const SSS_MAT &A, const int *mark, int kind
             pt.mark("ts fill");
             SSS_MAT Mn = mk(nrp, nci, nv), Ml = mk(lrp, lci, lv);
             std::vector<int> seg(split);   // absolute [N_i | L_i] cut of each row of Mn
-            const int tenc = (enc & ~(kEncDict | kEncXell)) | kEncMergedOnly;   // read by the ts_* kernels only
+            // read by the ts_* kernels only: merged groups, or the column ELL (SSS_HIP_XELL_TS=0: not)
+            const char *xz = getenv("SSS_HIP_XELL_TS");
+            const int tenc = (enc & ~(kEncDict | ((xz && *xz == '0') ? kEncXell : 0))) | kEncMergedOnly;
             if ((rc = devcsr_upload(ps.ts_nl, Mn, -1, tenc, seg.data())) || (rc = devcsr_upload(ps.ts_lo, Ml, -1, tenc)))
                 return rc;
             pt.mark("ts upload");
@@ -825,7 +827,38 @@ __global__ __launch_bounds__(kBlock) void ts_stage0(int lo, DevCSR M, const int 
         const double d = deff[r];
         y[q] = fabs(d) > SMALLFLOAT ? acc / d : x(r);
     };
-    if constexpr (PATH >= 3) {   // merged row groups, G = PATH, M.mg_W waves per group
+    if constexpr (PATH >= kXell) {   // column ELL rows of width PATH - kXell: one thread per row
+        constexpr int W = PATH - kXell;
+        __shared__ XellSmem es;
+        const int bq = blockIdx.x;
+        const int2 ba = M.bk[bq], be = M.bk[bq + 1];
+        const int q = ba.x + (int)threadIdx.x;
+        const bool live = q < be.x;
+        unsigned w[W];
+        double bq_v = 0.0;
+        int sp = 0;
+#pragma unroll
+        for (int t = 0; t < W; ++t) w[t] = 0xffffffffu;
+        if (live) {   // the row's codes, b and its [N | L] cut in flight across the barrier
+            xell_codes<W>(M.dv_xell, q, w);
+            bq_v = b[lo + q];
+            sp = split[q] - M.rp[q];
+        }
+        {
+            const int4 pq4 = M.dv_pd[bq];
+            for (int t = threadIdx.x; t < pq4.w; t += kBlock) es.vd[t] = M.dv_vd[pq4.z + t];
+        }
+        __syncthreads();
+        if (live) {
+            double xv[W];
+            int ds;
+            const int len = xell_gather<W>(w, -1, M.xell_shift, [&](int c) -> double { return x(c); }, xv, ds);
+            const double Pq = xell_sub(bq_v, w, xv, es, M.xell_shift, 0, sp);
+            P[q] = Pq;
+            finish(q, xell_sub(Pq, w, xv, es, M.xell_shift, sp, len));
+        }
+        return;
+    } else if constexpr (PATH >= 3) {   // merged row groups, G = PATH, M.mg_W waves per group
         constexpr int G = PATH;
         __shared__ double red[8 * G];
         auto prod = [&](int c, double a) { return a * x(c); };
@@ -929,7 +962,34 @@ __global__ __launch_bounds__(kBlock) void ts_inner(int lo, DevCSR M, const doubl
         const double d = deff[lo + q];
         y[q] = fabs(d) > SMALLFLOAT ? acc / d : ykeep[q];
     };
-    if constexpr (PATH >= 3) {   // merged row groups, G = PATH, M.mg_W waves per group
+    if constexpr (PATH >= kXell) {   // column ELL rows of width PATH - kXell: one thread per row
+        constexpr int W = PATH - kXell;
+        __shared__ XellSmem es;
+        const int bq = blockIdx.x;
+        const int2 ba = M.bk[bq], be = M.bk[bq + 1];
+        const int q = ba.x + (int)threadIdx.x;
+        const bool live = q < be.x;
+        unsigned w[W];
+        double pq = 0.0;
+#pragma unroll
+        for (int t = 0; t < W; ++t) w[t] = 0xffffffffu;
+        if (live) {
+            xell_codes<W>(M.dv_xell, q, w);
+            pq = P[q];
+        }
+        {
+            const int4 pq4 = M.dv_pd[bq];
+            for (int t = threadIdx.x; t < pq4.w; t += kBlock) es.vd[t] = M.dv_vd[pq4.z + t];
+        }
+        __syncthreads();
+        if (live) {
+            double xv[W];
+            int ds;
+            const int len = xell_gather<W>(w, -1, M.xell_shift, fetch, xv, ds);
+            finish(q, xell_sub(pq, w, xv, es, M.xell_shift, 0, len));
+        }
+        return;
+    } else if constexpr (PATH >= 3) {   // merged row groups, G = PATH, M.mg_W waves per group
         constexpr int G = PATH;
         __shared__ double red[8 * G];
         int g = 0, u = 0;
@@ -1000,6 +1060,12 @@ void launch_ts_stage0(const DevCSR &M, int lo, const int *split, const double *b
         hipLaunchKernelGGL(ts_stage0<2>, dim3((M.n + 3) / 4), dim3(kBlock), 0, s, lo, M, split, b, x, deff, P, y);
     else if (M.wave_rows)
         hipLaunchKernelGGL(ts_stage0<1>, dim3(M.ngrid), dim3(kBlock), 0, s, lo, M, split, b, x, deff, P, y);
+    else if (M.dv_xell)
+        with_tile_kind(M, [&](auto K) {
+            constexpr int KK = decltype(K)::value;
+            if constexpr (KK >= kXell)
+                hipLaunchKernelGGL(ts_stage0<KK>, dim3(M.nblk), dim3(kBlock), 0, s, lo, M, split, b, x, deff, P, y);
+        });
     else
         hipLaunchKernelGGL(ts_stage0<0>, dim3(M.nblk), dim3(kBlock), 0, s, lo, M, split, b, x, deff, P, y);
 }
@@ -1016,6 +1082,13 @@ void launch_ts_inner(const DevCSR &M, int lo, const double *deff, const double *
         hipLaunchKernelGGL(ts_inner<2>, dim3((M.n + 3) / 4), dim3(kBlock), 0, s, lo, M, deff, P, ycols, col_off, ykeep, y);
     else if (M.wave_rows)
         hipLaunchKernelGGL(ts_inner<1>, dim3(M.ngrid), dim3(kBlock), 0, s, lo, M, deff, P, ycols, col_off, ykeep, y);
+    else if (M.dv_xell)
+        with_tile_kind(M, [&](auto K) {
+            constexpr int KK = decltype(K)::value;
+            if constexpr (KK >= kXell)
+                hipLaunchKernelGGL(ts_inner<KK>, dim3(M.nblk), dim3(kBlock), 0, s, lo, M, deff, P, ycols, col_off, ykeep,
+                                   y);
+        });
     else
         hipLaunchKernelGGL(ts_inner<0>, dim3(M.nblk), dim3(kBlock), 0, s, lo, M, deff, P, ycols, col_off, ykeep, y);
 }

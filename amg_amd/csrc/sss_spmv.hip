@@ -643,69 +643,14 @@ static bool build_ell(const SSS_MAT &h, const std::vector<int> &blk, HostBuf<uns
 // Column ELL of a square matrix (DevCSR::dv_xell) over blocks of 256 rows: W 32-bit codes per row
 // (stored order, 0xFFFFFFFF pads), each block's distinct values (<= 128, ascending) in vd at
 // pd[q].z / .w (false when a block has more).  W = the longest row rounded up to 16, 20, 24 or 32.
-static int xell_width(int L) { return L <= 8 ? 8 : L <= 16 ? 16 : L <= 20 ? 20 : L <= 24 ? 24 : L <= 32 ? 32 : 0; }
-// column bits of a code: the smallest S >= 25 with ncols < 2^S (so the all-ones pad is never a
+static int xell_width(int L) { return L <= 8 ? 8 : L <= 16 ? 16 : L <= 20 ? 20 : L <= 24 ? 24 : L <= 32 ? 32 : L <= 40 ? 40 : 0; }
+// column bits of a code: the smallest S >= 23 with ncols < 2^S (so the all-ones pad is never a
 // column), 0 past 28 (fewer than 16 value slots)
 static int xell_shift_for(int ncols)
 {
-    for (int S = 25; S <= 28; ++S)
+    for (int S = 23; S <= 28; ++S)
         if ((long long)ncols < (1LL << S)) return S;
     return 0;
-}
-static bool build_xell(const SSS_MAT &h, const std::vector<int> &blk, int W, int S, HostBuf<unsigned> &codes,
-                       std::vector<int4> &pd, std::vector<double> &vd)
-{
-    const int vcap = std::min(kXellValues, 1 << (32 - S));
-    const unsigned cmask = (1u << S) - 1;
-    const int *rp = h.row_ptr, *ci = h.col_idx;
-    const double *v = h.val;
-    const int nb = (int)blk.size() - 1;
-    codes.resize((size_t)h.num_rows * W);
-    std::vector<int> nv_of(nb);
-    std::vector<double> bvf((size_t)nb * kXellValues);
-    std::atomic<int> ok{1};
-    parallel_chunks(nb, 64, [&](int qlo, int qhi) {
-        std::unique_ptr<SmallDict> Vd(new SmallDict());
-        std::vector<unsigned long long> vs;
-        for (int q = qlo; q < qhi && ok; ++q) {
-            Vd->clear();
-            for (int r = blk[q]; r < blk[q + 1]; ++r) {
-                unsigned *row = codes.data() + (size_t)r * W;
-                int s = 0;
-                for (int k = rp[r]; k < rp[r + 1]; ++k, ++s) {
-                    const int vi = Vd->insert(bits_of(v[k]), vcap);
-                    if (vi < 0) {
-                        ok = 0;
-                        return;
-                    }
-                    row[s] = (unsigned)vi << S | (unsigned)ci[k];
-                }
-                for (; s < W; ++s) row[s] = 0xffffffffu;
-            }
-            Vd->finish(vs);
-            nv_of[q] = (int)vs.size();
-            for (size_t t = 0; t < vs.size(); ++t) bvf[(size_t)q * kXellValues + t] = double_of(vs[t]);
-            for (int r = blk[q]; r < blk[q + 1]; ++r) {
-                unsigned *row = codes.data() + (size_t)r * W;
-                for (int s = 0; s < rp[r + 1] - rp[r]; ++s)
-                    row[s] = (unsigned)Vd->rk[row[s] >> S] << S | (row[s] & cmask);
-            }
-        }
-    });
-    if (!ok) return false;
-    pd.resize((size_t)nb);
-    size_t nv = 0;
-    for (int q = 0; q < nb; ++q) {
-        pd[q] = make_int4(0, 0, (int)nv, nv_of[q]);
-        nv += nv_of[q];
-    }
-    vd.resize(std::max<size_t>(nv, 1));
-    parallel_chunks(nb, 4096, [&](int qlo, int qhi) {
-        for (int q = qlo; q < qhi; ++q)
-            std::copy(bvf.begin() + (size_t)q * kXellValues, bvf.begin() + (size_t)q * kXellValues + nv_of[q],
-                      vd.begin() + pd[q].z);
-    });
-    return true;
 }
 // 256-row blocks (cut at the class split): the column ELL's blocking
 static int build_rows_blocks(int n, std::vector<int> &blk, int split)
@@ -718,6 +663,102 @@ static int build_rows_blocks(int n, std::vector<int> &blk, int split)
     }
     blk.push_back(n);
     return (int)blk.size() - 1;
+}
+// Distinct 64-bit values of a row range (up to kXellValues), open addressing; ranks = ascending order.
+struct XellValues {
+    static constexpr int kSlots = 4 * kXellValues;
+    unsigned long long key[kSlots];
+    short slot[kSlots];
+    unsigned long long val[kXellValues];
+    unsigned short rk[kXellValues];
+    int n = 0;
+    void clear()
+    {
+        std::memset(slot, 0xff, sizeof(slot));
+        n = 0;
+    }
+    int insert(unsigned long long u, int cap)   // local id, or -1 past cap distinct values
+    {
+        for (unsigned h = (unsigned)((u * 0x9E3779B97F4A7C15ull) >> 53) & (kSlots - 1);; h = (h + 1) & (kSlots - 1)) {
+            if (slot[h] < 0) {
+                if (n >= cap) return -1;
+                slot[h] = (short)n;
+                key[h] = u;
+                val[n] = u;
+                return n++;
+            }
+            if (key[h] == u) return slot[h];
+        }
+    }
+    void finish(std::vector<double> &sorted)
+    {
+        int ord[kXellValues];
+        for (int t = 0; t < n; ++t) ord[t] = t;
+        std::sort(ord, ord + n, [&](int a, int b) { return val[a] < val[b]; });
+        sorted.resize((size_t)n);
+        for (int t = 0; t < n; ++t) rk[ord[t]] = (unsigned short)t, sorted[t] = double_of(val[ord[t]]);
+    }
+};
+// Column ELL codes and blocking: the rows in chunks of 256 (cut at the class split); a chunk whose
+// rows hold more distinct values than a code can index (2^(32 - S), at most kXellValues) is halved
+// until its parts fit (false below 16 rows).  Blocks, their value dictionaries (ascending) and every
+// row's W codes in stored order.
+static bool build_xell(const SSS_MAT &h, int split, int W, int S, std::vector<int> &blk, HostBuf<unsigned> &codes,
+                       std::vector<int4> &pd, std::vector<double> &vd)
+{
+    const int vcap = std::min(kXellValues, 1 << (32 - S));
+    const int *rp = h.row_ptr, *ci = h.col_idx;
+    const double *v = h.val;
+    std::vector<int> chunks;
+    const int nc = build_rows_blocks(h.num_rows, chunks, split);
+    codes.resize((size_t)h.num_rows * W);
+    struct Part {
+        int r0;
+        std::vector<double> vals;
+    };
+    std::vector<std::vector<Part>> parts((size_t)nc);
+    std::atomic<int> ok{1};
+    parallel_chunks(nc, 64, [&](int clo, int chi) {
+        std::unique_ptr<XellValues> D(new XellValues());
+        // rows [r0, r1) as one block if their values fit, else halved
+        std::function<bool(int, int, std::vector<Part> &)> fit = [&](int r0, int r1, std::vector<Part> &out) -> bool {
+            D->clear();
+            bool fits = true;
+            for (int k = rp[r0]; k < rp[r1] && fits; ++k) fits = D->insert(bits_of(v[k]), vcap) >= 0;
+            if (!fits) {
+                if (r1 - r0 <= 16) return false;
+                const int mid = r0 + (r1 - r0) / 2;
+                return fit(r0, mid, out) && fit(mid, r1, out);
+            }
+            Part p;
+            p.r0 = r0;
+            D->finish(p.vals);
+            for (int r = r0; r < r1; ++r) {
+                unsigned *row = codes.data() + (size_t)r * W;
+                int s = 0;
+                for (int k = rp[r]; k < rp[r + 1]; ++k, ++s)
+                    row[s] = (unsigned)D->rk[D->insert(bits_of(v[k]), vcap)] << S | (unsigned)ci[k];
+                for (; s < W; ++s) row[s] = 0xffffffffu;
+            }
+            out.push_back(std::move(p));
+            return true;
+        };
+        for (int c = clo; c < chi && ok; ++c)
+            if (!fit(chunks[c], chunks[c + 1], parts[c])) ok = 0;
+    });
+    if (!ok) return false;
+    blk.clear();
+    pd.clear();
+    vd.clear();
+    for (int c = 0; c < nc; ++c)
+        for (const Part &p : parts[c]) {
+            blk.push_back(p.r0);
+            pd.push_back(make_int4(0, 0, (int)vd.size(), (int)p.vals.size()));
+            vd.insert(vd.end(), p.vals.begin(), p.vals.end());
+        }
+    blk.push_back(h.num_rows);
+    if (vd.empty()) vd.push_back(0.0);
+    return true;
 }
 static bool xell_on()
 {
@@ -847,12 +888,14 @@ int devcsr_upload(DevCSR &d, const SSS_MAT &h, int split, int enc, const int *se
         // 3.5 entries per row on average, 8 slots -- measured 258 -> 289 us with the column ELL)
         int W = xell_width(Lmax.load());
         if ((long long)d.nnz * 2 < (long long)W * d.n) W = 0;
+        // 40-slot rows only where no range relaxation reads them (two-stage levels' matrices and split
+        // copies): the relaxation kernels spill at that width
+        if (W == 40 && !(enc & kEncMergedOnly)) W = 0;
         std::vector<int> xb;
         HostBuf<unsigned> codes;
         std::vector<int4> pd;
         std::vector<double> vd;
-        if (W > 0) build_rows_blocks(d.n, xb, split);
-        if (W > 0 && build_xell(h, xb, W, xshift, codes, pd, vd)) {
+        if (W > 0 && build_xell(h, split, W, xshift, xb, codes, pd, vd)) {
             dev_free(d.blk);
             dev_free(d.bk);
             d.blk = nullptr;

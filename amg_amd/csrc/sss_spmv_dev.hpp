@@ -142,9 +142,9 @@ __device__ __forceinline__ int ell_row(const unsigned char *__restrict__ ell, in
 }
 // ---- column ELL: one thread per row, explicit columns ------------------------------------------
 // Row r's W codes  value index << S | column  (0xFFFFFFFF pads) at xell[r * W], S = DevDict::xshift
-// (the column bits of the matrix, >= 25), into the block's value dictionary (<= 2^(32 - S), at most
-// 128 values) in LDS.
-constexpr int kXellValues = 128;
+// (the column bits of the matrix, >= 23), into the block's value dictionary (<= 2^(32 - S), at most
+// 512 values) in LDS.
+constexpr int kXellValues = 512;
 struct XellSmem {
     double vd[kXellValues];
     double red[kBlock / 64];
@@ -152,7 +152,7 @@ struct XellSmem {
 __device__ __forceinline__ void xell_load_dict_nosync(const DevDict &dt, int bid, XellSmem &es)
 {
     const int4 p = dt.pd[bid];
-    if ((int)threadIdx.x < p.w) es.vd[threadIdx.x] = dt.vd[p.z + threadIdx.x];
+    for (int t = threadIdx.x; t < p.w; t += kBlock) es.vd[t] = dt.vd[p.z + t];
 }
 template <int W>
 __device__ __forceinline__ void xell_codes(const unsigned *__restrict__ xell, int r, unsigned (&w)[W])
