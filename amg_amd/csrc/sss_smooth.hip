@@ -534,7 +534,8 @@ __device__ __forceinline__ void relax_range_ell(int blo, const int2 *__restrict_
             double p[W];
             int dsl;
             double dv;
-            const int len = ell_decode<W>(w[j], rj, es[j], [&](int c) -> double { return xs(c); }, p, dsl, dv);
+            // the pass's own x_r only in MODE 3 (the residual of the row with x unchanged)
+            const int len = ell_decode<W, MODE == 3>(w[j], rj, es[j], [&](int c) -> double { return xs(c); }, p, dsl, dv);
             const double acc = dsl < 0 ? ell_sub(br[j], p, 0, len) : ell_sub(ell_sub(br[j], p, 0, dsl), p, dsl + 1, len);
             const double d = deff ? dr[j] : dv;
             if constexpr (MODE == 2) {
@@ -599,7 +600,7 @@ __device__ __forceinline__ void relax_range_xell(int blo, const int2 *__restrict
     if (live) {
         double xv[W];
         int dsl;
-        const int len = xell_gather<W>(w, r, dt.xshift, [&](int c) -> double { return xs(c); }, xv, dsl);
+        const int len = xell_gather<W, MODE == 3>(w, r, dt.xshift, [&](int c) -> double { return xs(c); }, xv, dsl);
         const double acc = dsl < 0 ? xell_sub(br, w, xv, es, dt.xshift, 0, len)
                                    : xell_sub(xell_sub(br, w, xv, es, dt.xshift, 0, dsl), w, xv, es, dt.xshift, dsl + 1, len);
         const double dv = dsl < 0 ? 0.0 : es.vd[w[dsl] >> dt.xshift];

@@ -108,8 +108,10 @@ __device__ __forceinline__ void ell_codes(const unsigned char *__restrict__ ell,
     }
 }
 // Products of row r in stored (slot) order from its codes: p[s] = a_s * x(c_s) for s < len;
-// dslot = the row's (last) diagonal slot or -1, dval its value.
-template <int W, class Fetch>
+// dslot = the row's (last) diagonal slot or -1, dval its value.  DIAG = false: the caller never
+// reads p[dslot] (a relaxation pass subtracts every other product), so x_r is not fetched for it
+// and p[dslot] = 0 -- the pass then reads no x of its own rows.
+template <int W, bool DIAG = true, class Fetch>
 __device__ __forceinline__ int ell_decode(const unsigned (&w)[W / 4], int r, const EllSmem &es, Fetch fetch,
                                           double (&p)[W], int &dslot, double &dval)
 {
@@ -126,10 +128,10 @@ __device__ __forceinline__ int ell_decode(const unsigned (&w)[W / 4], int r, con
         a[s] = es.vd[byte >> 5];
     }
 #pragma unroll
-    for (int s = 0; s < W; ++s) p[s] = s < len ? a[s] * fetch(c[s]) : 0.0;
-#pragma unroll
     for (int s = 0; s < W; ++s)
         if (s < len && c[s] == r) dslot = s, dval = a[s];
+#pragma unroll
+    for (int s = 0; s < W; ++s) p[s] = (s < len && (DIAG || s != dslot)) ? a[s] * fetch(c[s]) : 0.0;
     return len;
 }
 template <int W, class Fetch>
@@ -166,10 +168,10 @@ __device__ __forceinline__ void xell_codes(const unsigned *__restrict__ xell, in
     }
 }
 // Row r's x values in slot order, xv[s] = x(c_s) for s < len (0.0 past it); dslot = the row's
-// (last) diagonal slot or -1.  The products a_s * xv[s] are formed where they are summed
+// (last) diagonal slot or -1 (DIAG = false: xv[dslot] = 0 without a fetch, as ell_decode).  The products a_s * xv[s] are formed where they are summed
 // (xell_prod: the value from the LDS dictionary), so only the codes and the gathered x values
 // stay in registers.
-template <int W, class Fetch>
+template <int W, bool DIAG = true, class Fetch>
 __device__ __forceinline__ int xell_gather(const unsigned (&w)[W], int r, int shift, Fetch fetch, double (&xv)[W],
                                            int &dslot)
 {
@@ -180,10 +182,10 @@ __device__ __forceinline__ int xell_gather(const unsigned (&w)[W], int r, int sh
     for (int s = 0; s < W; ++s)
         if (w[s] == 0xffffffffu && len == W) len = s;
 #pragma unroll
-    for (int s = 0; s < W; ++s) xv[s] = s < len ? fetch((int)(w[s] & mask)) : 0.0;
-#pragma unroll
     for (int s = 0; s < W; ++s)
         if (s < len && (int)(w[s] & mask) == r) dslot = s;
+#pragma unroll
+    for (int s = 0; s < W; ++s) xv[s] = (s < len && (DIAG || s != dslot)) ? fetch((int)(w[s] & mask)) : 0.0;
     return len;
 }
 template <int W>
