@@ -525,7 +525,9 @@ static sss_hip_dist *dist_create_impl(sss_hip_dist *d, PartPlan &plan, const SSS
             if (l + 1 == d->nagg && !tinv.empty())
                 for (int &j : P.P.ci) j = tinv[j];
             SSS_MAT Pv = P.P.view(), Rv = P.R.view();
-            if (devcsr_upload(L.P, Pv, P.nF, transfer_encoding(d->opts)) ||
+            // (a C-rows-only prolongation keeps the tiles, as hb_level_pr)
+            const int tenc = transfer_encoding(d->opts);
+            if (devcsr_upload(L.P, Pv, P.nF, L.sm.f_overwritten ? (tenc & ~kEncXell) : tenc) ||
                 devcsr_upload(L.R, Rv, -1, transfer_encoding(d->opts)))
                 return "upload P/R";
             {   // which row blocks read ghosts (the blockings the uploads made, read back: the

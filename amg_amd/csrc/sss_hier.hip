@@ -437,7 +437,11 @@ static bool hb_level_pr(HierBuild &b, int l)
     auto &L = h->L[l];
     const bool rl = !L.perm.empty();
     const auto &pc = h->L[l + 1].perm;
+    // a prolongation applied to the C rows only (SmootherPlan::f_overwritten: one stored entry each)
+    // keeps the tiles -- the column ELL would read a padded row of codes per entry (7-pt level 0,
+    // 258 -> 289 us per V-cycle)
     const int tenc = transfer_encoding(h->opts);
+    const int penc = L.sm.f_overwritten ? (tenc & ~kEncXell) : tenc;
     const double t0 = PhaseTimer::now();
     if (rl || !pc.empty()) {
         PhaseTimer pt("P/R");
@@ -448,10 +452,10 @@ static bool hb_level_pr(HierBuild &b, int l)
         pt.mark("relabel R");
         // P's rows follow the level's F|C relabeling: blocks split there too, so a
         // prolongation can be limited to the C rows (SmootherPlan::f_overwritten)
-        if (devcsr_upload(L.P, P.view(C.P.num_rows, C.P.num_cols), rl ? b.nF[l] : -1, tenc) ||
+        if (devcsr_upload(L.P, P.view(C.P.num_rows, C.P.num_cols), rl ? b.nF[l] : -1, penc) ||
             devcsr_upload(L.R, R.view(C.R.num_rows, C.R.num_cols), -1, tenc))
             return hb_fail(b, "upload P/R");
-    } else if (devcsr_upload(L.P, C.P, -1, tenc) || devcsr_upload(L.R, C.R, -1, tenc)) {
+    } else if (devcsr_upload(L.P, C.P, -1, penc) || devcsr_upload(L.R, C.R, -1, tenc)) {
         return hb_fail(b, "upload P/R");
     }
     if (b.timing) fprintf(stderr, "[sss_hip] upload level %d: P/R %.2f s\n", l, PhaseTimer::now() - t0);

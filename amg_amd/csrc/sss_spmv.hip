@@ -884,10 +884,11 @@ int devcsr_upload(DevCSR &d, const SSS_MAT &h, int split, int enc, const int *se
             int cur = Lmax.load();
             while (L > cur && !Lmax.compare_exchange_weak(cur, L)) {}
         });
-        // rows padded to W: not where that more than doubles the codes (level-0 prolongation of 7-pt:
-        // 3.5 entries per row on average, 8 slots -- measured 258 -> 289 us with the column ELL)
+        // rows padded to W: not where that makes the codes larger than the CSR entries (4 W bytes
+        // per row against 12 per entry: at least W / 3 entries per row on average; 7-pt level-1
+        // prolongation, 3.2 entries in 8 slots: 362 -> 294 us per V-cycle)
         int W = xell_width(Lmax.load());
-        if ((long long)d.nnz * 2 < (long long)W * d.n) W = 0;
+        if ((long long)d.nnz * 3 < (long long)W * d.n) W = 0;
         // 40-slot rows only where no range relaxation reads them (two-stage levels' matrices and split
         // copies): the relaxation kernels spill at that width
         if (W == 40 && !(enc & kEncMergedOnly)) W = 0;
