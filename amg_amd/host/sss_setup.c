@@ -258,6 +258,7 @@ static int rs_split(const SSS_MAT *A, SSS_IMAT *S, SSS_IVEC *vertices)
     const double t0 = SSS_get_time();
     ncoarse = drop_weak(S);
     if (ncoarse < 0) return ncoarse;
+    const double tdrop = SSS_get_time();
     ST = SSS_imat_trans(S);
     const double t1 = SSS_get_time();
 
@@ -413,8 +414,8 @@ static int rs_split(const SSS_MAT *A, SSS_IMAT *S, SSS_IVEC *vertices)
     free(maybe);
 
     if (timing)
-        fprintf(stderr, "[setup]   RS split: drop+transpose %.3f s, lists %.3f s, first pass %.3f s, C1 %.3f s\n",
-                t1 - t0, t2 - t1, t3 - t2, SSS_get_time() - t3);
+        fprintf(stderr, "[setup]   RS split: drop %.3f s, transpose %.3f s, lists %.3f s, first pass %.3f s, C1 %.3f s\n",
+                tdrop - t0, t1 - tdrop, t2 - t1, t3 - t2, SSS_get_time() - t3);
     SSS_imat_destroy(&ST);
     for (int m = 0; m < B.cap; ++m) free(B.b[m].e);
     free(B.b);

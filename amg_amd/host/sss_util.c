@@ -17,6 +17,8 @@
 #include <strings.h>
 #include <sys/time.h>
 
+#include <omp.h>
+
 double SSS_get_time(void)
 {
     struct timeval now;
@@ -369,10 +371,84 @@ static void transpose_pattern_par(int nrows, int ncols, int nnz, const int *ia, 
     free(fill);
 }
 
+/* The same transpose without atomics or sorts, for matrices whose rows of one contiguous chunk
+ * touch a narrow column window (banded and grid-ordered operators, every AMG level of the stencil
+ * workloads): each thread counts its row chunk's entries per column of its own window, the counts
+ * of the chunks become per-chunk offsets inside each output row (chunk order = source-row order),
+ * and each thread then scatters its rows in stored order -- the sequential fill's order exactly.
+ * Returns 0 (nothing written) when the windows together exceed 4 * ncols ints. */
+static int transpose_pattern_chunked(int nrows, int ncols, int nnz, const int *ia, const int *ja,
+                                     const void *val, size_t vsize, int *tia, int *tja, void *tval)
+{
+    const int T = omp_get_max_threads() < 64 ? omp_get_max_threads() : 64;
+    int r0[65], lo[64], hi[64];
+    int *cnt[64];
+    r0[0] = 0;
+    for (int t = 1; t < T; ++t) {   /* row chunks of about nnz / T entries */
+        const long long want = (long long)nnz * t / T;
+        int a = r0[t - 1], b = nrows;
+        while (a < b) {
+            const int m = a + (b - a) / 2;
+            if (ia[m] < want) a = m + 1; else b = m;
+        }
+        r0[t] = a;
+    }
+    r0[T] = nrows;
+#pragma omp parallel for schedule(static, 1) num_threads(T)
+    for (int t = 0; t < T; ++t) {
+        int mn = ncols, mx = -1;
+        for (int k = ia[r0[t]]; k < ia[r0[t + 1]]; ++k) {
+            mn = ja[k] < mn ? ja[k] : mn;
+            mx = ja[k] > mx ? ja[k] : mx;
+        }
+        lo[t] = mn;
+        hi[t] = mx;
+    }
+    long long total = 0;
+    for (int t = 0; t < T; ++t) total += hi[t] >= lo[t] ? (long long)(hi[t] - lo[t] + 1) : 0;
+    if (total > 4LL * ncols + 4096) return 0;
+#pragma omp parallel for schedule(static, 1) num_threads(T)
+    for (int t = 0; t < T; ++t) {
+        cnt[t] = (int *)calloc(hi[t] >= lo[t] ? (size_t)(hi[t] - lo[t] + 1) : 1, sizeof(int));
+        int *c = cnt[t] - lo[t];
+        for (int k = ia[r0[t]]; k < ia[r0[t + 1]]; ++k) c[ja[k]]++;
+    }
+    /* per column: counts -> exclusive offsets of the chunks inside the output row, row length */
+    tia[0] = 0;
+#pragma omp parallel for schedule(static)
+    for (int col = 0; col < ncols; ++col) {
+        int run = 0;
+        for (int t = 0; t < T; ++t)
+            if (col >= lo[t] && col <= hi[t]) {
+                int *c = &cnt[t][col - lo[t]];
+                const int m = *c;
+                *c = run;
+                run += m;
+            }
+        tia[col + 1] = run;
+    }
+    for (int col = 0; col < ncols; ++col) tia[col + 1] += tia[col];
+#pragma omp parallel for schedule(static, 1) num_threads(T)
+    for (int t = 0; t < T; ++t) {
+        int *c = cnt[t] - lo[t];
+        for (int i = r0[t]; i < r0[t + 1]; ++i)
+            for (int k = ia[i]; k < ia[i + 1]; ++k) {
+                const int dst = tia[ja[k]] + c[ja[k]]++;
+                tja[dst] = i;
+                if (val) memcpy((char *)tval + (size_t)dst * vsize, (const char *)val + (size_t)k * vsize, vsize);
+            }
+        free(cnt[t]);
+    }
+    return 1;
+}
+
 static void transpose_pattern(int nrows, int ncols, int nnz, const int *ia, const int *ja,
                               const void *val, size_t vsize, int *tia, int *tja, void *tval)
 {
     if (nnz >= (1 << 20)) {
+        if (getenv("SSS_TRANSPOSE_ATOMIC") == NULL &&
+            transpose_pattern_chunked(nrows, ncols, nnz, ia, ja, val, vsize, tia, tja, tval))
+            return;
         transpose_pattern_par(nrows, ncols, nnz, ia, ja, val, vsize, tia, tja, tval);
         return;
     }

@@ -339,15 +339,30 @@ def test_outer_loop_vs_reference_solve(case, quiet):
 
 
 @needs_ref
-@pytest.mark.parametrize("gen", ["p7_64", "circuit"])
-def test_parallel_setup_paths_vs_reference(gen, quiet):
-    """Matrices above the parallel threshold (>= 2^20 entries): the OpenMP transpose
-    (transpose_pattern_par) and weak-coupling compaction give the reference's results exactly --
-    SSS_mat_trans of A and the RS C/F marks (SSS_amg_coarsen) against the compiled reference."""
+@pytest.mark.parametrize("transpose", ["chunked", "atomic"])
+@pytest.mark.parametrize("gen", ["p7_64", "circuit", "scrambled"])
+def test_parallel_setup_paths_vs_reference(gen, transpose, quiet, monkeypatch):
+    """Matrices above the parallel threshold (>= 2^20 entries): both OpenMP transposes
+    (transpose_pattern_chunked, and transpose_pattern_par under SSS_TRANSPOSE_ATOMIC) and the
+    weak-coupling compaction give the reference's results exactly -- SSS_mat_trans of A and the RS
+    C/F marks (SSS_amg_coarsen) against the compiled reference."""
     from amg_amd import workloads as W
+    if transpose == "atomic":
+        monkeypatch.setenv("SSS_TRANSPOSE_ATOMIC", "1")
+    else:
+        monkeypatch.delenv("SSS_TRANSPOSE_ATOMIC", raising=False)
     keep = None
     if gen == "p7_64":
         M = A.generate(7, 64)
+    elif gen == "scrambled":   # rows and columns randomly permuted: wide windows, atomic fallback
+        import scipy.sparse as sp
+        ia, ja, va = A.csr_arrays(A.generate(7, 64))
+        n = len(ia) - 1
+        perm = np.random.default_rng(3).permutation(n)
+        S = sp.csr_matrix((va, ja, ia), shape=(n, n))[perm][:, perm].tocsr()
+        S.sort_indices()
+        keep = A.NumpyCSR(S.indptr.astype(np.int32), S.indices.astype(np.int32), S.data.astype(np.float64))
+        M = keep.mat
     else:
         keep = W.circuit_csr(300000)
         M = keep.mat
