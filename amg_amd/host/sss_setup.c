@@ -244,6 +244,10 @@ static char *flag_unshared_rows(const SSS_IMAT *S, const int *mark, int *owner)
     return flag;
 }
 
+#ifndef PF_DEPTH
+#define PF_DEPTH 5
+#endif
+
 /* Classical Ruge-Stueben first pass + C1 fix-up.  Returns the C-point count (or <0). */
 static int rs_split(const SSS_MAT *A, SSS_IMAT *S, SSS_IVEC *vertices)
 {
@@ -313,13 +317,25 @@ static int rs_split(const SSS_MAT *A, SSS_IMAT *S, SSS_IVEC *vertices)
          * record / row accesses per pick, spread over three grid planes): request them all up
          * front -- the records of c's neighbours, their S rows, and the records of the S rows of
          * the neighbours that are about to become F. */
-        {   /* and the rows of the next candidates in the top bucket (the likely next picks) */
+        {   /* and, pipelined, the neighbourhoods of the next candidates in the top bucket (the
+             * likely next picks): row pointers PF_DEPTH picks ahead, their rows two ahead, the
+             * records of their neighbours one ahead -- each stage reads only what an earlier pick
+             * has already requested */
             const bucket_fifo *tq = &B.b[B.top];
-            for (size_t t = tq->head + 1; t < tq->tail && t < tq->head + 3; ++t) {
+            const size_t end = tq->tail < tq->head + 1 + PF_DEPTH ? tq->tail : tq->head + 1 + PF_DEPTH;
+            for (size_t t = tq->head + 1; t < end; ++t) {
                 const int nx = tq->e[t].pt;
-                __builtin_prefetch(&ST.row_ptr[nx]);
-                __builtin_prefetch(ST.col_idx + ST.row_ptr[nx]);
-                __builtin_prefetch(S->col_idx + S->row_ptr[nx]);
+                const size_t d = t - tq->head;
+                if (d >= 3) {
+                    __builtin_prefetch(&ST.row_ptr[nx]);
+                    __builtin_prefetch(&S->row_ptr[nx]);
+                } else if (d == 2) {
+                    __builtin_prefetch(ST.col_idx + ST.row_ptr[nx]);
+                    __builtin_prefetch(S->col_idx + S->row_ptr[nx]);
+                } else {
+                    for (int q = ST.row_ptr[nx]; q < ST.row_ptr[nx + 1]; ++q) __builtin_prefetch(&P[ST.col_idx[q]], 1);
+                    for (int q = S->row_ptr[nx]; q < S->row_ptr[nx + 1]; ++q) __builtin_prefetch(&P[S->col_idx[q]], 1);
+                }
             }
         }
         for (int q = ST.row_ptr[c]; q < ST.row_ptr[c + 1]; ++q) {
