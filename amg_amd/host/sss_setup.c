@@ -271,13 +271,14 @@ static int rs_split(const SSS_MAT *A, SSS_IMAT *S, SSS_IVEC *vertices)
     rs_point *P = B.pts;
     buckets_grow(&B, 64);
 
-    for (int i = 0; i < n; ++i) P[i].lambda = ST.row_ptr[i + 1] - ST.row_ptr[i];
+#pragma omp parallel for schedule(static) reduction(+ : undecided) if (n > 65536)
     for (int i = 0; i < n; ++i) {
         if (S->row_ptr[i + 1] == S->row_ptr[i]) {
             P[i].mark = ISPT;
             P[i].lambda = 0;
         } else {
             P[i].mark = UNPT;
+            P[i].lambda = ST.row_ptr[i + 1] - ST.row_ptr[i];
             undecided++;
         }
     }
