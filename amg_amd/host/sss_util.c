@@ -376,7 +376,7 @@ static void transpose_pattern_par(int nrows, int ncols, int nnz, const int *ia, 
  * workloads): each thread counts its row chunk's entries per column of its own window, the counts
  * of the chunks become per-chunk offsets inside each output row (chunk order = source-row order),
  * and each thread then scatters its rows in stored order -- the sequential fill's order exactly.
- * Returns 0 (nothing written) when the windows together exceed 4 * ncols ints. */
+ * Returns 0 (nothing written) when the windows together exceed both 4 * ncols and 2^26 ints. */
 static int transpose_pattern_chunked(int nrows, int ncols, int nnz, const int *ia, const int *ja,
                                      const void *val, size_t vsize, int *tia, int *tja, void *tval)
 {
@@ -406,7 +406,7 @@ static int transpose_pattern_chunked(int nrows, int ncols, int nnz, const int *i
     }
     long long total = 0;
     for (int t = 0; t < T; ++t) total += hi[t] >= lo[t] ? (long long)(hi[t] - lo[t] + 1) : 0;
-    if (total > 4LL * ncols + 4096) return 0;
+    if (total > 4LL * ncols + 4096 && total > (1LL << 26)) return 0;
 #pragma omp parallel for schedule(static, 1) num_threads(T)
     for (int t = 0; t < T; ++t) {
         cnt[t] = (int *)calloc(hi[t] >= lo[t] ? (size_t)(hi[t] - lo[t] + 1) : 1, sizeof(int));

@@ -354,7 +354,7 @@ def test_parallel_setup_paths_vs_reference(gen, transpose, quiet, monkeypatch):
     keep = None
     if gen == "p7_64":
         M = A.generate(7, 64)
-    elif gen == "scrambled":   # rows and columns randomly permuted: wide windows, atomic fallback
+    elif gen == "scrambled":   # rows and columns randomly permuted: every chunk's window is wide
         import scipy.sparse as sp
         ia, ja, va = A.csr_arrays(A.generate(7, 64))
         n = len(ia) - 1
