@@ -614,11 +614,16 @@ class Comm:
             import torch
             import torch.distributed as dist
             uid = C.create_string_buffer(128)
+            ok = 1
             if rank == 0:
-                assert lib().sss_hip_rccl_unique_id(uid) == 0
-            t = torch.frombuffer(bytearray(uid.raw), dtype=torch.uint8).clone()
+                ok = int(lib().sss_hip_rccl_unique_id(uid) == 0)
+            # the id and rank 0's status together: a failed id fails every rank, none waits
+            t = torch.frombuffer(bytearray(uid.raw[:128] + bytes([ok])), dtype=torch.uint8).clone()
             dist.broadcast(t, 0)
-            uid = C.create_string_buffer(bytes(t.numpy().tobytes()), 128)
+            raw = bytes(t.numpy().tobytes())
+            if not raw[128]:
+                raise RuntimeError("communicator (rccl) creation failed: no unique id on rank 0")
+            uid = C.create_string_buffer(raw[:128], 128)
             self.c = lib().sss_hip_comm_rccl(nranks, rank, uid, device)
         else:
             self.transport = TorchHostTransport()

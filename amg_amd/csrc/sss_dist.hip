@@ -125,7 +125,7 @@ struct sss_hip_dist {
     hipStream_t cstream = nullptr;
     hipEvent_t ev_packed = nullptr, ev_halo = nullptr;
     int overlap = 1;   // 0 off, 1 on (RCCL), 2 also split the launches over the host transport (tests)
-    // hipGraph of the whole cycle (SSS_HIP_DIST_GRAPH=1, RCCL transport, device-side coarse solve):
+    // hipGraph of the whole cycle (default over RCCL with a device-side coarse solve; SSS_HIP_DIST_GRAPH=0 off):
     // kernels, halo packs, the grouped RCCL send/recv on the communication stream (joined back by
     // events), the coarse all-gather and the replicated tail, captured once and replayed
     int use_graph = 0;
@@ -490,6 +490,9 @@ static sss_hip_dist *dist_create_impl(sss_hip_dist *d, PartPlan &plan, const SSS
                  hipEventCreateWithFlags(&d->ev_halo, hipEventDisableTiming) != hipSuccess))
         err = "communication stream";
     if (const char *ov = getenv("SSS_HIP_OVERLAP")) d->overlap = atoi(ov);
+    // the cycle is captured into one hipGraph by default over RCCL (SSS_HIP_DIST_GRAPH=0: eager
+    // launches); the host transport steers every exchange from the CPU and cannot be captured
+    d->use_graph = !c->host;
     if (const char *gz = getenv("SSS_HIP_DIST_GRAPH")) d->use_graph = atoi(gz) != 0 && !c->host;
     if (!err) d->nagg = plan.nagg;
 

@@ -82,10 +82,13 @@ def build(stencil: int, n: int, ranks: int, prefix: Path, agg_rows: int = 0, sum
            "setup_s": t1 - t0, "partition_s": t2 - t1,
            "peak_rss_gb": resource.getrusage(resource.RUSAGE_SELF).ru_maxrss / 2**20}
     H.close()
+    man["rank_file_bytes"] = [Path(f"{prefix}.r{r}").stat().st_size for r in range(ranks)]
+    man["tail_file_bytes"] = Path(f"{prefix}.tail").stat().st_size
     if summary:
         phase[0] = "reading the partition files back"
+        t3 = time.perf_counter()
         man["ranks_detail"] = rank_summary(prefix, ranks)
-        man["tail_file_bytes"] = Path(f"{prefix}.tail").stat().st_size
+        man["readback_s"] = time.perf_counter() - t3
     stop.set()
     Path(str(prefix) + ".json").write_text(json.dumps(man))
     return man
@@ -98,8 +101,10 @@ def main():
     p.add_argument("--ranks", type=int, required=True)
     p.add_argument("--prefix", required=True)
     p.add_argument("--agg-rows", type=int, default=0)
+    p.add_argument("--no-readback", action="store_true",
+                   help="skip reading every rank file back for the per-rank halo summary (bench.py)")
     a = p.parse_args()
-    man = build(a.stencil, a.n, a.ranks, Path(a.prefix), a.agg_rows)
+    man = build(a.stencil, a.n, a.ranks, Path(a.prefix), a.agg_rows, summary=not a.no_readback)
     print(json.dumps({k: v for k, v in man.items() if k not in ("levels", "ranks_detail")}), flush=True)
 
 

@@ -47,16 +47,17 @@ def parse():
     p.add_argument("--steps", type=int, default=10)
     p.add_argument("--warmup", type=int, default=3)
     p.add_argument("--grid", "--n", dest="n", type=int, default=None,
-                   help="grid edge (default: the BASELINE.json config of the rank count -- N=1, 2: 400 "
-                        "(64M rows); N=4: 27-pt 256; N=8: 512)")
+                   help="grid edge (default 400: the metric's 64M-row problem at every rank count, so that "
+                        "--gpus 1/2/4/8 form one strong-scaling curve; BASELINE.json's other configs: "
+                        "--n 512 --gpus 8, --stencil 27 --n 256 --gpus 4)")
     p.add_argument("--probe-ranks", action="store_true",
                    help="print one line per rank (rank, world size) and exit before any GPU call (tests)")
     p.add_argument("--hier-cache", default=None,
                    help="binary hierarchy file (SSS_amg_save): loaded when present, else written after setup "
                         "(rank 0; the other ranks load it)")
     p.add_argument("--stencil", type=int, default=None, choices=[7, 27],
-                   help="7: 7-pt Poisson (the metric's workload); 27: the 27-pt anisotropic operator of "
-                        "BASELINE.json configs[4] (SURVEY.md 8(d)); default 27 at N=4, else 7")
+                   help="7: 7-pt Poisson (the metric's workload, the default); 27: the 27-pt anisotropic "
+                        "operator of BASELINE.json configs[4] (SURVEY.md 8(d))")
     p.add_argument("--workload", default="stencil", choices=["stencil", "circuit"],
                    help="stencil: the --stencil operator on an --n grid; circuit: the G3_circuit stand-in "
                         "(BASELINE.json configs[3], amg_amd/workloads.py; --n = rows, default 1,585,478; 1 GPU)")
@@ -87,6 +88,13 @@ def parse():
                    help="0: stored CSR order everywhere (bitwise kernels); 1: tree-summed long rows "
                         "(default: 1 in throughput mode, 0 in parity mode)")
     p.add_argument("--sorted-tiles", type=int, default=None, help="column-sorted tile staging (default 1)")
+    p.add_argument("--keep-parts", action="store_true",
+                   help="N > 1: keep a partition set this run wrote (default: removed at the end unless "
+                        "SSS_PART_DIR is set; a set found already present is always kept)")
+    p.add_argument("--single-ref", default=None,
+                   help="N > 1: a 1-GPU bench record (JSON) of the same workload for parallel_efficiency "
+                        "(default: the record the last N = 1 run on this host left in the temp directory, "
+                        "else the newest committed profiles/r*_bench400_throughput.json of that workload)")
     argv = None
     if "WORLD_SIZE" in os.environ and "SSS_BENCH_ARGV" in os.environ:   # ranks spawned by spawn_ranks()
         argv = json.loads(os.environ["SSS_BENCH_ARGV"])
@@ -303,21 +311,46 @@ def vcycle_bytes(levels: list, sweeps: int) -> int:
     return int(tot)
 
 
+def select_workload(args, world: int):
+    """(stencil, n) of this run: the metric's 7-pt 400^3 problem at every rank count unless
+    --stencil / --n say otherwise, so that the driver's --gpus 1, 2, 4, 8 runs measure one problem
+    (a strong-scaling curve).  --workload circuit: the G3_circuit stand-in's row count."""
+    stencil = args.stencil if args.stencil is not None else 7
+    if args.n is not None:
+        return stencil, args.n
+    if args.workload == "circuit":
+        from amg_amd.workloads import G3_CIRCUIT_ROWS
+        return stencil, G3_CIRCUIT_ROWS
+    return stencil, 256 if stencil == 27 else 400
+
+
+def transport_policy(world: int, devices: int, rccl_ok_everywhere: bool) -> str:
+    """The halo transport of a multi-rank run: "rccl" when every rank created its communicator;
+    "host" (gloo) only when the ranks share GPUs (fewer visible devices than ranks: RCCL refuses
+    two ranks on one device, e.g. the one-GPU test box); "fail" when each rank owns a GPU and RCCL
+    still failed somewhere -- that is a broken node, not a configuration to measure around."""
+    if rccl_ok_everywhere:
+        return "rccl"
+    return "host" if devices < world else "fail"
+
+
 def part_prefix(stencil: int, n: int, world: int) -> Path:
     """Where the partition set of a multi-rank run lives (reused by later runs of the same
-    configuration): SSS_PART_DIR if set, else the first of /tmp, /dev/shm, the home directory and the
-    repository's parent with room for it -- the set takes ~490 B per row for the 7-point operator
-    and ~870 B per row for the 27-point one (profiles/r03_partition_*.json: 65 GB at 512^3)."""
+    configuration): SSS_PART_DIR if set; else an existing set of this configuration in any of /tmp,
+    /dev/shm, the home directory and the repository's parent; else the first of them with room for
+    it -- the set takes ~490 B per row for the 7-point operator and ~870 B per row for the 27-point
+    one (profiles/r03_partition_*.json: 65 GB at 512^3; r04_partition_p7_400_*.json at 400^3)."""
     import shutil
     name = f"sss_parts_{stencil}pt_{n}_{world}r"
     if os.environ.get("SSS_PART_DIR"):
         return Path(os.environ["SSS_PART_DIR"]) / name / "part"
     need = 1.25 * (870 if stencil == 27 else 490) * float(n) ** 3
     cands = [Path("/tmp"), Path("/dev/shm"), Path.home(), ROOT.parent]
+    for c in cands:   # an existing set of this configuration anywhere wins over free space
+        if (c / name / "part.json").exists():
+            return c / name / "part"
     best, room = None, -1.0
     for c in cands:
-        if (c / name / "part.json").exists():   # an existing set of this configuration
-            return c / name / "part"
         try:
             free = float(shutil.disk_usage(c).free)
         except OSError:
@@ -331,10 +364,62 @@ def part_prefix(stencil: int, n: int, world: int) -> Path:
     return (best or Path("/tmp")) / name / "part"
 
 
+def single_ref_path(workload: str) -> Path:
+    import tempfile
+    return Path(tempfile.gettempdir()) / f"sss_bench_single_{workload.replace('^', '')}.json"
+
+
+def single_gpu_reference(explicit, workload: str):
+    """The 1-GPU rate of the same workload for parallel_efficiency = value / (N x rate): --single-ref,
+    else the record the last N = 1 run on this host left (single_ref_path), else the newest
+    committed profiles/r*_bench*_throughput.json whose workload matches.  None if there is none."""
+    cands = [Path(explicit)] if explicit else []
+    cands.append(single_ref_path(workload))
+    cands += sorted((ROOT / "profiles").glob("r*_bench*_throughput.json"), reverse=True)
+    for c in cands:
+        try:
+            r = json.loads(c.read_text())
+        except (OSError, ValueError):
+            continue
+        if r.get("config", {}).get("workload") == workload and r.get("n_gpus", 1) == 1 and r.get("value"):
+            return {"value": r["value"], "ms_per_step": r.get("ms_per_step"), "source": str(c)}
+    return None
+
+
 def heartbeat(stop: threading.Event, t0: float):
     """A progress line on stderr every 60 s through the long host phases (setup, upload)."""
     while not stop.wait(60.0):
         print(f"[bench] working ({time.perf_counter() - t0:.0f} s)", file=sys.stderr, flush=True)
+
+
+def make_comm(A, D):
+    """N > 1: this rank's communicator, created before any setup so that a broken node fails in
+    seconds.  RCCL (xGMI) when every rank created it; the host transport only when the ranks share
+    GPUs (transport_policy); otherwise every rank exits non-zero."""
+    ndev = int(os.environ.get("SSS_BENCH_FAKE_DEVICES", "0")) or A.device_count()   # (tests: fake a node)
+    dev = D.local_rank % max(ndev, 1)
+    comm, ok, why = None, 1, ""
+    try:
+        comm = A.Comm(D.world, D.rank, "rccl", device=dev)
+    except Exception as e:  # noqa: BLE001
+        why = str(e)
+        print(f"[bench] rank {D.rank}: RCCL communicator failed on device {dev} ({e})", file=sys.stderr, flush=True)
+        ok = 0
+    policy = transport_policy(D.world, ndev, D.min(ok) >= 1)   # every rank decides the same
+    if policy == "fail":
+        if comm is not None:
+            comm.close()
+        D.close()
+        raise SystemExit(f"bench.py: rank {D.rank}: RCCL communicator creation failed with {ndev} GPUs for "
+                         f"{D.world} ranks{' (' + why + ')' if why else ' (on another rank)'}; no host-transport "
+                         f"fallback when every rank owns a device")
+    if policy == "host":   # ranks share GPUs (e.g. several ranks on the one-GPU test box)
+        if comm is not None:
+            comm.close()
+        print(f"[bench] rank {D.rank}: {D.world} ranks on {ndev} GPU(s): using the host transport (gloo)",
+              file=sys.stderr, flush=True)
+        return A.Comm(D.world, D.rank, "host"), dev, "host-gloo"
+    return comm, dev, "rccl"
 
 
 def main():
@@ -350,26 +435,25 @@ def main():
     D = Dist()
     if args.gpus is not None and args.gpus != D.world:
         raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={D.world}")
-    if args.probe_ranks:
-        # one write() per line: the ranks share the launcher's stdout pipe
-        os.write(json_fd, (json.dumps({"rank": D.rank, "world": D.world, "local_rank": D.local_rank}) + "\n").encode())
-        D.close()
-        return
-    # the BASELINE.json config of this rank count (configs[2]: 512^3 on 8 GPUs; configs[4]: 27-pt
-    # 256^3 on 4 GPUs; the metric's 64M-row 400^3 otherwise)
     circuit = args.workload == "circuit"
     if circuit and D.world > 1:
         raise SystemExit("bench.py: --workload circuit is a single-GPU configuration (BASELINE.json configs[3])")
-    if args.stencil is None:
-        args.stencil = 27 if D.world == 4 and args.n is None else 7
-    if args.n is None:
-        from amg_amd.workloads import G3_CIRCUIT_ROWS
-        args.n = G3_CIRCUIT_ROWS if circuit else 256 if args.stencil == 27 else {8: 512}.get(D.world, 400)
+    # one problem at every rank count (the metric's 7-pt 400^3 unless --stencil / --n): the driver's
+    # --gpus 1, 2, 4, 8 runs form one strong-scaling curve
+    args.stencil, args.n = select_workload(args, D.world)
+    workload = f"g3_circuit_standin_{args.n}" if circuit else f"poisson{args.stencil}_{args.n}^3"
+    if args.probe_ranks:
+        # one write() per line: the ranks share the launcher's stdout pipe
+        os.write(json_fd, (json.dumps({"rank": D.rank, "world": D.world, "local_rank": D.local_rank,
+                                       "workload": workload}) + "\n").encode())
+        D.close()
+        return
     if args.parity_converge is None:
         args.parity_converge = 1 if D.world == 1 else 0
     hb_stop = threading.Event()
     threading.Thread(target=heartbeat, args=(hb_stop, time.perf_counter()), daemon=True).start()
     import amg_amd as A
+    comm, dev, transport = make_comm(A, D) if D.world > 1 else (None, 0, None)
 
     n = args.n
     smoother, coarse = ("hybrid", "direct") if args.mode == "throughput" else ("exact", "krylov")
@@ -384,6 +468,7 @@ def main():
 
     t0 = time.perf_counter()
     hier_src = None
+    made_parts = False
     H = None
     DH = None   # set here when the mirror is built while the setup runs (sss_hip_setup_create)
     dh_kw = dict(smoother=smoother, coarse=coarse, device=-1, inner=args.inner, inner_from=args.inner_from,
@@ -430,9 +515,11 @@ def main():
         if D.rank == 0 and not manifest.exists():
             import subprocess
             subprocess.run([sys.executable, "-m", "amg_amd.partition", "--stencil", str(args.stencil), "--n", str(n),
-                            "--ranks", str(D.world), "--prefix", str(prefix)], check=True, cwd=str(ROOT),
-                           stdout=sys.stderr)
+                            "--ranks", str(D.world), "--prefix", str(prefix), "--no-readback"], check=True,
+                           cwd=str(ROOT), stdout=sys.stderr)
             hier_src = f"partition set written to {prefix.parent}"
+            # a set this run wrote is removed at the end (tens of GB of scratch per rank count)
+            made_parts = not args.keep_parts and not os.environ.get("SSS_PART_DIR")
         D.barrier()
         man = json.loads(manifest.read_text())
         table, pars = man["levels"], man["pars"]
@@ -447,31 +534,20 @@ def main():
     t0 = time.perf_counter()
     inner = args.inner if args.inner is not None else int(os.environ.get("SSS_HIP_INNER", "1"))
     inner_from = args.inner_from if args.inner_from is not None else int(os.environ.get("SSS_HIP_INNER_FROM", "2"))
-    transport = None
     if D.world == 1:
         if DH is None:
             DH = A.DeviceHierarchy(H, **dh_kw)
         eng = Single(DH, N)
     else:
-        # row-partitioned solve over RCCL (xGMI); every rank holds the same host hierarchy
-        dev = D.local_rank % max(A.device_count(), 1)
-        comm, ok = None, 1
-        try:
-            comm = A.Comm(D.world, D.rank, "rccl", device=dev)
-        except Exception as e:  # noqa: BLE001
-            print(f"[bench] rank {D.rank}: RCCL communicator failed ({e})", file=sys.stderr, flush=True)
-            ok = 0
-        if D.min(ok) < 1:   # every rank falls back together (e.g. two ranks sharing one GPU)
-            if comm is not None:
-                comm.close()
-            print(f"[bench] rank {D.rank}: using the host transport (gloo)", file=sys.stderr, flush=True)
-            comm = A.Comm(D.world, D.rank, "host")
-            transport = "host-gloo"
-        else:
-            transport = "rccl"
+        # row-partitioned solve over RCCL (xGMI): each rank reads only its own partition file
         DD = A.DistHierarchy(None, comm, smoother=smoother, coarse=coarse, device=dev, inner=args.inner,
                              inner_from=args.inner_from, sum_order=sum_order, sorted_tiles=sorted_tiles, parts=prefix)
         eng = Distributed(DD)
+        D.barrier()   # every rank has read its file: the set is no longer needed
+        if made_parts:
+            import shutil
+            shutil.rmtree(prefix.parent, ignore_errors=True)
+            print(f"[bench] removed the partition set {prefix.parent}", file=sys.stderr, flush=True)
     upload_s = time.perf_counter() - t0
     hbm_gb = D.max(A.hbm_used_bytes() / 1e9)   # the mirror resident in HBM (max over ranks)
     overlapped = D.world == 1 and getattr(DH, "times", None) is not None
@@ -486,6 +562,9 @@ def main():
         DH.cycle()
         DH.residual_norm()
     DH.sync()
+    # N > 1: the distributed cycle replays one captured hipGraph over RCCL unless the capture failed
+    # (then eager launches; SSS_HIP_DIST_GRAPH=0 forces them)
+    cycle_graph = DH.DH.level_flags(0)["cycle_graph"] if D.world > 1 else None
     D.barrier()
     t0 = time.perf_counter()
     absres = 0.0
@@ -739,11 +818,24 @@ def main():
         "cpu_baseline": cpu_baseline,
         "cpu_baseline_same_mode": cpu_mt,
     }
+    if D.world == 1 and not circuit:
+        # left for the N > 1 runs of the same workload on this host (parallel_efficiency)
+        try:
+            single_ref_path(workload).write_text(json.dumps({k: rec[k] for k in ("value", "ms_per_step", "config")}))
+        except OSError:
+            pass
+    else:
+        rec["config"]["cycle_graph"] = cycle_graph
+        ref = single_gpu_reference(args.single_ref, workload)
+        rec["single_gpu_reference"] = ref
+        rec["parallel_efficiency"] = value / (D.world * ref["value"]) if ref else None
     if cpu_baseline:
         rec["speedup_vs_cpu"] = value / cpu_baseline["value"]
     if cpu_mt:
         rec["speedup_vs_cpu_same_mode"] = value / cpu_mt["value"]
     DH.close()
+    if comm is not None:
+        comm.close()
     hb_stop.set()
     if D.rank == 0:
         sys.stdout.flush()

@@ -218,3 +218,55 @@ def test_bench_gpus_mismatch_fails_loudly():
     r = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--gpus", "2", "--probe-ranks"], capture_output=True,
                        text=True, env=env, timeout=120)
     assert r.returncode != 0 and "WORLD_SIZE" in r.stderr
+
+
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_bench_gpus_n_selects_the_metric_problem(world):
+    """The driver's `bench.py --gpus N` runs for N = 1, 2, 4, 8 measure ONE problem -- the metric's
+    7-pt 400^3 -- so that they form a strong-scaling curve (BASELINE.json's 512^3/8 and 27-pt
+    256^3/4 configs stay behind --n / --stencil).  Checked on the ranks the bench launches."""
+    import json
+    import subprocess
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    r = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--gpus", str(world), "--probe-ranks"],
+                       capture_output=True, text=True, env=env, timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    recs = [json.loads(l) for l in r.stdout.splitlines() if l.startswith('{"rank"')]
+    assert sorted(x["rank"] for x in recs) == list(range(world))
+    assert {x["workload"] for x in recs} == {"poisson7_400^3"}
+
+
+def test_bench_workload_flags():
+    import argparse
+    import bench
+    ns = lambda **kw: argparse.Namespace(**{"stencil": None, "n": None, "workload": "stencil", **kw})  # noqa: E731
+    for world in (1, 2, 4, 8):
+        assert bench.select_workload(ns(), world) == (7, 400)
+    assert bench.select_workload(ns(n=512), 8) == (7, 512)
+    assert bench.select_workload(ns(stencil=27), 4) == (27, 256)
+    assert bench.select_workload(ns(stencil=27, n=64), 4) == (27, 64)
+
+
+def test_bench_transport_policy_fails_loudly_on_distinct_gpus():
+    """RCCL failing when every rank owns a GPU is a fault, not a reason to fall back to the host
+    transport; the fallback is only for ranks sharing GPUs (the one-GPU test box)."""
+    import bench
+    assert bench.transport_policy(8, 8, True) == "rccl"
+    assert bench.transport_policy(8, 8, False) == "fail"
+    assert bench.transport_policy(2, 4, False) == "fail"
+    assert bench.transport_policy(2, 1, False) == "host"
+    assert bench.transport_policy(8, 1, True) == "rccl"
+
+
+def test_bench_rccl_failure_exits_nonzero(tmp_path):
+    """End to end on CPU: two ranks, RCCL creation fails on both (no GPU here) and the bench is told
+    each rank owns a device (SSS_BENCH_FAKE_DEVICES) -- it must exit non-zero naming RCCL, before
+    building anything, instead of printing a host-transport record."""
+    import subprocess
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env.update(SSS_BENCH_FAKE_DEVICES="2", SSS_PART_DIR=str(tmp_path))
+    r = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--gpus", "2", "--n", "12", "--no-cpu-baseline",
+                        "--steps", "1", "--warmup", "0"], capture_output=True, text=True, env=env, timeout=600)
+    assert r.returncode != 0
+    assert "RCCL communicator creation failed" in r.stderr, r.stderr[-3000:]
+    assert '"metric"' not in r.stdout

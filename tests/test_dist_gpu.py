@@ -63,8 +63,10 @@ def _worker(rank, world, port, kind, n, smoother, inner_from, agg_rows, cycles, 
         for _ in range(cycles):
             D.cycle()
             rel.append(D.residual_norm() / np.sqrt(N))
-        if os.environ.get("SSS_HIP_DIST_GRAPH") == "1" and transport == "rccl":
+        if os.environ.get("SSS_HIP_DIST_GRAPH", "1") != "0" and transport == "rccl":   # coarse "direct": on the device
             assert D.level_flags(0)["cycle_graph"], "the distributed cycle was not captured"
+        if os.environ.get("SSS_HIP_DIST_GRAPH") == "0" or transport != "rccl":
+            assert not D.level_flags(0)["cycle_graph"]
         x_own = D.download("x")
         parts = [None] * world
         dist.all_gather_object(parts, (D.lo, x_own))
@@ -108,19 +110,21 @@ def test_dist_equals_single_gpu(kind, n, smoother, inner_from, agg):
 
 
 @pytest.mark.parametrize("smoother", ["hybrid", "jacobi"])
-def test_dist_rccl_single_rank(smoother):
-    """The RCCL transport on the one GPU a test box has: communicator from a broadcast unique id,
-    the grouped send/recv of the coarse all-gather (no peers) and the ncclAllReduce of ||r||^2 --
-    bitwise the single-GPU engine.  (Two ranks cannot share a GPU under RCCL; the halo send/recv
-    pattern itself is covered by the host-transport tests above, which run the same plan.)"""
+def test_dist_rccl_single_rank(smoother, monkeypatch):
+    """The RCCL transport on the one GPU a test box has, eager launches (SSS_HIP_DIST_GRAPH=0):
+    communicator from a broadcast unique id, the grouped send/recv of the coarse all-gather (no
+    peers) and the ncclAllReduce of ||r||^2 -- bitwise the single-GPU engine.  (Two ranks cannot
+    share a GPU under RCCL; the halo send/recv pattern itself is covered by the host-transport
+    tests above, which run the same plan.)"""
+    monkeypatch.setenv("SSS_HIP_DIST_GRAPH", "0")
     _run(1, "rccl", 7, 24, smoother, 2, 100)
 
 
 @pytest.mark.parametrize("smoother", ["hybrid", "jacobi"])
 def test_dist_rccl_graph(smoother, monkeypatch):
-    """The distributed cycle captured into one hipGraph (SSS_HIP_DIST_GRAPH=1) over RCCL on the one
-    GPU: the captured and replayed cycles are bitwise the single-GPU engine's."""
-    monkeypatch.setenv("SSS_HIP_DIST_GRAPH", "1")
+    """The default over RCCL: the distributed cycle captured into one hipGraph and replayed --
+    bitwise the single-GPU engine's cycles, and reported as captured."""
+    monkeypatch.delenv("SSS_HIP_DIST_GRAPH", raising=False)
     _run(1, "rccl", 7, 24, smoother, 2, 100)
 
 

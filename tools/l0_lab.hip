@@ -1,0 +1,276 @@
+// l0_lab.hip — level-0 kernels of the 7-pt 400^3 hierarchy, rows per thread (lab only, not product code).
+//
+// The level-0 operator as the engine stores it: rows relabeled F-first / C-second (red-black: F =
+// odd points, C = even points), each row's stored-order entries as one-byte codes (value index << 5
+// | offset index, 0xFF pads) into per-256-row-block dictionaries of column offsets (col - row) and
+// values (sss_spmv_dev.hpp ell_decode).  Measures, for R = 1, 2, 4 consecutive rows per thread:
+//   F pass : x_r = (b_r - sum_{s != diag} a_s x_{c_s}) / a_rr over the F rows (relax_range MODE 0)
+//   resid  : y_r = b_r - sum_s a_s x_{c_s} over every row (spmv_adaptive RESID)
+// R >= 2 gathers the x of two neighbouring rows with one 16-byte load where their columns are
+// adjacent (c_{r+1,s} = c_{r,s} + 1: the same stencil offset); every row's sum keeps its stored order,
+// so every variant is bitwise the R = 1 kernel (checked).
+//   hipcc -O3 --offload-arch=gfx950 -ffp-contract=off tools/l0_lab.hip -o tools/l0_lab
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <vector>
+
+#define CK(x)                                                                                   \
+    do {                                                                                        \
+        hipError_t e = (x);                                                                     \
+        if (e != hipSuccess) { fprintf(stderr, "%s: %s\n", #x, hipGetErrorString(e)); exit(1); } \
+    } while (0)
+
+constexpr int B = 256;   // rows per dictionary block
+
+struct __attribute__((aligned(8))) D2 {
+    double a, b;
+};
+
+template <int R>
+struct Codes {
+    unsigned w[2 * R];
+};
+template <int R>
+__device__ __forceinline__ void load_codes(const unsigned char *ell, int r0, Codes<R> &c)
+{
+    if constexpr (R == 1) {
+        const uint2 q = *reinterpret_cast<const uint2 *>(ell + (size_t)r0 * 8);
+        c.w[0] = q.x, c.w[1] = q.y;
+    } else {
+#pragma unroll
+        for (int h = 0; h < R / 2; ++h) {
+            const uint4 q = *reinterpret_cast<const uint4 *>(ell + (size_t)r0 * 8 + 16 * h);
+            c.w[4 * h] = q.x, c.w[4 * h + 1] = q.y, c.w[4 * h + 2] = q.z, c.w[4 * h + 3] = q.w;
+        }
+    }
+}
+
+// MODE 0: F pass (in place, diagonal product skipped, no fetch of x_r); MODE 1: residual.
+// PAIR: pair loads for R >= 2.  Grid: one workgroup per R blocks of rows [lo, hi).
+template <int MODE, int R, bool PAIR>
+__global__ __launch_bounds__(B) void kpass(const unsigned char *__restrict__ ell, const int *__restrict__ ddf,
+                                           const double *__restrict__ vdf, const double *__restrict__ b,
+                                           double *x, double *__restrict__ y, int lo, int hi)
+{
+    __shared__ int dd[R][32];
+    __shared__ double vd[R][8];
+    const int blk0 = lo / B + blockIdx.x * R;
+    if (threadIdx.x < 32 * R) {
+        const int j = threadIdx.x >> 5, t = threadIdx.x & 31;
+        dd[j][t] = ddf[(size_t)(blk0 + j) * 32 + t];
+        if (t < 8) vd[j][t] = vdf[(size_t)(blk0 + j) * 8 + t];
+    }
+    const int r0 = lo + blockIdx.x * R * B + R * threadIdx.x;
+    const bool live = r0 < hi;   // hi a multiple of R (checked on the host)
+    Codes<R> cw;
+    double br[R];
+#pragma unroll
+    for (int i = 0; i < 2 * R; ++i) cw.w[i] = 0xffffffffu;
+#pragma unroll
+    for (int i = 0; i < R; ++i) br[i] = 0.0;
+    if (live) {
+        load_codes<R>(ell, r0, cw);
+        if constexpr (R == 1) br[0] = b[r0];
+        else {
+#pragma unroll
+            for (int h = 0; h < R / 2; ++h) {
+                const double2 q = *reinterpret_cast<const double2 *>(b + r0 + 2 * h);
+                br[2 * h] = q.x, br[2 * h + 1] = q.y;
+            }
+        }
+    }
+    __syncthreads();
+    if (!live) return;
+    const int j = (R * threadIdx.x) / B;
+    int c[R][8], len[R], ds[R];
+    double a[R][8], dv[R];
+#pragma unroll
+    for (int i = 0; i < R; ++i) {
+        len[i] = 8;
+        ds[i] = -1;
+        dv[i] = 0.0;
+#pragma unroll
+        for (int s = 0; s < 8; ++s) {
+            const unsigned byte = (cw.w[2 * i + (s >> 2)] >> (8 * (s & 3))) & 0xffu;
+            if (byte == 0xffu && len[i] == 8) len[i] = s;
+            c[i][s] = r0 + i + dd[j][byte & 31u];
+            a[i][s] = vd[j][byte >> 5];
+        }
+#pragma unroll
+        for (int s = 0; s < 8; ++s)
+            if (s < len[i] && c[i][s] == r0 + i) ds[i] = s, dv[i] = a[i][s];
+    }
+    double xv[R][8];
+#pragma unroll
+    for (int s = 0; s < 8; ++s) {
+        if constexpr (PAIR && R >= 2) {
+#pragma unroll
+            for (int i = 0; i < R; i += 2) {
+                const bool n0 = s < len[i] && (MODE == 1 || s != ds[i]);
+                const bool n1 = s < len[i + 1] && (MODE == 1 || s != ds[i + 1]);
+                if (n0 && n1 && c[i + 1][s] == c[i][s] + 1) {
+                    const D2 q = *reinterpret_cast<const D2 *>(x + c[i][s]);
+                    xv[i][s] = q.a, xv[i + 1][s] = q.b;
+                } else {
+                    xv[i][s] = n0 ? x[c[i][s]] : 0.0;
+                    xv[i + 1][s] = n1 ? x[c[i + 1][s]] : 0.0;
+                }
+            }
+        } else {
+#pragma unroll
+            for (int i = 0; i < R; ++i)
+                xv[i][s] = (s < len[i] && (MODE == 1 || s != ds[i])) ? x[c[i][s]] : 0.0;
+        }
+    }
+    double out[R];
+#pragma unroll
+    for (int i = 0; i < R; ++i) {
+        if constexpr (MODE == 0) {
+            double t = br[i];
+#pragma unroll
+            for (int s = 0; s < 8; ++s)
+                if (s < len[i] && s != ds[i]) t -= a[i][s] * xv[i][s];
+            out[i] = fabs(dv[i]) > 1e-20 ? t / dv[i] : x[r0 + i];
+        } else {
+            double t = 0.0;
+#pragma unroll
+            for (int s = 0; s < 8; ++s)
+                if (s < len[i]) t += a[i][s] * xv[i][s];
+            out[i] = br[i] + t * -1.0;
+        }
+    }
+    double *dst = MODE == 0 ? x : y;
+    if constexpr (R == 1) dst[r0] = out[0];
+    else {
+#pragma unroll
+        for (int h = 0; h < R / 2; ++h)
+            *reinterpret_cast<double2 *>(dst + r0 + 2 * h) = make_double2(out[2 * h], out[2 * h + 1]);
+    }
+}
+
+// stream floor: codes + b in, y out (MODE 1 bytes without the gathers)
+__global__ __launch_bounds__(B) void kstream(const unsigned char *ell, const double *x, const double *b, double *y, int n)
+{
+    const int r = blockIdx.x * B + threadIdx.x;
+    if (r >= n) return;
+    const uint2 q = *reinterpret_cast<const uint2 *>(ell + (size_t)r * 8);
+    y[r] = b[r] - x[r] * (double)(q.x ^ q.y);
+}
+
+int main(int argc, char **argv)
+{
+    const int N = argc > 1 ? atoi(argv[1]) : 400;
+    const int reps = argc > 2 ? atoi(argv[2]) : 20;
+    const long long nn = (long long)N * N * N;
+    const int n = (int)nn;
+    // red-black relabel: F = odd (i+j+k), first; C = even, second; ascending original index in each
+    std::vector<int> newid(n);
+    int nF = 0;
+    for (int g = 0; g < n; ++g) {
+        const int i = g % N, j = (g / N) % N, k = g / (N * N);
+        if ((i + j + k) & 1) newid[g] = nF++;
+    }
+    {
+        int nc = nF;
+        for (int g = 0; g < n; ++g) {
+            const int i = g % N, j = (g / N) % N, k = g / (N * N);
+            if (!((i + j + k) & 1)) newid[g] = nc++;
+        }
+    }
+    if (nF % (4 * B) || (n - nF) % 4) { fprintf(stderr, "sizes not multiples of the blocking\n"); return 1; }
+    std::vector<int> oldid(n);
+    for (int g = 0; g < n; ++g) oldid[newid[g]] = g;
+    const int nb = (n + B - 1) / B;
+    std::vector<unsigned char> ell((size_t)n * 8, 0xff);
+    std::vector<int> ddf((size_t)nb * 32, 0);
+    std::vector<double> vdf((size_t)nb * 8, 0.0);
+    int maxd = 0;
+    for (int q = 0; q < nb; ++q) {
+        int nd = 0;
+        vdf[(size_t)q * 8] = -1.0, vdf[(size_t)q * 8 + 1] = 6.0;
+        for (int r = q * B; r < std::min(n, (q + 1) * B); ++r) {
+            const int g = oldid[r];
+            const int i = g % N, j = (g / N) % N, k = g / (N * N);
+            const int nbr[7] = {g - N * N, g - N, g - 1, g, g + 1, g + N, g + N * N};
+            const bool in[7] = {k > 0, j > 0, i > 0, true, i < N - 1, j < N - 1, k < N - 1};
+            int s = 0;
+            for (int t = 0; t < 7; ++t) {
+                if (!in[t]) continue;
+                const int off = newid[nbr[t]] - r;
+                int d = 0;
+                while (d < nd && ddf[(size_t)q * 32 + d] != off) ++d;
+                if (d == nd) {
+                    if (nd == 31) { fprintf(stderr, "dictionary overflow\n"); return 1; }
+                    ddf[(size_t)q * 32 + nd++] = off;
+                }
+                ell[(size_t)r * 8 + s++] = (unsigned char)((t == 3 ? 1 : 0) << 5 | d);
+            }
+        }
+        maxd = std::max(maxd, nd);
+    }
+    printf("N=%d n=%d nF=%d max offsets per block %d\n", N, n, nF, maxd);
+    unsigned char *d_ell;
+    int *d_ddf;
+    double *d_vdf, *x, *b, *y, *xs;
+    CK(hipMalloc(&d_ell, ell.size()));
+    CK(hipMalloc(&d_ddf, ddf.size() * 4));
+    CK(hipMalloc(&d_vdf, vdf.size() * 8));
+    CK(hipMalloc(&x, (size_t)n * 8));
+    CK(hipMalloc(&xs, (size_t)n * 8));
+    CK(hipMalloc(&b, (size_t)n * 8));
+    CK(hipMalloc(&y, (size_t)n * 8));
+    CK(hipMemcpy(d_ell, ell.data(), ell.size(), hipMemcpyHostToDevice));
+    CK(hipMemcpy(d_ddf, ddf.data(), ddf.size() * 4, hipMemcpyHostToDevice));
+    CK(hipMemcpy(d_vdf, vdf.data(), vdf.size() * 8, hipMemcpyHostToDevice));
+    std::vector<double> hx(n), hb(n);
+    for (int r = 0; r < n; ++r) hx[r] = 1.0 + 1e-3 * (r % 977), hb[r] = 1.0 - 1e-3 * (r % 331);
+    CK(hipMemcpy(xs, hx.data(), (size_t)n * 8, hipMemcpyHostToDevice));
+    CK(hipMemcpy(b, hb.data(), (size_t)n * 8, hipMemcpyHostToDevice));
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0));
+    CK(hipEventCreate(&e1));
+    std::vector<double> ref, got(n);
+    auto run = [&](const char *name, int mode, double bytes, auto launch) {
+        CK(hipMemcpy(x, xs, (size_t)n * 8, hipMemcpyDeviceToDevice));
+        launch();   // the checked launch (an F pass from the same x each time)
+        CK(hipDeviceSynchronize());
+        CK(hipMemcpy(got.data(), mode == 0 ? x : y, (size_t)n * 8, hipMemcpyDeviceToHost));
+        const char *chk = "";
+        if (mode >= 0) {
+            if (ref.empty() || mode == 2) ref = got, chk = " (reference)";
+            else chk = memcmp(ref.data(), got.data(), (size_t)n * 8) ? " MISMATCH" : " bitwise ok";
+        }
+        for (int w = 0; w < 3; ++w) launch();
+        CK(hipEventRecord(e0));
+        for (int t = 0; t < reps; ++t) launch();
+        CK(hipEventRecord(e1));
+        CK(hipEventSynchronize(e1));
+        float ms;
+        CK(hipEventElapsedTime(&ms, e0, e1));
+        ms /= reps;
+        printf("%-30s %8.1f us  %7.0f GB/s (%4.1f%% of 8 TB/s)%s\n", name, ms * 1e3, bytes / (ms * 1e-3) / 1e9,
+               100.0 * bytes / (ms * 1e-3) / 8e12, chk);
+        fflush(stdout);
+    };
+    // F pass bytes: codes + b + x_F written + x_C read once (the other class)
+    const double fbytes = (double)nF * (8 + 8 + 8) + (double)(n - nF) * 8;
+    const double rbytes = (double)n * (8 + 8 + 8 + 8);
+#define FP(R, P) [&] { hipLaunchKernelGGL((kpass<0, R, P>), dim3(nF / (R * B)), dim3(B), 0, 0, d_ell, d_ddf, d_vdf, b, x, y, 0, nF); }
+#define RS(R, P) [&] { hipLaunchKernelGGL((kpass<1, R, P>), dim3((n + R * B - 1) / (R * B)), dim3(B), 0, 0, d_ell, d_ddf, d_vdf, b, x, y, 0, n); }
+    run("F pass R1", 2, fbytes, FP(1, false));
+    run("F pass R2 scalar", 0, fbytes, FP(2, false));
+    run("F pass R2 pair", 0, fbytes, FP(2, true));
+    run("F pass R4 scalar", 0, fbytes, FP(4, false));
+    run("F pass R4 pair", 0, fbytes, FP(4, true));
+    run("resid R1", 2, rbytes, RS(1, false));
+    run("resid R2 scalar", 1, rbytes, RS(2, false));
+    run("resid R2 pair", 1, rbytes, RS(2, true));
+    run("resid R4 scalar", 1, rbytes, RS(4, false));
+    run("resid R4 pair", 1, rbytes, RS(4, true));
+    run("stream floor (codes,b,x,y)", -1, rbytes, [&] { hipLaunchKernelGGL(kstream, dim3(nb), dim3(B), 0, 0, d_ell, x, b, y, n); });
+    return 0;
+}
