@@ -465,7 +465,7 @@ static bool hb_level_pr(HierBuild &b, int l)
 // The V-cycle's tail (sss_tail.hip): the coarsest levels whose passes are all tiny, run as one
 // single-workgroup launch.  A level qualifies when it is smoothed by the no-copy two-stage
 // C/F-Jacobi form on the tile paths (rows of at most one tile, so every row sum is a stored-order
-// chain) and is small (<= 8,192 rows, <= 256K nonzeros in A); the coarsest level needs the explicit
+// chain) and is small (<= 4,096 rows and <= SSS_HIP_TAIL_NNZ nonzeros in A, default 16,384); the coarsest level needs the explicit
 // inverse and <= 256 rows.  The tail is the longest such run above the coarsest level (level 0
 // never: its residual and smoothers have their own fused forms).  SSS_HIP_TAIL=0: no tail.
 static int max_row(const SSS_MAT &M)

@@ -20,6 +20,8 @@
 #include "sss_engine.hpp"
 
 #include <cstring>
+#include <memory>
+#include <mutex>
 #include <numeric>
 
 namespace sss {
@@ -299,15 +301,33 @@ extern "C" int sss_hip_rap(const SSS_MAT *Rh, const SSS_MAT *Ah, const SSS_MAT *
     // rows no table held (wider than 4,096 entries): counted on the host, in parallel chunks
     // (markers: ic while counting, nc + ic while filling)
     std::vector<long long> start((size_t)nc + 1, 0);
+    // one (mark, slot) pair of nc-sized arrays per worker, reused over its chunks and both passes
+    // (the markers of distinct rows and passes never collide), not one per 64-row chunk
+    std::mutex buf_mu;
+    std::vector<std::unique_ptr<std::pair<std::vector<int>, std::vector<int>>>> bufs;
+    std::vector<std::pair<std::vector<int>, std::vector<int>> *> idle;
     auto host_rows = [&](bool fill) {
         const int np = (int)pending.size();
         parallel_chunks(np, 64, [&](int a, int e) {
-            std::vector<int> mark((size_t)nc, -1), slot((size_t)nc, 0);
+            std::pair<std::vector<int>, std::vector<int>> *bf;
+            {
+                std::lock_guard<std::mutex> lk(buf_mu);
+                if (idle.empty()) {
+                    bufs.push_back(std::make_unique<std::pair<std::vector<int>, std::vector<int>>>(
+                        std::vector<int>((size_t)nc, -1), std::vector<int>((size_t)nc, 0)));
+                    idle.push_back(bufs.back().get());
+                }
+                bf = idle.back();
+                idle.pop_back();
+            }
+            int *mark = bf->first.data(), *slot = bf->second.data();
             for (int t = a; t < e; ++t) {
                 const int ic = pending[t];
-                if (fill) host_row(ic, nc + ic, *Rh, *Ah, *Ph, mark.data(), slot.data(), C->col_idx + start[ic], C->val + start[ic]);
-                else count[ic] = host_row(ic, ic, *Rh, *Ah, *Ph, mark.data(), slot.data(), nullptr, nullptr);
+                if (fill) host_row(ic, nc + ic, *Rh, *Ah, *Ph, mark, slot, C->col_idx + start[ic], C->val + start[ic]);
+                else count[ic] = host_row(ic, ic, *Rh, *Ah, *Ph, mark, slot, nullptr, nullptr);
             }
+            std::lock_guard<std::mutex> lk(buf_mu);
+            idle.push_back(bf);
         });
     };
     if (!rc && !pending.empty()) host_rows(false);

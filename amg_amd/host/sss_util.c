@@ -406,12 +406,24 @@ static int transpose_pattern_chunked(int nrows, int ncols, int nnz, const int *i
     }
     long long total = 0;
     for (int t = 0; t < T; ++t) total += hi[t] >= lo[t] ? (long long)(hi[t] - lo[t] + 1) : 0;
-    if (total > 4LL * ncols + 4096 && total > (1LL << 26)) return 0;
-#pragma omp parallel for schedule(static, 1) num_threads(T)
+    /* SSS_TRANSPOSE_CHUNK_CAP (tests): a lower cap on the windows, so the fallback stays exercised */
+    const char *cap_env = getenv("SSS_TRANSPOSE_CHUNK_CAP");
+    const long long cap = cap_env ? atoll(cap_env) : 1LL << 26;
+    if (total > 4LL * ncols + 4096 && total > cap) return 0;
+    int failed = 0;
+#pragma omp parallel for schedule(static, 1) num_threads(T) reduction(| : failed)
     for (int t = 0; t < T; ++t) {
         cnt[t] = (int *)calloc(hi[t] >= lo[t] ? (size_t)(hi[t] - lo[t] + 1) : 1, sizeof(int));
+        if (!cnt[t]) {
+            failed = 1;
+            continue;
+        }
         int *c = cnt[t] - lo[t];
         for (int k = ia[r0[t]]; k < ia[r0[t + 1]]; ++k) c[ja[k]]++;
+    }
+    if (failed) {   /* out of memory for the windows: nothing written, the atomic transpose runs */
+        for (int t = 0; t < T; ++t) free(cnt[t]);
+        return 0;
     }
     /* per column: counts -> exclusive offsets of the chunks inside the output row, row length */
     tia[0] = 0;

@@ -339,18 +339,23 @@ def test_outer_loop_vs_reference_solve(case, quiet):
 
 
 @needs_ref
-@pytest.mark.parametrize("transpose", ["chunked", "atomic"])
+@pytest.mark.parametrize("transpose", ["chunked", "atomic", "chunk-fallback"])
 @pytest.mark.parametrize("gen", ["p7_64", "circuit", "scrambled"])
 def test_parallel_setup_paths_vs_reference(gen, transpose, quiet, monkeypatch):
     """Matrices above the parallel threshold (>= 2^20 entries): both OpenMP transposes
     (transpose_pattern_chunked, and transpose_pattern_par under SSS_TRANSPOSE_ATOMIC) and the
     weak-coupling compaction give the reference's results exactly -- SSS_mat_trans of A and the RS
-    C/F marks (SSS_amg_coarsen) against the compiled reference."""
+    C/F marks (SSS_amg_coarsen) against the compiled reference.  chunk-fallback: the chunked
+    transpose's window cap lowered to 0 (SSS_TRANSPOSE_CHUNK_CAP), so on the scrambled matrix (windows
+    wider than 4 x ncols) it declines and the atomic transpose runs from inside transpose_pattern."""
     from amg_amd import workloads as W
+    monkeypatch.delenv("SSS_TRANSPOSE_CHUNK_CAP", raising=False)
     if transpose == "atomic":
         monkeypatch.setenv("SSS_TRANSPOSE_ATOMIC", "1")
     else:
         monkeypatch.delenv("SSS_TRANSPOSE_ATOMIC", raising=False)
+    if transpose == "chunk-fallback":
+        monkeypatch.setenv("SSS_TRANSPOSE_CHUNK_CAP", "0")
     keep = None
     if gen == "p7_64":
         M = A.generate(7, 64)
