@@ -130,8 +130,14 @@ __device__ __forceinline__ int ell_decode(const unsigned (&w)[W / 4], int r, con
 #pragma unroll
     for (int s = 0; s < W; ++s)
         if (s < len && c[s] == r) dslot = s, dval = a[s];
+    // every gather issued before any product: with the multiply under the load's condition the
+    // compiler waited for each load inside its branch (one HBM round trip per slot, in series)
+    double xv[W];
 #pragma unroll
-    for (int s = 0; s < W; ++s) p[s] = (s < len && (DIAG || s != dslot)) ? a[s] * fetch(c[s]) : 0.0;
+    for (int s = 0; s < W; ++s) xv[s] = (s < len && (DIAG || s != dslot)) ? fetch(c[s]) : 0.0;
+    // masked slots (past the row, the skipped diagonal) hold a * 0.0; no caller sums them
+#pragma unroll
+    for (int s = 0; s < W; ++s) p[s] = a[s] * xv[s];
     return len;
 }
 template <int W, class Fetch>
