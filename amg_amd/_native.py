@@ -85,7 +85,7 @@ class SSS_HIP_LEVEL_INFO(C.Structure):
     _fields_ = [("rows", C.c_int), ("nnz", C.c_int), ("nnz_p", C.c_int), ("dag_f", C.c_int),
                 ("dag_c", C.c_int), ("smoother_kind", C.c_int), ("gs_engine_f", C.c_int), ("gs_engine_c", C.c_int),
                 ("gs_stall", C.c_int), ("a_format", C.c_int), ("a_stream_bytes", C.c_longlong),
-                ("inner", C.c_int), ("pad_", C.c_int)]
+                ("inner", C.c_int), ("r_format", C.c_int), ("p_format", C.c_int), ("pad_", C.c_int)]
 
 
 SMOOTH = {"exact": 0, "hybrid": 1, "jacobi": 2}

@@ -531,7 +531,7 @@ static sss_hip_dist *dist_create_impl(sss_hip_dist *d, PartPlan &plan, const SSS
             // (a C-rows-only prolongation keeps the tiles, as hb_level_pr)
             const int tenc = transfer_encoding(d->opts);
             if (devcsr_upload(L.P, Pv, P.nF, L.sm.f_overwritten ? (tenc & ~kEncXell) : tenc) ||
-                devcsr_upload(L.R, Rv, -1, transfer_encoding(d->opts)))
+                devcsr_upload(L.R, Rv, -1, restriction_encoding(d->opts)))
                 return "upload P/R";
             {   // which row blocks read ghosts (the blockings the uploads made, read back: the
                 // column ELL replaces the CSR-adaptive blocking where it is chosen)

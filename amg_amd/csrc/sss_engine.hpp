@@ -254,7 +254,8 @@ static_assert(1 + kTileColBits + kTileShift == 32, "tile packing");
 // kEncMergedOnly: the matrix is only ever read through its merged copy when it gets one (the
 // two-stage split copies, launch_ts_*), so its CSR arrays need not be column-sorted
 // kEncXell: the column ELL may replace the tile storage (its own 256-row blocking)
-enum { kEncSortedTiles = 1, kEncFreeOrder = 2, kEncDict = 4, kEncMergedOnly = 8, kEncXell = 16 };
+enum { kEncSortedTiles = 1, kEncFreeOrder = 2, kEncDict = 4, kEncMergedOnly = 8, kEncXell = 16,
+       kEncEll = 32 };   // kEncEll: the one-byte dictionary ELL only (also rectangular; no dictionary tiles)
 // split >= 0 forces a row-block boundary at that row (the F|C class boundary of a relabeled level);
 // enc: kEnc* flags; seg (kEncFreeOrder only, optional): per row, the absolute CSR position that
 // splits the row into two independently summed segments (two-stage [N_i | L_i] rows).
@@ -263,6 +264,7 @@ int devcsr_upload(DevCSR &d, const SSS_MAT &h, int split = -1, int enc = 0, cons
 // transfer operators P_l, R_l
 int level_encoding(const sss_hip_opts &o);
 int transfer_encoding(const sss_hip_opts &o);
+int restriction_encoding(const sss_hip_opts &o);
 void devcsr_free(DevCSR &d);
 int build_row_blocks(const int *h_rp, int n, std::vector<int> &blk, int split = -1);
 int upload_block_bounds(int2 **dst, const std::vector<int> &blk, const int *h_rp);

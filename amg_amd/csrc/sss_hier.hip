@@ -161,6 +161,16 @@ int sss::transfer_encoding(const sss_hip_opts &o)
     const int enc = (e && *e == '1') ? level_encoding(o) : (level_encoding(o) & ~kEncDict);
     return (x && *x == '0') ? (enc & ~kEncXell) : enc;
 }
+// R_l: as transfer_encoding; SSS_HIP_ELL_R=1 also offers the one-byte dictionary ELL (rectangular:
+// offsets col - row).  Off by default: on the relabeled hierarchy a restriction's rows are the next
+// level's F-first order, so the offsets drift across a block (7-pt 400^3 R_0: no block fits 31
+// offsets; tools/fmt_probe.py reports the formats each operator got).
+int sss::restriction_encoding(const sss_hip_opts &o)
+{
+    const char *e = getenv("SSS_HIP_ELL_R");
+    const int enc = transfer_encoding(o);
+    return (e && *e == '1' && (level_encoding(o) & kEncDict)) ? (enc | kEncEll) : enc;
+}
 
 // Are the C and the F points of A each an independent set (no off-diagonal coupling inside a
 // class)?  Then exact GS-CF has no chains: each class pass is one C/F-Jacobi pass (7-pt level 0).
@@ -453,9 +463,9 @@ static bool hb_level_pr(HierBuild &b, int l)
         // P's rows follow the level's F|C relabeling: blocks split there too, so a
         // prolongation can be limited to the C rows (SmootherPlan::f_overwritten)
         if (devcsr_upload(L.P, P.view(C.P.num_rows, C.P.num_cols), rl ? b.nF[l] : -1, penc) ||
-            devcsr_upload(L.R, R.view(C.R.num_rows, C.R.num_cols), -1, tenc))
+            devcsr_upload(L.R, R.view(C.R.num_rows, C.R.num_cols), -1, restriction_encoding(h->opts)))
             return hb_fail(b, "upload P/R");
-    } else if (devcsr_upload(L.P, C.P, -1, penc) || devcsr_upload(L.R, C.R, -1, tenc)) {
+    } else if (devcsr_upload(L.P, C.P, -1, penc) || devcsr_upload(L.R, C.R, -1, restriction_encoding(h->opts))) {
         return hb_fail(b, "upload P/R");
     }
     if (b.timing) fprintf(stderr, "[sss_hip] upload level %d: P/R %.2f s\n", l, PhaseTimer::now() - t0);
@@ -1141,8 +1151,13 @@ extern "C" int sss_hip_level_info_get(sss_hip_hier *h, int level, sss_hip_level_
     unsigned ef = 0, ec = 0;
     if (gs_persist_error(L.sm.pass[0], &ef) || gs_persist_error(L.sm.pass[1], &ec)) return ERROR_MISC;
     out->gs_stall = (int)(ef | ec);
-    out->a_format = (L.A.pk ? 1 : 0) | (has_dict(L.A) ? 2 : 0) | (L.A.vec_rows ? 4 : 0) | (L.A.mg_G ? 8 : 0) |
-                    (L.A.wave_rows ? 16 : 0) | (L.A.dv_ell ? 64 : 0) | (L.A.dv_xell ? 128 : 0);
+    auto fmt = [](const DevCSR &M) {
+        return (M.pk ? 1 : 0) | (has_dict(M) ? 2 : 0) | (M.vec_rows ? 4 : 0) | (M.mg_G ? 8 : 0) | (M.wave_rows ? 16 : 0) |
+               (M.dv_ell ? 64 : 0) | (M.dv_xell ? 128 : 0);
+    };
+    out->a_format = fmt(L.A);
+    out->r_format = level + 1 < h->nl ? fmt(L.R) : 0;
+    out->p_format = level + 1 < h->nl ? fmt(L.P) : 0;
     out->a_stream_bytes = L.A.stream_bytes;
     return 0;
 }
@@ -1357,7 +1372,9 @@ extern "C" int sss_hip_host_spmv(int op, double alpha, const SSS_MAT *A, const d
     if (sss_hip_device_count() <= 0) return ERROR_MISC;
     sss_hip_opts o;
     sss_hip_opts_default(&o);   // SSS_HIP_SORTED_TILES; always the reference's summation order here
-    const int enc = level_encoding(o) & (kEncSortedTiles | kEncDict);
+    // rectangular operators (P, R) may take the dictionary ELL, as the hierarchy's restrictions
+    int enc = level_encoding(o) & (kEncSortedTiles | kEncDict);
+    if (A->num_rows != A->num_cols) enc = restriction_encoding(o) & (kEncSortedTiles | kEncEll);
     auto M = prepared().get<HostCSR>(matrix_key(*A, 0x5350ull ^ ((unsigned long long)enc << 8)), [&] {
         auto m = std::make_shared<HostCSR>();
         return devcsr_upload(m->d, *A, -1, enc) ? nullptr : m;

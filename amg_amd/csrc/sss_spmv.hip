@@ -573,7 +573,8 @@ static bool build_ell(const SSS_MAT &h, const std::vector<int> &blk, HostBuf<uns
     const int *rp = h.row_ptr, *ci = h.col_idx;
     const double *v = h.val;
     const int n = h.num_rows, nb = (int)blk.size() - 1;
-    if (n != h.num_cols || nb <= 0 || n <= 0) return false;
+    // rectangular matrices (a restriction) too: offsets col - row, no diagonal meaning
+    if (nb <= 0 || n <= 0) return false;
     std::atomic<int> Lmax{0};
     parallel_chunks(n, 1 << 16, [&](int lo, int hi) {
         int L = 0;
@@ -849,7 +850,8 @@ int devcsr_upload(DevCSR &d, const SSS_MAT &h, int split, int enc, const int *se
     // from them instead of the sorted copy)
     const char *dz = getenv("SSS_HIP_DICT");   // 0: never (tests compare both ways)
     const char *ez = getenv("SSS_HIP_ELL");    // 0: no ELL (dictionary tiles where they qualify)
-    if ((enc & kEncDict) && !(dz && *dz == '0') && !(ez && *ez == '0') && !d.wave_rows && !d.vec_rows && d.nnz > 0) {
+    if ((enc & (kEncDict | kEncEll)) && !(dz && *dz == '0') && !(ez && *ez == '0') && !d.wave_rows && !d.vec_rows &&
+        d.nnz > 0 && ((enc & kEncEll) || d.n == d.ncols)) {
         HostBuf<unsigned char> ell;
         std::vector<int4> pd;
         std::vector<int> dd;

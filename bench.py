@@ -586,12 +586,14 @@ def main():
     a_format = None
     launches, tail_from = None, None
     level_formats = None
+    transfer_formats = None
     level_smoothers = None
     csr_bytes = 12 * nnz + 4 * (N + 1) + 8 * N + 8 * N + 8 * N   # val+col, row_ptr, x, b, y
     if D.world == 1:
         info0 = DH.DH.level_info(0)
         a_format = A._native.a_format_name(info0.a_format)
         level_formats = [DH.DH.level_info(l).a_format for l in range(len(table) - 1)]
+        transfer_formats = [[DH.DH.level_info(l).r_format, DH.DH.level_info(l).p_format] for l in range(len(table) - 1)]
         level_smoothers = [(DH.DH.level_info(l).smoother_kind, DH.DH.level_info(l).inner) for l in range(len(table) - 1)]
         # the stored format's own bytes (dictionary ELL: 8 B per row + block dictionaries) + vectors
         spmv_bytes = info0.a_stream_bytes + 8 * N + 8 * N + 8 * N
@@ -773,6 +775,7 @@ def main():
                    "sum_order": "tree (long rows)" if sum_order == 1 else "stored CSR order",
                    "sorted_tiles": bool(sorted_tiles),
                    "level_storage_bits": level_formats,
+                   "transfer_storage_bits_r_p": transfer_formats,
                    "kernel_launches_per_cycle": launches,
                    "single_workgroup_tail_from_level": tail_from if tail_from is not None and tail_from >= 0 else None,
                    "level_smoothers": [["exact", "hybrid", "jacobi"][k] + (f"+inner{i}" if i else "")

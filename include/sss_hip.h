@@ -140,6 +140,7 @@ typedef struct sss_hip_level_info {
     int gs_engine_f, gs_engine_c, gs_stall, a_format;
     long long a_stream_bytes;   /* bytes of A_l's stored format one tile-path SpMV reads (no vectors) */
     int inner;
+    int r_format, p_format;     /* R_l / P_l storage, the a_format bits */
     int pad_;
 } sss_hip_level_info;
 int sss_hip_level_info_get(sss_hip_hier *h, int level, sss_hip_level_info *out);
