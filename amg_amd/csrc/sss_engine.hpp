@@ -351,6 +351,7 @@ struct GsPersist {
     int engine = 0;
     int lo = 0, hi = 0;                 // the pass's contiguous rows
     int G = 64;                         // flow: lanes per row (64 / G rows of one depth per ticket)
+    bool overlap = false;               // flow: the chain runs while pending granules are polled (long rows)
     bool natural = false, desc = false; // natural-order GS (x = t * d), descending row order
     int nchunks = 0, grid = 0;
     int *ck = nullptr;                  // flow, short rows: chunk -> first position (nchunks + 1)

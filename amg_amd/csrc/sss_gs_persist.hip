@@ -148,7 +148,7 @@ __global__ __launch_bounds__(kBlock) void gs_flow_group(int nchunks, const int *
                                                         const int *__restrict__ ci, const double *__restrict__ v,
                                                         const double *__restrict__ b, double *x,
                                                         const double *__restrict__ deff, unsigned long long *gran,
-                                                        int lo, int hi, unsigned *ctl, unsigned *err, int spin)
+                                                        int lo, int hi, unsigned *ctl, unsigned *err, int spin, int ovl)
 {
     constexpr int R = 64 / G, CAP = kGroupBuf / R, U = 8;
     // a same-pass row this row reads the NEW value of (published by its granules)
@@ -201,22 +201,97 @@ __global__ __launch_bounds__(kBlock) void gs_flow_group(int nchunks, const int *
                     if (dynamic(c[u], i)) {
                         double g = 0.0;
                         if (granule_get(gran + 2 * (size_t)(c[u] - lo), epoch, g)) val = a[u] * g;
-                        else pend |= 1u << (j0 + u);
+                        else {
+                            pend |= 1u << (j0 + u);
+                            if (ovl) val = __longlong_as_double((long long)c[u]);   // its column, until resolved
+                        }
                     } else if (c[u] != i) {
                         val = a[u] * xv[u];
                     }
                     mine[t] = val;
                 }
             }
-            while (pend) {   // (B)
-                const int j = __builtin_ctz(pend);
-                pend &= pend - 1;
-                const int t = gl + G * j;
-                const int c = ci[kb + t];
-                mine[t] = v[kb + t] * granule_wait(gran + 2 * (size_t)(c - lo), epoch, err, spin);
+            if (!ovl) {
+                while (pend) {   // (B)
+                    const int j = __builtin_ctz(pend);
+                    pend &= pend - 1;
+                    const int t = gl + G * j;
+                    const int c = ci[kb + t];
+                    mine[t] = v[kb + t] * granule_wait(gran + 2 * (size_t)(c - lo), epoch, err, spin);
+                }
+                wave_sync();
+                if (gl == 0 && m > 0) acc = chain_sub_pipe(acc, mine, 0, m);   // (C)
+                wave_sync();
+                continue;
             }
+            // (B) and (C) interleaved: the row's first lane chains over the prefix of entries whose
+            // products are staged while the pending granules are polled, the poll loads issued
+            // before each chain segment and read after it.  The chain still adds every product in
+            // stored order from b_i; it only stops at the first entry still pending.
             wave_sync();
-            if (gl == 0 && m > 0) acc = chain_sub_pipe(acc, mine, 0, m);   // (C)
+            int k = 0, idle = 0;
+            for (;;) {
+                // the row group's first pending entry: the chain may run up to it
+                int first = pend ? gl + G * __builtin_ctz(pend) : CAP;
+#pragma unroll
+                for (int off = G / 2; off > 0; off >>= 1) first = min(first, __shfl_xor(first, off, 64));
+                const int lim = min(first, m);
+                // issue this lane's two lowest pending polls (column from LDS, granule halves, value)
+                constexpr int NP = 2;
+                int tp[NP];
+                unsigned long long ga[NP], gc[NP];
+                double ap[NP];
+                {
+                    unsigned q = pend;
+#pragma unroll
+                    for (int h = 0; h < NP; ++h) {
+                        tp[h] = -1;
+                        ga[h] = gc[h] = 0;
+                        ap[h] = 0.0;
+                        if (q) {
+                            tp[h] = gl + G * __builtin_ctz(q);
+                            q &= q - 1;
+                            const int cp = (int)__double_as_longlong(mine[tp[h]]);
+                            const unsigned long long *gg = gran + 2 * (size_t)(cp - lo);
+                            ga[h] = __hip_atomic_load(const_cast<unsigned long long *>(gg), RLX_AGENT);
+                            gc[h] = __hip_atomic_load(const_cast<unsigned long long *>(gg + 1), RLX_AGENT);
+                            ap[h] = v[kb + tp[h]];
+                        }
+                    }
+                }
+                const bool advance = gl == 0 && k < lim;
+                if (advance) acc = chain_sub_pipe(acc, mine, k, lim);   // (C), overlapping the polls
+                if (gl == 0) k = max(k, lim);
+                bool got = false;
+#pragma unroll
+                for (int h = 0; h < NP; ++h)
+                    if (tp[h] >= 0 && (unsigned)(ga[h] >> 32) == epoch && (unsigned)(gc[h] >> 32) == epoch) {
+                        mine[tp[h]] = ap[h] * __longlong_as_double((long long)((gc[h] << 32) | (ga[h] & 0xffffffffull)));
+                        pend &= ~(1u << ((tp[h] - gl) / G));
+                        got = true;
+                    }
+                const bool rowdone = gl != 0 || k >= m;
+                if (__all(rowdone && !pend)) break;
+                wave_sync();   // resolved products visible to the chain lane (LDS, same wave)
+                if (__any(got || advance)) {
+                    idle = 0;
+                } else {
+                    // give up after the limit (as granule_wait), or at once when another wave did
+                    if (++idle >= spin || ((idle & 63) == 63 && __hip_atomic_load(err, RLX_AGENT))) {
+                        if (gl == 0) __hip_atomic_store(err, 1u, RLX_AGENT);
+                        while (pend) {   // garbage results, but every wave reaches the exit
+                            mine[gl + G * __builtin_ctz(pend)] = 0.0;
+                            pend &= pend - 1;
+                        }
+                        wave_sync();
+                        if (gl == 0 && k < m) acc = chain_sub_pipe(acc, mine, k, m);
+                        if (gl == 0) k = m;
+                        break;
+                    }
+                    if (idle < 16) __builtin_amdgcn_s_sleep(1);
+                    else __builtin_amdgcn_s_sleep(8);
+                }
+            }
             wave_sync();
         }
         if (active && gl == 0) {
@@ -406,6 +481,11 @@ int gs_persist_build(PassSchedule &ps, const SSS_MAT &A, int lo, int hi, bool lo
     g.G = avg <= 24 ? 4 : avg <= 48 ? 8 : avg <= 96 ? 16 : avg <= 192 ? 32 : 64;
     if (const char *gg = getenv("SSS_HIP_GS_LANES")) g.G = atoi(gg);
     if (g.G != 4 && g.G != 8 && g.G != 16 && g.G != 32 && g.G != 64) g.G = 64;
+    // the row's chain overlapping the polls of its pending granules: measured at 7-pt 256^3
+    // (tools/gpu/gs_overlap.sh, pre-smoother per call) 19 % faster on the levels of 700-1400
+    // entries per row (level 7: 106 -> 86 ms, level 8: 108 -> 87), 5 % on level 5 (407), but
+    // 9-12 % slower on levels 3-4 (64 and 198), where the chain is short against the loop's polls
+    g.overlap = avg >= 300;
     (void)long_rows;
     g.gran = dev_alloc<unsigned long long>(2 * (size_t)(hi - lo));
     g.ctl = dev_alloc<unsigned>(kCtlWords);
@@ -451,6 +531,16 @@ void gs_persist_free(PassSchedule &ps)
     g = GsPersist();
 }
 
+// SSS_HIP_GS_OVERLAP=0: the flow engine waits for every pending granule of a row before its chain
+static bool gs_overlap_on()
+{
+    static const bool on = [] {
+        const char *e = getenv("SSS_HIP_GS_OVERLAP");
+        return !(e && *e == '0');
+    }();
+    return on;
+}
+
 int gs_persist_run(const PassSchedule &ps, const DevCSR &A, const double *b, double *x, const double *deff,
                    hipStream_t s)
 {
@@ -461,7 +551,7 @@ int gs_persist_run(const PassSchedule &ps, const DevCSR &A, const double *b, dou
     } else if (g.engine == 1) {
         auto go = [&](auto kern) {
             hipLaunchKernelGGL(kern, dim3(g.grid), dim3(kBlock), 0, s, g.nchunks, g.ck, ps.rows, A.rp, A.ci, A.v, b, x,
-                               deff, g.gran, g.lo, g.hi, g.ctl, g.err, g.spin);
+                               deff, g.gran, g.lo, g.hi, g.ctl, g.err, g.spin, g.overlap && gs_overlap_on() ? 1 : 0);
         };
         auto by_g = [&](auto nat, auto desc) {
             constexpr bool N = decltype(nat)::value, D = decltype(desc)::value;

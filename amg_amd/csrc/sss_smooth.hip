@@ -499,7 +499,7 @@ __device__ __forceinline__ void relax_range_ell(int blo, const int2 *__restrict_
 {
     constexpr int RPT = kEllRpt;
     __shared__ EllSmem es[RPT];
-    const int g = (RPT == 1 && dt.remap) ? xcd_remap(blockIdx.x, gridDim.x) : (int)blockIdx.x;
+    const int g = dt.remap ? xcd_remap(blockIdx.x, gridDim.x) : (int)blockIdx.x;
     unsigned w[RPT][W / 4];
     double br[RPT], dr[RPT];
     int r[RPT];

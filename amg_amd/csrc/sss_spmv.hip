@@ -1097,7 +1097,7 @@ __global__ __launch_bounds__(kBlock) void spmv_adaptive(const int2 *__restrict__
         constexpr int W = DICT;   // from 0.0 in stored order; kEllRpt row blocks per workgroup
         constexpr int RPT = kEllRpt;
         __shared__ EllSmem es[RPT];
-        const int g = (RPT == 1 && dt.remap) ? xcd_remap(blockIdx.x, gridDim.x) : (int)blockIdx.x;
+        const int g = dt.remap ? xcd_remap(blockIdx.x, gridDim.x) : (int)blockIdx.x;
         unsigned w[RPT][W / 4];
         double br[RPT];
         int r[RPT];
