@@ -114,24 +114,11 @@ __device__ __forceinline__ int flow_ticket(unsigned *ctl)
     return __builtin_amdgcn_readfirstlane((int)__hip_atomic_fetch_add(&ctl[kCtlTicket], inc, RLX_AGENT));
 }
 
-// s - p[a] - p[a+1] - ... - p[e-1] in order, with the next batch's LDS reads issued before the
-// current batch's subtractions (the chain is one dependent fp64 subtraction per entry)
+// s - p[a] - p[a+1] - ... - p[e-1] in order (chain_pipe16: the next 16 products read as 16-byte
+// pairs while the current 16 are subtracted; the chain is one dependent fp64 subtraction per entry)
 __device__ __forceinline__ double chain_sub_pipe(double s, const double *p, int a, int e)
 {
-    int k = a;
-    if (e - k >= 16) {
-        double c0 = p[k], c1 = p[k + 1], c2 = p[k + 2], c3 = p[k + 3];
-        double c4 = p[k + 4], c5 = p[k + 5], c6 = p[k + 6], c7 = p[k + 7];
-        for (k += 8; k + 8 <= e; k += 8) {
-            const double n0 = p[k], n1 = p[k + 1], n2 = p[k + 2], n3 = p[k + 3];
-            const double n4 = p[k + 4], n5 = p[k + 5], n6 = p[k + 6], n7 = p[k + 7];
-            s -= c0; s -= c1; s -= c2; s -= c3; s -= c4; s -= c5; s -= c6; s -= c7;
-            c0 = n0, c1 = n1, c2 = n2, c3 = n3, c4 = n4, c5 = n5, c6 = n6, c7 = n7;
-        }
-        s -= c0; s -= c1; s -= c2; s -= c3; s -= c4; s -= c5; s -= c6; s -= c7;
-    }
-    for (; k < e; ++k) s -= p[k];
-    return s;
+    return chain_pipe16<true>(s, p, a, e);
 }
 
 constexpr int kGroupBuf = 2048;   // staged products per wave (16 KiB; 64 KiB per workgroup)
@@ -154,7 +141,7 @@ __global__ __launch_bounds__(kBlock) void gs_flow_group(int nchunks, const int *
     // a same-pass row this row reads the NEW value of (published by its granules)
     auto dynamic = [&](int c, int i) { return DESC ? (c > i && c < hi) : (c >= lo && c < i); };
     static_assert(CAP / G == 32, "one pending bit per staged entry of a lane");
-    __shared__ double buf[kBlock / 64][kGroupBuf];
+    __shared__ __attribute__((aligned(16))) double buf[kBlock / 64][kGroupBuf];
     const int lane = threadIdx.x & 63, grp = lane / G, gl = lane % G;
     double *mine = buf[threadIdx.x >> 6] + grp * CAP;
     const unsigned epoch = __hip_atomic_load(&ctl[kCtlEpoch], RLX_AGENT) + 1u;
@@ -315,7 +302,7 @@ __global__ __launch_bounds__(64 * kCuWaves) void gs_cu(int nrows, int ndepth, co
 {
     __shared__ int done[kCuMaxDepth];
     __shared__ int ticket, abort_flag;
-    __shared__ double strips[kCuWaves][kWaveStage];
+    __shared__ __attribute__((aligned(16))) double strips[kCuWaves][kWaveStage];
     for (int t = threadIdx.x; t < ndepth; t += blockDim.x) done[t] = 0;
     if (threadIdx.x == 0) ticket = 0, abort_flag = 0;
     __syncthreads();

@@ -420,7 +420,7 @@ __global__ __launch_bounds__(kBlock) void gs_depth_wave(const int *__restrict__ 
                                                         const double *__restrict__ v, const double *__restrict__ b,
                                                         double *x, const double *__restrict__ deff)
 {
-    __shared__ double strips[4][kWaveStage];
+    __shared__ __attribute__((aligned(16))) double strips[4][kWaveStage];
     const int wave = threadIdx.x >> 6;
     const int t = blockIdx.x * 4 + wave;
     if (t >= cnt) return;
@@ -460,7 +460,7 @@ __global__ __launch_bounds__(kBlock) void relax_wave(int m, const int *__restric
                                                      const double *__restrict__ b, double *x, double *__restrict__ y,
                                                      const double *__restrict__ deff)
 {
-    __shared__ double strips[4][kWaveStage];
+    __shared__ __attribute__((aligned(16))) double strips[4][kWaveStage];
     const int wave = threadIdx.x >> 6;
     const int r = xcd_bid() * 4 + wave;
     if (r >= m) return;
@@ -797,7 +797,7 @@ __global__ __launch_bounds__(kBlock) void relax_range_wave(int lo, int hi, const
                                                            const double *__restrict__ yp, double *__restrict__ y,
                                                            const double *__restrict__ deff, XSrc xs)
 {
-    __shared__ double strips[TREE ? 1 : 4][TREE ? 1 : kWaveStage];
+    __shared__ __attribute__((aligned(16))) double strips[TREE ? 1 : 4][TREE ? 1 : kWaveStage];
     const int wave = threadIdx.x >> 6;
     const int r = lo + xcd_bid() * 4 + wave;
     if (r >= hi) return;
@@ -887,7 +887,7 @@ __global__ __launch_bounds__(kBlock) void ts_stage0(int lo, DevCSR M, const int 
         }
         return;
     } else if constexpr (PATH == 1) {
-        __shared__ double strips[4][kWaveStage];
+        __shared__ __attribute__((aligned(16))) double strips[4][kWaveStage];
         const int wave = threadIdx.x >> 6, q = xcd_bid() * 4 + wave;
         if (q >= M.n) return;
         auto prod = [&](int c, double a) { return a * x(c); };
@@ -1009,7 +1009,7 @@ __global__ __launch_bounds__(kBlock) void ts_inner(int lo, DevCSR M, const doubl
         if ((threadIdx.x & 63) == 0) finish(q, acc);
         return;
     } else if constexpr (PATH == 1) {
-        __shared__ double strips[4][kWaveStage];
+        __shared__ __attribute__((aligned(16))) double strips[4][kWaveStage];
         const int wave = threadIdx.x >> 6, q = xcd_bid() * 4 + wave;
         if (q >= M.n) return;
         const double acc = wave_row_chain<true>(

@@ -1165,7 +1165,7 @@ __global__ __launch_bounds__(kBlock) void spmv_wave(int n, const int *__restrict
                                                     const double *__restrict__ b, double *__restrict__ y, double alpha,
                                                     int cap, double *__restrict__ partial)
 {
-    __shared__ double strips[TREE ? 1 : 4][TREE ? 1 : kWaveStage];
+    __shared__ __attribute__((aligned(16))) double strips[TREE ? 1 : 4][TREE ? 1 : kWaveStage];
     __shared__ double red[kBlock / 64];
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int r = xcd_bid() * 4 + wave;

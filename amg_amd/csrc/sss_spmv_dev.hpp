@@ -263,6 +263,52 @@ __device__ __forceinline__ double chain_sub(double s, const double *p, int a, in
     return s;
 }
 
+// One lane's in-order chain over a long run of LDS products (the exact GS-CF engines, the parity
+// wave-per-row kernels): s -/+= p[a], p[a+1], ... in order, with the next 16 products read as eight
+// 16-byte pairs while the current 16 are added -- tools/chain_lab.hip on MI355X: 10.0 cycles per
+// entry against 13.4 for eight 8-byte reads ahead, the dependent fp64 subtraction alone 8.5.  p must
+// be 16-byte aligned.
+template <bool SUB>
+__device__ __forceinline__ double chain_pipe16(double s, const double *p, int a, int e)
+{
+    int k = a;
+    if ((k & 1) && k < e) s = SUB ? s - p[k++] : s + p[k++];
+    if (e - k >= 32) {
+        double2 c[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) c[u] = *reinterpret_cast<const double2 *>(p + k + 2 * u);
+        for (k += 16; k + 16 <= e; k += 16) {
+            double2 nx[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) nx[u] = *reinterpret_cast<const double2 *>(p + k + 2 * u);
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                if (SUB) {
+                    s -= c[u].x;
+                    s -= c[u].y;
+                } else {
+                    s += c[u].x;
+                    s += c[u].y;
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < 8; ++u) c[u] = nx[u];
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            if (SUB) {
+                s -= c[u].x;
+                s -= c[u].y;
+            } else {
+                s += c[u].x;
+                s += c[u].y;
+            }
+        }
+    }
+    for (; k < e; ++k) s = SUB ? s - p[k] : s + p[k];
+    return s;
+}
+
 // Fixed-order block reduction (xor butterfly inside the wave, then waves in order).
 // Result valid in thread 0.  Must be reached by every thread of the block.
 __device__ __forceinline__ double block_sum(double v, double *red)
@@ -683,18 +729,25 @@ __device__ __forceinline__ double wave_row_chain(int k0, int k1, const int *__re
         int c[U];
         double a[U];
 #pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const int q = lane + 64 * u;
-            c[u] = q < m ? ci[base + q] : 0;
-            a[u] = q < m ? v[base + q] : 0.0;
+        for (int u = 0; u < U; ++u) {   // unconditional loads (clamped into the row): no branch per load
+            const int q = lane + 64 * u, qc = q < m ? q : m - 1;
+            const int cv = ci[base + qc];
+            const double av = v[base + qc];
+            c[u] = q < m ? cv : 0;
+            a[u] = q < m ? av : 0.0;
         }
+        // every product formed before any is stored (a lane past the row uses column 0, value 0.0):
+        // with the store's condition around it the compiler waited for each gather in turn
+        double pv[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) pv[u] = prod(c[u], a[u]);
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             const int q = lane + 64 * u;
-            if (q < m) strip[q] = prod(c[u], a[u]);
+            if (q < m) strip[q] = pv[u];
         }
         wave_sync();
-        if (lane == 0) acc = SUB ? chain_sub(acc, strip, 0, m) : chain_add(acc, strip, 0, m);
+        if (lane == 0) acc = chain_pipe16<SUB>(acc, strip, 0, m);
         wave_sync();
     }
     return acc;
@@ -714,14 +767,19 @@ __device__ __forceinline__ double wave_row_sum(int k0, int k1, const int *__rest
         int c[U];
         double a[U];
 #pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const int kk = k + 64 * u;
-            c[u] = kk < k1 ? ci[kk] : -1;
-            a[u] = kk < k1 ? v[kk] : 0.0;
+        for (int u = 0; u < U; ++u) {   // unconditional loads (clamped into the row): no branch per load
+            const int kk = k + 64 * u, kc = kk < k1 ? kk : k1 - 1;
+            const int cv = ci[kc];
+            const double av = v[kc];
+            c[u] = kk < k1 ? cv : -1;
+            a[u] = kk < k1 ? av : 0.0;
         }
+        double pv[U];   // every gather issued before any is used (masked lanes: column 0, value 0.0)
+#pragma unroll
+        for (int u = 0; u < U; ++u) pv[u] = prod(c[u] >= 0 ? c[u] : 0, a[u]);
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-            const double p = c[u] >= 0 ? prod(c[u], a[u]) : 0.0;
+            const double p = c[u] >= 0 ? pv[u] : 0.0;
             if (u & 1) s1 += p;
             else s0 += p;
         }
