@@ -137,13 +137,13 @@ typedef struct {
     int live;                /* live entries = points in this bucket */
 } bucket_fifo;
 
-/* Per-point state of the first pass in one 16-byte record (one cache line holds four points; the
- * pass touches measure, mark and version of the same neighbours). */
+/* Per-point state of the first pass in one 8-byte record (one cache line holds eight points; the
+ * pass touches measure, mark and version of the same neighbours).  A point's version moves once
+ * per bucket move -- a few dozen times at most -- so 29 bits never wrap. */
 typedef struct {
     int lambda;              /* measure */
-    int mark;                /* UNPT / CGPT / FGPT / ISPT */
-    unsigned ver;            /* current version: a bucket entry is live iff it matches */
-    int pad;
+    int mark : 3;            /* UNPT / CGPT / FGPT / ISPT */
+    unsigned ver : 29;       /* current version: a bucket entry is live iff it matches */
 } rs_point;
 
 typedef struct {
@@ -197,6 +197,18 @@ static inline void bucket_remove(measure_buckets *B, int m, int pt)
     }
     B->pts[pt].ver++;
     if (--B->b[m].live == 0) B->b[m].head = B->b[m].tail = 0;
+}
+
+/* bucket_remove(from) + bucket_insert(to) with one version step: the insert's new version already
+ * makes the old entry stale (same buckets, same order as the two calls). */
+static inline void bucket_move(measure_buckets *B, int from, int to, int pt)
+{
+    if (from < 0 || from >= B->cap || B->b[from].live == 0) {
+        printf("### ERROR: This list is empty! %s : %d\n", __FILE__, __LINE__);
+        return;
+    }
+    if (--B->b[from].live == 0) B->b[from].head = B->b[from].tail = 0;
+    bucket_insert(B, to, pt);
 }
 
 /* Head point of the largest non-empty bucket, or -1 if every bucket is empty. */
@@ -369,9 +381,8 @@ static int rs_split(const SSS_MAT *A, SSS_IMAT *S, SSS_IVEC *vertices)
             for (int r = S->row_ptr[j]; r < S->row_ptr[j + 1]; ++r) {
                 int k = S->col_idx[r];
                 if (P[k].mark != UNPT) continue;
-                bucket_remove(&B, P[k].lambda, k);
+                bucket_move(&B, P[k].lambda, P[k].lambda + 1, k);
                 P[k].lambda++;
-                bucket_insert(&B, P[k].lambda, k);
             }
         }
         /* points that strongly influence c lose one unit of measure */
@@ -379,20 +390,20 @@ static int rs_split(const SSS_MAT *A, SSS_IMAT *S, SSS_IVEC *vertices)
             int j = S->col_idx[q], m;
             if (P[j].mark != UNPT) continue;
             m = P[j].lambda;
-            bucket_remove(&B, m, j);
-            P[j].lambda = --m;
-            if (m > 0) {
-                bucket_insert(&B, m, j);
+            if (m - 1 > 0) {
+                bucket_move(&B, m, m - 1, j);
+                P[j].lambda = m - 1;
                 continue;
             }
+            bucket_remove(&B, m, j);
+            P[j].lambda = --m;
             P[j].mark = FGPT;
             undecided--;
             for (int r = S->row_ptr[j]; r < S->row_ptr[j + 1]; ++r) {
                 int k = S->col_idx[r];
                 if (P[k].mark != UNPT) continue;
-                bucket_remove(&B, P[k].lambda, k);
+                bucket_move(&B, P[k].lambda, P[k].lambda + 1, k);
                 P[k].lambda++;
-                bucket_insert(&B, P[k].lambda, k);
             }
         }
     }
