@@ -38,6 +38,7 @@
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
+#include <map>
 #include <string>
 #include <type_traits>
 
@@ -135,7 +136,8 @@ __global__ __launch_bounds__(kBlock) void gs_flow_group(int nchunks, const int *
                                                         const int *__restrict__ ci, const double *__restrict__ v,
                                                         const double *__restrict__ b, double *x,
                                                         const double *__restrict__ deff, unsigned long long *gran,
-                                                        int lo, int hi, unsigned *ctl, unsigned *err, int spin, int ovl)
+                                                        int lo, int hi, unsigned *ctl, unsigned *err, int spin, int ovl,
+                                                        unsigned long long *trace)
 {
     constexpr int R = 64 / G, CAP = kGroupBuf / R, U = 8;
     // a same-pass row this row reads the NEW value of (published by its granules)
@@ -147,16 +149,20 @@ __global__ __launch_bounds__(kBlock) void gs_flow_group(int nchunks, const int *
     const unsigned epoch = __hip_atomic_load(&ctl[kCtlEpoch], RLX_AGENT) + 1u;
     for (;;) {
         const int q = flow_ticket(ctl);
+        // diagnostic builds (SSS_GS_TRACE): per row, 100 MHz stamps at the ticket, after staging, at the publish
+        const unsigned long long t_ticket = trace ? __builtin_amdgcn_s_memrealtime() : 0ull;
+        unsigned long long t_staged = 0ull;
         if (q >= nchunks) break;
         const int p = ck[q] + grp;
         const bool active = p < ck[q + 1];
         int i = -1, k0 = 0, len = 0;
-        double acc = 0.0;
+        double acc = 0.0, dr = 0.0;
         if (active) {
             i = rows[p];
             k0 = rp[i];
             len = rp[i + 1] - k0;
             acc = b[i];
+            dr = deff[i];   // loaded now: after the chain it would be a round trip on the critical path
         }
         int maxlen = len;
         for (int off = 32; off > 0; off >>= 1) maxlen = max(maxlen, __shfl_xor(maxlen, off, 64));
@@ -211,6 +217,7 @@ __global__ __launch_bounds__(kBlock) void gs_flow_group(int nchunks, const int *
                 wave_sync();
                 continue;
             }
+            if (trace && base == 0) t_staged = __builtin_amdgcn_s_memrealtime();
             // (B) and (C) interleaved: the row's first lane chains over the prefix of entries whose
             // products are staged while the pending granules are polled, the poll loads issued
             // before each chain segment and read after it.  The chain still adds every product in
@@ -224,7 +231,10 @@ __global__ __launch_bounds__(kBlock) void gs_flow_group(int nchunks, const int *
                 for (int off = G / 2; off > 0; off >>= 1) first = min(first, __shfl_xor(first, off, 64));
                 const int lim = min(first, m);
                 // issue this lane's two lowest pending polls (column from LDS, granule halves, value)
-                constexpr int NP = 2;
+#ifndef SSS_GS_NP
+#define SSS_GS_NP 2
+#endif
+                constexpr int NP = SSS_GS_NP;
                 int tp[NP];
                 unsigned long long ga[NP], gc[NP];
                 double ap[NP];
@@ -282,11 +292,16 @@ __global__ __launch_bounds__(kBlock) void gs_flow_group(int nchunks, const int *
             wave_sync();
         }
         if (active && gl == 0) {
-            const double d = deff[i];
+            const double d = dr;
             // natural order (Solve/SSS_smooth.c:112): x_i = t * d, d the carried reciprocal
             const double xn = NAT ? acc * d : fabs(d) > SMALLFLOAT ? acc / d : x_own(x, i);
-            x[i] = xn;
+            // the granules first: this pass's readers of x_i wait on them, x itself is read later
             granule_put(gran + 2 * (size_t)(i - lo), epoch, xn);
+            if (trace) {
+                unsigned long long *tr = trace + 4 * (size_t)p;
+                tr[0] = t_ticket, tr[1] = t_staged, tr[2] = __builtin_amdgcn_s_memrealtime(), tr[3] = (unsigned)len;
+            }
+            x[i] = xn;
         }
     }
     flow_exit(ctl, epoch, err, spin);
@@ -528,6 +543,43 @@ static bool gs_overlap_on()
     return on;
 }
 
+// Diagnostic builds only (make EXTRA=-DSSS_GS_TRACE): each flow pass writes its rows' stamps to a
+// buffer that gs_trace_dump appends, with the pass's depth offsets, to $SSS_GS_TRACE_FILE.
+#ifdef SSS_GS_TRACE
+static std::map<const PassSchedule *, unsigned long long *> &gs_traces()
+{
+    static std::map<const PassSchedule *, unsigned long long *> m;
+    return m;
+}
+static unsigned long long *gs_trace_buf(const PassSchedule &ps)
+{
+    auto &m = gs_traces();
+    auto it = m.find(&ps);
+    if (it != m.end()) return it->second;
+    unsigned long long *d = dev_alloc<unsigned long long>(4 * (size_t)std::max(ps.nrows, 1));
+    m[&ps] = d;
+    return d;
+}
+static void gs_trace_dump(const PassSchedule &ps, hipStream_t s)
+{
+    const char *f = getenv("SSS_GS_TRACE_FILE");
+    if (!f || hipStreamSynchronize(s) != hipSuccess) return;
+    std::vector<unsigned long long> h(4 * (size_t)ps.nrows);
+    if (hipMemcpy(h.data(), gs_trace_buf(ps), sizeof(unsigned long long) * h.size(), hipMemcpyDeviceToHost) != hipSuccess)
+        return;
+    FILE *fp = fopen(f, "ab");
+    if (!fp) return;
+    const int hdr[2] = {ps.nrows, ps.depth};
+    fwrite(hdr, sizeof hdr, 1, fp);
+    fwrite(ps.h_off.data(), sizeof(int), (size_t)ps.depth + 1, fp);
+    fwrite(h.data(), sizeof(unsigned long long), h.size(), fp);
+    fclose(fp);
+}
+#else
+static unsigned long long *gs_trace_buf(const PassSchedule &) { return nullptr; }
+static void gs_trace_dump(const PassSchedule &, hipStream_t) {}
+#endif
+
 int gs_persist_run(const PassSchedule &ps, const DevCSR &A, const double *b, double *x, const double *deff,
                    hipStream_t s)
 {
@@ -538,7 +590,8 @@ int gs_persist_run(const PassSchedule &ps, const DevCSR &A, const double *b, dou
     } else if (g.engine == 1) {
         auto go = [&](auto kern) {
             hipLaunchKernelGGL(kern, dim3(g.grid), dim3(kBlock), 0, s, g.nchunks, g.ck, ps.rows, A.rp, A.ci, A.v, b, x,
-                               deff, g.gran, g.lo, g.hi, g.ctl, g.err, g.spin, g.overlap && gs_overlap_on() ? 1 : 0);
+                               deff, g.gran, g.lo, g.hi, g.ctl, g.err, g.spin, g.overlap && gs_overlap_on() ? 1 : 0,
+                               gs_trace_buf(ps));
         };
         auto by_g = [&](auto nat, auto desc) {
             constexpr bool N = decltype(nat)::value, D = decltype(desc)::value;
@@ -555,6 +608,7 @@ int gs_persist_run(const PassSchedule &ps, const DevCSR &A, const double *b, dou
         if (g.natural && g.desc) by_g(T(), T());
         else if (g.natural) by_g(T(), F());
         else by_g(F(), F());
+        gs_trace_dump(ps, s);
     } else {
         return ERROR_INPUT_PAR;
     }
