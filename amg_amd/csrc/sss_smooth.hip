@@ -567,6 +567,70 @@ __device__ __forceinline__ void relax_range_ell(int blo, const int2 *__restrict_
     }
 }
 
+// relax_range_ell for W = 8 with two consecutive rows per thread (sss_spmv_dev.hpp ell_pair_rows):
+// every row's arithmetic exactly as relax_range_ell's, x / y / rr / b moved as 16-byte pairs.
+template <int MODE>
+__device__ __forceinline__ void relax_range_ell2(int blo, const int2 *__restrict__ blk, int lo,
+                                                 const double *__restrict__ b, double *x, double *__restrict__ y,
+                                                 const double *__restrict__ deff, double *__restrict__ rr,
+                                                 double *__restrict__ partial, XSrc xs, const DevDict &dt)
+{
+    __shared__ EllSmem es[2];
+    const int g = dt.remap ? xcd_remap(blockIdx.x, gridDim.x) : (int)blockIdx.x;
+    const EllPairRows pr = ell_pair_rows(blk, blo + 2 * g, dt.bend);
+    unsigned w[2][2];
+    double br[2], dr[2] = {0.0, 0.0};
+    ell_pair_codes(dt.ell, pr, w);   // every row's codes, b and divisor in flight across the barrier
+    pair_load(b, pr.r, pr.l0, pr.l1, br);
+    if (deff) pair_load(deff, pr.r, pr.l0, pr.l1, dr);
+    if (pr.v0) ell_load_dicts_nosync(dt, pr.b0, es[0]);
+    if (pr.v1) ell_load_dicts_nosync(dt, pr.b0 + 1, es[1]);
+    __syncthreads();
+    double xo[2] = {0.0, 0.0}, ro[2] = {0.0, 0.0}, sq[2] = {0.0, 0.0};
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+        const int rj = pr.r + i;
+        if (!(i == 0 ? pr.l0 : pr.l1)) continue;
+        const int j = rj < pr.mid ? 0 : 1;
+        double p[8];
+        int dsl;
+        double dv;
+        const int len = ell_decode<8, MODE == 3>(w[i], rj, es[j], [&](int c) -> double { return xs(c); }, p, dsl, dv);
+        const double acc = dsl < 0 ? ell_sub(br[i], p, 0, len) : ell_sub(ell_sub(br[i], p, 0, dsl), p, dsl + 1, len);
+        const double d = deff ? dr[i] : dv;
+        if constexpr (MODE == 2) {
+            const double xn = fabs(d) > SMALLFLOAT ? acc / d : x[rj];
+            xo[i] = xn;
+            double t = ell_add(0.0, p, 0, dsl);
+            t += d * xn;
+            t = ell_add(t, p, dsl + 1, len);
+            ro[i] = br[i] + t * -1.0;
+            sq[j] += ro[i] * ro[i];
+        } else if constexpr (MODE == 3) {
+            ro[i] = br[i] + ell_add(0.0, p, 0, len) * -1.0;
+            sq[j] += ro[i] * ro[i];
+            xo[i] = fabs(d) > SMALLFLOAT ? acc / d : x[rj];
+        } else if constexpr (MODE == 1) {
+            xo[i] = fabs(d) > SMALLFLOAT ? acc / d : xs(rj);
+        } else {
+            xo[i] = fabs(d) > SMALLFLOAT ? acc / d : x[rj];   // (a row with |d| <= 1e-20 keeps its value)
+        }
+    }
+    if constexpr (MODE == 0 || MODE == 2) pair_store(x, pr.r, pr.l0, pr.l1, xo);
+    if constexpr (MODE == 1 || MODE == 3) pair_store(y, pr.r - lo, pr.l0, pr.l1, xo);
+    if constexpr (MODE >= 2) pair_store(rr, pr.r, pr.l0, pr.l1, ro);
+    if constexpr (MODE >= 2) {
+        if (partial && pr.v0) {   // (uniform over the workgroup)
+            const double t0 = block_sum(sq[0], es[0].red);
+            if (threadIdx.x == 0) partial[pr.b0] = t0;
+            if (pr.v1) {
+                const double t1 = block_sum(sq[1], es[1].red);
+                if (threadIdx.x == 0) partial[pr.b0 + 1] = t1;
+            }
+        }
+    }
+}
+
 // Column ELL rows (DICT = kXell + W): relax_range_ell's per-row arithmetic, one row block per
 // workgroup, the row's products in registers from its explicit-column codes.
 template <int MODE, int W>
@@ -600,10 +664,11 @@ __device__ __forceinline__ void relax_range_xell(int blo, const int2 *__restrict
     if (live) {
         double xv[W];
         int dsl;
-        const int len = xell_gather<W, MODE == 3>(w, r, dt.xshift, [&](int c) -> double { return xs(c); }, xv, dsl);
+        unsigned dcode;
+        const int len = xell_gather<W, MODE == 3>(w, r, dt.xshift, [&](int c) -> double { return xs(c); }, xv, dsl, dcode);
         const double acc = dsl < 0 ? xell_sub(br, w, xv, es, dt.xshift, 0, len)
                                    : xell_sub(xell_sub(br, w, xv, es, dt.xshift, 0, dsl), w, xv, es, dt.xshift, dsl + 1, len);
-        const double dv = dsl < 0 ? 0.0 : es.vd[w[dsl] >> dt.xshift];
+        const double dv = dsl < 0 ? 0.0 : es.vd[dcode >> dt.xshift];
         const double d = deff ? dr : dv;
         if constexpr (MODE == 2) {
             const double xn = fabs(d) > SMALLFLOAT ? acc / d : x[r];
@@ -646,6 +711,8 @@ __device__ __forceinline__ void relax_range_body(int blo, const int2 *__restrict
 {
     if constexpr (DICT >= kXell) {
         relax_range_xell<MODE, DICT - kXell>(blo, blk, lo, b, x, y, deff, rr, partial, xs, dt);
+    } else if constexpr (DICT == 8 && kEllPairs) {
+        relax_range_ell2<MODE>(blo, blk, lo, b, x, y, deff, rr, partial, xs, dt);
     } else if constexpr (DICT >= 8) {
         relax_range_ell<MODE, DICT>(blo, blk, lo, b, x, y, deff, rr, partial, xs, dt);
     } else {

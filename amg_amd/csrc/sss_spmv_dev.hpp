@@ -148,6 +148,79 @@ __device__ __forceinline__ int ell_row(const unsigned char *__restrict__ ell, in
     ell_codes<W>(ell, r, w);
     return ell_decode<W>(w, r, es, fetch, p, dslot, dval);
 }
+// ---- dictionary ELL, two consecutive rows per thread (W = 8) --------------------------------------
+// A workgroup covers its kEllRpt = 2 row blocks as one run of rows [ra, re) (the blocks are
+// consecutive: the first ends where the second starts, at `mid`); thread t takes rows ra + 2t and
+// ra + 2t + 1, so the codes of both rows come in one 16-byte load and b, x, y move as 16-byte pairs
+// (loads and stores of 8-byte aligned pairs: gfx950 takes them unaligned).  Each row is decoded
+// with its own block's dictionaries and summed exactly as ell_decode / ell_add do: bitwise the
+// one-row-per-thread kernels.  tools/l0_lab.hip (7-pt 400^3, relabeled level 0): residual
+// 589 -> 542 us, class pass 290 -> 284 us.  SSS_ELL_PAIRS=0 at build time: one row per thread.
+#ifndef SSS_ELL_PAIRS
+#define SSS_ELL_PAIRS 1
+#endif
+constexpr bool kEllPairs = SSS_ELL_PAIRS != 0 && kEllRpt == 2;
+struct alignas(8) CodePair {
+    unsigned x, y, z, w;
+};
+struct alignas(8) DoublePair {
+    double a, b;
+};
+struct EllPairRows {
+    int r = 0, mid = 0;             // first row of the pair; first row of the workgroup's second block
+    bool l0 = false, l1 = false;    // rows r, r + 1 exist
+    bool v0 = false, v1 = false;    // the workgroup's blocks exist
+    int b0 = 0;                     // the first block
+};
+__device__ __forceinline__ EllPairRows ell_pair_rows(const int2 *__restrict__ blk, int b0, int bend)
+{
+    EllPairRows p;
+    p.b0 = b0;
+    p.v0 = b0 < bend;
+    p.v1 = b0 + 1 < bend;
+    if (!p.v0) return p;
+    const int ra = blk[b0].x;
+    p.mid = blk[b0 + 1].x;
+    const int re = p.v1 ? blk[b0 + 2].x : p.mid;
+    p.r = ra + 2 * (int)threadIdx.x;
+    p.l0 = p.r < re;
+    p.l1 = p.r + 1 < re;
+    return p;
+}
+// the pair's codes (rows r, r + 1), 0xFF... where a row does not exist
+__device__ __forceinline__ void ell_pair_codes(const unsigned char *__restrict__ ell, const EllPairRows &p,
+                                               unsigned (&w)[2][2])
+{
+    w[0][0] = w[0][1] = w[1][0] = w[1][1] = 0xffffffffu;
+    if (p.l1) {
+        const CodePair q = *reinterpret_cast<const CodePair *>(ell + (size_t)p.r * 8);
+        w[0][0] = q.x, w[0][1] = q.y, w[1][0] = q.z, w[1][1] = q.w;
+    } else if (p.l0) {
+        const uint2 q = *reinterpret_cast<const uint2 *>(ell + (size_t)p.r * 8);
+        w[0][0] = q.x, w[0][1] = q.y;
+    }
+}
+__device__ __forceinline__ void pair_load(const double *__restrict__ v, int r, bool l0, bool l1, double (&o)[2])
+{
+    o[0] = o[1] = 0.0;
+    if (l1) {
+        const DoublePair q = *reinterpret_cast<const DoublePair *>(v + r);
+        o[0] = q.a, o[1] = q.b;
+    } else if (l0) {
+        o[0] = v[r];
+    }
+}
+__device__ __forceinline__ void pair_store(double *v, int r, bool l0, bool l1, const double (&o)[2])
+{
+    if (l1) {
+        DoublePair q;
+        q.a = o[0], q.b = o[1];
+        *reinterpret_cast<DoublePair *>(v + r) = q;
+    } else if (l0) {
+        v[r] = o[0];
+    }
+}
+
 // ---- column ELL: one thread per row, explicit columns ------------------------------------------
 // Row r's W codes  value index << S | column  (0xFFFFFFFF pads) at xell[r * W], S = DevDict::xshift
 // (the column bits of the matrix, >= 23), into the block's value dictionary (<= 2^(32 - S), at most
@@ -179,62 +252,80 @@ __device__ __forceinline__ void xell_codes(const unsigned *__restrict__ xell, in
 // stay in registers.
 template <int W, bool DIAG = true, class Fetch>
 __device__ __forceinline__ int xell_gather(const unsigned (&w)[W], int r, int shift, Fetch fetch, double (&xv)[W],
-                                           int &dslot)
+                                           int &dslot, unsigned &dcode)
 {
     const unsigned mask = (1u << shift) - 1;
     int len = W;
     dslot = -1;
+    dcode = 0u;
 #pragma unroll
     for (int s = 0; s < W; ++s)
         if (w[s] == 0xffffffffu && len == W) len = s;
 #pragma unroll
     for (int s = 0; s < W; ++s)
-        if (s < len && (int)(w[s] & mask) == r) dslot = s;
+        if (s < len && (int)(w[s] & mask) == r) dslot = s, dcode = w[s];
 #pragma unroll
     for (int s = 0; s < W; ++s) xv[s] = (s < len && (DIAG || s != dslot)) ? fetch((int)(w[s] & mask)) : 0.0;
     return len;
 }
-template <int W>
-__device__ __forceinline__ double xell_prod(const unsigned (&w)[W], const double (&xv)[W], const XellSmem &es, int shift,
-                                            int s)
+template <int W, bool DIAG = true, class Fetch>
+__device__ __forceinline__ int xell_gather(const unsigned (&w)[W], int r, int shift, Fetch fetch, double (&xv)[W],
+                                           int &dslot)
 {
-    return es.vd[w[s] >> shift] * xv[s];
+    unsigned dcode;
+    return xell_gather<W, DIAG>(w, r, shift, fetch, xv, dslot, dcode);
 }
-// s0 + (or -) the products of slots [a, e) in slot order
+// s0 + (or -) the products a_s * xv[s] of slots [a, e) in slot order, a_s = the block's value of slot
+// s (LDS).  Branch-free: every slot's LDS value is read first (slots outside [a, e) read entry 0) and
+// each step is a select, so the chain is a run of dependent fp64 operations -- with a branch per
+// slot the compiler waited for each slot's LDS read in turn (the level-1 kernels were issue-bound).
+template <bool SUB, int W>
+__device__ __forceinline__ double xell_sum(double s0, const unsigned (&w)[W], const double (&xv)[W], const XellSmem &es,
+                                           int shift, int a, int e)
+{
+    double av[W];
+#pragma unroll
+    for (int s = 0; s < W; ++s) av[s] = es.vd[(s >= a && s < e) ? (w[s] >> shift) : 0u];
+#pragma unroll
+    for (int s = 0; s < W; ++s) {
+        const double p = av[s] * xv[s];
+        const double t = SUB ? s0 - p : s0 + p;
+        s0 = (s >= a && s < e) ? t : s0;
+    }
+    return s0;
+}
 template <int W>
 __device__ __forceinline__ double xell_add(double s0, const unsigned (&w)[W], const double (&xv)[W], const XellSmem &es,
                                            int shift, int a, int e)
 {
-#pragma unroll
-    for (int s = 0; s < W; ++s)
-        if (s >= a && s < e) s0 += xell_prod(w, xv, es, shift, s);
-    return s0;
+    return xell_sum<false>(s0, w, xv, es, shift, a, e);
 }
 template <int W>
 __device__ __forceinline__ double xell_sub(double s0, const unsigned (&w)[W], const double (&xv)[W], const XellSmem &es,
                                            int shift, int a, int e)
 {
-#pragma unroll
-    for (int s = 0; s < W; ++s)
-        if (s >= a && s < e) s0 -= xell_prod(w, xv, es, shift, s);
-    return s0;
+    return xell_sum<true>(s0, w, xv, es, shift, a, e);
 }
 
-// sum of p[a, e) from s0 in slot order
+// sum of p[a, e) from s0 in slot order (branch-free: a select per slot)
 template <int W>
 __device__ __forceinline__ double ell_add(double s0, const double (&p)[W], int a, int e)
 {
 #pragma unroll
-    for (int s = 0; s < W; ++s)
-        if (s >= a && s < e) s0 += p[s];
+    for (int s = 0; s < W; ++s) {
+        const double t = s0 + p[s];
+        s0 = (s >= a && s < e) ? t : s0;
+    }
     return s0;
 }
 template <int W>
 __device__ __forceinline__ double ell_sub(double s0, const double (&p)[W], int a, int e)
 {
 #pragma unroll
-    for (int s = 0; s < W; ++s)
-        if (s >= a && s < e) s0 -= p[s];
+    for (int s = 0; s < W; ++s) {
+        const double t = s0 - p[s];
+        s0 = (s >= a && s < e) ? t : s0;
+    }
     return s0;
 }
 
@@ -812,18 +903,24 @@ __device__ __forceinline__ void merged_sums(int k0, int k1, const unsigned *__re
     for (int u = 0; u < G; ++u) s0[u] = 0.0, s1[u] = 0.0;
     for (int k = k0 + lane; k < k1; k += 64 * U) {
         unsigned q[U];
-        double a[U];
+        double a[U], pv[U];
+        // every load unconditional (clamped into the group) and every product formed before any is
+        // added: with the gather under a per-entry `break` the compiler waited for each in turn.  An
+        // entry past the group adds +0.0 to row 0's accumulator -- an exact identity, as the +0.0s
+        // every entry already adds to the other rows' accumulators (no accumulator is ever -0.0)
 #pragma unroll
         for (int t = 0; t < U; ++t) {
-            const int kk = k + 64 * t;
-            q[t] = kk < k1 ? mk[kk] : 0u;
-            a[t] = kk < k1 ? mv[kk] : 0.0;
+            const int kk = k + 64 * t, kc = kk < k1 ? kk : k1 - 1;
+            q[t] = mk[kc];
+            a[t] = mv[kc];
         }
 #pragma unroll
+        for (int t = 0; t < U; ++t) pv[t] = prod((int)(q[t] >> kMergeShift), a[t]);
+#pragma unroll
         for (int t = 0; t < U; ++t) {
-            if (k + 64 * t >= k1) break;
-            const double p = prod((int)(q[t] >> kMergeShift), a[t]);
-            const unsigned key = q[t] & ((1u << kMergeShift) - 1);
+            const bool live = k + 64 * t < k1;
+            const double p = live ? pv[t] : 0.0;
+            const unsigned key = live ? q[t] & ((1u << kMergeShift) - 1) : 0u;
 #pragma unroll
             for (int u = 0; u < G; ++u) {
                 s0[u] += key == (unsigned)u ? p : 0.0;
