@@ -903,13 +903,14 @@ __global__ __launch_bounds__(kBlock) void ts_stage0(int lo, DevCSR M, const int 
         const int q = ba.x + (int)threadIdx.x;
         const bool live = q < be.x;
         unsigned w[W];
-        double bq_v = 0.0;
+        double bq_v = 0.0, dq = 0.0;
         int sp = 0;
 #pragma unroll
         for (int t = 0; t < W; ++t) w[t] = 0xffffffffu;
-        if (live) {   // the row's codes, b and its [N | L] cut in flight across the barrier
+        if (live) {   // the row's codes, b, divisor and its [N | L] cut in flight across the barrier
             xell_codes<W>(M.dv_xell, q, w);
             bq_v = b[lo + q];
+            dq = deff[lo + q];
             sp = split[q] - M.rp[q];
         }
         {
@@ -923,7 +924,8 @@ __global__ __launch_bounds__(kBlock) void ts_stage0(int lo, DevCSR M, const int 
             const int len = xell_gather<W>(w, -1, M.xell_shift, [&](int c) -> double { return x(c); }, xv, ds);
             const double Pq = xell_sub(bq_v, w, xv, es, M.xell_shift, 0, sp);
             P[q] = Pq;
-            finish(q, xell_sub(Pq, w, xv, es, M.xell_shift, sp, len));
+            const double acc = xell_sub(Pq, w, xv, es, M.xell_shift, sp, len);
+            y[q] = fabs(dq) > SMALLFLOAT ? acc / dq : x(lo + q);   // finish() with the divisor loaded early
         }
         return;
     } else if constexpr (PATH >= 3) {   // merged row groups, G = PATH, M.mg_W waves per group
@@ -1038,12 +1040,13 @@ __global__ __launch_bounds__(kBlock) void ts_inner(int lo, DevCSR M, const doubl
         const int q = ba.x + (int)threadIdx.x;
         const bool live = q < be.x;
         unsigned w[W];
-        double pq = 0.0;
+        double pq = 0.0, dq = 0.0;
 #pragma unroll
         for (int t = 0; t < W; ++t) w[t] = 0xffffffffu;
-        if (live) {
+        if (live) {   // codes, P_q and the divisor in flight across the barrier
             xell_codes<W>(M.dv_xell, q, w);
             pq = P[q];
+            dq = deff[lo + q];
         }
         {
             const int4 pq4 = M.dv_pd[bq];
@@ -1054,7 +1057,8 @@ __global__ __launch_bounds__(kBlock) void ts_inner(int lo, DevCSR M, const doubl
             double xv[W];
             int ds;
             const int len = xell_gather<W>(w, -1, M.xell_shift, fetch, xv, ds);
-            finish(q, xell_sub(pq, w, xv, es, M.xell_shift, 0, len));
+            const double acc = xell_sub(pq, w, xv, es, M.xell_shift, 0, len);
+            y[q] = fabs(dq) > SMALLFLOAT ? acc / dq : ykeep[q];   // finish() with the divisor loaded early
         }
         return;
     } else if constexpr (PATH >= 3) {   // merged row groups, G = PATH, M.mg_W waves per group

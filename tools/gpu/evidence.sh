@@ -1,13 +1,16 @@
-# Evidence at HEAD on one GPU: level-0 PMC traffic (both storages) into profiles/r03_level0_spmv_pmc.json
-# (the bench reads the newest such file for roofline.traffic), smoke, the default bench, the
-# kernel-trace profile of a short bench with its per-level split, and the SQ occupancy/stall pass.
-# COMMIT (env): the commit the tree is at (stamped into the PMC file).
+# Evidence at HEAD on one GPU lease (ROUND, default r04; COMMIT stamped into the PMC file):
+#  1. level-0 PMC traffic of both storages -> profiles/${ROUND}_level0_spmv_pmc.json (the bench reads
+#     the newest such file for roofline.traffic)
+#  2. smoke, then the default bench -> gpurun_out/bench.json
+#  3. the kernel-trace profile of a short bench with its per-level split (prof.sh)
+#  4. the SQ occupancy / stall pass (pmc_sq.sh)
 cd "$GRAFT_REPO_ROOT" || exit 1
 export TMPDIR=/tmp
+ROUND=${ROUND:-r04}
 mkdir -p gpurun_out
 bash tools/gpu/pmc.sh || exit 1
-python3 tools/pmc_summarize.py gpurun_out profiles/r03_level0_spmv_pmc.json "${COMMIT:-unknown}" > /dev/null || exit 1
-cp profiles/r03_level0_spmv_pmc.json gpurun_out/level0_spmv_pmc.json
+python3 tools/pmc_summarize.py gpurun_out profiles/${ROUND}_level0_spmv_pmc.json "${COMMIT:-unknown}" > /dev/null || exit 1
+cp profiles/${ROUND}_level0_spmv_pmc.json gpurun_out/level0_spmv_pmc.json
 rm -rf gpurun_out/pmc_FETCH_SIZE gpurun_out/pmc_WRITE_SIZE
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 || { tail -20 gpurun_out/smoke.log; exit 1; }
 echo smoke-ok
