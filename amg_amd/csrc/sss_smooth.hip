@@ -922,9 +922,9 @@ __global__ __launch_bounds__(kBlock) void ts_stage0(int lo, DevCSR M, const int 
             double xv[W];
             int ds;
             const int len = xell_gather<W>(w, -1, M.xell_shift, [&](int c) -> double { return x(c); }, xv, ds);
-            const double Pq = xell_sub(bq_v, w, xv, es, M.xell_shift, 0, sp);
+            const double Pq = xell_sum_bf<true>(bq_v, w, xv, es, M.xell_shift, 0, sp);
             P[q] = Pq;
-            const double acc = xell_sub(Pq, w, xv, es, M.xell_shift, sp, len);
+            const double acc = xell_sum_bf<true>(Pq, w, xv, es, M.xell_shift, sp, len);
             y[q] = fabs(dq) > SMALLFLOAT ? acc / dq : x(lo + q);   // finish() with the divisor loaded early
         }
         return;

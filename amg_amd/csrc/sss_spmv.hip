@@ -1093,7 +1093,7 @@ __global__ __launch_bounds__(kBlock) void spmv_adaptive(const int2 *__restrict__
             const double t = block_sum(sq, es.red);
             if (threadIdx.x == 0) partial[bid] = t;
         }
-    } else if constexpr (DICT == 8 && kEllPairs) {   // dictionary ELL, two consecutive rows per thread
+    } else if constexpr (DICT == 8 && kEllPairs && kEllPairsSpmv) {   // dictionary ELL, two consecutive rows per thread
         __shared__ EllSmem es[2];
         const int g = dt.remap ? xcd_remap(blockIdx.x, gridDim.x) : (int)blockIdx.x;
         const EllPairRows pr = ell_pair_rows(blk, 2 * g, dt.bend);

@@ -160,6 +160,13 @@ __device__ __forceinline__ int ell_row(const unsigned char *__restrict__ ell, in
 #define SSS_ELL_PAIRS 1
 #endif
 constexpr bool kEllPairs = SSS_ELL_PAIRS != 0 && kEllRpt == 2;
+// ... in the relaxation kernels; the residual SpMV keeps one row per thread: measured in the cycle
+// at 400^3 the pairs took the relaxation passes 3.5-4.6 % faster but the F-row residual 5 % slower
+// (280 -> 294 us per V-cycle), so the SpMV path is off unless built with SSS_ELL_PAIRS_SPMV=1
+#ifndef SSS_ELL_PAIRS_SPMV
+#define SSS_ELL_PAIRS_SPMV 0
+#endif
+constexpr bool kEllPairsSpmv = SSS_ELL_PAIRS_SPMV != 0;
 struct alignas(8) CodePair {
     unsigned x, y, z, w;
 };
@@ -276,12 +283,13 @@ __device__ __forceinline__ int xell_gather(const unsigned (&w)[W], int r, int sh
     return xell_gather<W, DIAG>(w, r, shift, fetch, xv, dslot, dcode);
 }
 // s0 + (or -) the products a_s * xv[s] of slots [a, e) in slot order, a_s = the block's value of slot
-// s (LDS).  Branch-free: every slot's LDS value is read first (slots outside [a, e) read entry 0) and
-// each step is a select, so the chain is a run of dependent fp64 operations -- with a branch per
-// slot the compiler waited for each slot's LDS read in turn (the level-1 kernels were issue-bound).
+// s (LDS).  Branch-free form: every slot's LDS value is read first (slots outside [a, e) read entry 0)
+// and each step is a select.  It holds W more doubles live than the per-slot form (xell_add /
+// xell_sub): measured at 400^3 the two-stage stage-0 kernel ran 4 % faster with it, the level-1
+// relaxation (122 VGPRs instead of 70: 4 waves per SIMD instead of 7) 3 % slower, so only the former uses it.
 template <bool SUB, int W>
-__device__ __forceinline__ double xell_sum(double s0, const unsigned (&w)[W], const double (&xv)[W], const XellSmem &es,
-                                           int shift, int a, int e)
+__device__ __forceinline__ double xell_sum_bf(double s0, const unsigned (&w)[W], const double (&xv)[W], const XellSmem &es,
+                                              int shift, int a, int e)
 {
     double av[W];
 #pragma unroll
@@ -298,13 +306,19 @@ template <int W>
 __device__ __forceinline__ double xell_add(double s0, const unsigned (&w)[W], const double (&xv)[W], const XellSmem &es,
                                            int shift, int a, int e)
 {
-    return xell_sum<false>(s0, w, xv, es, shift, a, e);
+#pragma unroll
+    for (int s = 0; s < W; ++s)
+        if (s >= a && s < e) s0 += es.vd[w[s] >> shift] * xv[s];
+    return s0;
 }
 template <int W>
 __device__ __forceinline__ double xell_sub(double s0, const unsigned (&w)[W], const double (&xv)[W], const XellSmem &es,
                                            int shift, int a, int e)
 {
-    return xell_sum<true>(s0, w, xv, es, shift, a, e);
+#pragma unroll
+    for (int s = 0; s < W; ++s)
+        if (s >= a && s < e) s0 -= es.vd[w[s] >> shift] * xv[s];
+    return s0;
 }
 
 // sum of p[a, e) from s0 in slot order (branch-free: a select per slot)
@@ -901,13 +915,36 @@ __device__ __forceinline__ void merged_sums(int k0, int k1, const unsigned *__re
     const int lane = threadIdx.x & 63;
 #pragma unroll
     for (int u = 0; u < G; ++u) s0[u] = 0.0, s1[u] = 0.0;
-    for (int k = k0 + lane; k < k1; k += 64 * U) {
+    for (int k = k0 + lane; k < k1 && S == 2; k += 64 * U) {   // two segments (the two-stage split copies)
+        unsigned q[U];
+        double a[U];
+#pragma unroll
+        for (int t = 0; t < U; ++t) {
+            const int kk = k + 64 * t;
+            q[t] = kk < k1 ? mk[kk] : 0u;
+            a[t] = kk < k1 ? mv[kk] : 0.0;
+        }
+#pragma unroll
+        for (int t = 0; t < U; ++t) {
+            if (k + 64 * t >= k1) break;
+            const double p = prod((int)(q[t] >> kMergeShift), a[t]);
+            const unsigned key = q[t] & ((1u << kMergeShift) - 1);
+#pragma unroll
+            for (int u = 0; u < G; ++u) {
+                s0[u] += key == (unsigned)u ? p : 0.0;
+                s1[u] += key == (unsigned)(8 + u) ? p : 0.0;
+            }
+        }
+    }
+    for (int k = k0 + lane; k < k1 && S == 1; k += 64 * U) {
         unsigned q[U];
         double a[U], pv[U];
         // every load unconditional (clamped into the group) and every product formed before any is
         // added: with the gather under a per-entry `break` the compiler waited for each in turn.  An
         // entry past the group adds +0.0 to row 0's accumulator -- an exact identity, as the +0.0s
-        // every entry already adds to the other rows' accumulators (no accumulator is ever -0.0)
+        // every entry already adds to the other rows' accumulators (no accumulator is ever -0.0).
+        // Measured at 400^3: spmv_merged 4 % faster; the two-segment stage-0 kernel (above) 10 %
+        // slower this way, so it keeps the per-entry form
 #pragma unroll
         for (int t = 0; t < U; ++t) {
             const int kk = k + 64 * t, kc = kk < k1 ? kk : k1 - 1;
