@@ -620,14 +620,24 @@ __device__ __forceinline__ void relax_range_ell2(int blo, const int2 *__restrict
     if constexpr (MODE == 1 || MODE == 3) pair_store(y, pr.r - lo, pr.l0, pr.l1, xo);
     if constexpr (MODE >= 2) pair_store(rr, pr.r, pr.l0, pr.l1, ro);
     if constexpr (MODE >= 2) {
+        // per-block sums of squares in the residual SpMV's order (one row per thread, block_sum's
+        // fixed tree): each row's square goes through LDS to the thread that row has there, so the
+        // norm is bitwise the unfused residual's (tests/test_gpu_parity.py test_fused_residual_bitwise)
+        __shared__ double sqrow[2 * kBlock];
         if (partial && pr.v0) {   // (uniform over the workgroup)
-            const double t0 = block_sum(sq[0], es[0].red);
+            const int ra = pr.r - 2 * (int)threadIdx.x;
+            if (pr.l0) sqrow[pr.r - ra] = ro[0] * ro[0];
+            if (pr.l1) sqrow[pr.r + 1 - ra] = ro[1] * ro[1];
+            __syncthreads();
+            const int n0 = pr.mid - ra, n1 = pr.v1 ? ell_block_rows(pr) - n0 : 0;
+            const double t0 = block_sum((int)threadIdx.x < n0 ? sqrow[threadIdx.x] : 0.0, es[0].red);
             if (threadIdx.x == 0) partial[pr.b0] = t0;
             if (pr.v1) {
-                const double t1 = block_sum(sq[1], es[1].red);
+                const double t1 = block_sum((int)threadIdx.x < n1 ? sqrow[n0 + threadIdx.x] : 0.0, es[1].red);
                 if (threadIdx.x == 0) partial[pr.b0 + 1] = t1;
             }
         }
+        (void)sq;
     }
 }
 

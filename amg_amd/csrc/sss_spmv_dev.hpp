@@ -175,6 +175,7 @@ struct alignas(8) DoublePair {
 };
 struct EllPairRows {
     int r = 0, mid = 0;             // first row of the pair; first row of the workgroup's second block
+    int end = 0;                    // one past the workgroup's last row
     bool l0 = false, l1 = false;    // rows r, r + 1 exist
     bool v0 = false, v1 = false;    // the workgroup's blocks exist
     int b0 = 0;                     // the first block
@@ -189,11 +190,14 @@ __device__ __forceinline__ EllPairRows ell_pair_rows(const int2 *__restrict__ bl
     const int ra = blk[b0].x;
     p.mid = blk[b0 + 1].x;
     const int re = p.v1 ? blk[b0 + 2].x : p.mid;
+    p.end = re;
     p.r = ra + 2 * (int)threadIdx.x;
     p.l0 = p.r < re;
     p.l1 = p.r + 1 < re;
     return p;
 }
+// rows of the workgroup's two blocks together
+__device__ __forceinline__ int ell_block_rows(const EllPairRows &p) { return p.end - (p.r - 2 * (int)threadIdx.x); }
 // the pair's codes (rows r, r + 1), 0xFF... where a row does not exist
 __device__ __forceinline__ void ell_pair_codes(const unsigned char *__restrict__ ell, const EllPairRows &p,
                                                unsigned (&w)[2][2])
