@@ -306,23 +306,52 @@ __device__ __forceinline__ double xell_sum_bf(double s0, const unsigned (&w)[W],
     }
     return s0;
 }
+// Per-slot form in groups of XG slots: the group's LDS values read together, then a select per slot
+// (XG = 1: a branch per slot, the group of one value read and waited for inside it)
+#ifndef SSS_XELL_GROUP
+#define SSS_XELL_GROUP 1
+#endif
+template <bool SUB, int W>
+__device__ __forceinline__ double xell_sum_g(double s0, const unsigned (&w)[W], const double (&xv)[W], const XellSmem &es,
+                                             int shift, int a, int e)
+{
+    constexpr int XG = SSS_XELL_GROUP;
+    if constexpr (XG == 1) {
+#pragma unroll
+        for (int s = 0; s < W; ++s)
+            if (s >= a && s < e) s0 = SUB ? s0 - es.vd[w[s] >> shift] * xv[s] : s0 + es.vd[w[s] >> shift] * xv[s];
+    } else {
+#pragma unroll
+        for (int g = 0; g < W; g += XG) {
+            double av[XG];
+#pragma unroll
+            for (int u = 0; u < XG; ++u) {
+                const int s = g + u;
+                av[u] = s < W ? es.vd[(s >= a && s < e) ? (w[s < W ? s : 0] >> shift) : 0u] : 0.0;
+            }
+#pragma unroll
+            for (int u = 0; u < XG; ++u) {
+                const int s = g + u;
+                if (s >= W) break;
+                const double p = av[u] * xv[s];
+                const double t = SUB ? s0 - p : s0 + p;
+                s0 = (s >= a && s < e) ? t : s0;
+            }
+        }
+    }
+    return s0;
+}
 template <int W>
 __device__ __forceinline__ double xell_add(double s0, const unsigned (&w)[W], const double (&xv)[W], const XellSmem &es,
                                            int shift, int a, int e)
 {
-#pragma unroll
-    for (int s = 0; s < W; ++s)
-        if (s >= a && s < e) s0 += es.vd[w[s] >> shift] * xv[s];
-    return s0;
+    return xell_sum_g<false>(s0, w, xv, es, shift, a, e);
 }
 template <int W>
 __device__ __forceinline__ double xell_sub(double s0, const unsigned (&w)[W], const double (&xv)[W], const XellSmem &es,
                                            int shift, int a, int e)
 {
-#pragma unroll
-    for (int s = 0; s < W; ++s)
-        if (s >= a && s < e) s0 -= es.vd[w[s] >> shift] * xv[s];
-    return s0;
+    return xell_sum_g<true>(s0, w, xv, es, shift, a, e);
 }
 
 // sum of p[a, e) from s0 in slot order (branch-free: a select per slot)
