@@ -941,10 +941,10 @@ __global__ __launch_bounds__(kBlock) void ts_stage0(int lo, DevCSR M, const int 
     } else if constexpr (PATH >= 3) {   // merged row groups, G = PATH, M.mg_W waves per group
         constexpr int G = PATH;
         __shared__ double red[8 * G];
-        auto prod = [&](int c, double a) { return a * x(c); };
         int g = 0, u = 0;
         double n_sum = 0.0, l_sum = 0.0;
-        if (merged_block<G, 2>(M.mg_gp, M.mg_ng, M.mg_W, M.mg_k, M.mg_v, prod, red, g, u, n_sum, l_sum)) {
+        if (merged_block<G, 2>(M.mg_gp, M.mg_ng, M.mg_W, M.mg_k, M.mg_v, [&](int c) -> double { return x(c); }, red, g, u,
+                               n_sum, l_sum)) {
             const int q = g * G + u;
             if (q < M.n) {
                 const double Pq = b[lo + q] - n_sum;
@@ -1076,7 +1076,7 @@ __global__ __launch_bounds__(kBlock) void ts_inner(int lo, DevCSR M, const doubl
         __shared__ double red[8 * G];
         int g = 0, u = 0;
         double l_sum = 0.0, unused = 0.0;
-        if (merged_block<G, 1>(M.mg_gp, M.mg_ng, M.mg_W, M.mg_k, M.mg_v, [&](int c, double a) { return a * fetch(c); },
+        if (merged_block<G, 1>(M.mg_gp, M.mg_ng, M.mg_W, M.mg_k, M.mg_v, fetch,
                                red, g, u, l_sum, unused)) {
             const int q = g * G + u;
             if (q < M.n) finish(q, P[q] - l_sum);

@@ -1245,7 +1245,7 @@ __global__ __launch_bounds__(kBlock) void spmv_merged(int n, int ng, int W, cons
     __shared__ double nred[kBlock / 64];
     int g = 0, u = 0;
     double sr = 0.0, unused = 0.0, sq = 0.0;
-    if (merged_block<G, 1>(gp, ng, W, mk, mv, [&](int c, double a) { return a * x[c]; }, red, g, u, sr, unused)) {
+    if (merged_block<G, 1>(gp, ng, W, mk, mv, [&](int c) -> double { return x[c]; }, red, g, u, sr, unused)) {
         const int r = g * G + u;
         if (r < n) {
             bool write = true;

@@ -933,22 +933,25 @@ __device__ __forceinline__ double wave_row_sum(int k0, int k1, const int *__rest
 // flight; lane l accumulates its entries in increasing position into the accumulator of the
 // entry's (segment, row), then each accumulator's 64 lane sums are xor-reduced.  Fixed order:
 // deterministic.  s0[u] / s1[u] = sum over row u's first- / second-segment entries of
-// prod(col, val), valid in every lane (S = 1: single-segment matrices, s1 untouched).
+// val * fetch(col), valid in every lane (S = 1: single-segment matrices, s1 untouched).
 #ifndef SSS_MERGE_U
 #define SSS_MERGE_U 8
 #endif
 // (U, the loads in flight per lane, changes no sum: each lane still adds its entries in increasing
 // position into the same accumulators)
-template <int G, int S, class Prod>
+template <int G, int S, class Fetch>
 __device__ __forceinline__ void merged_sums(int k0, int k1, const unsigned *__restrict__ mk,
-                                            const double *__restrict__ mv, Prod prod, double (&s0)[G],
+                                            const double *__restrict__ mv, Fetch fetch, double (&s0)[G],
                                             double (&s1)[G])
 {
     constexpr int U = SSS_MERGE_U;
     const int lane = threadIdx.x & 63;
 #pragma unroll
     for (int u = 0; u < G; ++u) s0[u] = 0.0, s1[u] = 0.0;
-    for (int k = k0 + lane; k < k1 && S == 2; k += 64 * U) {   // two segments (the two-stage split copies)
+    // two segments (the two-stage split copies, ts_stage0): the product formed where the entry is
+    // added.  Measured at 400^3 (levels 5-6, the longest groups) 8-10 % faster than the form below,
+    // which holds every gather in flight at once (86 VGPRs against 64: 5 waves per SIMD)
+    for (int k = k0 + lane; k < k1 && S == 2; k += 64 * U) {
         unsigned q[U];
         double a[U];
 #pragma unroll
@@ -960,7 +963,7 @@ __device__ __forceinline__ void merged_sums(int k0, int k1, const unsigned *__re
 #pragma unroll
         for (int t = 0; t < U; ++t) {
             if (k + 64 * t >= k1) break;
-            const double p = prod((int)(q[t] >> kMergeShift), a[t]);
+            const double p = a[t] * fetch((int)(q[t] >> kMergeShift));
             const unsigned key = q[t] & ((1u << kMergeShift) - 1);
 #pragma unroll
             for (int u = 0; u < G; ++u) {
@@ -971,13 +974,12 @@ __device__ __forceinline__ void merged_sums(int k0, int k1, const unsigned *__re
     }
     for (int k = k0 + lane; k < k1 && S == 1; k += 64 * U) {
         unsigned q[U];
-        double a[U], pv[U];
-        // every load unconditional (clamped into the group) and every product formed before any is
-        // added: with the gather under a per-entry `break` the compiler waited for each in turn.  An
-        // entry past the group adds +0.0 to row 0's accumulator -- an exact identity, as the +0.0s
-        // every entry already adds to the other rows' accumulators (no accumulator is ever -0.0).
-        // Measured at 400^3: spmv_merged 4 % faster; the two-segment stage-0 kernel (above) 10 %
-        // slower this way, so it keeps the per-entry form
+        double a[U], xv[U];
+        // keys and values loaded unconditionally (clamped into the group), every x gather issued
+        // before any product is formed: with the multiply under each gather's condition the
+        // compiler waited for each gather in turn.  An entry past the group adds +0.0 to row 0's
+        // accumulator -- an exact identity, as the +0.0s every entry adds to the other rows'
+        // accumulators (no accumulator is ever -0.0)
 #pragma unroll
         for (int t = 0; t < U; ++t) {
             const int kk = k + 64 * t, kc = kk < k1 ? kk : k1 - 1;
@@ -985,11 +987,11 @@ __device__ __forceinline__ void merged_sums(int k0, int k1, const unsigned *__re
             a[t] = mv[kc];
         }
 #pragma unroll
-        for (int t = 0; t < U; ++t) pv[t] = prod((int)(q[t] >> kMergeShift), a[t]);
+        for (int t = 0; t < U; ++t) xv[t] = k + 64 * t < k1 ? fetch((int)(q[t] >> kMergeShift)) : 0.0;
 #pragma unroll
         for (int t = 0; t < U; ++t) {
             const bool live = k + 64 * t < k1;
-            const double p = live ? pv[t] : 0.0;
+            const double p = live ? a[t] * xv[t] : 0.0;
             const unsigned key = live ? q[t] & ((1u << kMergeShift) - 1) : 0u;
 #pragma unroll
             for (int u = 0; u < G; ++u) {
@@ -1012,9 +1014,9 @@ __device__ __forceinline__ void merged_sums(int k0, int k1, const unsigned *__re
 // (merged_sums each), then thread t < (4/W) G reports (group t / G, row t % G): the W partials
 // added in wave order (fixed: deterministic).  Returns false for threads without a row.
 // red: 8G doubles of LDS.  Must be reached by every thread of the block.
-template <int G, int S, class Prod>
+template <int G, int S, class Fetch>
 __device__ __forceinline__ bool merged_block(const int *__restrict__ gp, int ng, int W, const unsigned *__restrict__ mk,
-                                             const double *__restrict__ mv, Prod prod, double *red, int &g_out,
+                                             const double *__restrict__ mv, Fetch fetch, double *red, int &g_out,
                                              int &u_out, double &t0, double &t1)
 {
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, gpb = 4 / W;
@@ -1022,7 +1024,7 @@ __device__ __forceinline__ bool merged_block(const int *__restrict__ gp, int ng,
     double s0[G], s1[G];
     if (g < ng) {
         const int k0 = gp[g], k1 = gp[g + 1], len = k1 - k0, per = (len + W - 1) / W;
-        merged_sums<G, S>(k0 + min(len, part * per), k0 + min(len, (part + 1) * per), mk, mv, prod, s0, s1);
+        merged_sums<G, S>(k0 + min(len, part * per), k0 + min(len, (part + 1) * per), mk, mv, fetch, s0, s1);
     } else {
 #pragma unroll
         for (int u = 0; u < G; ++u) s0[u] = 0.0, s1[u] = 0.0;
