@@ -68,11 +68,11 @@ struct HostBuf {
 
 // Persistent host worker pool for the upload-time data preparation (sss_spmv.hip): the workers
 // are started once and reused, so a parallel loop costs a wake-up instead of thread creation
-// (h2d alone issued one loop per 32 MiB chunk).  One job at a time; a loop issued from a worker,
-// or while another thread holds the pool, runs inline on its caller.
+// (h2d alone issued one loop per 32 MiB chunk).  Up to 8 callers' loops at once, idle workers
+// joining any of them; a loop issued from a worker runs inline on it.
 int host_pool_threads();
 void host_thread_background();   // lower the calling thread's CPU priority (SSS_HOST_NICE)
-bool host_pool_run(const std::function<void()> &work);   // false: pool busy (caller runs inline)
+bool host_pool_run(const std::function<void()> &work);   // false: caller runs inline
 
 // Host-side data preparation at upload: fn(lo, hi) over [0, n) in chunks of `grain` items taken
 // from a shared counter by the pool's threads and the caller (the .hip units are compiled

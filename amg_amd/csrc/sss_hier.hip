@@ -12,6 +12,7 @@
 #include "sss_engine.hpp"
 #include "sss_tail.hpp"
 
+#include <atomic>
 #include <condition_variable>
 #include <mutex>
 #include <thread>
@@ -313,7 +314,7 @@ struct HierBuild {
     const SSS_AMG *mg = nullptr;
     std::vector<std::vector<int>> inv = std::vector<std::vector<int>>(kMaxLevels);
     std::vector<int> nF = std::vector<int>(kMaxLevels, -1);
-    const char *err = nullptr;
+    std::atomic<const char *> err{nullptr};
     bool timing = getenv("SSS_HIP_TIMING") != nullptr;   // per-level upload phases on stderr
 };
 
@@ -609,7 +610,7 @@ sss_hip_hier *sss::hier_create_impl(const SSS_AMG *mg, const sss_hip_opts *o, in
     HierBuild b;
     if (!hb_begin(b, mg, o, level_base, stream)) {
         if (b.h) hier_release(b.h);
-        if (b.err) fprintf(stderr, "### ERROR: sss_hip_hier_create: %s\n", b.err);
+        if (b.err) fprintf(stderr, "### ERROR: sss_hip_hier_create: %s\n", b.err.load());
         return nullptr;
     }
     const int nl = mg->num_levels;
@@ -628,6 +629,11 @@ sss_hip_hier *sss::hier_create_impl(const SSS_AMG *mg, const sss_hip_opts *o, in
 // (Setup/SSS_coarsen.c:294-498) keep one core busy.  Results are those of SSS_amg_setup followed by
 // sss_hip_hier_create.
 namespace {
+// The mirror's level tasks: A(l) = relabel + A_l + smoother plan (once the setup has moved past level
+// l), PR(l) = P_l / R_l (once A(l) has finished and level l + 1's relabeling is known).  While the
+// setup runs, one background worker takes them in order; once it has returned, the calling thread
+// and SSS_HIP_UPLOAD_HELPERS more threads (default 2) take whatever is runnable, so the levels the
+// setup produced last -- each an independent plan build -- are uploaded side by side.
 struct Pipeline {
     HierBuild b;
     std::mutex mu;
@@ -636,27 +642,72 @@ struct Pipeline {
     bool finished = false;
     int device = 0;
     double t_setup_end = 0, t_worker_end = 0;
+    int a_next = 0, pr_next = 0, busy = 0;
+    std::vector<char> a_fin = std::vector<char>(kMaxLevels, 0), perm_fin = std::vector<char>(kMaxLevels, 0);
+    // under mu: the next runnable task (+l: A(l - 1), -l: PR(l - 1)), 0 = none now
+    int claim()
+    {
+        if (b.err) return 0;
+        // PR(l): A(l) done, and level l + 1's relabeling known (or l + 1 the coarsest, which keeps
+        // the identity; the calling thread uploads that last PR after the setup)
+        if (pr_next + 1 < done && a_fin[pr_next] && perm_fin[pr_next + 1]) return -(++pr_next);
+        if (a_next < done) return ++a_next;
+        return 0;
+    }
+    void run(int task)
+    {
+        if (task > 0) {
+            const int l = task - 1;
+            hb_perm(b, l);
+            {
+                std::lock_guard<std::mutex> lk(mu);
+                perm_fin[l] = 1;
+            }
+            cv.notify_all();
+            hb_level_a(b, l, false);
+            std::lock_guard<std::mutex> lk(mu);
+            a_fin[l] = 1;
+        } else {
+            hb_level_pr(b, -task - 1);
+        }
+    }
+    // take tasks until none is left; the background worker also waits for the setup's progress
+    void loop(bool background)
+    {
+        for (;;) {
+            int t;
+            {
+                std::unique_lock<std::mutex> lk(mu);
+                cv.wait(lk, [&] {
+                    if (b.err) return true;
+                    if (claim_peek()) return true;
+                    return !background ? busy == 0 : finished && busy == 0;
+                });
+                t = claim();
+                if (!t) {
+                    if (b.err || busy == 0) break;
+                    continue;
+                }
+                ++busy;
+            }
+            run(t);
+            {
+                std::lock_guard<std::mutex> lk(mu);
+                --busy;
+            }
+            cv.notify_all();
+        }
+        cv.notify_all();
+    }
+    bool claim_peek() const
+    {
+        return !b.err && ((pr_next + 1 < done && a_fin[pr_next] && perm_fin[pr_next + 1]) || a_next < done);
+    }
     void worker()
     {
         (void)hipSetDevice(device);
         host_thread_background();
-        int a_next = 0, pr_next = 0;
-        for (;;) {
-            int d;
-            bool fin;
-            {
-                std::unique_lock<std::mutex> lk(mu);
-                cv.wait(lk, [&] { return finished || done > a_next; });
-                d = done;
-                fin = finished;
-            }
-            for (; a_next < d && !b.err; ++a_next) {
-                hb_perm(b, a_next);
-                hb_level_a(b, a_next, false);
-            }
-            for (; pr_next + 1 < d && !b.err; ++pr_next) hb_level_pr(b, pr_next);
-            if (fin || b.err) break;
-        }
+        loop(true);
         t_worker_end = PhaseTimer::now();
     }
 };
@@ -699,6 +750,18 @@ extern "C" sss_hip_hier *sss_hip_setup_create(SSS_AMG *mg, SSS_MAT *A, SSS_AMG_P
         P.finished = true;
     }
     P.cv.notify_all();
+    {   // the setup has returned: this thread and the helpers take the remaining level tasks
+        const char *hz = getenv("SSS_HIP_UPLOAD_HELPERS");
+        const int nh = std::max(0, std::min(8, (hz && *hz) ? atoi(hz) : 2));
+        std::vector<std::thread> helpers;
+        for (int k = 0; k < nh; ++k)
+            helpers.emplace_back([&] {
+                (void)hipSetDevice(P.device);
+                P.loop(false);
+            });
+        P.loop(false);
+        for (auto &t : helpers) t.join();
+    }
     th.join();
     const double t_join = PhaseTimer::now();
     HierBuild &b = P.b;

@@ -71,54 +71,72 @@ void host_thread_background()
 }
 
 namespace {
+// Several callers may hold jobs at once (the mirror's level tasks run side by side after the setup):
+// each job is a loop body that returns once its shared chunk counter is exhausted; an idle worker
+// joins any open job, and a job closes for newcomers as soon as one of its threads has returned.
 struct HostPool {
-    std::mutex job_mu, mu;
+    struct Job {
+        const std::function<void()> *work = nullptr;
+        int inside = 0;
+        bool open = false;
+    };
+    static constexpr int kJobs = 8;
+    std::mutex mu;
     std::condition_variable cv, done_cv;
-    const std::function<void()> *job = nullptr;
-    unsigned long long gen = 0;
-    int running = 0;
-    int nt = 1;
+    Job jobs[kJobs];
+    int nt = 1, rr = 0;
     static thread_local bool in_worker;
     HostPool()
     {
         nt = usable_cpus();
         for (int t = 1; t < nt; ++t) std::thread([this] { loop(); }).detach();   // lives as long as the process
     }
+    int open_job() const
+    {
+        for (int k = 0; k < kJobs; ++k)
+            if (jobs[(rr + k) % kJobs].open) return (rr + k) % kJobs;
+        return -1;
+    }
     void loop()
     {
         in_worker = true;
         host_thread_background();
-        unsigned long long seen = 0;
         for (;;) {
-            const std::function<void()> *w;
+            int j;
             {
                 std::unique_lock<std::mutex> lk(mu);
-                cv.wait(lk, [&] { return gen != seen; });
-                seen = gen;
-                w = job;
+                cv.wait(lk, [&] { return open_job() >= 0; });
+                j = open_job();
+                rr = (j + 1) % kJobs;
+                ++jobs[j].inside;
             }
-            (*w)();
+            (*jobs[j].work)();
             std::lock_guard<std::mutex> lk(mu);
-            if (--running == 0) done_cv.notify_all();
+            jobs[j].open = false;   // its counter is exhausted: nothing left to join
+            if (--jobs[j].inside == 0) done_cv.notify_all();
         }
     }
     bool run(const std::function<void()> &work)
     {
-        if (in_worker || !job_mu.try_lock()) return false;
+        if (in_worker) return false;
+        int j = -1;
         {
             std::lock_guard<std::mutex> lk(mu);
-            job = &work;
-            running = nt - 1;
-            ++gen;
+            for (int k = 0; k < kJobs && j < 0; ++k)
+                if (!jobs[k].work) j = k;
+            if (j < 0) return false;
+            jobs[j].work = &work;
+            jobs[j].inside = 0;
+            jobs[j].open = true;
         }
         cv.notify_all();
         work();
         {
             std::unique_lock<std::mutex> lk(mu);
-            done_cv.wait(lk, [&] { return running == 0; });
-            job = nullptr;
+            jobs[j].open = false;
+            done_cv.wait(lk, [&] { return jobs[j].inside == 0; });
+            jobs[j].work = nullptr;
         }
-        job_mu.unlock();
         return true;
     }
 };
