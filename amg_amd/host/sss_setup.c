@@ -9,6 +9,8 @@
  *   F-F cleanup ................. Setup/SSS_coarsen.c:501-574
  *   direct P pattern ............ Setup/SSS_coarsen.c:577-630
  *   direct interpolation ........ Setup/SSS_inter.cu:400-547 (the host twin interp_DIR)
+ *   standard P pattern .......... Setup/SSS_coarsen.c:633-725 (interp_type 2)
+ *   standard interpolation ...... Setup/SSS_inter.cu:550-715 (interp_STD)
  *   truncation .................. Setup/SSS_inter.cu:16-102
  *   Galerkin RAP ................ SSS_matvec.c:398-534
  *   level loop .................. Setup/SSS_SETUP.cu:36-178
@@ -540,6 +542,70 @@ static void direct_pattern(SSS_MAT *P, const SSS_IMAT *S, const SSS_IVEC *vertic
     }
 }
 
+/* Threads for a row-parallel loop whose threads each hold `bytes_per_item` x n of scratch (at most
+ * 2 GiB of scratch together). */
+static int scratch_threads(int n, size_t bytes_per_item)
+{
+    int T = omp_get_max_threads();
+    while (T > 1 && (size_t)T * (size_t)(n > 0 ? n : 1) * bytes_per_item > ((size_t)2 << 30)) T--;
+    return T;
+}
+
+/* Setup/SSS_coarsen.c:633-725 (form_P_pattern_std): an F row takes its strong C neighbours and the
+ * strong C neighbours of its strong F neighbours, each once, in discovery order; a C row its own
+ * index; any other row nothing.  The reference's one `visited` array only ever answers "taken by
+ * this row already?", so rows are independent: two row-parallel passes (count, then fill at the
+ * prefix offsets), each thread with its own row-stamped array. */
+static void std_pattern(SSS_MAT *P, const SSS_IMAT *S, const SSS_IVEC *vertices, int n, int ncoarse)
+{
+    const int *mark = vertices->d;
+    const int T = scratch_threads(n, sizeof(int));
+    P->num_rows = n;
+    P->num_cols = ncoarse;
+    P->row_ptr = (int *)SSS_calloc((size_t)n + 1, sizeof(int));
+    for (int fill = 0; fill < 2; ++fill) {
+        if (fill) {
+            for (int i = 0; i < n; ++i) P->row_ptr[i + 1] += P->row_ptr[i];
+            P->num_nnzs = P->row_ptr[n] - P->row_ptr[0];
+            P->col_idx = (int *)SSS_calloc((size_t)(P->num_nnzs > 0 ? P->num_nnzs : 1), sizeof(int));
+            P->val = (double *)SSS_calloc((size_t)(P->num_nnzs > 0 ? P->num_nnzs : 1), sizeof(double));
+        }
+#pragma omp parallel num_threads(T) if (n > 4096)
+        {
+            int *seen = (int *)malloc(sizeof(int) * (size_t)(n > 0 ? n : 1));
+            for (int i = 0; i < n; ++i) seen[i] = -1;
+#pragma omp for schedule(dynamic, 1024)
+            for (int i = 0; i < n; ++i) {
+                int cnt = 0, o = fill ? P->row_ptr[i] : 0;
+                if (mark[i] == FGPT) {
+                    for (int q = S->row_ptr[i]; q < S->row_ptr[i + 1]; ++q) {
+                        const int k = S->col_idx[q];
+                        if (mark[k] == CGPT && seen[k] != i) {
+                            seen[k] = i;
+                            if (fill) P->col_idx[o++] = k;
+                            cnt++;
+                        } else if (mark[k] == FGPT && k != i) {
+                            for (int r = S->row_ptr[k]; r < S->row_ptr[k + 1]; ++r) {
+                                const int h = S->col_idx[r];
+                                if (mark[h] == CGPT && seen[h] != i) {
+                                    seen[h] = i;
+                                    if (fill) P->col_idx[o++] = h;
+                                    cnt++;
+                                }
+                            }
+                        }
+                    }
+                } else if (mark[i] == CGPT) {
+                    cnt = 1;
+                    if (fill) P->col_idx[o] = i;
+                }
+                if (!fill) P->row_ptr[i + 1] = cnt;
+            }
+            free(seen);
+        }
+    }
+}
+
 int SSS_amg_coarsen(SSS_MAT *A, SSS_IVEC *vertices, SSS_MAT *P, SSS_IMAT *S, SSS_AMG_PARS *pars)
 {
     int ncoarse = 0;
@@ -558,9 +624,13 @@ int SSS_amg_coarsen(SSS_MAT *A, SSS_IVEC *vertices, SSS_MAT *P, SSS_IMAT *S, SSS
         if (timing)
             fprintf(stderr, "[setup]   coarsen: strength %.3f s, RS split %.3f s, F-F cleanup %.3f s, P pattern %.3f s\n",
                     t1 - t0, t2 - t1, t3 - t2, SSS_get_time() - t3);
+    } else if (pars->interp_type == intERP_STD) {   /* no F-F cleanup before the standard pattern */
+        const double t3 = SSS_get_time();
+        std_pattern(P, S, vertices, A->num_rows, ncoarse);
+        if (timing)
+            fprintf(stderr, "[setup]   coarsen: strength %.3f s, RS split %.3f s, standard P pattern %.3f s\n", t1 - t0,
+                    t2 - t1, SSS_get_time() - t3);
     } else {
-        /* Standard interpolation (form_P_pattern_std / interp_STD) is not part of this
-         * engine: the reference's default and every BASELINE config use direct. */
         SSS_exit_on_errcode(ERROR_AMG_interp_type, __func__);
     }
     return 0;
@@ -765,10 +835,120 @@ void interp_DIR(SSS_MAT *A, SSS_IVEC *vertices, SSS_MAT *P, SSS_AMG_PARS *pars)
     SSS_amg_interp_trunc(P, pars);
 }
 
+/*
+ * Setup/SSS_inter.cu:550-715 (interp_STD), on the pattern std_pattern built.  Per F row i, with
+ * hat a the row's entries eliminated through its strong F neighbours k:
+ *   hat a_ii = a_ii - sum_k (a_ik / a_kk) a_ki,   hat a_il = a_il [l in C_i^s] - sum_k (a_ik / a_kk) a_kl [l in C_k^s]
+ *   alpha = (psum_i - sum_k f_k (nsum_k - a_ki + a_kk)) / (csum_i - sum_k f_k csum_k),
+ *   p_il = -alpha hat a_il / hat a_ii
+ * (psum: off-diagonal entries whose column is not isolated; nsum: all off-diagonal entries; csum:
+ * the entries of strong C neighbours; every sum in stored order).  The reference's per-row scratch
+ * (reverse indices of rows i and k, hat a) is reset or fully rewritten for each row before it is
+ * read, so the rows are computed in parallel with per-thread scratch; each row's arithmetic is the
+ * reference's, in its order.  (The reference also sets the process's OpenMP thread count to 8 here,
+ * a speed-only side effect not reproduced.)  Then the coarse renumbering and the truncation.
+ */
+static void interp_STD(SSS_MAT *A, SSS_IVEC *vertices, SSS_MAT *P, SSS_IMAT *S, SSS_AMG_PARS *pars)
+{
+    const int n = A->num_rows, nc = A->num_cols > n ? A->num_cols : n;
+    const int *mark = vertices->d;
+    const int *ia = A->row_ptr, *ja = A->col_idx;
+    const double *a = A->val;
+    double *csum = (double *)SSS_calloc((size_t)(n > 0 ? n : 1), sizeof(double));
+    double *psum = (double *)SSS_calloc((size_t)(n > 0 ? n : 1), sizeof(double));
+    double *nsum = (double *)SSS_calloc((size_t)(n > 0 ? n : 1), sizeof(double));
+    double *diag = (double *)SSS_calloc((size_t)(n > 0 ? n : 1), sizeof(double));
+
+    /* step 0: diagonal (the row's last diagonal entry), strong-C, off-diagonal and non-isolated sums */
+#pragma omp parallel for schedule(dynamic, 4096) if (n > 65536)
+    for (int i = 0; i < n; ++i) {
+        double cs = 0.0, ns = 0.0, ps = 0.0, d = 0.0;
+        for (int j = ia[i]; j < ia[i + 1]; ++j) {
+            const int k = ja[j];
+            int strong_c = 0;
+            if (mark[k] == CGPT)
+                for (int q = S->row_ptr[i]; q < S->row_ptr[i + 1] && !strong_c; ++q) strong_c = S->col_idx[q] == k;
+            if (strong_c) cs += a[j];
+            if (k == i) {
+                d = a[j];
+            } else {
+                ns += a[j];
+                if (mark[k] != ISPT) ps += a[j];
+            }
+        }
+        csum[i] = cs, nsum[i] = ns, psum[i] = ps, diag[i] = d;
+    }
+
+    /* step 1: the weights */
+    const int T = scratch_threads(nc, 2 * sizeof(int) + sizeof(double));
+#pragma omp parallel num_threads(T) if (n > 4096)
+    {
+        int *rindi = (int *)malloc(sizeof(int) * (size_t)nc), *rindk = (int *)malloc(sizeof(int) * (size_t)nc);
+        double *ahat = (double *)malloc(sizeof(double) * (size_t)nc);
+#pragma omp for schedule(dynamic, 1024)
+        for (int i = 0; i < n; ++i) {
+            if (mark[i] == CGPT) {
+                P->val[P->row_ptr[i]] = 1.0;
+                continue;
+            }
+            if (mark[i] != FGPT) continue;
+            double alN = psum[i], alP = csum[i], alpha = 0.0;
+            for (int j = ia[i]; j < ia[i + 1]; ++j) rindi[ja[j]] = j;
+            for (int j = P->row_ptr[i]; j < P->row_ptr[i + 1]; ++j) ahat[P->col_idx[j]] = 0.0;
+            ahat[i] = diag[i];
+            for (int j = S->row_ptr[i]; j < S->row_ptr[i + 1]; ++j) {
+                const int k = S->col_idx[j];
+                const double aik = a[rindi[k]];
+                if (mark[k] == CGPT) {
+                    ahat[k] += aik;
+                } else if (mark[k] == FGPT) {
+                    const double akk = diag[k];
+                    for (int m = ia[k]; m < ia[k + 1]; ++m) rindk[ja[m]] = m;
+                    const double factor = aik / akk;
+                    double aki = 0.0;
+                    for (int m = ia[k]; m < ia[k + 1]; ++m)
+                        if (ja[m] == i) {
+                            aki = a[m];
+                            ahat[i] -= factor * aki;
+                        }
+                    for (int m = S->row_ptr[k]; m < S->row_ptr[k + 1]; ++m) {
+                        const int l = S->col_idx[m];
+                        const double akl = a[rindk[l]];
+                        if (mark[l] == CGPT) ahat[l] -= factor * akl;
+                    }
+                    alN -= factor * (nsum[k] - aki + akk);
+                    alP -= factor * csum[k];
+                }
+            }
+            if (P->row_ptr[i + 1] > P->row_ptr[i]) alpha = alN / alP;
+            for (int j = P->row_ptr[i]; j < P->row_ptr[i + 1]; ++j) P->val[j] = -alpha * ahat[P->col_idx[j]] / ahat[i];
+        }
+        free(rindi);
+        free(rindk);
+        free(ahat);
+    }
+
+    /* step 2: coarse renumbering of the columns */
+    int *cmap = (int *)SSS_calloc((size_t)(n > 0 ? n : 1), sizeof(int));
+    int ncoarse = 0;
+    for (int i = 0; i < n; ++i)
+        if (mark[i] == CGPT) cmap[i] = ncoarse++;
+    P->num_cols = ncoarse;
+#pragma omp parallel for schedule(static) if (P->num_nnzs > 65536)
+    for (int q = 0; q < P->row_ptr[P->num_rows]; ++q) P->col_idx[q] = cmap[P->col_idx[q]];
+    free(cmap);
+    free(csum);
+    free(psum);
+    free(nsum);
+    free(diag);
+    /* step 3 */
+    SSS_amg_interp_trunc(P, pars);
+}
+
 void SSS_amg_interp(SSS_MAT *A, SSS_IVEC *vertices, SSS_MAT *P, SSS_IMAT *S, SSS_AMG_PARS *pars)
 {
-    (void)S;
     if (pars->interp_type == intERP_DIR) interp_DIR(A, vertices, P, pars);
+    else if (pars->interp_type == intERP_STD) interp_STD(A, vertices, P, S, pars);
     else SSS_exit_on_errcode(ERROR_AMG_interp_type, __func__);
 }
 

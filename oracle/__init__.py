@@ -60,6 +60,7 @@ def load():
             "ora_solve": (SSS_RTN, [P(SSS_AMG), P(SSS_VEC), P(SSS_VEC), P(ORA_OPTS), dp, dp, C.c_int]),
             "ora_coarse_seconds": (C.c_double, []),
             "ora_reset_timers": (None, []),
+            "ora_interp_std": (None, [P(SSS_MAT), ip, P(SSS_MAT), P(SSS_IMAT), C.c_double]),
         }
         for name, (res, args) in sigs.items():
             fn = getattr(lib, name)

@@ -20,6 +20,9 @@
  *   ora_coarest_solve ............. Solve/SSS_cycle.cu:819-846
  *   ora_cycle ..................... Solve/SSS_cycle.cu:848-967
  *   ora_solve ..................... Solve/SSS_SOLVE.c:4-87
+ *   ora_interp_std ................ Setup/SSS_inter.cu:550-715 + the truncation, :16-102 (setup;
+ *                                    the standard pattern itself is pinned by the compiled
+ *                                    SSS_coarsen.c)
  *
  * Only stop_type STOP_REL_RES is restated for the Krylov methods: it is the only one the
  * coarse solver uses (Solve/SSS_cycle.cu:833).
@@ -766,4 +769,123 @@ SSS_RTN ora_solve(SSS_AMG *mg, SSS_VEC *x, SSS_VEC *b, const ora_opts *o, double
     }
     if (verbose) printf("AMG solve time: %g s\n", now_s() - t0);
     return rtn;
+}
+
+/* ---------------------------------------------------------------------------------------------
+ * Setup/SSS_inter.cu:16-102: per row, keep entries >= eps * (largest positive) or <= eps *
+ * (smallest negative), rescale the kept positives / negatives to the row's full sums.
+ * ------------------------------------------------------------------------------------------- */
+static void ora_interp_trunc(SSS_MAT *P, double eps)
+{
+    int nz = 0, w1 = 0, w2 = 0;
+    for (int i = 0; i < P->num_rows; ++i) {
+        const int lo = P->row_ptr[i], hi = P->row_ptr[i + 1];
+        double mneg = 0, mpos = 0, sneg = 0, spos = 0, tneg = 0, tpos = 0;
+        P->row_ptr[i] = nz;
+        for (int j = lo; j < hi; ++j) {
+            if (P->val[j] > 0) {
+                spos += P->val[j];
+                mpos = mpos > P->val[j] ? mpos : P->val[j];
+            } else if (P->val[j] < 0) {
+                sneg += P->val[j];
+                mneg = mneg < P->val[j] ? mneg : P->val[j];
+            }
+        }
+        mpos *= eps;
+        mneg *= eps;
+        for (int j = lo; j < hi; ++j) {
+            if (P->val[j] >= mpos) {
+                nz++;
+                P->col_idx[w1++] = P->col_idx[j];
+                tpos += P->val[j];
+            } else if (P->val[j] <= mneg) {
+                nz++;
+                P->col_idx[w1++] = P->col_idx[j];
+                tneg += P->val[j];
+            }
+        }
+        const double fpos = tpos > SMALLFLOAT ? spos / tpos : 1.0;
+        const double fneg = tneg < -SMALLFLOAT ? sneg / tneg : 1.0;
+        for (int j = lo; j < hi; ++j) {
+            if (P->val[j] >= mpos) P->val[w2++] = P->val[j] * fpos;
+            else if (P->val[j] <= mneg) P->val[w2++] = P->val[j] * fneg;
+        }
+    }
+    P->num_nnzs = P->row_ptr[P->num_rows] = nz;
+}
+
+/* Setup/SSS_inter.cu:550-715, the reference's row loop with its shared scratch arrays. */
+void ora_interp_std(const SSS_MAT *A, const int *mark, SSS_MAT *P, const SSS_IMAT *S, double trunc)
+{
+    const int n = A->num_rows;
+    const size_t m = (size_t)(n > 0 ? n : 1);
+    int *cindex = malloc(sizeof(int) * m), *rindi = malloc(sizeof(int) * 2 * m), *rindk = malloc(sizeof(int) * 2 * m);
+    double *csum = calloc(m, sizeof(double)), *psum = calloc(m, sizeof(double)), *nsum = calloc(m, sizeof(double));
+    double *diag = calloc(m, sizeof(double)), *ahat = calloc(m, sizeof(double));
+    double alpha = 0.0;
+    for (int i = 0; i < n; ++i) cindex[i] = -1;
+    /* step 0 (SSS_inter.cu:587-614) */
+    for (int i = 0; i < n; ++i) {
+        for (int j = S->row_ptr[i]; j < S->row_ptr[i + 1]; ++j)
+            if (mark[S->col_idx[j]] == CGPT) cindex[S->col_idx[j]] = i;
+        for (int j = A->row_ptr[i]; j < A->row_ptr[i + 1]; ++j) {
+            const int k = A->col_idx[j];
+            if (cindex[k] == i) csum[i] += A->val[j];
+            if (k == i) {
+                diag[i] = A->val[j];
+            } else {
+                nsum[i] += A->val[j];
+                if (mark[k] != ISPT) psum[i] += A->val[j];
+            }
+        }
+    }
+    /* step 1 (:616-687) */
+    for (int i = 0; i < n; ++i) {
+        if (mark[i] == FGPT) {
+            double alN = psum[i], alP = csum[i];
+            for (int j = A->row_ptr[i]; j < A->row_ptr[i + 1]; ++j) rindi[A->col_idx[j]] = j;
+            for (int j = P->row_ptr[i]; j < P->row_ptr[i + 1]; ++j) ahat[P->col_idx[j]] = 0.0;
+            ahat[i] = diag[i];
+            for (int j = S->row_ptr[i]; j < S->row_ptr[i + 1]; ++j) {
+                const int k = S->col_idx[j];
+                const double aik = A->val[rindi[k]];
+                if (mark[k] == CGPT) {
+                    ahat[k] += aik;
+                } else if (mark[k] == FGPT) {
+                    const double akk = diag[k];
+                    double aki = 0.0, factor;
+                    for (int q = A->row_ptr[k]; q < A->row_ptr[k + 1]; ++q) rindk[A->col_idx[q]] = q;
+                    factor = aik / akk;
+                    for (int q = A->row_ptr[k]; q < A->row_ptr[k + 1]; ++q)
+                        if (A->col_idx[q] == i) {
+                            aki = A->val[q];
+                            ahat[i] -= factor * aki;
+                        }
+                    for (int q = S->row_ptr[k]; q < S->row_ptr[k + 1]; ++q) {
+                        const int l = S->col_idx[q];
+                        const double akl = A->val[rindk[l]];
+                        if (mark[l] == CGPT) ahat[l] -= factor * akl;
+                    }
+                    alN -= factor * (nsum[k] - aki + akk);
+                    alP -= factor * csum[k];
+                }
+            }
+            if (P->row_ptr[i + 1] > P->row_ptr[i]) alpha = alN / alP;
+            for (int j = P->row_ptr[i]; j < P->row_ptr[i + 1]; ++j) {
+                const int k = P->col_idx[j];
+                P->val[j] = -alpha * ahat[k] / ahat[i];
+            }
+        } else if (mark[i] == CGPT) {
+            P->val[P->row_ptr[i]] = 1.0;
+        }
+    }
+    /* step 2 (:689-700) */
+    int index = 0;
+    for (int i = 0; i < n; ++i)
+        if (mark[i] == CGPT) cindex[i] = index++;
+    P->num_cols = index;
+    for (int q = 0; q < P->row_ptr[P->num_rows]; ++q) P->col_idx[q] = cindex[P->col_idx[q]];
+    free(cindex), free(rindi), free(rindk), free(csum), free(psum), free(nsum), free(diag), free(ahat);
+    /* step 3 (:713-714) */
+    ora_interp_trunc(P, trunc);
 }

@@ -57,6 +57,11 @@ void ora_cycle(SSS_AMG *mg, const ora_opts *o);
 SSS_RTN ora_solve(SSS_AMG *mg, SSS_VEC *x, SSS_VEC *b, const ora_opts *o, double *relres_hist,
                   double *absres_hist, int hist_cap);
 
+/* Setup/SSS_inter.cu:550-715 (interp_STD) + :16-102 (SSS_amg_interp_trunc), sequential: fills the
+ * values of the standard-interpolation pattern P (fine column indices, as SSS_amg_coarsen returns
+ * it), renumbers its columns to coarse indices and truncates with `trunc`. */
+void ora_interp_std(const SSS_MAT *A, const int *mark, SSS_MAT *P, const SSS_IMAT *S, double trunc);
+
 /* Seconds spent inside ora_coarest_solve since the last reset (baseline split). */
 double ora_coarse_seconds(void);
 void ora_reset_timers(void);

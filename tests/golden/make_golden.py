@@ -100,6 +100,19 @@ def ref_units() -> dict:
     pci = np.ctypeslib.as_array(P.col_idx, shape=(P.num_nnzs,)).copy()
     out["bus_coarsen"] = {"rc": rc, "mark": ihash(mark), "nC_col": P.num_cols, "n_c_points": int((mark == 1).sum()),
                           "P_rp": ihash(prp), "P_ci": ihash(pci), "P_nnz": P.num_nnzs}
+    # the standard-interpolation pattern (SSS_coarsen.c:633-725 through SSS_amg_coarsen, interp_type 2)
+    pars = A.default_pars()
+    pars.interp_type = 2
+    verts = ref.SSS_ivec_create(M.num_rows)
+    P = SSS_MAT()
+    S = SSS_IMAT()
+    rc = ref.SSS_amg_coarsen(C.byref(M), C.byref(verts), C.byref(P), C.byref(S), C.cast(C.byref(pars), C.c_void_p))
+    mark = np.ctypeslib.as_array(verts.d, shape=(M.num_rows,)).copy()
+    prp = np.ctypeslib.as_array(P.row_ptr, shape=(P.num_rows + 1,)).copy()
+    pci = np.ctypeslib.as_array(P.col_idx, shape=(P.num_nnzs,)).copy()
+    out["bus_coarsen_std"] = {"rc": rc, "mark": ihash(mark), "nC_col": P.num_cols,
+                              "n_c_points": int((mark == 1).sum()), "P_rp": ihash(prp), "P_ci": ihash(pci),
+                              "P_nnz": P.num_nnzs}
     # transpose + RAP on the product hierarchy's level-0 P (values from the product's interp_DIR)
     H = A.Hierarchy(M)
     L0 = H.level(0)
