@@ -335,6 +335,8 @@ int level_inner_of(const sss_hip_opts &o, int global_level);
 // sum-of-squares of the written y per row block, for a deterministic fused norm.
 int launch_spmv(const DevCSR &A, int op, double alpha, const double *x, const double *b, double *y,
                 int cap, double *partial, hipStream_t stream);
+// x[lo + q] += e[col[q]] for q < m, with the AMXPY epilogue's arithmetic of a row holding one 1.0.
+int launch_prolong_inject(int m, int lo, const int *col, const double *e, double *x, hipStream_t stream);
 // As launch_spmv, tile path only, over the row blocks [blo, bhi) of A (partial indexed by block).
 int launch_spmv_range(const DevCSR &A, int blo, int bhi, int op, double alpha, const double *x, const double *b,
                       double *y, double *partial, hipStream_t stream);

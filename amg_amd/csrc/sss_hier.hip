@@ -38,6 +38,9 @@ struct sss_hip_hier {
     struct Level {
         DevCSR A, P, R;
         double *b = nullptr, *x = nullptr, *wp = nullptr;
+        // the C rows of P as injections (each one stored 1.0): their coarse columns, for the
+        // prolongation into the C rows only (hb_level_pr); null = the tile path
+        int *pinj = nullptr;
         SmootherPlan sm;
         // Relabeling (new -> old) of this level's unknowns: F points first, then C points, each in
         // ascending original order; empty = identity (coarsest level, or relabeling off).
@@ -222,6 +225,8 @@ static void hier_release(sss_hip_hier *h)
         devcsr_free(L.A);
         devcsr_free(L.P);
         devcsr_free(L.R);
+        dev_free(L.pinj);
+        L.pinj = nullptr;
         dev_free(L.b);
         dev_free(L.x);
         dev_free(L.wp);
@@ -463,9 +468,29 @@ static bool hb_level_pr(HierBuild &b, int l)
         pt.mark("relabel R");
         // P's rows follow the level's F|C relabeling: blocks split there too, so a
         // prolongation can be limited to the C rows (SmootherPlan::f_overwritten)
-        if (devcsr_upload(L.P, P.view(C.P.num_rows, C.P.num_cols), rl ? b.nF[l] : -1, penc) ||
+        const SSS_MAT Pv = P.view(C.P.num_rows, C.P.num_cols);
+        if (devcsr_upload(L.P, Pv, rl ? b.nF[l] : -1, penc) ||
             devcsr_upload(L.R, R.view(C.R.num_rows, C.R.num_cols), -1, restriction_encoding(h->opts)))
             return hb_fail(b, "upload P/R");
+        // the prolongation into the C rows only (f_overwritten): when every C row of P is one stored
+        // 1.0, its columns alone (SSS_HIP_INJECT=0: the tile path)
+        const char *iz = getenv("SSS_HIP_INJECT");
+        if (rl && L.sm.f_overwritten && b.nF[l] > 0 && !(iz && *iz == '0')) {
+            const int n = Pv.num_rows, lo = b.nF[l];
+            std::vector<int> col((size_t)(n - lo));
+            std::atomic<bool> ok{true};
+            parallel_chunks(n - lo, 1 << 16, [&](int a, int e) {
+                for (int q = a; q < e && ok; ++q) {
+                    const int k = Pv.row_ptr[lo + q];
+                    if (Pv.row_ptr[lo + q + 1] != k + 1 || Pv.val[k] != 1.0) ok = false;
+                    else col[q] = Pv.col_idx[k];
+                }
+            });
+            if (ok) {
+                L.pinj = dev_alloc<int>(col.size());
+                if (!L.pinj || h2d(L.pinj, col.data(), sizeof(int) * col.size())) return hb_fail(b, "upload P injection");
+            }
+        }
     } else if (devcsr_upload(L.P, C.P, -1, penc) || devcsr_upload(L.R, C.R, -1, restriction_encoding(h->opts))) {
         return hb_fail(b, "upload P/R");
     }
@@ -932,6 +957,10 @@ static int walk_cycle(sss_hip_hier *h, CoarseFn coarse, bool pend = false)
             // only (depth-1 GS F pass, all |d| > 1e-20), the F rows' correction is dead: prolong
             // into the C rows only (the iterates are bitwise unchanged).
             if (L.sm.f_overwritten && h->pars.post_iter > 0 && L.P.split_row == L.sm.pass[0].hi &&
+                L.P.split_row > 0 && L.pinj) {
+                if ((rc = launch_prolong_inject(L.P.n - L.P.split_row, L.P.split_row, L.pinj, h->L[l + 1].x, L.x, s)))
+                    return rc;
+            } else if (L.sm.f_overwritten && h->pars.post_iter > 0 && L.P.split_row == L.sm.pass[0].hi &&
                 L.P.split_row > 0 && !L.P.wave_rows && !L.P.vec_rows) {
                 if ((rc = launch_spmv_range(L.P, L.P.split_blk, L.P.nblk, SSS_HIP_SPMV_AMXPY, 1.0, h->L[l + 1].x, nullptr,
                                             L.x, nullptr, s)))

@@ -1330,6 +1330,28 @@ int launch_spmv(const DevCSR &A, int op, double alpha, const double *x, const do
     return 0;
 }
 
+// x_r += P e over C rows whose prolongation row is one stored 1.0 (the injection of the C point's
+// coarse value; sss_hier.hip hb_level_pr finds them): the tile AMXPY epilogue's arithmetic --
+// s = 0.0 + 1.0 * e_c from the stored-order chain, out = x_r + s * 1.0 -- without the CSR arrays,
+// their row blocks or the LDS staging.
+__global__ __launch_bounds__(kBlock) void prolong_inject(int m, int lo, const int *__restrict__ col,
+                                                         const double *__restrict__ e, double *__restrict__ x)
+{
+    const int q = blockIdx.x * kBlock + (int)threadIdx.x;
+    if (q < m) {
+        const double s = 0.0 + 1.0 * e[col[q]];
+        x[lo + q] = x[lo + q] + s * 1.0;
+    }
+}
+
+int launch_prolong_inject(int m, int lo, const int *col, const double *e, double *x, hipStream_t s)
+{
+    if (m <= 0) return 0;
+    hipLaunchKernelGGL(prolong_inject, dim3((m + kBlock - 1) / kBlock), dim3(kBlock), 0, s, m, lo, col, e, x);
+    SSS_HIP(hipGetLastError());
+    return 0;
+}
+
 int launch_spmv_range(const DevCSR &A, int blo, int bhi, int op, double alpha, const double *x, const double *b,
                       double *y, double *partial, hipStream_t s)
 {

@@ -4,7 +4,7 @@
 
 Walks the kernels in start order.  A cycle ends at the residual-norm kernel
 (spmv_*<2, true>, or relax_range<3> when it also computes the next first F pass); inside a cycle, a restriction (spmv_*<0, ...>, SSS_HIP_SPMV_MXY) moves the
-level counter down, a prolongation (spmv_*<1, ...>) moves it up, the dense GEMV / Krylov kernels
+level counter down, a prolongation (spmv_*<1, ...> or prolong_inject) moves it up, the dense GEMV / Krylov kernels
 are the coarsest level.  Prints, per level, the kernel time of one average cycle split into
 smoother / residual / restriction / prolongation / other, and, when the bench JSON (its
 `config.hierarchy`) is given, the effective GB/s of 5 passes over the level's matrix
@@ -59,6 +59,10 @@ def main():
                 cur[(lvl, "prolong")] += dur
             else:
                 cur[(lvl, "resid")] += dur
+            continue
+        if "prolong_inject" in name:   # the C-row prolongation of a P whose C rows are injections
+            lvl -= 1
+            cur[(lvl, "prolong")] += dur
             continue
         if "dense_gemv" in name or "k_" in name.split("(")[0]:
             cur[("coarse", "solve")] += dur
