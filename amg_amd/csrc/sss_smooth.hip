@@ -499,7 +499,7 @@ __device__ __forceinline__ void relax_range_ell(int blo, const int2 *__restrict_
 {
     constexpr int RPT = kEllRpt;
     __shared__ EllSmem es[RPT];
-    const int g = dt.remap ? xcd_remap(blockIdx.x, gridDim.x) : (int)blockIdx.x;
+    const int g = ell_block_order(dt.remap, (int)blockIdx.x, (int)gridDim.x);
     unsigned w[RPT][W / 4];
     double br[RPT], dr[RPT];
     int r[RPT];
@@ -576,7 +576,7 @@ __device__ __forceinline__ void relax_range_ell2(int blo, const int2 *__restrict
                                                  double *__restrict__ partial, XSrc xs, const DevDict &dt)
 {
     __shared__ EllSmem es[2];
-    const int g = dt.remap ? xcd_remap(blockIdx.x, gridDim.x) : (int)blockIdx.x;
+    const int g = ell_block_order(dt.remap, (int)blockIdx.x, (int)gridDim.x);
     const EllPairRows pr = ell_pair_rows(blk, blo + 2 * g, dt.bend);
     unsigned w[2][2];
     double br[2], dr[2] = {0.0, 0.0};

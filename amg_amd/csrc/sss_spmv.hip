@@ -1113,7 +1113,7 @@ __global__ __launch_bounds__(kBlock) void spmv_adaptive(const int2 *__restrict__
         }
     } else if constexpr (DICT == 8 && kEllPairs && kEllPairsSpmv) {   // dictionary ELL, two consecutive rows per thread
         __shared__ EllSmem es[2];
-        const int g = dt.remap ? xcd_remap(blockIdx.x, gridDim.x) : (int)blockIdx.x;
+        const int g = ell_block_order(dt.remap, (int)blockIdx.x, (int)gridDim.x);
         const EllPairRows pr = ell_pair_rows(blk, 2 * g, dt.bend);
         unsigned w[2][2];
         double br[2] = {0.0, 0.0};
@@ -1154,7 +1154,7 @@ __global__ __launch_bounds__(kBlock) void spmv_adaptive(const int2 *__restrict__
         constexpr int W = DICT;   // from 0.0 in stored order; kEllRpt row blocks per workgroup
         constexpr int RPT = kEllRpt;
         __shared__ EllSmem es[RPT];
-        const int g = dt.remap ? xcd_remap(blockIdx.x, gridDim.x) : (int)blockIdx.x;
+        const int g = ell_block_order(dt.remap, (int)blockIdx.x, (int)gridDim.x);
         unsigned w[RPT][W / 4];
         double br[RPT];
         int r[RPT];

@@ -27,6 +27,20 @@ __device__ __forceinline__ int xcd_remap(int b, int nb)
     const int per = nb >> 3, rem = nb & 7, xcd = b & 7, idx = b >> 3;
     return xcd < rem ? xcd * (per + 1) + idx : rem * (per + 1) + (xcd - rem) * per + idx;
 }
+// The ELL launches' block order (DevCSR::ell_remap): 0 the dispatch order, 1 xcd_remap, G >= 2 runs of
+// G consecutive blocks per XCD in turn (block b of XCD b % 8 takes run (b / 8) / G of that XCD's
+// share): the row neighbours of a block (the +-n stencil offsets) stay on its XCD's L2 while the
+// eight XCDs still stream one region of the matrix together.  The grid's last partial round of 8G
+// keeps the dispatch order (a bijection either way).
+__device__ __forceinline__ int ell_block_order(int remap, int b, int nb)
+{
+    if (remap == 0) return b;
+    if (remap == 1) return xcd_remap(b, nb);
+    const int span = 8 * remap, full = nb - nb % span;
+    if (b >= full) return b;
+    const int base = b - b % span, w = b % span;   // position inside the round
+    return base + (w & 7) * remap + (w >> 3);
+}
 __device__ __forceinline__ int xcd_bid()
 {
     if (!SSS_XCD_REMAP) return blockIdx.x;
