@@ -218,6 +218,11 @@ struct DevCSR {
     // ell_w bytes per row (8 for 7-pt) instead of 12 per entry.  pk and dv_code stay null.
     unsigned char *dv_ell = nullptr;
     int ell_w = 0;
+    // A rectangular operator's dictionary ELL may store its offsets against a per-row base column
+    // (the row's first column) instead of the row index: dv_ell_base[r] (null: the row index).  A
+    // restriction's rows follow the next level's F-first relabeling, so col - row drifts across a
+    // block while col - (first col) repeats the stencil.
+    int *dv_ell_base = nullptr;
     // Column ELL (kEncDict, when the offsets do not fit a 1-byte dictionary but every row has at
     // most 32 entries, every 256-row block few enough distinct values and the columns fit the code -- the Galerkin
     // level of a stencil, 7-pt level 1: 19 entries per row): row r's entries in stored order as
@@ -255,7 +260,8 @@ static_assert(1 + kTileColBits + kTileShift == 32, "tile packing");
 // two-stage split copies, launch_ts_*), so its CSR arrays need not be column-sorted
 // kEncXell: the column ELL may replace the tile storage (its own 256-row blocking)
 enum { kEncSortedTiles = 1, kEncFreeOrder = 2, kEncDict = 4, kEncMergedOnly = 8, kEncXell = 16,
-       kEncEll = 32 };   // kEncEll: the one-byte dictionary ELL only (also rectangular; no dictionary tiles)
+       kEncEll = 32,      // kEncEll: the one-byte dictionary ELL only (also rectangular; no dictionary tiles)
+       kEncEllBase = 64 };   // kEncEllBase: a rectangular matrix's dictionary ELL with per-row bases (dv_ell_base)
 // split >= 0 forces a row-block boundary at that row (the F|C class boundary of a relabeled level);
 // enc: kEnc* flags; seg (kEncFreeOrder only, optional): per row, the absolute CSR position that
 // splits the row into two independently summed segments (two-stage [N_i | L_i] rows).

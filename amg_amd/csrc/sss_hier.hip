@@ -172,7 +172,9 @@ int sss::transfer_encoding(const sss_hip_opts &o)
 int sss::restriction_encoding(const sss_hip_opts &o)
 {
     const char *e = getenv("SSS_HIP_ELL_R");
-    const int enc = transfer_encoding(o);
+    const char *bz = getenv("SSS_HIP_ELL_BASE");   // 0: no per-row-based dictionary ELL for R
+    int enc = transfer_encoding(o);
+    if ((level_encoding(o) & kEncDict) && !(bz && *bz == '0')) enc |= kEncEllBase;
     return (e && *e == '1' && (level_encoding(o) & kEncDict)) ? (enc | kEncEll) : enc;
 }
 

@@ -454,6 +454,7 @@ DevDict devdict(const DevCSR &A, int blo)
     if (!has_dict(A)) return t;
     t.code = A.dv_code;
     t.ell = A.dv_ell;
+    t.ellb = A.dv_ell_base;
     t.ellw = A.ell_w;
     t.xell = A.dv_xell;
     t.xshift = A.xell_shift;
@@ -586,7 +587,7 @@ static bool build_value_dict(const std::vector<int> &blk, const int *rp, const H
 // most 31 distinct column offsets and 8 distinct value bit patterns (false otherwise); width W =
 // 8, 16 or 32 bytes per row, codes in stored order, 0xFF pads.
 static bool build_ell(const SSS_MAT &h, const std::vector<int> &blk, HostBuf<unsigned char> &ell, int &W,
-                      std::vector<int4> &pd, std::vector<int> &dd, std::vector<double> &vd)
+                      std::vector<int4> &pd, std::vector<int> &dd, std::vector<double> &vd, const int *base = nullptr)
 {
     const int *rp = h.row_ptr, *ci = h.col_idx;
     const double *v = h.val;
@@ -619,7 +620,7 @@ static bool build_ell(const SSS_MAT &h, const std::vector<int> &blk, HostBuf<uns
             std::memset(row0, 0xff, (size_t)(blk[q + 1] - blk[q]) * W);
             for (int r = blk[q]; r < blk[q + 1]; ++r)
                 for (int k = rp[r]; k < rp[r + 1]; ++k) {
-                    const int di = Dd->insert((unsigned long long)(long long)(ci[k] - r), 31);
+                    const int di = Dd->insert((unsigned long long)(long long)(ci[k] - (base ? base[r] : r)), 31);
                     const int vi = Vd->insert(bits_of(v[k]), 8);
                     if (di < 0 || vi < 0) {
                         ok = 0;
@@ -868,14 +869,27 @@ int devcsr_upload(DevCSR &d, const SSS_MAT &h, int split, int enc, const int *se
     // from them instead of the sorted copy)
     const char *dz = getenv("SSS_HIP_DICT");   // 0: never (tests compare both ways)
     const char *ez = getenv("SSS_HIP_ELL");    // 0: no ELL (dictionary tiles where they qualify)
-    if ((enc & (kEncDict | kEncEll)) && !(dz && *dz == '0') && !(ez && *ez == '0') && !d.wave_rows && !d.vec_rows &&
-        d.nnz > 0 && ((enc & kEncEll) || d.n == d.ncols)) {
+    const bool based = (enc & kEncEllBase) && d.n != d.ncols;
+    if ((enc & (kEncDict | kEncEll | kEncEllBase)) && !(dz && *dz == '0') && !(ez && *ez == '0') && !d.wave_rows &&
+        !d.vec_rows && d.nnz > 0 && ((enc & kEncEll) || based || d.n == d.ncols)) {
         HostBuf<unsigned char> ell;
         std::vector<int4> pd;
         std::vector<int> dd;
         std::vector<double> vd;
+        std::vector<int> base;
+        if (based) {   // each row's first column (0 for an empty row)
+            base.resize((size_t)d.n);
+            parallel_chunks(d.n, 1 << 16, [&](int lo, int hi) {
+                for (int r = lo; r < hi; ++r) base[r] = h.row_ptr[r] < h.row_ptr[r + 1] ? h.col_idx[h.row_ptr[r]] : 0;
+            });
+        }
         int W = 0;
-        if (build_ell(h, blk, ell, W, pd, dd, vd)) {
+        if (build_ell(h, blk, ell, W, pd, dd, vd, based ? base.data() : nullptr)) {
+            if (based) {
+                d.dv_ell_base = dev_alloc<int>(base.size());
+                if (!d.dv_ell_base) return hip_fail(hipErrorOutOfMemory, "hipMalloc(ELL bases)", __FILE__, __LINE__);
+                if (int rc = h2d(d.dv_ell_base, base.data(), sizeof(int) * base.size())) return rc;
+            }
             d.ell_w = W;
             const char *rz = getenv("SSS_HIP_ELL_REMAP");
             d.ell_remap = (rz && *rz) ? atoi(rz) : 0;
@@ -1003,7 +1017,7 @@ int devcsr_upload(DevCSR &d, const SSS_MAT &h, int split, int enc, const int *se
         if (nb > 0) SSS_HIP(hipMemcpy(pd.data(), d.dv_pd, sizeof(int4) * (size_t)nb, hipMemcpyDeviceToHost));
         for (const auto &p : pd) dict += 4LL * p.y + 8LL * p.w;
         d.stream_bytes = d.dv_xell ? 4LL * d.xell_w * rows + 8 * (nb + 1) + 16 * nb + dict
-                         : d.dv_ell ? (long long)d.ell_w * rows + 8 * (nb + 1) + 16 * nb + dict
+                         : d.dv_ell ? (long long)(d.ell_w + (d.dv_ell_base ? 4 : 0)) * rows + 8 * (nb + 1) + 16 * nb + dict
                                   : (d.dv_vi ? 5 * nnz + 8 * nb : 4 * nnz) + 4 * (rows + 1) + 8 * (nb + 1) + 16 * nb + dict;
     } else if (d.pk) {
         d.stream_bytes = 12 * nnz + 4 * (rows + 1) + 8 * (nb + 1) + 8 * nb;
@@ -1041,6 +1055,7 @@ void devcsr_free(DevCSR &d)
     dev_free(d.mg_v);
     dev_free(d.dv_code);
     dev_free(d.dv_ell);
+    dev_free(d.dv_ell_base);
     dev_free(d.dv_xell);
     dev_free(d.dv_vi);
     dev_free(d.dv_pd);
@@ -1157,7 +1172,7 @@ __global__ __launch_bounds__(kBlock) void spmv_adaptive(const int2 *__restrict__
         const int g = ell_block_order(dt.remap, (int)blockIdx.x, (int)gridDim.x);
         unsigned w[RPT][W / 4];
         double br[RPT];
-        int r[RPT];
+        int r[RPT], rb[RPT];   // rb: the row's offset base (its own index, or dt.ellb[r])
         bool live[RPT], valid[RPT];
 #pragma unroll
         for (int j = 0; j < RPT; ++j) {   // codes (and b) in flight across the dictionaries' barrier
@@ -1165,7 +1180,7 @@ __global__ __launch_bounds__(kBlock) void spmv_adaptive(const int2 *__restrict__
             valid[j] = bid < dt.bend;
             live[j] = false;
             br[j] = 0.0;
-            r[j] = 0;
+            r[j] = rb[j] = 0;
 #pragma unroll
             for (int t = 0; t < W / 4; ++t) w[j][t] = 0u;
             if (valid[j]) {
@@ -1174,6 +1189,7 @@ __global__ __launch_bounds__(kBlock) void spmv_adaptive(const int2 *__restrict__
                 live[j] = r[j] < be.x;
                 if (live[j]) {
                     ell_codes<W>(dt.ell, r[j], w[j]);
+                    rb[j] = dt.ellb ? dt.ellb[r[j]] : r[j];
                     if constexpr (OP == SSS_HIP_SPMV_RESID) br[j] = b[r[j]];
                 }
                 ell_load_dicts_nosync(dt, bid, es[j]);
@@ -1187,7 +1203,7 @@ __global__ __launch_bounds__(kBlock) void spmv_adaptive(const int2 *__restrict__
                 double p[W];
                 int ds;
                 double dv;
-                const int len = ell_decode<W>(w[j], r[j], es[j], [&](int c) -> double { return x[c]; }, p, ds, dv);
+                const int len = ell_decode<W>(w[j], rb[j], es[j], [&](int c) -> double { return x[c]; }, p, ds, dv);
                 if constexpr (OP == SSS_HIP_SPMV_RESID) {
                     const double out = br[j] + ell_add(0.0, p, 0, len) * alpha;
                     y[r[j]] = out;

@@ -71,6 +71,7 @@ struct DevDict {
     const int2 *pb = nullptr;
     int tree_long = 0;   // DevCSR::tree_long (set for every matrix, dictionary or not)
     const unsigned char *ell = nullptr;   // dictionary ELL (DevCSR::dv_ell), ell_w bytes per row
+    const int *ellb = nullptr;            // its per-row base columns (DevCSR::dv_ell_base) or null
     int ellw = 0;
     int remap = 0;   // ELL launches: XCD-contiguous block order (DevCSR::ell_remap)
     int bend = 0x7fffffff;   // ELL launches: first block past the launch's range (kEllRpt blocks per workgroup)

@@ -427,7 +427,7 @@ def test_solve_hybrid_krylov_bitwise(request, hname, inner, inner_from, row_path
 
 
 @pytest.mark.parametrize("knob", ["SSS_HIP_FUSE_RESID", "SSS_HIP_DEAD_PROLONG", "SSS_HIP_TILE_DIAG", "SSS_HIP_PEND_F",
-                                  "SSS_HIP_ZERO_FIRST", "SSS_HIP_INJECT"])
+                                  "SSS_HIP_ZERO_FIRST", "SSS_HIP_INJECT", "SSS_HIP_ELL_BASE"])
 @pytest.mark.parametrize("smoother,coarse", [("exact", "krylov"), ("hybrid", "direct")])
 def test_fused_residual_bitwise(p32_h, smoother, coarse, knob, monkeypatch):
     """Level 0 of 7-pt Poisson is red-black.  SSS_HIP_FUSE_RESID: the last C pass of each smoother
@@ -438,7 +438,9 @@ def test_fused_residual_bitwise(p32_h, smoother, coarse, knob, monkeypatch):
     computes the next cycle's first F pass, which the cycle then skips.  SSS_HIP_ZERO_FIRST: the
     first C/F-Jacobi or two-stage pass of a coarse level's pre-smoother (x just zeroed) reduces to
     t = b without reading the matrix.  SSS_HIP_INJECT: that C-row prolongation, whose rows are each
-    one stored 1.0, reads only their columns (prolong_inject) instead of the tiles.  With each
+    one stored 1.0, reads only their columns (prolong_inject) instead of the tiles.
+    SSS_HIP_ELL_BASE: the restriction as a dictionary ELL whose offsets are taken against each row's
+    first column (DevCSR::dv_ell_base) instead of the column ELL.  With each
     on/off: x, the in-cycle residual wp and the
     outer residual norm are bitwise
     identical over several cycles."""
