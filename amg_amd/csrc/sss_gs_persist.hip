@@ -175,16 +175,28 @@ __global__ __launch_bounds__(kBlock) void gs_flow_group(int nchunks, const int *
             for (int j0 = 0; j0 < nj; j0 += U) {   // (A)
                 int c[U];
                 double a[U], xv[U];
+                // every load of the group unconditional (slots past the row re-read its entry gl,
+                // then read as the diagonal): loads under a condition were issued one round trip
+                // at a time; the x value of a same-pass entry is fetched too and left unused
+#pragma unroll
+                for (int u = 0; u < U; ++u) c[u] = ci[kb + (j0 + u < nj ? gl + G * (j0 + u) : gl)];
+#pragma unroll
+                for (int u = 0; u < U; ++u) a[u] = v[kb + (j0 + u < nj ? gl + G * (j0 + u) : gl)];
+#pragma unroll
+                for (int u = 0; u < U; ++u) xv[u] = x[c[u]];
+#pragma unroll
+                for (int u = 0; u < U; ++u) c[u] = j0 + u < nj ? c[u] : i;
+                // the group's granule polls issued together, read after the loop (a poll read
+                // inside its own condition waited for its round trip before the next was issued)
+                unsigned long long ga[U], gc[U];
 #pragma unroll
                 for (int u = 0; u < U; ++u) {
-                    const int t = gl + G * (j0 + u);
-                    c[u] = j0 + u < nj ? ci[kb + t] : i;
-                    a[u] = j0 + u < nj ? v[kb + t] : 0.0;
-                }
-#pragma unroll
-                for (int u = 0; u < U; ++u) {
-                    xv[u] = 0.0;
-                    if (c[u] != i && !dynamic(c[u], i)) xv[u] = x[c[u]];
+                    ga[u] = gc[u] = 0ull;
+                    if (dynamic(c[u], i)) {
+                        const unsigned long long *gg = gran + 2 * (size_t)(c[u] - lo);
+                        ga[u] = __hip_atomic_load(const_cast<unsigned long long *>(gg), RLX_AGENT);
+                        gc[u] = __hip_atomic_load(const_cast<unsigned long long *>(gg + 1), RLX_AGENT);
+                    }
                 }
 #pragma unroll
                 for (int u = 0; u < U; ++u) {
@@ -192,8 +204,8 @@ __global__ __launch_bounds__(kBlock) void gs_flow_group(int nchunks, const int *
                     const int t = gl + G * (j0 + u);
                     double val = 0.0;   // the diagonal: subtracting +0.0 is the identity
                     if (dynamic(c[u], i)) {
-                        double g = 0.0;
-                        if (granule_get(gran + 2 * (size_t)(c[u] - lo), epoch, g)) val = a[u] * g;
+                        if ((unsigned)(ga[u] >> 32) == epoch && (unsigned)(gc[u] >> 32) == epoch)
+                            val = a[u] * __longlong_as_double((long long)((gc[u] << 32) | (ga[u] & 0xffffffffull)));
                         else {
                             pend |= 1u << (j0 + u);
                             if (ovl) val = __longlong_as_double((long long)c[u]);   // its column, until resolved
