@@ -139,7 +139,10 @@ __global__ __launch_bounds__(kBlock) void gs_flow_group(int nchunks, const int *
                                                         int lo, int hi, unsigned *ctl, unsigned *err, int spin, int ovl,
                                                         unsigned long long *trace)
 {
-    constexpr int R = 64 / G, CAP = kGroupBuf / R, U = 8;
+#ifndef SSS_GS_U
+#define SSS_GS_U 8
+#endif
+    constexpr int R = 64 / G, CAP = kGroupBuf / R, U = SSS_GS_U;   // U: a lane's entries per staging group
     // a same-pass row this row reads the NEW value of (published by its granules)
     auto dynamic = [&](int c, int i) { return DESC ? (c > i && c < hi) : (c >= lo && c < i); };
     static_assert(CAP / G == 32, "one pending bit per staged entry of a lane");
