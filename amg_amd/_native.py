@@ -110,7 +110,7 @@ ABI_SYMBOLS = [
     "sss_hip_upload_vec", "sss_hip_download_vec", "sss_hip_cycle", "sss_hip_residual_norm", "sss_hip_pcg",
     "SSS_amg_save", "SSS_amg_load",
     "sss_hip_coarse_solve", "sss_hip_smooth", "sss_hip_sync", "sss_hip_level_info_get", "sss_hip_num_levels", "sss_hip_tail_from",
-    "sss_hip_cycle_launches",
+    "sss_hip_cycle_launches", "sss_hip_cycle_bytes",
     "sss_hip_spmv_plan_create", "sss_hip_spmv_plan_destroy", "sss_hip_spmv", "sss_hip_host_spmv",
     "sss_hip_host_smooth", "sss_hip_host_coarse_solve", "sss_hip_host_cache_clear", "sss_hip_time_level0_spmv", "sss_hip_time_iterations",
     "sss_hip_time_level0_spmv_csr",
@@ -196,6 +196,7 @@ def _declare(lib):
         "sss_hip_num_levels": (C.c_int, [C.c_void_p]),
         "sss_hip_tail_from": (C.c_int, [C.c_void_p]),
         "sss_hip_cycle_launches": (C.c_int, [C.c_void_p]),
+        "sss_hip_cycle_bytes": (C.c_int, [C.c_void_p, C.POINTER(C.c_double), C.c_int]),
         "sss_hip_host_spmv": (C.c_int, [C.c_int, C.c_double, P(SSS_MAT), _dbl_p, _dbl_p, _dbl_p, C.c_int]),
         "sss_hip_host_smooth": (C.c_int, [P(SSS_SMTR), C.c_int]),
         "sss_hip_host_coarse_solve": (C.c_int, [P(SSS_MAT), P(SSS_VEC), P(SSS_VEC), C.c_double, C.c_int,
@@ -432,6 +433,15 @@ class DeviceHierarchy:
         ms = C.c_double()
         self._check(lib().sss_hip_time_level0_spmv(self.h, reps, C.byref(ms)), "time_level0_spmv")
         return ms.value
+
+    def cycle_bytes(self) -> dict:
+        """Stored-format bytes of one outer iteration (sss_hip_cycle_bytes): per level, the outer
+        residual + norm, the coarsest solve, and their total."""
+        nl = lib().sss_hip_num_levels(self.h)
+        buf = (C.c_double * (nl + 2))()
+        self._check(lib().sss_hip_cycle_bytes(self.h, buf, nl + 2), "cycle_bytes")
+        v = list(buf)
+        return {"levels": v[:nl], "outer": v[nl], "coarse": v[nl + 1], "total": sum(v)}
 
     def time_level0_spmv_csr(self, reps: int) -> float:
         """the same residual SpMV from A_0's plain CSR arrays (the metric's fine-level CSR SpMV)"""

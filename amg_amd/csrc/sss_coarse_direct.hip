@@ -133,6 +133,7 @@ void coarse_direct_free(CoarseDirect &cd)
 
 int coarse_direct_apply(const CoarseDirect &cd, const double *b, double *x, hipStream_t s)
 {
+    ledger_add(8.0 * cd.n * (double)cd.n + 16.0 * cd.n);
     hipLaunchKernelGGL(dense_gemv, dim3((cd.n + 3) / 4), dim3(256), 0, s, cd.inv, cd.n, b, x);
     SSS_HIP(hipGetLastError());
     return 0;

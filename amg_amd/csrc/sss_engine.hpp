@@ -170,6 +170,7 @@ struct DevCSR {
     int nblk = 0;          // SpMV row blocks
     int *blk = nullptr;    // block -> first row (nblk + 1 entries)
     int2 *bk = nullptr;    // block -> {first row, first entry} (nblk + 1): one load, no rp[blk[.]] chain
+    const int2 *h_bk = nullptr;   // host copy of bk (the byte ledger's block -> rows / entries)
     int split_row = -1;    // class split row the blocks were cut at (-1: none)
     int split_blk = 0;     // index of the block starting at split_row
     bool wave_rows = false;  // long rows: wave-per-row kernels (avg nnz/row >= kWaveRowMin)
@@ -273,7 +274,8 @@ int transfer_encoding(const sss_hip_opts &o);
 int restriction_encoding(const sss_hip_opts &o);
 void devcsr_free(DevCSR &d);
 int build_row_blocks(const int *h_rp, int n, std::vector<int> &blk, int split = -1);
-int upload_block_bounds(int2 **dst, const std::vector<int> &blk, const int *h_rp);
+// *host (optional): a new[]-allocated host copy (DevCSR::h_bk, released by devcsr_free)
+int upload_block_bounds(int2 **dst, const std::vector<int> &blk, const int *h_rp, const int2 **host = nullptr);
 int wave_row_min();
 int free_row_min();
 // Re-upload a free-order matrix's CSR rows column-sorted (one uploaded kEncMergedOnly whose
@@ -321,6 +323,28 @@ inline void with_tile_kind(const DevCSR &A, F f)
         f(std::integral_constant<int, 0>{});
     }
 }
+
+// ---- stored-format byte ledger (bench.py `vcycle_stored`, tools/level_breakdown.py) -------------
+// While a ledger is installed on the calling thread (sss_hip_cycle_bytes: one eager walk of the
+// cycle with launches enqueued as usual), every launch helper adds the bytes its kernel reads and
+// writes: the stored format of the rows it covers (codes, dictionaries, values, row bounds --
+// DevCSR::stream_bytes pro rata: by rows for the ELL formats, by entries otherwise), 8 B per covered
+// row for every row vector it streams (b, y read and/or written, divisors, P), and the x it gathers
+// counted once per covered row (8 B x covered rows x ncols / n).  Slot kMaxLevels is the outer
+// residual + norm, kMaxLevels + 1 the coarsest solve.
+struct ByteLedger {
+    double bytes[kMaxLevels + 2] = {};
+    int slot = 0;
+};
+extern thread_local ByteLedger *g_ledger;
+inline void ledger_add(double b)
+{
+    if (g_ledger) g_ledger->bytes[g_ledger->slot] += b;
+}
+inline bool ledger_on() { return g_ledger != nullptr; }
+double matrix_bytes(const DevCSR &A, int blo, int bhi);   // stored bytes of row blocks [blo, bhi)
+double matrix_bytes_rows(const DevCSR &A, int lo, int hi);   // ... of rows [lo, hi) (block granularity)
+inline double xgather_bytes(const DevCSR &A, double rows) { return A.n ? 8.0 * rows * A.ncols / A.n : 0.0; }
 
 // ---- hierarchy internals shared with the distributed engine (sss_hier.hip) ------------------
 // A hierarchy over mg->cg[0 .. num_levels); its L[0] is global level `level_base` (smoother

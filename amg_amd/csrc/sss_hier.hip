@@ -559,12 +559,22 @@ static int tail_build(sss_hip_hier *h, const SSS_AMG *mg)
             tp.nrp = ps.ts_nl.rp, tp.nci = ps.ts_nl.ci, tp.nv = ps.ts_nl.v, tp.split = ps.ts_split;
             tp.lrp = ps.ts_lo.rp, tp.lci = ps.ts_lo.ci, tp.lv = ps.ts_lo.v, tp.P = ps.ts_P;
         }
+        // ledger: per sweep each class pass streams its [N | L] rows and `inner` times its L rows
+        // (+ 40 B of vectors per row each), then the residual, R and P
+        const int sweeps = h->pars.pre_iter + h->pars.post_iter;
+        for (int c = 0; c < 2; ++c)
+            if (sp.pass[c].nrows > 0)
+                h->tail.ledger_bytes += sweeps * ((double)sp.pass[c].ts_nl.stream_bytes + 40.0 * sp.pass[c].nrows +
+                                                  sp.inner * ((double)sp.pass[c].ts_lo.stream_bytes + 40.0 * sp.pass[c].nrows));
+        h->tail.ledger_bytes += (double)L.A.stream_bytes + (double)L.R.stream_bytes + (double)L.P.stream_bytes +
+                                32.0 * L.A.n + 16.0 * t.nc;
         t.arp = L.A.rp, t.aci = L.A.ci, t.av = L.A.v;
         t.rrp = L.R.rp, t.rci = L.R.ci, t.rv = L.R.v;
         t.prp = L.P.rp, t.pci = L.P.ci, t.pv = L.P.v;
         lv.push_back(t);
     }
     const auto &Cl = h->L[nl - 1];
+    h->tail.ledger_bytes += 8.0 * h->direct.n * (double)h->direct.n + 16.0 * h->direct.n;
     h->tail.inv = h->direct.inv;
     h->tail.nc = h->direct.n;
     h->tail.cb = Cl.b;
@@ -936,6 +946,7 @@ static int walk_cycle(sss_hip_hier *h, CoarseFn coarse, bool pend = false)
     hipStream_t s = h->stream;
     for (;;) {
         while (l < nl - 1) {
+            if (g_ledger) g_ledger->slot = l;
             if (h->tail.from > 0 && l == h->tail.from && cycle_type == 1) {
                 // levels tail.from .. nl-1: descent, coarsest solve and ascent in one launch
                 if ((rc = tail_launch(h->tail, s))) return rc;
@@ -948,12 +959,15 @@ static int walk_cycle(sss_hip_hier *h, CoarseFn coarse, bool pend = false)
             if ((rc = smooth_then_residual(h, l, 0, nullptr, pend && first ? h->pend_f : nullptr, l > 0))) return rc;
             if ((rc = launch_spmv(L.R, SSS_HIP_SPMV_MXY, 1.0, L.wp, nullptr, h->L[l + 1].b, 0, nullptr, s))) return rc;
             l++;
+            ledger_add(8.0 * h->L[l].A.n);
             SSS_HIP(hipMemsetAsync(h->L[l].x, 0, sizeof(double) * (size_t)h->L[l].A.n, s));
         }
+        if (g_ledger) g_ledger->slot = kMaxLevels + 1;
         if ((rc = coarse(h))) return rc;
     ascent:
         while (l > 0) {
             l--;
+            if (g_ledger) g_ledger->slot = l;
             auto &L = h->L[l];
             // x_l += P e.  When the post-smoother's first pass overwrites every F row from C values
             // only (depth-1 GS F pass, all |d| > 1e-20), the F rows' correction is dead: prolong
@@ -1220,6 +1234,44 @@ extern "C" int sss_hip_sync(sss_hip_hier *h)
 }
 
 extern "C" int sss_hip_num_levels(sss_hip_hier *h) { return h ? h->nl : 0; }
+
+// The stored-format bytes one outer iteration's kernels read and write (sss_engine.hpp ByteLedger):
+// the cycle as sss_hip_cycle would run it next, and the residual + norm after it, walked into a
+// stream capture that is discarded (nothing executes).  out[l] for level l < nslots - 2 (coarse
+// levels of a single-workgroup tail land on its first level), out[nslots - 2] the outer residual +
+// norm, out[nslots - 1] the coarsest solve (explicit inverse; the device Krylov solver is not
+// counted).  nslots >= num_levels + 2.
+extern "C" int sss_hip_cycle_bytes(sss_hip_hier *h, double *out, int nslots)
+{
+    if (!h || !out || nslots < h->nl + 2) return ERROR_INPUT_PAR;
+    const bool pend = h->pending_f && h->nl > 1 && h->pars.pre_iter > 0;
+    const bool f_only_next = h->nl > 1 && h->L[0].sm.fuse_resid && h->pars.post_iter > 0;
+    const bool keep_pending = h->pending_f, keep_ready = h->resid_c_ready;
+    ByteLedger led;
+    SSS_HIP(hipStreamSynchronize(h->stream));
+    SSS_HIP(hipStreamBeginCapture(h->stream, hipStreamCaptureModeThreadLocal));
+    g_ledger = &led;
+    int rc = walk_cycle(h, [](sss_hip_hier *hh) {
+        return hh->coarse_mode == SSS_HIP_COARSE_DIRECT ? coarse_direct_apply(hh->direct, hh->L[hh->nl - 1].b,
+                                                                              hh->L[hh->nl - 1].x, hh->stream)
+                                                        : 0;
+    }, pend);
+    led.slot = kMaxLevels;
+    if (!rc) rc = enqueue_residual_norm(h, f_only_next);
+    g_ledger = nullptr;
+    hipGraph_t g = nullptr;
+    hipError_t e = hipStreamEndCapture(h->stream, &g);
+    if (g) (void)hipGraphDestroy(g);
+    h->pending_f = keep_pending;
+    h->resid_c_ready = keep_ready;
+    if (rc) return rc;
+    SSS_HIP(e);
+    for (int i = 0; i < nslots; ++i) out[i] = 0.0;
+    for (int l = 0; l < h->nl && l < kMaxLevels; ++l) out[l] = led.bytes[l];
+    out[nslots - 2] = led.bytes[kMaxLevels];
+    out[nslots - 1] = led.bytes[kMaxLevels + 1];
+    return 0;
+}
 
 extern "C" int sss_hip_tail_from(sss_hip_hier *h) { return h ? h->tail.from : -1; }
 

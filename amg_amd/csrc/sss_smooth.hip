@@ -1130,10 +1130,21 @@ __global__ __launch_bounds__(kBlock) void ts_inner(int lo, DevCSR M, const doubl
     }
 }
 
+// ledger (sss_engine.hpp ByteLedger): a pass's matrix bytes -- the rows [lo, hi) of a contiguous class,
+// else the pass's share of A -- + the x it gathers (8 B per row) + `vec` bytes of row vectors per row
+static void ledger_pass(const DevCSR &A, const PassSchedule &ps, double vec)
+{
+    if (!ledger_on()) return;
+    const double mat = ps.range ? matrix_bytes_rows(A, ps.lo, ps.hi)
+                                : (A.n ? (double)A.stream_bytes * ps.nrows / A.n : 0.0);
+    ledger_add(mat + (8.0 + vec) * ps.nrows);
+}
+
 void launch_ts_stage0(const DevCSR &M, int lo, const int *split, const double *b, XSrc x, const double *deff,
                       double *P, double *y, hipStream_t s)
 {
     if (M.n == 0) return;
+    ledger_add((double)M.stream_bytes + 40.0 * M.n);   // + x gathers, b, deff, P and y
     if (M.mg_G == 8 && M.mg_two)
         hipLaunchKernelGGL(ts_stage0<8>, dim3(M.ngrid), dim3(kBlock), 0, s, lo, M, split, b, x, deff, P, y);
     else if (M.mg_G == 4 && M.mg_two)
@@ -1156,6 +1167,7 @@ void launch_ts_inner(const DevCSR &M, int lo, const double *deff, const double *
                      const double *ykeep, double *y, hipStream_t s)
 {
     if (M.n == 0) return;
+    ledger_add((double)M.stream_bytes + 40.0 * M.n);   // + y gathers, deff, P, ykeep and y
     if (M.mg_G == 8)
         hipLaunchKernelGGL(ts_inner<8>, dim3(M.ngrid), dim3(kBlock), 0, s, lo, M, deff, P, ycols, col_off, ykeep, y);
     else if (M.mg_G == 4)
@@ -1217,6 +1229,7 @@ int launch_f_residual_pending(const SmootherPlan &sp, const DevCSR &A, const dou
     if (!sp.pend_ok) return ERROR_INPUT_PAR;
     const PassSchedule &F = sp.pass[0];
     const double *deff = (sp.own_diag && (A.pk || has_dict(A))) ? nullptr : sp.d_first;
+    ledger_pass(A, F, deff ? 40.0 : 32.0);   // b, r, pend (and deff)
     with_tile_kind(A, [&](auto K) {
         launch_relax_range<3, decltype(K)::value>(F.blo, F.bhi - F.blo, s, devdict(A, 0), A.bk, A.rp, A.ci, A.v,
                                                   sp.diag_pos, F.lo, b, const_cast<double *>(x), (const double *)nullptr,
@@ -1237,6 +1250,7 @@ __global__ __launch_bounds__(kBlock) void scatter_rows(int m, const int *__restr
 static int depth_launches(const PassSchedule &ps, bool long_rows, bool nat, const DevCSR &A, const double *b, double *x,
                           const double *deff, hipStream_t s)
 {
+    ledger_pass(A, ps, 24.0);   // b, deff, x written
     for (int l = 0; l < ps.depth; ++l) {
         const int off = ps.h_off[l], cnt = ps.h_off[l + 1] - off;
         if (cnt == 0) continue;
@@ -1323,6 +1337,7 @@ int smoother_run(const SmootherPlan &sp, const DevCSR &A, const double *b, doubl
         if (ps.nrows == 0) return 0;
         for (int sw = 0; sw < sweeps; ++sw) {
             const double *deff = post ? (sw == 0 ? sp.nd_first : sp.nd_later) : (sw == 0 ? sp.d_first : sp.d_later);
+            if (ps.gp.engine) ledger_pass(A, ps, 24.0);
             int rc = ps.gp.engine ? gs_persist_run(ps, A, b, x, deff, s) : depth_launches(ps, sp.long_rows, true, A, b, x, deff, s);
             if (rc) return rc;
         }
@@ -1364,6 +1379,7 @@ int smoother_run(const SmootherPlan &sp, const DevCSR &A, const double *b, doubl
                 const bool tile_d = sp.own_diag && (A.pk != nullptr || has_dict(A));
                 auto relax = [&](auto mode, const int *cols, const double *yp, double *y) -> int {
                     constexpr int M = decltype(mode)::value;
+                    ledger_pass(A, ps, (tile_d && !wave) ? 16.0 : 24.0);   // b, the written row (and deff)
                     if (wave && A.vec_rows)
                         hipLaunchKernelGGL((relax_range_wave<M, true>), dim3(nw), dim3(kBlock), 0, s, ps.lo, ps.hi,
                                            A.rp, cols, A.v, b, x, yp, y, deff, xs);
@@ -1390,16 +1406,18 @@ int smoother_run(const SmootherPlan &sp, const DevCSR &A, const double *b, doubl
                     // this class) are refreshed after every stage
                     const DevCSR &Mn = ps.ts_nl, &Ml = ps.ts_lo;
                     double *wcur = hk->w0, *wnxt = hk->w1;
-                    if (zfirst)
+                    if (zfirst) {
+                        ledger_add(32.0 * m);
                         hipLaunchKernelGGL(zero_first_pass<true>, dim3((m + kBlock - 1) / kBlock), dim3(kBlock), 0, s,
                                            ps.lo, m, Mn.rp, Mn.ci, Mn.v, ps.ts_split, b, deff, ps.ts_P, wcur + ps.lo);
-                    else
+                    } else
                         launch_ts_stage0(Mn, ps.lo, ps.ts_split, b, xsrc_of(x), deff, ps.ts_P, wcur + ps.lo, s);
                     for (int st = 0; st < sp.inner; ++st) {
                         if ((rc = hk->exchange(hk->ctx, wcur))) return rc;
                         launch_ts_inner(Ml, ps.lo, deff, ps.ts_P, wcur, 0, wcur + ps.lo, wnxt + ps.lo, s);
                         std::swap(wcur, wnxt);
                     }
+                    ledger_add(16.0 * m);
                     SSS_HIP(hipMemcpyAsync(x + ps.lo, wcur + ps.lo, sizeof(double) * (size_t)m, hipMemcpyDeviceToDevice,
                                            s));
                 } else if (sp.kind == SSS_HIP_SMOOTH_JACOBI && nocopy) {
@@ -1407,6 +1425,7 @@ int smoother_run(const SmootherPlan &sp, const DevCSR &A, const double *b, doubl
                     // class's previous iterate, so they alternate between the two buffers in place
                     double *prev = cur[c] == x ? sp.x2 : x, *next = cur[c];
                     const int zg = (m + kBlock - 1) / kBlock;
+                    if (zfirst) ledger_add((sp.inner > 0 ? 32.0 : 24.0) * m);   // b, deff, y (and P)
                     if (zfirst && sp.inner > 0)
                         hipLaunchKernelGGL(zero_first_pass<true>, dim3(zg), dim3(kBlock), 0, s, ps.lo, m, ps.ts_nl.rp,
                                            ps.ts_nl.ci, ps.ts_nl.v, ps.ts_split, b, deff, ps.ts_P, prev + ps.lo);
@@ -1430,16 +1449,20 @@ int smoother_run(const SmootherPlan &sp, const DevCSR &A, const double *b, doubl
                         launch_ts_inner(Ml, ps.lo, deff, ps.ts_P, ycur, ps.lo, ycur, ynxt, s);
                         std::swap(ycur, ynxt);
                     }
+                    ledger_add(16.0 * m);
                     SSS_HIP(hipMemcpyAsync(x + ps.lo, ycur, sizeof(double) * (size_t)m, hipMemcpyDeviceToDevice, s));
                 } else if (sp.kind == SSS_HIP_SMOOTH_JACOBI && zfirst) {
                     // the pass reads no x at all, so it may write x in place
+                    ledger_add(24.0 * m);
                     hipLaunchKernelGGL(zero_first_pass<false>, dim3((m + kBlock - 1) / kBlock), dim3(kBlock), 0, s,
                                        ps.lo, m, A.rp, A.ci, A.v, (const int *)nullptr, b, deff, (double *)nullptr,
                                        x + ps.lo);
                 } else if (sp.kind == SSS_HIP_SMOOTH_JACOBI) {
                     if ((rc = relax(std::integral_constant<int, 1>(), A.ci, (const double *)nullptr, ps.y))) return rc;
+                    ledger_add(16.0 * m);
                     SSS_HIP(hipMemcpyAsync(x + ps.lo, ps.y, sizeof(double) * (size_t)m, hipMemcpyDeviceToDevice, s));
                 } else if (fused_pass) {
+                    ledger_pass(A, ps, tile_d ? 24.0 : 32.0);   // b, x and r written (and deff)
                     auto go = [&](int b0, int b1) {
                         with_tile_kind(A, [&](auto K) {
                             launch_relax_range<2, decltype(K)::value>(
@@ -1457,11 +1480,14 @@ int smoother_run(const SmootherPlan &sp, const DevCSR &A, const double *b, doubl
                 } else if ((rc = relax(std::integral_constant<int, 0>(), A.ci, (const double *)nullptr, (double *)nullptr))) {
                     return rc;
                 }
-                if (pre_f && sw == 0 && c == 1 && sweeps == 1)   // no later F pass overwrites x_F
+                if (pre_f && sw == 0 && c == 1 && sweeps == 1) {   // no later F pass overwrites x_F
+                    ledger_add(16.0 * sp.pass[0].hi);
                     SSS_HIP(hipMemcpyAsync(x, pre_f, sizeof(double) * (size_t)sp.pass[0].hi, hipMemcpyDeviceToDevice, s));
+                }
                 continue;
             }
             if (sp.kind == SSS_HIP_SMOOTH_JACOBI) {
+                ledger_add((double)ps.sub.stream_bytes + (8.0 + 24.0 + 20.0) * ps.nrows);   // + the scatter
                 if (ps.sub.wave_rows)
                     hipLaunchKernelGGL(relax_wave<false>, dim3(ps.sub.ngrid), dim3(kBlock), 0, s, ps.nrows, ps.sub.rp,
                                        ps.sub.ci, ps.sub.v, ps.map, b, x, ps.y, sp.d_first);
@@ -1473,6 +1499,7 @@ int smoother_run(const SmootherPlan &sp, const DevCSR &A, const double *b, doubl
                 continue;
             }
             if (ps.compact) {
+                ledger_add((double)ps.sub.stream_bytes + (8.0 + 24.0 + 4.0) * ps.nrows);   // + the row map
                 if (ps.sub.wave_rows)
                     hipLaunchKernelGGL(relax_wave<true>, dim3(ps.sub.ngrid), dim3(kBlock), 0, s, ps.nrows, ps.sub.rp,
                                        ps.sub.ci, ps.sub.v, ps.map, b, x, (double *)nullptr, deff);
@@ -1482,6 +1509,7 @@ int smoother_run(const SmootherPlan &sp, const DevCSR &A, const double *b, doubl
                 continue;
             }
             if (ps.gp.engine) {
+                ledger_pass(A, ps, 24.0);
                 if ((rc = gs_persist_run(ps, A, b, x, deff, s))) return rc;
                 continue;
             }
@@ -1489,9 +1517,11 @@ int smoother_run(const SmootherPlan &sp, const DevCSR &A, const double *b, doubl
         }
     }
     for (int c = 0; c < 2; ++c)   // odd number of writes to a class (odd sweeps x (1 + inner))
-        if (cur[c] != x)
+        if (cur[c] != x) {
+            ledger_add(16.0 * (sp.pass[c].hi - sp.pass[c].lo));
             SSS_HIP(hipMemcpyAsync(x + sp.pass[c].lo, cur[c] + sp.pass[c].lo,
                                    sizeof(double) * (size_t)(sp.pass[c].hi - sp.pass[c].lo), hipMemcpyDeviceToDevice, s));
+        }
     SSS_HIP(hipGetLastError());
     return 0;
 }

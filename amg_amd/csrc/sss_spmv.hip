@@ -223,13 +223,47 @@ static int merge_group_size(int n)
 }
 
 // {first row, first entry} of every block, so a block's bounds are one independent load.
-int upload_block_bounds(int2 **dst, const std::vector<int> &blk, const int *h_rp)
+int upload_block_bounds(int2 **dst, const std::vector<int> &blk, const int *h_rp, const int2 **host)
 {
     std::vector<int2> bk(blk.size());
     for (size_t q = 0; q < blk.size(); ++q) bk[q] = make_int2(blk[q], h_rp[blk[q]]);
     *dst = dev_alloc<int2>(bk.size());
     if (!*dst) return hip_fail(hipErrorOutOfMemory, "hipMalloc(bk)", __FILE__, __LINE__);
+    if (host) {
+        delete[] *host;
+        int2 *c = new int2[bk.size()];
+        std::copy(bk.begin(), bk.end(), c);
+        *host = c;
+    }
     return h2d(*dst, bk.data(), sizeof(int2) * bk.size());
+}
+
+thread_local ByteLedger *g_ledger = nullptr;
+
+double matrix_bytes(const DevCSR &A, int blo, int bhi)
+{
+    if (bhi <= blo || A.n == 0) return 0.0;
+    if (!A.h_bk || A.nblk == 0 || (blo == 0 && bhi >= A.nblk)) return (double)A.stream_bytes;
+    const bool by_rows = A.dv_ell || A.dv_xell || A.nnz == 0;
+    const double part = by_rows ? (double)(A.h_bk[bhi].x - A.h_bk[blo].x) / A.n
+                                : (double)(A.h_bk[bhi].y - A.h_bk[blo].y) / A.nnz;
+    return part * (double)A.stream_bytes;
+}
+
+double matrix_bytes_rows(const DevCSR &A, int lo, int hi)
+{
+    if (hi <= lo || A.n == 0) return 0.0;
+    if (!A.h_bk || A.nblk == 0) return (double)A.stream_bytes * (hi - lo) / A.n;
+    auto blk_of = [&](int r) {   // first block starting at or after row r
+        int a = 0, b = A.nblk;
+        while (a < b) {
+            const int m = (a + b) / 2;
+            if (A.h_bk[m].x < r) a = m + 1;
+            else b = m;
+        }
+        return a;
+    };
+    return matrix_bytes(A, blk_of(lo), blk_of(hi));
 }
 
 int build_row_blocks(const int *h_rp, int n, std::vector<int> &blk, int split)
@@ -831,7 +865,7 @@ int devcsr_upload(DevCSR &d, const SSS_MAT &h, int split, int enc, const int *se
     d.blk = dev_alloc<int>(blk.size());
     if (!d.blk) return hip_fail(hipErrorOutOfMemory, "hipMalloc(blk)", __FILE__, __LINE__);
     if (int rc = h2d(d.blk, blk.data(), sizeof(int) * blk.size())) return rc;
-    if (int rc = upload_block_bounds(&d.bk, blk, h.row_ptr)) return rc;
+    if (int rc = upload_block_bounds(&d.bk, blk, h.row_ptr, &d.h_bk)) return rc;
     d.ngrid = (d.wave_rows || d.vec_rows) ? (d.n + 3) / 4 : d.nblk;
     pt.mark("blocks");
     if (d.mg_G > 0 && device_builders_on()) {   // from the stored-order CSR just uploaded
@@ -945,7 +979,7 @@ int devcsr_upload(DevCSR &d, const SSS_MAT &h, int split, int enc, const int *se
             d.blk = dev_alloc<int>(blk.size());
             if (!d.blk) return hip_fail(hipErrorOutOfMemory, "hipMalloc(blk)", __FILE__, __LINE__);
             if (int rc = h2d(d.blk, blk.data(), sizeof(int) * blk.size())) return rc;
-            if (int rc = upload_block_bounds(&d.bk, blk, h.row_ptr)) return rc;
+            if (int rc = upload_block_bounds(&d.bk, blk, h.row_ptr, &d.h_bk)) return rc;
             d.xell_w = W;
             d.xell_shift = xshift;
             d.dv_xell = dev_alloc<unsigned>(codes.size());
@@ -1061,6 +1095,7 @@ void devcsr_free(DevCSR &d)
     dev_free(d.dv_pd);
     dev_free(d.dv_dd);
     dev_free(d.dv_vd);
+    delete[] d.h_bk;
     d = DevCSR();
 }
 
@@ -1328,10 +1363,15 @@ static void launch_op(const DevCSR &A, double alpha, const double *x, const doub
         });
 }
 
+// ledger: row vectors an SpMV op streams besides the gathered x (MXY writes y; the others read b or y
+// and write y)
+static double spmv_row_bytes(int op) { return op == SSS_HIP_SPMV_MXY ? 8.0 : 16.0; }
+
 int launch_spmv(const DevCSR &A, int op, double alpha, const double *x, const double *b, double *y, int cap,
                 double *partial, hipStream_t stream)
 {
     if (A.n == 0 || A.nblk == 0) return 0;
+    if (ledger_on()) ledger_add(matrix_bytes(A, 0, A.nblk) + xgather_bytes(A, A.n) + spmv_row_bytes(op) * A.n);
     switch (op) {
     case SSS_HIP_SPMV_MXY: launch_op<SSS_HIP_SPMV_MXY, false>(A, alpha, x, b, y, cap, nullptr, stream); break;
     case SSS_HIP_SPMV_AMXPY: launch_op<SSS_HIP_SPMV_AMXPY, false>(A, alpha, x, b, y, cap, nullptr, stream); break;
@@ -1363,6 +1403,7 @@ __global__ __launch_bounds__(kBlock) void prolong_inject(int m, int lo, const in
 int launch_prolong_inject(int m, int lo, const int *col, const double *e, double *x, hipStream_t s)
 {
     if (m <= 0) return 0;
+    ledger_add(28.0 * m);   // col, the gathered e, x read and written
     hipLaunchKernelGGL(prolong_inject, dim3((m + kBlock - 1) / kBlock), dim3(kBlock), 0, s, m, lo, col, e, x);
     SSS_HIP(hipGetLastError());
     return 0;
@@ -1375,6 +1416,10 @@ int launch_spmv_range(const DevCSR &A, int blo, int bhi, int op, double alpha, c
     if (op != SSS_HIP_SPMV_RESID && op != SSS_HIP_SPMV_AMXPY && op != SSS_HIP_SPMV_MXY) return ERROR_INPUT_PAR;
     const int nb = bhi - blo;
     if (nb <= 0) return 0;
+    if (ledger_on()) {
+        const double rows = A.h_bk ? A.h_bk[bhi].x - A.h_bk[blo].x : (double)A.n * nb / A.nblk;
+        ledger_add(matrix_bytes(A, blo, bhi) + xgather_bytes(A, rows) + spmv_row_bytes(op) * rows);
+    }
     // the kernel indexes blocks from 0: shift the block-indexed arrays
     const int2 *pb = A.pb ? A.pb + blo : nullptr;
     double *pp = partial ? partial + blo : nullptr;
@@ -1441,6 +1486,7 @@ __global__ __launch_bounds__(1024) void final_sum_kernel(const double *__restric
 // partials must have room for n + kFinalChunks doubles (the tail is the first stage's scratch)
 int launch_final_sum(double *partials, int n, double *out, bool take_sqrt, hipStream_t s)
 {
+    ledger_add(8.0 * n);
     if (n > 4 * 1024) {
         const int chunk = (n + kFinalChunks - 1) / kFinalChunks, nb = (n + chunk - 1) / chunk;
         hipLaunchKernelGGL(final_sum_chunks, dim3(nb), dim3(1024), 0, s, partials, n, chunk, partials + n);

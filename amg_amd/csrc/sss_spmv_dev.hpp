@@ -886,11 +886,12 @@ __device__ __forceinline__ double wave_row_chain(int k0, int k1, const int *__re
             const int q = lane + 64 * u, qc = q < m ? q : m - 1;
             const int cv = ci[base + qc];
             const double av = v[base + qc];
-            c[u] = q < m ? cv : 0;
+            c[u] = cv;
             a[u] = q < m ? av : 0.0;
         }
-        // every product formed before any is stored (a lane past the row uses column 0, value 0.0):
-        // with the store's condition around it the compiler waited for each gather in turn
+        // every product formed before any is stored (a lane past the row reuses the row's last column
+        // with value 0.0, so an offset fetch stays inside its segment): with the store's condition
+        // around it the compiler waited for each gather in turn
         double pv[U];
 #pragma unroll
         for (int u = 0; u < U; ++u) pv[u] = prod(c[u], a[u]);
@@ -924,15 +925,17 @@ __device__ __forceinline__ double wave_row_sum(int k0, int k1, const int *__rest
             const int kk = k + 64 * u, kc = kk < k1 ? kk : k1 - 1;
             const int cv = ci[kc];
             const double av = v[kc];
-            c[u] = kk < k1 ? cv : -1;
+            c[u] = cv;
             a[u] = kk < k1 ? av : 0.0;
         }
-        double pv[U];   // every gather issued before any is used (masked lanes: column 0, value 0.0)
+        // every gather issued before any is used (masked lanes: the row's last column, value 0.0, so
+        // an offset fetch stays inside its segment; the product is dropped)
+        double pv[U];
 #pragma unroll
-        for (int u = 0; u < U; ++u) pv[u] = prod(c[u] >= 0 ? c[u] : 0, a[u]);
+        for (int u = 0; u < U; ++u) pv[u] = prod(c[u], a[u]);
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-            const double p = c[u] >= 0 ? pv[u] : 0.0;
+            const double p = k + 64 * u < k1 ? pv[u] : 0.0;
             if (u & 1) s1 += p;
             else s0 += p;
         }

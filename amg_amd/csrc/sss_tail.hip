@@ -173,6 +173,7 @@ __global__ __launch_bounds__(kTailThreads) void tail_cycle(const TailLevel *__re
 
 int tail_launch(const TailPlan &t, hipStream_t s)
 {
+    ledger_add(t.ledger_bytes);
     hipLaunchKernelGGL(tail_cycle, dim3(1), dim3(kTailThreads), 0, s, t.d_levels, t.nlev, t.inv, t.nc, t.cb, t.cx);
     SSS_HIP(hipGetLastError());
     return 0;

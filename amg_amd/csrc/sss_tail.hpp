@@ -32,6 +32,7 @@ struct TailPlan {
     const double *inv = nullptr;   // the coarsest level's explicit inverse (row-major nc x nc)
     int nc = 0;
     double *cb = nullptr, *cx = nullptr;   // the coarsest level's b and x
+    double ledger_bytes = 0.0;     // stored bytes one tail launch streams (sss_engine.hpp ByteLedger)
 };
 
 int tail_upload(TailPlan &t, const std::vector<TailLevel> &levels);

@@ -135,6 +135,14 @@ class Dist:
         self.dist.all_reduce(t, op=self.dist.ReduceOp.MIN)
         return float(t.item())
 
+    def gather(self, v: float) -> list:
+        """Every rank's value, in rank order (on every rank)."""
+        if self.world == 1:
+            return [v]
+        out = [None] * self.world
+        self.dist.all_gather_object(out, v)
+        return out
+
     def close(self):
         if self.world > 1:
             self.dist.destroy_process_group()
@@ -364,24 +372,30 @@ def part_prefix(stencil: int, n: int, world: int) -> Path:
     return (best or Path("/tmp")) / name / "part"
 
 
-def single_ref_path(workload: str) -> Path:
+def single_ref_path(workload: str, mode: str) -> Path:
     import tempfile
-    return Path(tempfile.gettempdir()) / f"sss_bench_single_{workload.replace('^', '')}.json"
+    return Path(tempfile.gettempdir()) / f"sss_bench_single_{workload.replace('^', '')}_{mode}.json"
 
 
-def single_gpu_reference(explicit, workload: str):
-    """The 1-GPU rate of the same workload for parallel_efficiency = value / (N x rate): --single-ref,
-    else the record the last N = 1 run on this host left (single_ref_path), else the newest
-    committed profiles/r*_bench*_throughput.json whose workload matches.  None if there is none."""
+REF_KEYS = ("workload", "mode", "smoother", "sum_order")   # what a 1-GPU reference record must share
+
+
+def single_gpu_reference(explicit, cfg: dict):
+    """The 1-GPU rate of the same configuration for parallel_efficiency = value / (N x rate):
+    --single-ref, else the record the last N = 1 run on this host left (single_ref_path), else the
+    newest committed profiles/r*_bench*_throughput.json -- only a record whose workload, mode,
+    smoother and sum order all equal this run's (a parity-mode or differently smoothed 1-GPU rate is
+    no denominator).  None if there is none."""
     cands = [Path(explicit)] if explicit else []
-    cands.append(single_ref_path(workload))
+    cands.append(single_ref_path(cfg["workload"], cfg["mode"]))
     cands += sorted((ROOT / "profiles").glob("r*_bench*_throughput.json"), reverse=True)
     for c in cands:
         try:
             r = json.loads(c.read_text())
         except (OSError, ValueError):
             continue
-        if r.get("config", {}).get("workload") == workload and r.get("n_gpus", 1) == 1 and r.get("value"):
+        rc = r.get("config", {})
+        if all(rc.get(k) == cfg.get(k) for k in REF_KEYS) and r.get("n_gpus", 1) == 1 and r.get("value"):
             return {"value": r["value"], "ms_per_step": r.get("ms_per_step"), "source": str(c)}
     return None
 
@@ -469,6 +483,7 @@ def main():
     t0 = time.perf_counter()
     hier_src = None
     made_parts = False
+    part_rec = None
     H = None
     DH = None   # set here when the mirror is built while the setup runs (sss_hip_setup_create)
     dh_kw = dict(smoother=smoother, coarse=coarse, device=-1, inner=args.inner, inner_from=args.inner_from,
@@ -523,6 +538,8 @@ def main():
         D.barrier()
         man = json.loads(manifest.read_text())
         table, pars = man["levels"], man["pars"]
+        part_rec = {k: man.get(k) for k in ("setup_s", "partition_s", "peak_rss_gb", "rank_file_bytes",
+                                            "tail_file_bytes", "agg_rows")}
         hier_src = hier_src or f"partition set read from {prefix.parent}"
         if D.rank == 0:
             print(f"[bench] partition set: setup {man['setup_s']:.1f} s, partition {man['partition_s']:.1f} s, "
@@ -549,7 +566,10 @@ def main():
             shutil.rmtree(prefix.parent, ignore_errors=True)
             print(f"[bench] removed the partition set {prefix.parent}", file=sys.stderr, flush=True)
     upload_s = time.perf_counter() - t0
-    hbm_gb = D.max(A.hbm_used_bytes() / 1e9)   # the mirror resident in HBM (max over ranks)
+    # HBM in use on each rank's device once its mirror is resident (ranks sharing one GPU all see
+    # the device total)
+    hbm_ranks = D.gather(A.hbm_used_bytes() / 1e9)
+    hbm_gb = max(hbm_ranks)
     overlapped = D.world == 1 and getattr(DH, "times", None) is not None
     if overlapped:   # levels were uploaded during the setup: what is left after it returned
         upload_s = DH.times[1]
@@ -579,6 +599,9 @@ def main():
     elapsed = D.max(t1 - t0)
     ms_per_step = elapsed * 1e3 / args.steps
     value = args.steps / elapsed   # global V-cycles per second (strong scaling at N > 1)
+    # the stored-format bytes the timed step's kernels read and write (the next cycle as it would run
+    # now -- the steady state of the loop above -- and the residual + norm; sss_hip_cycle_bytes)
+    cyc_bytes = DH.DH.cycle_bytes() if D.world == 1 else None
 
     # roofline of the dominant streaming kernel: level-0 fused residual SpMV (wp = b - A0 x);
     # N > 1: rank 0's share (its rows, x with ghosts), no exchange inside the timed launches
@@ -617,9 +640,11 @@ def main():
     its = 0
     t0 = time.perf_counter()
     relres = 1.0
+    history = []
     while its < args.converge_max:
         DH.cycle()
         relres = DH.residual_norm() / sumb
+        history.append(relres)
         its += 1
         print(f"[bench] converge iteration {its}: relres {relres:.6e}", file=sys.stderr, flush=True)
         if relres < pars["tol"]:
@@ -690,7 +715,8 @@ def main():
     levels = [(L["rows"], L["nnz"]) for L in table]
     vbytes = vcycle_bytes(table, pars["pre_iter"] + pars["post_iter"])
     import resource
-    rss_gb = D.max(resource.getrusage(resource.RUSAGE_SELF).ru_maxrss / 2**20)   # peak over the ranks
+    rss_ranks = D.gather(resource.getrusage(resource.RUSAGE_SELF).ru_maxrss / 2**20)
+    rss_gb = max(rss_ranks)   # peak over the ranks
 
     # {"csr": bytes, "stored": bytes} per launch: the newest committed PMC record of this workload and
     # format (tools/gpu/pmc.sh: separate rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes cannot run
@@ -790,7 +816,11 @@ def main():
                    "setup_plus_upload_s": setup_s + upload_s,
                    "parallelism": f"rowpart{D.world}" if D.world > 1 else "single-gpu",
                    "host_peak_rss_gb_max_over_ranks": rss_gb,
+                   "host_peak_rss_gb_per_rank": rss_ranks,
                    "hbm_used_gb_max_over_ranks": hbm_gb,
+                   "hbm_used_gb_per_rank": hbm_ranks,
+                   "partition_set": part_rec,
+                   "relres_history": history,
                    "transport": transport},
         "roofline": {"bound": "hbm", "kernel": "spmv_adaptive<RESID> level 0 from its CSR arrays (y = b - A0 x)",
                      "achieved": achieved, "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": achieved / PEAK_HBM_GBS,
@@ -803,19 +833,32 @@ def main():
                          "avg_launch_ms": spmv_ms, "bytes_per_launch": spmv_bytes, "GBps": format_gbps,
                          "frac": format_gbps / PEAK_HBM_GBS,
                          "traffic": traffic.get("stored") if traffic else None,
-                         "csr_equivalent_GBps": csr_bytes / (spmv_ms * 1e-3) / 1e9,
+                         "csr_equivalent_rate_GBps": csr_bytes / (spmv_ms * 1e-3) / 1e9,
                          "note": "bytes = the stored format of A_0 (dictionary ELL: 8 B per row of codes + block "
                                  "dictionaries) + x, b, y; csr_equivalent = SURVEY 8(d) CSR bytes over this "
                                  "kernel's time, the rate a CSR SpMV would need to match it"}},
+        # the V-cycle's roofline: the bytes its kernels actually move in their stored formats
+        "vcycle_stored": ({
+            "bytes_per_step": cyc_bytes["total"], "GBps": cyc_bytes["total"] / (ms_per_step * 1e-3) / 1e9,
+            "peak": PEAK_HBM_GBS, "unit": "GB/s",
+            "frac": cyc_bytes["total"] / (ms_per_step * 1e-3) / 1e9 / PEAK_HBM_GBS,
+            "bytes_per_level": [round(b) for b in cyc_bytes["levels"]],
+            "bytes_outer_residual": round(cyc_bytes["outer"]), "bytes_coarse": round(cyc_bytes["coarse"]),
+            "definition": "sum over the launches of one outer iteration (the captured V-cycle + residual + "
+                          "norm, sss_hip_cycle_bytes) of the bytes each reads and writes in the engine's stored "
+                          "formats: the matrix storage of the rows it covers (codes, dictionaries, values, row "
+                          "bounds), the x it gathers counted once per covered row, 8 B per covered row of every "
+                          "row vector it streams (b, y, divisors, iterates); divided by ms_per_step"}
+                          if cyc_bytes else None),
+        # SURVEY.md 8(d)'s CSR-storage V-cycle bytes over the step time: the rate a CSR engine would need
         "vcycle_csr_equivalent": {
-            "bytes_per_step": vbytes, "achieved": vbytes / (ms_per_step * 1e-3) / 1e9, "peak": PEAK_HBM_GBS,
-            "unit": "GB/s", "frac": vbytes / (ms_per_step * 1e-3) / 1e9 / PEAK_HBM_GBS,
+            "bytes_per_step": vbytes, "csr_equivalent_rate_GBps": vbytes / (ms_per_step * 1e-3) / 1e9,
             "definition": "SURVEY.md 8(d) V-cycle algorithmic bytes of CSR storage (12 B/entry): per smoothed "
                           "level 4 GS-CF sweeps, residual, restriction, prolongation, zero-fill; plus the outer "
                           "residual+norm; coarse solve excluded -- divided by the measured time per outer "
                           "iteration (whole-job bytes / max-over-ranks time at N > 1).  The engine stores the "
-                          "stencil levels as dictionary tiles and skips exactly-dead work, so it moves fewer "
-                          "bytes than this: a CSR-equivalent rate, not a roofline fraction",
+                          "stencil levels in compressed formats and skips exactly-dead work, so it moves fewer "
+                          "bytes than this: a CSR-equivalent rate, not a roofline fraction (vcycle_stored is)",
         },
         "parity_mode": parity,
         "cpu_baseline": cpu_baseline,
@@ -824,12 +867,13 @@ def main():
     if D.world == 1 and not circuit:
         # left for the N > 1 runs of the same workload on this host (parallel_efficiency)
         try:
-            single_ref_path(workload).write_text(json.dumps({k: rec[k] for k in ("value", "ms_per_step", "config")}))
+            single_ref_path(workload, args.mode).write_text(
+                json.dumps({k: rec[k] for k in ("value", "ms_per_step", "config", "n_gpus")}))
         except OSError:
             pass
     else:
         rec["config"]["cycle_graph"] = cycle_graph
-        ref = single_gpu_reference(args.single_ref, workload)
+        ref = single_gpu_reference(args.single_ref, rec["config"])
         rec["single_gpu_reference"] = ref
         rec["parallel_efficiency"] = value / (D.world * ref["value"]) if ref else None
     if cpu_baseline:

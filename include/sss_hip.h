@@ -151,6 +151,12 @@ int sss_hip_tail_from(sss_hip_hier *h);
 /* Kernel launches of one V-cycle as captured in its hipGraph (host-steered Krylov coarse solves
  * excluded), or -1 before the first captured cycle / without graphs. */
 int sss_hip_cycle_launches(sss_hip_hier *h);
+/* Stored-format bytes the kernels of one outer iteration read and write (the next sss_hip_cycle and
+ * the residual + norm after it; walked into a discarded stream capture, nothing runs): the stored
+ * matrix bytes of the rows each launch covers, the x it gathers counted once per covered row, and
+ * 8 B per covered row of every row vector it streams.  out[l] for level l, out[nslots - 2] the outer
+ * residual + norm, out[nslots - 1] the coarsest solve; nslots >= sss_hip_num_levels(h) + 2. */
+int sss_hip_cycle_bytes(sss_hip_hier *h, double *out, int nslots);
 
 /* ---- kernel-level entry points on device memory (tests, bench, roofline) ------------- */
 enum {

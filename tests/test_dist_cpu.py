@@ -270,3 +270,22 @@ def test_bench_rccl_failure_exits_nonzero(tmp_path):
     assert r.returncode != 0
     assert "RCCL communicator creation failed" in r.stderr, r.stderr[-3000:]
     assert '"metric"' not in r.stdout
+
+
+def test_bench_single_gpu_reference_matches_configuration(tmp_path):
+    """parallel_efficiency's 1-GPU denominator must share workload, mode, smoother and sum order
+    with the N > 1 run: a parity-mode (or differently smoothed) 1-GPU record is never used."""
+    import json
+    import bench
+    cfg = {"workload": "poisson7_64^3", "mode": "throughput", "smoother": "hybrid", "sum_order": "tree (long rows)"}
+    par = tmp_path / "parity.json"
+    par.write_text(json.dumps({"value": 0.5, "n_gpus": 1, "config": dict(cfg, mode="parity", smoother="exact",
+                                                                         sum_order="stored CSR order")}))
+    assert bench.single_gpu_reference(str(par), dict(cfg, workload="poisson7_63^3")) is None
+    thr = tmp_path / "thr.json"
+    thr.write_text(json.dumps({"value": 50.0, "n_gpus": 1, "config": dict(cfg, workload="poisson7_63^3")}))
+    ref = bench.single_gpu_reference(str(thr), dict(cfg, workload="poisson7_63^3"))
+    assert ref and ref["value"] == 50.0 and ref["source"] == str(thr)
+    # same workload, other smoother: not a denominator
+    assert bench.single_gpu_reference(str(thr), dict(cfg, workload="poisson7_63^3", smoother="jacobi")) is None
+    assert bench.single_ref_path("poisson7_64^3", "parity") != bench.single_ref_path("poisson7_64^3", "throughput")

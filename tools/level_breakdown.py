@@ -6,9 +6,10 @@ Walks the kernels in start order.  A cycle ends at the residual-norm kernel
 (spmv_*<2, true>, or relax_range<3> when it also computes the next first F pass); inside a cycle, a restriction (spmv_*<0, ...>, SSS_HIP_SPMV_MXY) moves the
 level counter down, a prolongation (spmv_*<1, ...> or prolong_inject) moves it up, the dense GEMV / Krylov kernels
 are the coarsest level.  Prints, per level, the kernel time of one average cycle split into
-smoother / residual / restriction / prolongation / other, and, when the bench JSON (its
-`config.hierarchy`) is given, the effective GB/s of 5 passes over the level's matrix
-(4 smoother sweeps + 1 residual at 12 B per nonzero; vectors and transfers not counted).
+smoother / residual / restriction / prolongation / other, and, when the bench JSON is given, each
+level's stored-format rate: the bytes its launches read and write in the engine's stored formats
+(`vcycle_stored.bytes_per_level`, sss_hip_cycle_bytes) over its kernel time, and the same for the
+outer residual, the coarsest solve and the whole cycle (kernel time, not the step's wall time).
 """
 from __future__ import annotations
 
@@ -21,12 +22,12 @@ from collections import defaultdict
 
 def main():
     db = sys.argv[1]
-    hier = None
+    stored = None
     if len(sys.argv) > 2:
         with open(sys.argv[2]) as f:
             for line in f:
                 if line.startswith("{"):
-                    hier = json.loads(line)["config"]["hierarchy"]
+                    stored = json.loads(line).get("vcycle_stored")
     c = sqlite3.connect(db)
     rows = list(c.execute("select name, start, end from kernels order by start"))
     # drop everything before the first cycle: upload / explicit inverse; start after the first residual norm
@@ -84,21 +85,27 @@ def main():
     levels = sorted({k[0] for k in tot if isinstance(k[0], int)})
     kinds = ["smooth", "resid", "restrict", "prolong", "other"]
     print(f"{nc} cycles; average kernel microseconds per cycle")
-    print("level " + "".join(f"{k:>10}" for k in kinds) + f"{'total':>10}" + ("   5xA GB/s" if hier else ""))
+    print("level " + "".join(f"{k:>10}" for k in kinds) + f"{'total':>10}" +
+          ("   stored GB   GB/s  frac" if stored else ""))
+    per = stored["bytes_per_level"] if stored else []
+
+    def rate(nbytes, t):
+        if not stored or t <= 0:
+            return ""
+        g = nbytes / (t * 1e-6) / 1e9
+        return f"   {nbytes / 1e9:9.3f} {g:6.0f} {g / 8000.0:5.2f}"
+
     grand = 0.0
     for l in levels:
         vals = [tot.get((l, k), 0.0) for k in kinds]
         t = sum(vals)
         grand += t
-        extra = ""
-        if hier and l < len(hier):
-            nnz = hier[l][1]
-            extra = f"   {5 * 12 * nnz / (t * 1e-6) / 1e9:9.0f}"
-        print(f"{l:5d} " + "".join(f"{v:10.1f}" for v in vals) + f"{t:10.1f}" + extra)
-    for k in (("coarse", "solve"), ("out", "resid")):
-        grand += tot.get(k, 0.0)
-        print(f"{k[0]:>6} {tot.get(k, 0.0):10.1f}")
-    print(f"total {grand:10.1f} us")
+        print(f"{l:5d} " + "".join(f"{v:10.1f}" for v in vals) + f"{t:10.1f}" + (rate(per[l], t) if l < len(per) else ""))
+    for k, key in ((("coarse", "solve"), "bytes_coarse"), (("out", "resid"), "bytes_outer_residual")):
+        t = tot.get(k, 0.0)
+        grand += t
+        print(f"{k[0]:>6} {t:10.1f}" + (" " * 50 + rate(stored[key], t) if stored else ""))
+    print(f"total {grand:10.1f} us" + (" " * 44 + rate(stored["bytes_per_step"], grand) if stored else ""))
 
 
 if __name__ == "__main__":
