@@ -13,8 +13,8 @@ from pathlib import Path
 import numpy as np
 
 ROOT = Path(__file__).resolve().parent.parent
-# SSS_AMG_LIB: an alternative build of the same library (kernel-variant experiments, e.g.
-# `make BUILD=build_xcd LIBDIR=amg_amd/lib_xcd EXTRA=-DSSS_XCD_REMAP=1`)
+# SSS_AMG_LIB: an alternative build of the same library (A/B runs against a previous commit's
+# build, tools/gpu/ab_env.sh)
 LIB_PATH = Path(os.environ["SSS_AMG_LIB"]) if os.environ.get("SSS_AMG_LIB") else ROOT / "amg_amd" / "lib" / "libsss_amg.so"
 BIN_PATH = ROOT / "amg_amd" / "bin" / "amg"
 

@@ -234,7 +234,6 @@ struct DevCSR {
     unsigned *dv_xell = nullptr;
     int xell_w = 0;
     int xell_shift = 0;   // column bits S of a code (value index << S | column); >= 23
-    int ell_remap = 0;   // ELL kernels take their blocks XCD-contiguously (SSS_HIP_ELL_REMAP)
     long long stream_bytes = 0;   // bytes of the stored format one tile-path SpMV streams (no vectors)
     unsigned *dv_code = nullptr;
     unsigned char *dv_vi = nullptr;
@@ -297,11 +296,8 @@ inline bool has_dict(const DevCSR &A)
 // Storage argument K of the tile kernels: 0 plain or sorted tiles, 1 dictionary tiles (either kind),
 // 8 / 16 / 32 dictionary ELL of that row width, kXell + W column ELL of row width W (8/16/20/24/32/40).
 constexpr int kXell = 256;
-#ifndef SSS_ELL_RPT
-#define SSS_ELL_RPT 2
-#endif
-// row blocks per workgroup of a launch over storage K
-constexpr int rows_per_wg(int K) { return K >= kXell ? 1 : K >= 8 ? SSS_ELL_RPT : 1; }
+// row blocks per workgroup of a launch over storage K (dictionary ELL: 2, measured against 1 and 4)
+constexpr int rows_per_wg(int K) { return K >= kXell ? 1 : K >= 8 ? 2 : 1; }
 // f(std::integral_constant<int, K>) with the storage argument K of A
 template <class F>
 inline void with_tile_kind(const DevCSR &A, F f)

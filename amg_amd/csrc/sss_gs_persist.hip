@@ -139,10 +139,8 @@ __global__ __launch_bounds__(kBlock) void gs_flow_group(int nchunks, const int *
                                                         int lo, int hi, unsigned *ctl, unsigned *err, int spin, int ovl,
                                                         unsigned long long *trace)
 {
-#ifndef SSS_GS_U
-#define SSS_GS_U 8
-#endif
-    constexpr int R = 64 / G, CAP = kGroupBuf / R, U = SSS_GS_U;   // U: a lane's entries per staging group
+    // U: a lane's entries per staging group (8; 4 and 16 measured no faster at 400^3)
+    constexpr int R = 64 / G, CAP = kGroupBuf / R, U = 8;
     // a same-pass row this row reads the NEW value of (published by its granules)
     auto dynamic = [&](int c, int i) { return DESC ? (c > i && c < hi) : (c >= lo && c < i); };
     static_assert(CAP / G == 32, "one pending bit per staged entry of a lane");
@@ -246,10 +244,7 @@ __global__ __launch_bounds__(kBlock) void gs_flow_group(int nchunks, const int *
                 for (int off = G / 2; off > 0; off >>= 1) first = min(first, __shfl_xor(first, off, 64));
                 const int lim = min(first, m);
                 // issue this lane's two lowest pending polls (column from LDS, granule halves, value)
-#ifndef SSS_GS_NP
-#define SSS_GS_NP 2
-#endif
-                constexpr int NP = SSS_GS_NP;
+                constexpr int NP = 2;
                 int tp[NP];
                 unsigned long long ga[NP], gc[NP];
                 double ap[NP];
@@ -496,8 +491,6 @@ int gs_persist_build(PassSchedule &ps, const SSS_MAT &A, int lo, int hi, bool lo
     }
     // lanes per row from the average row length: about 8 entries per lane and round
     g.G = avg <= 24 ? 4 : avg <= 48 ? 8 : avg <= 96 ? 16 : avg <= 192 ? 32 : 64;
-    if (const char *gg = getenv("SSS_HIP_GS_LANES")) g.G = atoi(gg);
-    if (g.G != 4 && g.G != 8 && g.G != 16 && g.G != 32 && g.G != 64) g.G = 64;
     // the row's chain overlapping the polls of its pending granules: measured at 7-pt 256^3
     // (tools/gpu/gs_overlap.sh, pre-smoother per call) 19 % faster on the levels of 700-1400
     // entries per row (level 7: 106 -> 86 ms, level 8: 108 -> 87), 5 % on level 5 (407), but
@@ -532,7 +525,6 @@ int gs_persist_build(PassSchedule &ps, const SSS_MAT &A, int lo, int hi, bool lo
     // their polls load the memory system), capped by the tickets and by 8 per CU
     const double per_depth = (double)g.nchunks / std::max(1, ps.depth);
     int waves = (int)std::min<double>(1024.0, std::max(32.0, 4.0 * per_depth));
-    if (const char *w = getenv("SSS_HIP_GS_WAVES")) waves = std::max(1, atoi(w));
     waves = std::min(waves, std::min(g.nchunks, cus * 8));
     g.grid = std::max(1, (waves + 3) / 4);
     return 0;
@@ -548,15 +540,6 @@ void gs_persist_free(PassSchedule &ps)
     g = GsPersist();
 }
 
-// SSS_HIP_GS_OVERLAP=0: the flow engine waits for every pending granule of a row before its chain
-static bool gs_overlap_on()
-{
-    static const bool on = [] {
-        const char *e = getenv("SSS_HIP_GS_OVERLAP");
-        return !(e && *e == '0');
-    }();
-    return on;
-}
 
 // Diagnostic builds only (make EXTRA=-DSSS_GS_TRACE): each flow pass writes its rows' stamps to a
 // buffer that gs_trace_dump appends, with the pass's depth offsets, to $SSS_GS_TRACE_FILE.
@@ -605,7 +588,7 @@ int gs_persist_run(const PassSchedule &ps, const DevCSR &A, const double *b, dou
     } else if (g.engine == 1) {
         auto go = [&](auto kern) {
             hipLaunchKernelGGL(kern, dim3(g.grid), dim3(kBlock), 0, s, g.nchunks, g.ck, ps.rows, A.rp, A.ci, A.v, b, x,
-                               deff, g.gran, g.lo, g.hi, g.ctl, g.err, g.spin, g.overlap && gs_overlap_on() ? 1 : 0,
+                               deff, g.gran, g.lo, g.hi, g.ctl, g.err, g.spin, g.overlap ? 1 : 0,
                                gs_trace_buf(ps));
         };
         auto by_g = [&](auto nat, auto desc) {

@@ -153,29 +153,20 @@ int sss::level_encoding(const sss_hip_opts &o)
     return (o.sorted_tiles ? kEncSortedTiles : 0) | (o.sum_order == 1 ? kEncFreeOrder : 0) | dict | (dict ? kEncXell : 0);
 }
 int sss::level_inner_of(const sss_hip_opts &o, int l) { return level_inner(o, l); }
-// P_l and R_l: the level matrices' encodings; dictionary forms only with SSS_HIP_DICT_PR=1.
-// Measured at 7-pt 400^3 (tools/gpu/ab.sh): 22.15 -> 22.25 ms per V-cycle, level-0 prolongation
-// 255 -> 325 us (P's F rows have 1-8 irregular columns, so the per-tile dictionaries rarely
-// shrink a row and the extra indirection costs more than the 3 bytes saved per entry).
-// The column ELL (kEncXell) is offered to them unless SSS_HIP_XELL_PR=0.
-int sss::transfer_encoding(const sss_hip_opts &o)
-{
-    const char *e = getenv("SSS_HIP_DICT_PR");
-    const char *x = getenv("SSS_HIP_XELL_PR");
-    const int enc = (e && *e == '1') ? level_encoding(o) : (level_encoding(o) & ~kEncDict);
-    return (x && *x == '0') ? (enc & ~kEncXell) : enc;
-}
-// R_l: as transfer_encoding; SSS_HIP_ELL_R=1 also offers the one-byte dictionary ELL (rectangular:
-// offsets col - row).  Off by default: on the relabeled hierarchy a restriction's rows are the next
-// level's F-first order, so the offsets drift across a block (7-pt 400^3 R_0: no block fits 31
-// offsets; tools/fmt_probe.py reports the formats each operator got).
+// P_l and R_l: the level matrices' encodings without the dictionary tiles (measured at 7-pt 400^3:
+// 22.15 -> 22.25 ms per V-cycle with them, level-0 prolongation 255 -> 325 us -- P's F rows have
+// 1-8 irregular columns, so the per-tile dictionaries rarely shrink a row and the extra
+// indirection costs more than the 3 bytes saved per entry); the column ELL is offered to them.
+int sss::transfer_encoding(const sss_hip_opts &o) { return level_encoding(o) & ~kEncDict; }
+// R_l: as transfer_encoding, plus the one-byte dictionary ELL with per-row base columns (a
+// restriction's rows follow the next level's F-first order, so offsets col - row drift across a
+// block while col - first col repeats; tools/fmt_probe.py reports the formats each operator got).
 int sss::restriction_encoding(const sss_hip_opts &o)
 {
-    const char *e = getenv("SSS_HIP_ELL_R");
     const char *bz = getenv("SSS_HIP_ELL_BASE");   // 0: no per-row-based dictionary ELL for R
     int enc = transfer_encoding(o);
     if ((level_encoding(o) & kEncDict) && !(bz && *bz == '0')) enc |= kEncEllBase;
-    return (e && *e == '1' && (level_encoding(o) & kEncDict)) ? (enc | kEncEll) : enc;
+    return enc;
 }
 
 // Are the C and the F points of A each an independent set (no off-diagonal coupling inside a
@@ -669,7 +660,7 @@ namespace {
 // The mirror's level tasks: A(l) = relabel + A_l + smoother plan (once the setup has moved past level
 // l), PR(l) = P_l / R_l (once A(l) has finished and level l + 1's relabeling is known).  While the
 // setup runs, one background worker takes them in order; once it has returned, the calling thread
-// and SSS_HIP_UPLOAD_HELPERS more threads (default 2) take whatever is runnable, so the levels the
+// and two more threads take whatever is runnable, so the levels the
 // setup produced last -- each an independent plan build -- are uploaded side by side.
 struct Pipeline {
     HierBuild b;
@@ -788,8 +779,7 @@ extern "C" sss_hip_hier *sss_hip_setup_create(SSS_AMG *mg, SSS_MAT *A, SSS_AMG_P
     }
     P.cv.notify_all();
     {   // the setup has returned: this thread and the helpers take the remaining level tasks
-        const char *hz = getenv("SSS_HIP_UPLOAD_HELPERS");
-        const int nh = std::max(0, std::min(8, (hz && *hz) ? atoi(hz) : 2));
+        const int nh = 2;
         std::vector<std::thread> helpers;
         for (int k = 0; k < nh; ++k)
             helpers.emplace_back([&] {

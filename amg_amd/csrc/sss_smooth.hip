@@ -289,9 +289,8 @@ int smoother_build(SmootherPlan &sp, const SSS_MAT &A, const int *mark, int kind
             pt.mark("ts fill");
             SSS_MAT Mn = mk(nrp, nci, nv), Ml = mk(lrp, lci, lv);
             std::vector<int> seg(split);   // absolute [N_i | L_i] cut of each row of Mn
-            // read by the ts_* kernels only: merged groups, or the column ELL (SSS_HIP_XELL_TS=0: not)
-            const char *xz = getenv("SSS_HIP_XELL_TS");
-            const int tenc = (enc & ~(kEncDict | ((xz && *xz == '0') ? kEncXell : 0))) | kEncMergedOnly;
+            // read by the ts_* kernels only: merged groups, or the column ELL
+            const int tenc = (enc & ~kEncDict) | kEncMergedOnly;
             if ((rc = devcsr_upload(ps.ts_nl, Mn, -1, tenc, seg.data())) || (rc = devcsr_upload(ps.ts_lo, Ml, -1, tenc)))
                 return rc;
             pt.mark("ts upload");
@@ -499,7 +498,7 @@ __device__ __forceinline__ void relax_range_ell(int blo, const int2 *__restrict_
 {
     constexpr int RPT = kEllRpt;
     __shared__ EllSmem es[RPT];
-    const int g = ell_block_order(dt.remap, (int)blockIdx.x, (int)gridDim.x);
+    const int g = (int)blockIdx.x;
     unsigned w[RPT][W / 4];
     double br[RPT], dr[RPT];
     int r[RPT];
@@ -576,7 +575,7 @@ __device__ __forceinline__ void relax_range_ell2(int blo, const int2 *__restrict
                                                  double *__restrict__ partial, XSrc xs, const DevDict &dt)
 {
     __shared__ EllSmem es[2];
-    const int g = ell_block_order(dt.remap, (int)blockIdx.x, (int)gridDim.x);
+    const int g = (int)blockIdx.x;
     const EllPairRows pr = ell_pair_rows(blk, blo + 2 * g, dt.bend);
     unsigned w[2][2];
     double br[2], dr[2] = {0.0, 0.0};
@@ -830,21 +829,10 @@ __global__ __launch_bounds__(kBlock) void relax_range(SSS_RELAX_ARGS)
 // profiles/r03_kernels_sq_pmc_400.txt) and wait on memory 70 % of their cycles.  Measured at
 // 400^3 (tools/gpu/ab.sh): level-1 smoothing 4.61 -> 4.23 ms per V-cycle at 5 waves (96 VGPRs);
 // 6 waves (the LDS limit) spill to scratch and take 6.90 ms.
-#ifndef SSS_RELAX_WPE
-#define SSS_RELAX_WPE 5
-#endif
 template <int MODE, int DICT = 0>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(SSS_RELAX_WPE, 8))) void relax_range_occ(SSS_RELAX_ARGS)
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5, 8))) void relax_range_occ(SSS_RELAX_ARGS)
 {
     relax_range_body<MODE, DICT>(SSS_RELAX_PASS);
-}
-static bool relax_occ_on()
-{
-    static const bool on = [] {
-        const char *e = getenv("SSS_HIP_RELAX_OCC");
-        return !(e && *e == '0');
-    }();
-    return on;
 }
 // relax_range / relax_range_occ over the row blocks [blo, blo + nb): one workgroup per block, or
 // per kEllRpt blocks on dictionary ELL (K >= 8)
@@ -852,11 +840,7 @@ template <int M, int K, class... Args>
 static void launch_relax_range(int blo, int nb, hipStream_t s, DevDict dt, Args... args)
 {
     if constexpr (K < 8) {
-        if (relax_occ_on()) {
-            hipLaunchKernelGGL((relax_range_occ<M, K>), dim3(nb), dim3(kBlock), 0, s, blo, args..., dt);
-            return;
-        }
-        hipLaunchKernelGGL((relax_range<M, K>), dim3(nb), dim3(kBlock), 0, s, blo, args..., dt);
+        hipLaunchKernelGGL((relax_range_occ<M, K>), dim3(nb), dim3(kBlock), 0, s, blo, args..., dt);
     } else {
         dt.bend = blo + nb;
         hipLaunchKernelGGL((relax_range<M, K>), dim3((nb + rows_per_wg(K) - 1) / rows_per_wg(K)), dim3(kBlock), 0, s, blo,

@@ -492,7 +492,6 @@ DevDict devdict(const DevCSR &A, int blo)
     t.ellw = A.ell_w;
     t.xell = A.dv_xell;
     t.xshift = A.xell_shift;
-    t.remap = A.ell_remap;
     t.pd = A.dv_pd + blo;
     t.dd = A.dv_dd;
     t.vd = A.dv_vd;
@@ -925,8 +924,6 @@ int devcsr_upload(DevCSR &d, const SSS_MAT &h, int split, int enc, const int *se
                 if (int rc = h2d(d.dv_ell_base, base.data(), sizeof(int) * base.size())) return rc;
             }
             d.ell_w = W;
-            const char *rz = getenv("SSS_HIP_ELL_REMAP");
-            d.ell_remap = (rz && *rz) ? atoi(rz) : 0;
             d.dv_ell = dev_alloc<unsigned char>(ell.size());
             d.dv_pd = dev_alloc<int4>(pd.size());
             d.dv_dd = dev_alloc<int>(dd.size());
@@ -1161,50 +1158,11 @@ __global__ __launch_bounds__(kBlock) void spmv_adaptive(const int2 *__restrict__
             const double t = block_sum(sq, es.red);
             if (threadIdx.x == 0) partial[bid] = t;
         }
-    } else if constexpr (DICT == 8 && kEllPairs && kEllPairsSpmv) {   // dictionary ELL, two consecutive rows per thread
-        __shared__ EllSmem es[2];
-        const int g = ell_block_order(dt.remap, (int)blockIdx.x, (int)gridDim.x);
-        const EllPairRows pr = ell_pair_rows(blk, 2 * g, dt.bend);
-        unsigned w[2][2];
-        double br[2] = {0.0, 0.0};
-        ell_pair_codes(dt.ell, pr, w);   // codes (and b) in flight across the dictionaries' barrier
-        if constexpr (OP == SSS_HIP_SPMV_RESID) pair_load(b, pr.r, pr.l0, pr.l1, br);
-        if (pr.v0) ell_load_dicts_nosync(dt, pr.b0, es[0]);
-        if (pr.v1) ell_load_dicts_nosync(dt, pr.b0 + 1, es[1]);
-        __syncthreads();
-        double out[2] = {0.0, 0.0}, sq[2] = {0.0, 0.0};   // sq[j]: this thread's squares in block j
-#pragma unroll
-        for (int i = 0; i < 2; ++i) {
-            const int r = pr.r + i;
-            if (!(i == 0 ? pr.l0 : pr.l1)) continue;
-            const int j = r < pr.mid ? 0 : 1;
-            double p[8];
-            int ds;
-            double dv;
-            const int len = ell_decode<8>(w[i], r, es[j], [&](int c) -> double { return x[c]; }, p, ds, dv);
-            const double s = ell_add(0.0, p, 0, len);
-            if constexpr (OP == SSS_HIP_SPMV_RESID) {
-                out[i] = br[i] + s * alpha;
-                if (NORM) sq[j] += out[i] * out[i];
-            } else {
-                const double e = epi(r, s);
-                if (NORM) sq[j] += e;
-            }
-        }
-        if constexpr (OP == SSS_HIP_SPMV_RESID) pair_store(y, pr.r, pr.l0, pr.l1, out);
-        if (NORM && pr.v0) {   // (uniform over the workgroup)
-            const double t0 = block_sum(sq[0], es[0].red);
-            if (threadIdx.x == 0) partial[pr.b0] = t0;
-            if (pr.v1) {
-                const double t1 = block_sum(sq[1], es[1].red);
-                if (threadIdx.x == 0) partial[pr.b0 + 1] = t1;
-            }
-        }
     } else if constexpr (DICT >= 8) {   // dictionary ELL rows of width DICT: one thread per row, its sum
         constexpr int W = DICT;   // from 0.0 in stored order; kEllRpt row blocks per workgroup
         constexpr int RPT = kEllRpt;
         __shared__ EllSmem es[RPT];
-        const int g = ell_block_order(dt.remap, (int)blockIdx.x, (int)gridDim.x);
+        const int g = (int)blockIdx.x;
         unsigned w[RPT][W / 4];
         double br[RPT];
         int r[RPT], rb[RPT];   // rb: the row's offset base (its own index, or dt.ellb[r])

@@ -10,42 +10,10 @@
 
 namespace sss {
 
-#ifndef SSS_XCD_REMAP
-#define SSS_XCD_REMAP 0
-#endif
-// Workgroups are dealt round-robin over the 8 XCDs (MI355X_MICROARCH.md, workgroup dispatch), so
-// consecutive row blocks -- which gather the same x lines -- land on 8 different L2s.  xcd_bid()
-// renumbers the grid so that the workgroups sharing an XCD (b, b + 8, ...) cover one contiguous run
-// of blocks instead.  A bijection on [0, gridDim.x); speed only (placement is not a contract).
-// Measured OFF by default: on the 7-pt 400^3 hierarchy the V-cycle took 39.8 ms with the remap
-// against 37.4 ms without (level-0 residual 1.32 vs 1.40 ms, but the restriction 1.09 vs 0.79 ms,
-// the level-1 residual 2.44 vs 1.97 ms and every coarse level slower): the x lines neighbouring
-// blocks share are served from the Infinity Cache either way, and eight XCDs streaming eight
-// distant regions lose more than the L2 reuse gains.
-__device__ __forceinline__ int xcd_remap(int b, int nb)
-{
-    const int per = nb >> 3, rem = nb & 7, xcd = b & 7, idx = b >> 3;
-    return xcd < rem ? xcd * (per + 1) + idx : rem * (per + 1) + (xcd - rem) * per + idx;
-}
-// The ELL launches' block order (DevCSR::ell_remap): 0 the dispatch order, 1 xcd_remap, G >= 2 runs of
-// G consecutive blocks per XCD in turn (block b of XCD b % 8 takes run (b / 8) / G of that XCD's
-// share): the row neighbours of a block (the +-n stencil offsets) stay on its XCD's L2 while the
-// eight XCDs still stream one region of the matrix together.  The grid's last partial round of 8G
-// keeps the dispatch order (a bijection either way).
-__device__ __forceinline__ int ell_block_order(int remap, int b, int nb)
-{
-    if (remap == 0) return b;
-    if (remap == 1) return xcd_remap(b, nb);
-    const int span = 8 * remap, full = nb - nb % span;
-    if (b >= full) return b;
-    const int base = b - b % span, w = b % span;   // position inside the round
-    return base + (w & 7) * remap + (w >> 3);
-}
-__device__ __forceinline__ int xcd_bid()
-{
-    if (!SSS_XCD_REMAP) return blockIdx.x;
-    return xcd_remap(blockIdx.x, gridDim.x);
-}
+// Block numbers are the dispatch order.  Measured and rejected: an XCD-contiguous
+// renumbering of the grid (V-cycle 37.4 -> 39.8 ms at 400^3) and, for the ELL kernels, runs of G
+// consecutive blocks per XCD (level 0 unchanged within noise, fabric bytes 3.5 -> 2.6 GB).
+__device__ __forceinline__ int xcd_bid() { return blockIdx.x; }
 
 struct SpmvSmem {
     double v[kTileEntries];    // products a_k * x_{c_k} of the tile
@@ -73,7 +41,6 @@ struct DevDict {
     const unsigned char *ell = nullptr;   // dictionary ELL (DevCSR::dv_ell), ell_w bytes per row
     const int *ellb = nullptr;            // its per-row base columns (DevCSR::dv_ell_base) or null
     int ellw = 0;
-    int remap = 0;   // ELL launches: XCD-contiguous block order (DevCSR::ell_remap)
     int bend = 0x7fffffff;   // ELL launches: first block past the launch's range (kEllRpt blocks per workgroup)
     const unsigned *xell = nullptr;   // column ELL (DevCSR::dv_xell), W 32-bit codes per row
     int xshift = 0;                   // its column bits (DevCSR::xell_shift)
@@ -82,10 +49,7 @@ struct DevDict {
 // loads in flight per thread, one dictionary barrier for all of them).  Measured at 400^3
 // (tools/gpu/ab.sh): 2 blocks took level 0's smoothing 3.12 -> 3.02 ms and its residual 389 ->
 // 374 us per V-cycle; 4 blocks (70 VGPRs) were slower than 1 (3.36 ms).
-#ifndef SSS_ELL_RPT
-#define SSS_ELL_RPT 2
-#endif
-constexpr int kEllRpt = SSS_ELL_RPT;
+constexpr int kEllRpt = 2;
 
 // ---- dictionary ELL: one thread per row ----------------------------------------------------
 // The block's dictionaries in LDS (small: the kernels instantiated for ELL keep their LDS
@@ -170,18 +134,10 @@ __device__ __forceinline__ int ell_row(const unsigned char *__restrict__ ell, in
 // (loads and stores of 8-byte aligned pairs: gfx950 takes them unaligned).  Each row is decoded
 // with its own block's dictionaries and summed exactly as ell_decode / ell_add do: bitwise the
 // one-row-per-thread kernels.  tools/l0_lab.hip (7-pt 400^3, relabeled level 0): residual
-// 589 -> 542 us, class pass 290 -> 284 us.  SSS_ELL_PAIRS=0 at build time: one row per thread.
-#ifndef SSS_ELL_PAIRS
-#define SSS_ELL_PAIRS 1
-#endif
-constexpr bool kEllPairs = SSS_ELL_PAIRS != 0 && kEllRpt == 2;
-// ... in the relaxation kernels; the residual SpMV keeps one row per thread: measured in the cycle
-// at 400^3 the pairs took the relaxation passes 3.5-4.6 % faster but the F-row residual 5 % slower
-// (280 -> 294 us per V-cycle), so the SpMV path is off unless built with SSS_ELL_PAIRS_SPMV=1
-#ifndef SSS_ELL_PAIRS_SPMV
-#define SSS_ELL_PAIRS_SPMV 0
-#endif
-constexpr bool kEllPairsSpmv = SSS_ELL_PAIRS_SPMV != 0;
+// 589 -> 542 us, class pass 290 -> 284 us.  Used by the relaxation kernels; the residual SpMV keeps
+// one row per thread (measured in the cycle at 400^3: the pairs took the relaxation passes 3.5-4.6 %
+// faster but the F-row residual 5 % slower, 280 -> 294 us per V-cycle).
+constexpr bool kEllPairs = kEllRpt == 2;
 struct alignas(8) CodePair {
     unsigned x, y, z, w;
 };
@@ -321,39 +277,15 @@ __device__ __forceinline__ double xell_sum_bf(double s0, const unsigned (&w)[W],
     }
     return s0;
 }
-// Per-slot form in groups of XG slots: the group's LDS values read together, then a select per slot
-// (XG = 1: a branch per slot, the group of one value read and waited for inside it)
-#ifndef SSS_XELL_GROUP
-#define SSS_XELL_GROUP 1
-#endif
+// Per-slot form: a branch per slot, its LDS value read inside it (groups of values read ahead and
+// selected per slot were measured no faster on level 1 at 400^3).
 template <bool SUB, int W>
 __device__ __forceinline__ double xell_sum_g(double s0, const unsigned (&w)[W], const double (&xv)[W], const XellSmem &es,
                                              int shift, int a, int e)
 {
-    constexpr int XG = SSS_XELL_GROUP;
-    if constexpr (XG == 1) {
 #pragma unroll
-        for (int s = 0; s < W; ++s)
-            if (s >= a && s < e) s0 = SUB ? s0 - es.vd[w[s] >> shift] * xv[s] : s0 + es.vd[w[s] >> shift] * xv[s];
-    } else {
-#pragma unroll
-        for (int g = 0; g < W; g += XG) {
-            double av[XG];
-#pragma unroll
-            for (int u = 0; u < XG; ++u) {
-                const int s = g + u;
-                av[u] = s < W ? es.vd[(s >= a && s < e) ? (w[s < W ? s : 0] >> shift) : 0u] : 0.0;
-            }
-#pragma unroll
-            for (int u = 0; u < XG; ++u) {
-                const int s = g + u;
-                if (s >= W) break;
-                const double p = av[u] * xv[s];
-                const double t = SUB ? s0 - p : s0 + p;
-                s0 = (s >= a && s < e) ? t : s0;
-            }
-        }
-    }
+    for (int s = 0; s < W; ++s)
+        if (s >= a && s < e) s0 = SUB ? s0 - es.vd[w[s] >> shift] * xv[s] : s0 + es.vd[w[s] >> shift] * xv[s];
     return s0;
 }
 template <int W>
@@ -593,10 +525,7 @@ __device__ __forceinline__ void stage_sorted(double *__restrict__ sm, int k0, in
 // dictionary in LDS (vd[vi[k]], the same bit pattern pv[k] held).
 // The slots of one pass of the loop below (U per thread): stage_dict loads the first pass ahead of
 // the dictionary barrier, so the slot stream is in flight while the dictionary arrives.
-#ifndef SSS_VDICT_U
-#define SSS_VDICT_U 8
-#endif
-constexpr int kVdictU = SSS_VDICT_U;
+constexpr int kVdictU = 8;
 __device__ __forceinline__ void vdict_load(int kb, int k1, const unsigned *__restrict__ pk,
                                            const unsigned char *__restrict__ vi, unsigned (&q)[kVdictU],
                                            unsigned (&w)[kVdictU])
@@ -952,9 +881,7 @@ __device__ __forceinline__ double wave_row_sum(int k0, int k1, const int *__rest
 // entry's (segment, row), then each accumulator's 64 lane sums are xor-reduced.  Fixed order:
 // deterministic.  s0[u] / s1[u] = sum over row u's first- / second-segment entries of
 // val * fetch(col), valid in every lane (S = 1: single-segment matrices, s1 untouched).
-#ifndef SSS_MERGE_U
-#define SSS_MERGE_U 8
-#endif
+
 // (U, the loads in flight per lane, changes no sum: each lane still adds its entries in increasing
 // position into the same accumulators)
 template <int G, int S, class Fetch>
@@ -962,7 +889,7 @@ __device__ __forceinline__ void merged_sums(int k0, int k1, const unsigned *__re
                                             const double *__restrict__ mv, Fetch fetch, double (&s0)[G],
                                             double (&s1)[G])
 {
-    constexpr int U = SSS_MERGE_U;
+    constexpr int U = 8;
     const int lane = threadIdx.x & 63;
 #pragma unroll
     for (int u = 0; u < G; ++u) s0[u] = 0.0, s1[u] = 0.0;

@@ -1,6 +1,6 @@
 # A/B of engine variants on the per-level kernel times of the bench workload (kernel-trace profile
 # of a short bench per variant).  Variants: label=ENV=VAL[,ENV=VAL...] arguments, e.g.
-#   bash tools/gpu/ab.sh base=SSS_HIP_RELAX_OCC=0 occ6= wpe5=SSS_AMG_LIB=amg_amd/lib_wpe5/libsss_amg.so
+#   bash tools/gpu/ab.sh head= prev=SSS_AMG_LIB=amg_amd/lib_ab/libsss_amg.so nodict=SSS_HIP_DICT=0
 cd "$GRAFT_REPO_ROOT" || exit 1
 mkdir -p gpurun_out/ab
 for v in "$@"; do

@@ -38,12 +38,7 @@ def main():
     levels = [int(x) for x in a.levels.split(",")] if a.levels else list(range(1, H.num_levels - 1))
     out = []
     for eng in a.engines.split(","):
-        base, _, waves = eng.partition(":")   # flow:64 -> SSS_HIP_GS_WAVES=64
-        os.environ["SSS_HIP_GS_ENGINE"] = base
-        if waves:
-            os.environ["SSS_HIP_GS_WAVES"] = waves
-        else:
-            os.environ.pop("SSS_HIP_GS_WAVES", None)
+        os.environ["SSS_HIP_GS_ENGINE"] = eng
         D = A.DeviceHierarchy(H, smoother="exact", coarse="direct", device=0)
         rng = np.random.default_rng(1)
         for l in levels:
