@@ -24,29 +24,30 @@ from conftest import build_hierarchy, quiet_ctx  # noqa: E402
 pytestmark = pytest.mark.gpu
 
 
-@pytest.fixture(scope="module", params=[96, 64])
+@pytest.fixture(scope="module", params=[(96, ""), (96, "11"), (64, "")])
 def grid_h(request):
-    H = build_hierarchy(A.generate(7, request.param), quiet_ctx)
-    yield request.param, H
+    edge, cap = request.param
+    H = build_hierarchy(A.generate(7, edge), quiet_ctx)
+    yield edge, cap, H
     H.close()
 
 
 @pytest.mark.parametrize("smoother,coarse,cycles", [("hybrid", "direct", 4), ("exact", "direct", 2)])
 def test_ell_runs_bitwise(grid_h, smoother, coarse, cycles, monkeypatch):
-    edge, H = grid_h
+    edge, cap, H = grid_h
     n = H.level(0).A.num_rows
     out = []
-    for on in ("1", "0"):
+    for on in (cap, "0"):
         monkeypatch.setenv("SSS_HIP_ELL_RUNS", on)
         D = A.DeviceHierarchy(H, smoother=smoother, coarse=coarse, device=0)
         info = D.level_info(0)
-        if on == "1":
+        if on != "0":
             assert info.a_format & 64, "level 0 is not a dictionary ELL"
             assert 0 < info.a_run_rows <= n, info.a_run_rows
-            if edge == 96:
-                assert info.a_run_rows == n   # every block fits kEllRuns runs
-            else:
+            if cap:
                 assert info.a_run_rows < n    # the mixed path
+            else:
+                assert info.a_run_rows == n   # every block fits kEllRuns runs
         else:
             assert info.a_run_rows == 0
         D.upload(0, "b", np.ones(n))

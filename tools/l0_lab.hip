@@ -152,6 +152,107 @@ __global__ __launch_bounds__(B) void kpass(const unsigned char *__restrict__ ell
     }
 }
 
+
+// ---- persistent, software-pipelined pass (round 5 lab; measured and rejected) -------------------
+// At 400^3: F pass 314-436 us for G = 4096..512 workgroups against 281 us for kpass<0, 1> (one block
+// per workgroup); residual 654-811 us against 577 us.  The compiler branches around every gather and
+// waits vmcnt(0) at the loop latch, so the next block's loads never overlap this block's gathers.
+// (Run-coded dictionary ELL blocks -- codes stored once per run of equal rows, 2.1 GB fewer bytes per
+// V-cycle -- measured in the engine the same round: level-0 smoothing 2112 -> 2301 us: the level-0
+// passes are bound by each workgroup's chain of dependent loads, not by bytes.)
+// Each workgroup loops over the blocks bq = blockIdx.x, + gridDim.x, ...  While block k's gathers are
+// in flight, block k + 1's codes, b and dictionary values are loaded (registers), then stored to the
+// other LDS dictionary buffer after block k's results: one barrier per block, and the dependent
+// chain (dictionaries -> barrier -> decode -> gathers) of the next block overlaps this block's.
+template <int MODE>
+__global__ __launch_bounds__(B) void kpipe(const unsigned char *__restrict__ ell, const int *__restrict__ ddf,
+                                           const double *__restrict__ vdf, const double *__restrict__ b,
+                                           double *x, double *__restrict__ y, int lo, int hi)
+{
+    __shared__ int dd[2][32];
+    __shared__ double vd[2][8];
+    const int nb = (hi - lo + B - 1) / B, b0 = lo / B;
+    int bq = blockIdx.x;
+    if (bq >= nb) return;
+    const int t = threadIdx.x;
+    auto codes = [&](int q, unsigned (&w)[2], double &bv) {
+        const int r = lo + q * B + t;
+        w[0] = w[1] = 0xffffffffu;
+        bv = 0.0;
+        if (r < hi) {
+            const uint2 c = *reinterpret_cast<const uint2 *>(ell + (size_t)r * 8);
+            w[0] = c.x, w[1] = c.y;
+            bv = b[r];
+        }
+    };
+    int dreg = 0;
+    double vreg = 0.0;
+    auto dict_load = [&](int q) {
+        if (t < 32) dreg = ddf[(size_t)(b0 + q) * 32 + t];
+        else if (t < 40) vreg = vdf[(size_t)(b0 + q) * 8 + t - 32];
+    };
+    auto dict_store = [&](int buf) {
+        if (t < 32) dd[buf][t] = dreg;
+        else if (t < 40) vd[buf][t - 32] = vreg;
+    };
+    unsigned wc[2];
+    double bc;
+    codes(bq, wc, bc);
+    dict_load(bq);
+    dict_store(0);
+    int buf = 0;
+    for (;;) {
+        __syncthreads();   // dictionaries of bq in dd[buf]; every reader of dd[buf ^ 1] is done
+        const int r = lo + bq * B + t;
+        const bool live = r < hi;
+        int c[8], len = 8, ds = -1;
+        double a[8], dv = 0.0;
+#pragma unroll
+        for (int s = 0; s < 8; ++s) {
+            const unsigned byte = (wc[s >> 2] >> (8 * (s & 3))) & 0xffu;
+            if (byte == 0xffu && len == 8) len = s;
+            c[s] = r + dd[buf][byte & 31u];
+            a[s] = vd[buf][byte >> 5];
+        }
+#pragma unroll
+        for (int s = 0; s < 8; ++s)
+            if (s < len && c[s] == r) ds = s, dv = a[s];
+        double xv[8];
+#pragma unroll
+        for (int s = 0; s < 8; ++s) xv[s] = (live && s < len && (MODE == 1 || s != ds)) ? x[c[s]] : 0.0;
+        const int nq = bq + gridDim.x;
+        unsigned wn[2];
+        double bn = 0.0;
+        if (nq < nb) {   // the next block's loads, behind this block's gathers
+            codes(nq, wn, bn);
+            dict_load(nq);
+        }
+        if (live) {
+            double out;
+            if constexpr (MODE == 0) {
+                double tt = bc;
+#pragma unroll
+                for (int s = 0; s < 8; ++s)
+                    if (s < len && s != ds) tt -= a[s] * xv[s];
+                out = fabs(dv) > 1e-20 ? tt / dv : x[r];
+                x[r] = out;
+            } else {
+                double tt = 0.0;
+#pragma unroll
+                for (int s = 0; s < 8; ++s)
+                    if (s < len) tt += a[s] * xv[s];
+                y[r] = bc + tt * -1.0;
+            }
+        }
+        if (nq >= nb) break;
+        dict_store(buf ^ 1);
+        buf ^= 1;
+        bq = nq;
+        wc[0] = wn[0], wc[1] = wn[1];
+        bc = bn;
+    }
+}
+
 // stream floor: codes + b in, y out (MODE 1 bytes without the gathers)
 __global__ __launch_bounds__(B) void kstream(const unsigned char *ell, const double *x, const double *b, double *y, int n)
 {
@@ -381,7 +482,17 @@ int main(int argc, char **argv)
         run("eng rpt2 (none)", 0, fbytes, EN(2, false, false, false));
         run("eng rpt1 (none)", 0, fbytes, EN(1, false, false, false));
     }
+    for (int g : {512, 1024, 2048, 4096}) {
+        char nm[64];
+        snprintf(nm, sizeof nm, "F pass pipe G=%d", g);
+        run(nm, 0, fbytes, [&] { hipLaunchKernelGGL(kpipe<0>, dim3(g), dim3(B), 0, 0, d_ell, d_ddf, d_vdf, b, x, y, 0, nF); });
+    }
     run("resid R1", 3, rbytes, RS(1, false));
+    for (int g : {512, 1024, 2048, 4096}) {
+        char nm[64];
+        snprintf(nm, sizeof nm, "resid pipe G=%d", g);
+        run(nm, 1, rbytes, [&] { hipLaunchKernelGGL(kpipe<1>, dim3(g), dim3(B), 0, 0, d_ell, d_ddf, d_vdf, b, x, y, 0, n); });
+    }
     run("resid R2 scalar", 1, rbytes, RS(2, false));
     run("resid R2 pair", 1, rbytes, RS(2, true));
     run("resid R4 scalar", 1, rbytes, RS(4, false));
