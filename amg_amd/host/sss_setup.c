@@ -30,6 +30,7 @@
 #include <stdlib.h>
 #include <string.h>
 #include <sys/time.h>
+#include <unistd.h>
 #ifdef _OPENMP
 #include <omp.h>
 #endif
@@ -542,13 +543,32 @@ static void direct_pattern(SSS_MAT *P, const SSS_IMAT *S, const SSS_IVEC *vertic
     }
 }
 
-/* Threads for a row-parallel loop whose threads each hold `bytes_per_item` x n of scratch (at most
- * 2 GiB of scratch together). */
-static int scratch_threads(int n, size_t bytes_per_item)
+/* Per-thread scratch of a row-parallel loop: one buffer of `bytes` for each of up to
+ * omp_get_max_threads() threads (at most 256), all of them together within a quarter of the
+ * machine's memory (at least 2 GiB), fewer threads when an allocation fails.  Returns the threads
+ * that got one; the loop runs on that many.  With none (even one buffer failed) the setup cannot go
+ * on: the reference's allocation failure path (a warning, then the error exit). */
+enum { kScratchMax = 256 };
+static int scratch_alloc(size_t bytes, void **buf)
 {
+    const long pages = sysconf(_SC_PHYS_PAGES), psz = sysconf(_SC_PAGESIZE);
+    size_t budget = (pages > 0 && psz > 0) ? (size_t)pages * (size_t)psz / 4 : 0;
+    if (budget < ((size_t)2 << 30)) budget = (size_t)2 << 30;
+    if (bytes == 0) bytes = 1;
     int T = omp_get_max_threads();
-    while (T > 1 && (size_t)T * (size_t)(n > 0 ? n : 1) * bytes_per_item > ((size_t)2 << 30)) T--;
-    return T;
+    if (T > kScratchMax) T = kScratchMax;
+    while (T > 1 && (size_t)T * bytes > budget) T--;
+    int got = 0;
+    while (got < T && (buf[got] = malloc(bytes)) != NULL) ++got;
+    if (got == 0) {
+        printf("### WARNING: Cannot allocate %.3lf MB RAM!\n", (double)bytes / 1048576);
+        SSS_exit_on_errcode(ERROR_ALLOC_MEM, __func__);
+    }
+    return got;
+}
+static void scratch_free(void **buf, int T)
+{
+    for (int t = 0; t < T; ++t) free(buf[t]);
 }
 
 /* Setup/SSS_coarsen.c:633-725 (form_P_pattern_std): an F row takes its strong C neighbours and the
@@ -559,7 +579,8 @@ static int scratch_threads(int n, size_t bytes_per_item)
 static void std_pattern(SSS_MAT *P, const SSS_IMAT *S, const SSS_IVEC *vertices, int n, int ncoarse)
 {
     const int *mark = vertices->d;
-    const int T = scratch_threads(n, sizeof(int));
+    void *scr[kScratchMax];
+    const int T = scratch_alloc(sizeof(int) * (size_t)(n > 0 ? n : 1), scr);
     P->num_rows = n;
     P->num_cols = ncoarse;
     P->row_ptr = (int *)SSS_calloc((size_t)n + 1, sizeof(int));
@@ -572,7 +593,7 @@ static void std_pattern(SSS_MAT *P, const SSS_IMAT *S, const SSS_IVEC *vertices,
         }
 #pragma omp parallel num_threads(T) if (n > 4096)
         {
-            int *seen = (int *)malloc(sizeof(int) * (size_t)(n > 0 ? n : 1));
+            int *seen = (int *)scr[omp_get_thread_num()];
             for (int i = 0; i < n; ++i) seen[i] = -1;
 #pragma omp for schedule(dynamic, 1024)
             for (int i = 0; i < n; ++i) {
@@ -601,9 +622,9 @@ static void std_pattern(SSS_MAT *P, const SSS_IMAT *S, const SSS_IVEC *vertices,
                 }
                 if (!fill) P->row_ptr[i + 1] = cnt;
             }
-            free(seen);
         }
     }
+    scratch_free(scr, T);
 }
 
 int SSS_amg_coarsen(SSS_MAT *A, SSS_IVEC *vertices, SSS_MAT *P, SSS_IMAT *S, SSS_AMG_PARS *pars)
@@ -880,11 +901,14 @@ static void interp_STD(SSS_MAT *A, SSS_IVEC *vertices, SSS_MAT *P, SSS_IMAT *S, 
     }
 
     /* step 1: the weights */
-    const int T = scratch_threads(nc, 2 * sizeof(int) + sizeof(double));
+    /* per thread: rindi and rindk (ints) and ahat (doubles), nc each, in one buffer */
+    void *scr[kScratchMax];
+    const size_t ncs = (size_t)(nc > 0 ? nc : 1);
+    const int T = scratch_alloc(ncs * (2 * sizeof(int) + sizeof(double)), scr);
 #pragma omp parallel num_threads(T) if (n > 4096)
     {
-        int *rindi = (int *)malloc(sizeof(int) * (size_t)nc), *rindk = (int *)malloc(sizeof(int) * (size_t)nc);
-        double *ahat = (double *)malloc(sizeof(double) * (size_t)nc);
+        double *ahat = (double *)scr[omp_get_thread_num()];
+        int *rindi = (int *)(ahat + ncs), *rindk = rindi + ncs;
 #pragma omp for schedule(dynamic, 1024)
         for (int i = 0; i < n; ++i) {
             if (mark[i] == CGPT) {
@@ -923,10 +947,8 @@ static void interp_STD(SSS_MAT *A, SSS_IVEC *vertices, SSS_MAT *P, SSS_IMAT *S, 
             if (P->row_ptr[i + 1] > P->row_ptr[i]) alpha = alN / alP;
             for (int j = P->row_ptr[i]; j < P->row_ptr[i + 1]; ++j) P->val[j] = -alpha * ahat[P->col_idx[j]] / ahat[i];
         }
-        free(rindi);
-        free(rindk);
-        free(ahat);
     }
+    scratch_free(scr, T);
 
     /* step 2: coarse renumbering of the columns */
     int *cmap = (int *)SSS_calloc((size_t)(n > 0 ? n : 1), sizeof(int));
