@@ -518,7 +518,8 @@ static sss_hip_dist *dist_create_impl(sss_hip_dist *d, PartPlan &plan, const SSS
             L.m = P.m;
             L.g = P.g;
             L.perm = P.perm;
-            const int kind = level_kind_of(d->opts, l), inner = level_inner_of(d->opts, l);
+            const int kind = level_kind_of(d->opts, l);
+            const int inner = level_inner_of(d->opts, l, plan.cut[l][plan.nranks], plan.gnnz[l]);
             SSS_MAT Av = P.A.view();
             const int enc = level_encoding(d->opts);
             if (devcsr_upload(L.A, Av, P.nF, enc)) return "upload A";

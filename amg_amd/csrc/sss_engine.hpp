@@ -355,7 +355,9 @@ int hier_stall_check(sss_hip_hier *h);
 unsigned *hier_err_word(sss_hip_hier *h);
 bool hier_coarse_on_device(sss_hip_hier *h);   // the coarsest solve is device-only (explicit inverse)
 void hier_set_err_word(sss_hip_hier *h, unsigned *err);
-int level_inner_of(const sss_hip_opts &o, int global_level);
+// two-stage inner steps of a global level of `rows` rows and `nnz` entries (the whole level's, on
+// every rank of a partitioned one)
+int level_inner_of(const sss_hip_opts &o, int global_level, long long rows, long long nnz);
 
 // y <- op(A x) on `stream` (see SSS_HIP_SPMV_*).  `partial` (optional, RESID only): one
 // sum-of-squares of the written y per row block, for a deterministic fused norm.

@@ -102,6 +102,7 @@ extern "C" void sss_hip_opts_default(sss_hip_opts *o)
     o->relabel = env_int("SSS_HIP_RELABEL", 1);
     o->inner = env_int("SSS_HIP_INNER", 1);
     o->inner_from = env_int("SSS_HIP_INNER_FROM", 2);
+    o->inner_long = env_int("SSS_HIP_INNER_LONG", 1);
     o->sorted_tiles = env_int("SSS_HIP_SORTED_TILES", 1);
     o->sum_order = env_int("SSS_HIP_SUM_ORDER", 0);
     if (const char *s = getenv("SSS_HIP_SMOOTHER")) {
@@ -139,9 +140,12 @@ static int level_smoother_kind(const sss_hip_opts &o, int l)
 }
 
 // two-stage inner steps of level l (0 = plain C/F-Jacobi there, or not a C/F-Jacobi level)
-static int level_inner(const sss_hip_opts &o, int l)
+// rows / nnz: the whole (global) level's, so every rank of a partitioned level decides alike
+static int level_inner(const sss_hip_opts &o, int l, long long rows, long long nnz)
 {
-    return level_smoother_kind(o, l) == SSS_HIP_SMOOTH_JACOBI && l >= o.inner_from ? o.inner : 0;
+    if (level_smoother_kind(o, l) != SSS_HIP_SMOOTH_JACOBI || l < o.inner_from || o.inner <= 0) return 0;
+    const bool long_rows = rows > 0 && nnz >= (long long)SSS_HIP_LONG_ROW_MIN * rows;
+    return o.inner + (long_rows ? std::max(0, o.inner_long) : 0);
 }
 int sss::level_kind_of(const sss_hip_opts &o, int l) { return level_smoother_kind(o, l); }
 int sss::level_encoding(const sss_hip_opts &o)
@@ -152,7 +156,10 @@ int sss::level_encoding(const sss_hip_opts &o)
     const int dict = (dz && *dz == '0') ? 0 : kEncDict;
     return (o.sorted_tiles ? kEncSortedTiles : 0) | (o.sum_order == 1 ? kEncFreeOrder : 0) | dict | (dict ? kEncXell : 0);
 }
-int sss::level_inner_of(const sss_hip_opts &o, int l) { return level_inner(o, l); }
+int sss::level_inner_of(const sss_hip_opts &o, int l, long long rows, long long nnz)
+{
+    return level_inner(o, l, rows, nnz);
+}
 // P_l and R_l: the level matrices' encodings without the dictionary tiles (measured at 7-pt 400^3:
 // 22.15 -> 22.25 ms per V-cycle with them, level-0 prolongation 255 -> 325 us -- P's F rows have
 // 1-8 irregular columns, so the per-tile dictionaries rarely shrink a row and the extra
@@ -196,10 +203,10 @@ static int hier_kind(const sss_hip_hier *h, int gl)
     if (gl == 0 && h->hybrid0_two_stage) return SSS_HIP_SMOOTH_JACOBI;
     return level_smoother_kind(h->opts, gl);
 }
-static int hier_inner(const sss_hip_hier *h, int gl)
+static int hier_inner(const sss_hip_hier *h, int gl, const SSS_MAT &A)
 {
     if (gl == 0 && h->hybrid0_two_stage) return std::max(1, h->opts.inner);
-    return level_inner(h->opts, gl);
+    return level_inner(h->opts, gl, A.num_rows, A.num_nnzs);
 }
 
 // Natural-order GS (SSS_amg_smoother_pre/post with cf_order = 0, Solve/SSS_smooth.c:171-176,
@@ -362,7 +369,7 @@ static void hb_perm(HierBuild &b, int l)
     if (!C.cfmark.d || C.cfmark.n < n) return;
     // two-stage levels need contiguous classes; otherwise follow opts.relabel
     const int gl = h->level_base + l;
-    const bool two_stage = hier_inner(h, gl) > 0;
+    const bool two_stage = hier_inner(h, gl, C.A) > 0;
     if (natural_level(h, gl)) return;   // the natural order is the stored row order
     if (!two_stage && !(h->opts.relabel == 1 || (h->opts.relabel == 2 && gl > 0))) return;
     auto &perm = h->L[l].perm;
@@ -393,7 +400,7 @@ static bool hb_level_a(HierBuild &b, int l, bool coarsest)
     // the relaxation reads the split copies, and the level matrix's own free-order products go
     // through its merged copy (residual) or are order-free (zero-first pass): no sorted rows needed
     int enc = !coarsest ? level_encoding(h->opts) : (level_encoding(h->opts) & kEncSortedTiles);
-    if (!coarsest && hier_kind(h, h->level_base + l) == SSS_HIP_SMOOTH_JACOBI && hier_inner(h, h->level_base + l) > 0)
+    if (!coarsest && hier_kind(h, h->level_base + l) == SSS_HIP_SMOOTH_JACOBI && hier_inner(h, h->level_base + l, C.A) > 0)
         enc |= kEncMergedOnly;
     if (rl) {
         RelabeledCSR B;
@@ -408,7 +415,7 @@ static bool hb_level_a(HierBuild &b, int l, bool coarsest)
             for (int i = lo; i < hi; ++i) mark[i] = C.cfmark.d[L.perm[i]];
         });
         if (smoother_build(L.sm, Av, mark.data(), hier_kind(h, h->level_base + l), &L.A,
-                           hier_inner(h, h->level_base + l), nullptr, enc))
+                           hier_inner(h, h->level_base + l, C.A), nullptr, enc))
             return hb_fail(b, "smoother plan");
         if (L.sm.inner == 0 && devcsr_sort_rows(L.A, Av)) return hb_fail(b, "upload A");   // plain passes read A's rows
         t_sm = PhaseTimer::now();

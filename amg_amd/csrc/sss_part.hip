@@ -146,6 +146,8 @@ static int part_plan_build_impl(PartPlan &p, const SSS_AMG *mg, int nranks, int 
     if (int rc = part_cuts(mg, N, agg_rows, nagg, p.cut)) return rc;
     p.nagg = nagg;
     p.L.assign((size_t)nagg, PartLevel());
+    p.gnnz.resize((size_t)nagg);
+    for (int l = 0; l < nagg; ++l) p.gnnz[l] = mg->cg[l].A.num_nnzs;
 
     // pass 1: own rows and their F|C relabeling
     std::vector<std::vector<int>> inv((size_t)nagg);
@@ -248,13 +250,14 @@ int part_save_all(const SSS_AMG *mg, int nranks, int agg_rows, const char *prefi
 namespace sss {
 
 // ---- partition files -------------------------------------------------------------------------
-// Layout (little-endian, native LP64):  "SSSPART1"  int32 version=1  int32 sizeof(SSS_AMG_PARS)
-//   SSS_AMG_PARS  int32 nranks, rank, nl, nagg;  nagg+1 cut vectors;  per level l < nagg:
+// Layout (little-endian, native LP64):  "SSSPART1"  int32 version=2  int32 sizeof(SSS_AMG_PARS)
+//   SSS_AMG_PARS  int32 nranks, rank, nl, nagg;  nagg+1 cut vectors;  int64 vector gnnz;  per level l < nagg:
 //   int32 lo, hi, m, g, nF;  int vectors perm, ghosts, mark, gcls, gclass;  matrices A, P, R;
 //   int vectors sdst, scount, sidx, rsrc, rcount.   vector := int64 count + data;
 //   matrix := int32 rows, cols + int vectors rp, ci + double vector v.
 namespace {
 const char kPartMagic[8] = {'S', 'S', 'S', 'P', 'A', 'R', 'T', '1'};
+constexpr int kPartVersion = 2;
 
 struct Out {
     FILE *f;
@@ -339,7 +342,7 @@ int part_plan_write(const PartPlan &p, const SSS_AMG_PARS &pars, const char *pat
     if (!f) return ERROR_OPEN_FILE;
     Out o{f};
     o.raw(kPartMagic, sizeof(kPartMagic));
-    o.i32(1);
+    o.i32(kPartVersion);
     o.i32((int)sizeof(SSS_AMG_PARS));
     o.raw(&pars, sizeof(pars));
     o.i32(p.nranks);
@@ -347,6 +350,7 @@ int part_plan_write(const PartPlan &p, const SSS_AMG_PARS &pars, const char *pat
     o.i32(p.nl);
     o.i32(p.nagg);
     for (const auto &c : p.cut) o.vec(c);
+    o.vec(p.gnnz);
     for (const auto &L : p.L) {
         o.i32(L.lo), o.i32(L.hi), o.i32(L.m), o.i32(L.g), o.i32(L.nF);
         o.vec(L.perm), o.vec(L.ghosts), o.vec(L.mark), o.vec(L.gcls), o.vec(L.gclass);
@@ -389,7 +393,8 @@ int part_plan_read(PartPlan &p, SSS_AMG_PARS &pars, const char *path)
     In in{f};
     char magic[8];
     in.raw(magic, sizeof(magic));
-    if (in.bad || memcmp(magic, kPartMagic, sizeof(magic)) || in.i32() != 1 || in.i32() != (int)sizeof(SSS_AMG_PARS)) {
+    if (in.bad || memcmp(magic, kPartMagic, sizeof(magic)) || in.i32() != kPartVersion ||
+        in.i32() != (int)sizeof(SSS_AMG_PARS)) {
         fclose(f);
         return ERROR_WRONG_FILE;
     }
@@ -409,6 +414,8 @@ int part_plan_read(PartPlan &p, SSS_AMG_PARS &pars, const char *path)
         in.vec(c);
         if (c.size() != (size_t)p.nranks + 1) in.bad = true;
     }
+    in.vec(p.gnnz);
+    if (p.gnnz.size() != (size_t)p.nagg) in.bad = true;
     p.L.resize((size_t)p.nagg);
     for (auto &L : p.L) {
         L.lo = in.i32(), L.hi = in.i32(), L.m = in.i32(), L.g = in.i32(), L.nF = in.i32();

@@ -54,6 +54,7 @@ struct PartLevel {
 struct PartPlan {
     int nranks = 1, rank = 0, nl = 0, nagg = 0;
     std::vector<std::vector<int>> cut;   // cut[l][q] = first row of rank q on level l (l <= nagg), size nranks + 1
+    std::vector<long long> gnnz;         // nnz of the whole level l (l < nagg): per-level choices every rank makes alike
     std::vector<PartLevel> L;            // l < nagg
 };
 
@@ -61,7 +62,8 @@ struct PartPlan {
 // replicated (the coarsest always is).  Returns 0 or an SSS error code.
 int part_plan_build(PartPlan &p, const SSS_AMG *mg, int nranks, int rank, int agg_rows);
 
-// Partition file of one rank (sss_part_save): its PartPlan plus the solve parameters.  The
+// Partition file of one rank (sss_part_save): its PartPlan plus the solve parameters (format 2:
+// with the levels' global nnz).  The
 // replicated tail levels (cg[nagg..]) live in a separate hierarchy file (SSS_amg_save format)
 // that every rank loads.  Returns 0 or ERROR_OPEN_FILE / ERROR_WRONG_FILE.
 int part_plan_write(const PartPlan &p, const SSS_AMG_PARS &pars, const char *path);

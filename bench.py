@@ -78,6 +78,9 @@ def parse():
     p.add_argument("--mode-coarse", default=None, help="override: krylov|direct")
     p.add_argument("--inner", type=int, default=None,
                    help="two-stage inner steps on C/F-Jacobi levels (default: SSS_HIP_INNER or 1; 0 = plain C/F-Jacobi)")
+    p.add_argument("--inner-long", type=int, default=None,
+                   help="extra inner steps on the two-stage levels of long rows (>= 300 entries per row; default: "
+                        "SSS_HIP_INNER_LONG or 1)")
     p.add_argument("--inner-from", type=int, default=None,
                    help="first level with the two-stage form (default: SSS_HIP_INNER_FROM or 2)")
     p.add_argument("--converge-max", type=int, default=100, help="max V-cycles of the iterations-to-tol run (0: skip)")
@@ -487,6 +490,7 @@ def main():
     H = None
     DH = None   # set here when the mirror is built while the setup runs (sss_hip_setup_create)
     dh_kw = dict(smoother=smoother, coarse=coarse, device=-1, inner=args.inner, inner_from=args.inner_from,
+                 inner_long=args.inner_long,
                  sum_order=sum_order, sorted_tiles=sorted_tiles)
     if D.world == 1:
         cache = Path(args.hier_cache) if args.hier_cache else None
@@ -551,6 +555,7 @@ def main():
     t0 = time.perf_counter()
     inner = args.inner if args.inner is not None else int(os.environ.get("SSS_HIP_INNER", "1"))
     inner_from = args.inner_from if args.inner_from is not None else int(os.environ.get("SSS_HIP_INNER_FROM", "2"))
+    inner_long = args.inner_long if args.inner_long is not None else int(os.environ.get("SSS_HIP_INNER_LONG", "1"))
     if D.world == 1:
         if DH is None:
             DH = A.DeviceHierarchy(H, **dh_kw)
@@ -558,6 +563,7 @@ def main():
     else:
         # row-partitioned solve over RCCL (xGMI): each rank reads only its own partition file
         DD = A.DistHierarchy(None, comm, smoother=smoother, coarse=coarse, device=dev, inner=args.inner,
+                             inner_long=args.inner_long,
                              inner_from=args.inner_from, sum_order=sum_order, sorted_tiles=sorted_tiles, parts=prefix)
         eng = Distributed(DD)
         D.barrier()   # every rank has read its file: the set is no longer needed
@@ -770,9 +776,12 @@ def main():
             # the device's per-level smoothers (hybrid: level 0 exact only where chain-free)
             jac = [l for l, (k, _) in enumerate(level_smoothers) if k == 2]   # SSS_HIP_SMOOTH_JACOBI
             mask = sum(1 << l for l, (_, i) in enumerate(level_smoothers) if i > 0)
+            steps = sorted({i for _, i in level_smoothers if i > 0})   # base, and the long-row levels'
+            base = steps[0] if steps else 0
             mode = dict(smoother=1, jacobi_from=jac[0] if jac else len(level_smoothers),
-                        coarse_mode=1 if coarse == "direct" else 0,
-                        inner=max((i for _, i in level_smoothers), default=0), inner_mask=mask if mask else 1 << 30)
+                        coarse_mode=1 if coarse == "direct" else 0, inner=base, inner_mask=mask if mask else 1 << 30,
+                        inner_long=steps[-1] - base if steps else 0,
+                        long_mask=sum(1 << l for l, (_, i) in enumerate(level_smoothers) if steps and i == steps[-1] > base))
         cpu_iterations(Hc, mt, threads=thr, iters=args.cpu_iters, warmup=args.cpu_warmup, **mode)
         cpu_mt = {
             "value": 1.0 / mt["seconds"], "unit": "V-cycle iter/s", "cores": mt["threads"], "kind": "port",
@@ -798,6 +807,7 @@ def main():
                    "mode": args.mode, "smoother": smoother, "coarse": coarse,
                    "inner": inner if smoother != "exact" else None,
                    "inner_from": inner_from if smoother != "exact" else None,
+                   "inner_long": inner_long if smoother != "exact" else None,
                    "sum_order": "tree (long rows)" if sum_order == 1 else "stored CSR order",
                    "sorted_tiles": bool(sorted_tiles),
                    "level_storage_bits": level_formats,

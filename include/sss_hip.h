@@ -57,13 +57,18 @@ typedef struct sss_hip_opts {
                           summed by a wave in a fixed tree order over column-sorted rows --
                           deterministic, within the reordered-summation bound of the reference,
                           not bitwise (throughput mode) */
+    int inner_long;    /* extra Jacobi-Richardson steps on the two-stage levels of long rows (at least
+                          SSS_HIP_LONG_ROW_MIN = 300 entries per row on average over the whole level):
+                          their lower triangles are the densest, and the extra step keeps throughput
+                          mode within the reference's iteration count + 2 at 7-pt 512^3 (default 1) */
 } sss_hip_opts;
 
+#define SSS_HIP_LONG_ROW_MIN 300
 /* Defaults, overridable by environment: SSS_HIP_SMOOTHER=exact|hybrid|jacobi,
  * SSS_HIP_COARSE=krylov|direct, SSS_HIP_ROWCAP=<n>, SSS_HIP_GRAPH=0|1, SSS_HIP_DEVICE=<n>,
  * SSS_HIP_VERBOSE=0|1, SSS_HIP_RELABEL=0|1|2 (default 1), SSS_HIP_INNER=<k> (default 1),
  * SSS_HIP_SORTED_TILES=0|1 (default 1), SSS_HIP_SUM_ORDER=0|1 (default 0),
- * SSS_HIP_INNER_FROM=<level> (default 2). */
+ * SSS_HIP_INNER_FROM=<level> (default 2), SSS_HIP_INNER_LONG=<k> (default 1). */
 void sss_hip_opts_default(sss_hip_opts *o);
 
 /* Number of usable HIP devices (0 when none; never exits). */

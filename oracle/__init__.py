@@ -24,7 +24,7 @@ class ORA_OPTS(C.Structure):
     _fields_ = [("row_cap", C.c_int), ("coarse_mode", C.c_int), ("smoother", C.c_int), ("jacobi_from", C.c_int),
                 ("verbose", C.c_int),
                 ("jacobi_l1", C.c_int), ("omega", C.c_double), ("inner", C.c_int),
-                ("inner_mask", C.c_int)]
+                ("inner_mask", C.c_int), ("inner_long", C.c_int), ("long_mask", C.c_int)]
 
 
 _ora = None

@@ -361,7 +361,8 @@ static void smoother_dispatch(SSS_SMTR *s, int post, const char *fname)
     case SSS_SM_JACOBI:
         if (g_cur_opts && g_cur_opts->inner > 0 &&
             (!g_cur_opts->inner_mask || (g_cur_opts->inner_mask >> g_cur_level & 1))) {
-            ora_cf_twostage(s->x->d, s->A, s->b->d, s->nsweeps, use_cf ? s->ordering : NULL, g_cur_opts->inner);
+            const int extra = (g_cur_opts->long_mask >> g_cur_level & 1) ? g_cur_opts->inner_long : 0;
+            ora_cf_twostage(s->x->d, s->A, s->b->d, s->nsweeps, use_cf ? s->ordering : NULL, g_cur_opts->inner + extra);
             break;
         }
         ora_cf_jacobi_w(s->x->d, s->A, s->b->d, s->nsweeps, use_cf ? s->ordering : NULL,

@@ -25,6 +25,9 @@ typedef struct {
     int inner;        /* > 0: two-stage GS-CF instead of C/F-Jacobi, with `inner` Jacobi-Richardson
                          steps on the same-class lower triangle (ora_cf_twostage) */
     int inner_mask;   /* experiments: bit l set = level l uses two-stage (0 = every C/F-Jacobi level) */
+    int inner_long;   /* extra inner steps on the two-stage levels whose bit is set in long_mask (the
+                         engine's long-row levels, sss_hip_opts::inner_long) */
+    int long_mask;
 } ora_opts;
 
 void ora_opts_default(ora_opts *o);

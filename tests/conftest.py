@@ -104,8 +104,13 @@ def device_mode_oracle_opts(H, **device_kw) -> dict:
         D.close()
     jac = [l for l, i in enumerate(info) if i.smoother_kind == 2]   # SSS_HIP_SMOOTH_JACOBI
     mask = sum(1 << l for l, i in enumerate(info) if i.inner > 0)
-    kw = dict(smoother=1, jacobi_from=jac[0] if jac else len(info),
-              inner=max((i.inner for i in info), default=0), inner_mask=mask if mask else 1 << 30)
+    steps = sorted({i.inner for i in info if i.inner > 0})
+    assert len(steps) <= 2, steps   # the base count, and the long-row levels' (sss_hip_opts::inner_long)
+    base = steps[0] if steps else 0
+    kw = dict(smoother=1, jacobi_from=jac[0] if jac else len(info), inner=base,
+              inner_mask=mask if mask else 1 << 30,
+              inner_long=steps[-1] - base if steps else 0,
+              long_mask=sum(1 << l for l, i in enumerate(info) if steps and i.inner == steps[-1] > base))
     if device_kw.get("coarse") == "direct":
         kw["coarse_mode"] = 1
     return kw

@@ -7,7 +7,8 @@ Each mode: smoother[/coarse][/inner/inner_from][/sum_order], e.g.
   parity        exact GS-CF + reference CG(beta=1)+GMRES   (x bitwise the reference's)
   exact-direct  exact GS-CF + explicit-inverse coarse solve
   throughput    bench default (hybrid, direct, inner 1 from level 2, tree long-row sums)
-  hyb:I:F       hybrid with I inner steps from level F (direct coarse, tree sums)
+  hyb:I:F[:L]   hybrid with I inner steps from level F, L more on long-row levels (default 1;
+                direct coarse, tree sums)
 """
 from __future__ import annotations
 
@@ -31,9 +32,10 @@ def mode_kwargs(m: str) -> dict:
         return dict(smoother="exact", coarse="direct", sum_order=0)
     if m == "throughput":
         return dict(smoother="hybrid", coarse="direct", sum_order=1)
-    if m.startswith("hyb:"):
-        _, i, f = m.split(":")
-        return dict(smoother="hybrid", coarse="direct", sum_order=1, inner=int(i), inner_from=int(f))
+    if m.startswith("hyb:"):   # hyb:I:F[:L] -- L extra inner steps on the long-row levels (default 1)
+        f = m.split(":")
+        return dict(smoother="hybrid", coarse="direct", sum_order=1, inner=int(f[1]), inner_from=int(f[2]),
+                    inner_long=int(f[3]) if len(f) > 3 else 1)
     if m.startswith("mc"):
         return dict(smoother="multicolor", coarse="direct", sum_order=1)
     raise ValueError(m)
