@@ -392,6 +392,22 @@ struct GsPersist {
     int spin = 0;                       // polls before a waiting wave gives up (< 0: test hook)
     unsigned long long *gran = nullptr; // flow: two {epoch, half of x_i} granules per row
 };
+// Every sweep's F and C passes of one exact GS-CF smoother call as ONE dataflow launch
+// (sss_gs_persist.hip, "fused" engine): nodes (row, sweep) in fused-DAG depth order.
+struct GsFused {
+    int engine = 0;                     // 1: built
+    int sweeps = 0;                     // the call's sweeps this plan is for
+    int n = 0, split = 0;               // rows; F rows [0, split), C rows [split, n)
+    int G = 64;                         // lanes per row
+    bool overlap = false;               // the chain runs while pending granules are polled
+    int depth = 0, nchunks = 0, grid = 0;
+    int *ck = nullptr;                  // chunk -> first position in nodes (nchunks + 1)
+    int *nodes = nullptr;               // sweep * n + row, by fused depth
+    unsigned *ctl = nullptr;            // epoch, ticket, exit count, error
+    unsigned *err = nullptr;
+    int spin = 0;
+    unsigned long long *gran = nullptr; // two {epoch << 4 | version, half of x_i} granules per row
+};
 struct PassSchedule {          // rows of one class (F or C), grouped by DAG depth
     int depth = 0;
     std::vector<int> h_off;    // depth + 1 offsets into rows
@@ -425,6 +441,11 @@ void gs_persist_free(PassSchedule &ps);
 int gs_persist_run(const PassSchedule &ps, const DevCSR &A, const double *b, double *x, const double *deff,
                    hipStream_t s);
 int gs_persist_error(const PassSchedule &ps, unsigned *out);
+// cls: per row 1 = C; pdepth: per row its depth within its class pass (same-class lower couplings)
+int gs_fused_build(GsFused &f, const SSS_MAT &A, const int *cls, const int *pdepth, int sweeps);
+int gs_fused_run(const GsFused &f, const DevCSR &A, const double *b, double *x, const double *d_first,
+                 const double *d_later, hipStream_t s);
+void gs_fused_free(GsFused &f);
 struct SmootherPlan;
 // Report the one-launch passes' stalls into *err (a word of the owning hierarchy).
 void smoother_set_err(SmootherPlan &sp, unsigned *err);
@@ -439,6 +460,7 @@ struct SmootherPlan {
     bool natural = false;
     double *nd_first = nullptr, *nd_later = nullptr;
     PassSchedule pass[2];      // [0] = F pass (mark != 1), [1] = C pass (mark == 1)
+    GsFused fz;                // exact GS-CF: all passes of a call in one launch (when built)
     double *d_first = nullptr; // effective divisor for the first sweep of a call
     double *d_later = nullptr; // ... for later sweeps (aliases d_first when all rows have a diagonal)
     int *cls = nullptr;        // per row: 1 if mark == 1 else 0

@@ -35,6 +35,7 @@
 #include "sss_spmv_dev.hpp"
 
 #include <algorithm>
+#include <atomic>
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
@@ -317,6 +318,205 @@ __global__ __launch_bounds__(kBlock) void gs_flow_group(int nchunks, const int *
     flow_exit(ctl, epoch, err, spin);
 }
 
+// ---- fused engine: all passes of a smoother call in one launch ---------------------------------
+// Node (i, s) is row i's update in sweep s; it produces version s + 1 of x_i (version 0: x before
+// the call).  Per sweep the F pass runs before the C pass (Solve/SSS_smooth.c:4-87, both smoother
+// directions), so the version of a neighbour j that node (i, s) reads is
+//     same class: j < i -> s + 1, j > i -> s;     j in F, i in C: s + 1;     j in C, i in F: s.
+// Version 0 is read from x (no node writes x before the last sweep); later versions from j's
+// granules, tagged epoch << 4 | version.  On a structurally symmetric level a granule holds every
+// version long enough: each reader of version v of x_j is read by j's next update (at a version
+// the reader produces), so version v + 1 cannot be published before all readers of v are done,
+// and tickets in fused-DAG depth order (every dependency one depth lower) are a topological order
+// -- the same progress argument as the per-pass flow engine.  Versions s of row i and every
+// neighbour's versions are therefore ordered before node (i, s) publishes, which overlaps the
+// tail of each pass with the head of the next (the per-pass launches wait for a whole pass).
+__device__ __forceinline__ int fused_need(int c, int i, int s, int split)
+{
+    const bool cc = c >= split, ic = i >= split;
+    return cc == ic ? (c < i ? s + 1 : s) : (cc ? s : s + 1);
+}
+
+template <int G>
+__global__ __launch_bounds__(kBlock) void gs_fused_group(int nchunks, const int *__restrict__ ck,
+                                                         const int *__restrict__ nodes, int n, int split, int last,
+                                                         const int *__restrict__ rp, const int *__restrict__ ci,
+                                                         const double *__restrict__ v, const double *__restrict__ b,
+                                                         double *x, const double *__restrict__ d_first,
+                                                         const double *__restrict__ d_later, unsigned long long *gran,
+                                                         unsigned *ctl, unsigned *err, int spin, int ovl)
+{
+    constexpr int R = 64 / G, CAP = kGroupBuf / R, U = 8;
+    static_assert(CAP / G == 32, "one pending bit per staged entry of a lane");
+    __shared__ __attribute__((aligned(16))) double buf[kBlock / 64][kGroupBuf];
+    const int lane = threadIdx.x & 63, grp = lane / G, gl = lane % G;
+    double *mine = buf[threadIdx.x >> 6] + grp * CAP;
+    const unsigned epoch = __hip_atomic_load(&ctl[kCtlEpoch], RLX_AGENT) + 1u;
+    auto tag = [&](int ver) { return (epoch << 4) | (unsigned)ver; };
+    for (;;) {
+        const int q = flow_ticket(ctl);
+        if (q >= nchunks) break;
+        const int p = ck[q] + grp;
+        const bool active = p < ck[q + 1];
+        int i = -1, s = 0, k0 = 0, len = 0;
+        double acc = 0.0, dr = 0.0;
+        if (active) {
+            const int node = nodes[p];
+            s = node / n;
+            i = node - s * n;
+            k0 = rp[i];
+            len = rp[i + 1] - k0;
+            acc = b[i];
+            dr = (s == 0 ? d_first : d_later)[i];
+        }
+        bool linked = false;   // an off-diagonal entry: some neighbour orders version s of x_i first
+        int maxlen = len;
+        for (int off = 32; off > 0; off >>= 1) maxlen = max(maxlen, __shfl_xor(maxlen, off, 64));
+        maxlen = __builtin_amdgcn_readfirstlane(maxlen);
+        for (int base = 0; base < maxlen; base += CAP) {
+            const int m = active ? min(CAP, len - base) : 0;
+            const int nj = m > gl ? (m - gl + G - 1) / G : 0;
+            const int kb = k0 + base;
+            unsigned pend = 0;
+            for (int j0 = 0; j0 < nj; j0 += U) {   // (A) stage every product whose version exists
+                int c[U], nd[U];
+                double a[U], xv[U];
+                unsigned long long ga[U], gc[U];
+#pragma unroll
+                for (int u = 0; u < U; ++u) c[u] = ci[kb + (j0 + u < nj ? gl + G * (j0 + u) : gl)];
+#pragma unroll
+                for (int u = 0; u < U; ++u) a[u] = v[kb + (j0 + u < nj ? gl + G * (j0 + u) : gl)];
+#pragma unroll
+                for (int u = 0; u < U; ++u) nd[u] = (j0 + u < nj && c[u] != i) ? fused_need(c[u], i, s, split) : -1;
+                // the group's loads issued together and read after the loop
+#pragma unroll
+                for (int u = 0; u < U; ++u) {
+                    xv[u] = 0.0;
+                    ga[u] = gc[u] = 0ull;
+                    if (nd[u] == 0) {
+                        xv[u] = x[c[u]];
+                    } else if (nd[u] > 0) {
+                        const unsigned long long *gg = gran + 2 * (size_t)c[u];
+                        ga[u] = __hip_atomic_load(const_cast<unsigned long long *>(gg), RLX_AGENT);
+                        gc[u] = __hip_atomic_load(const_cast<unsigned long long *>(gg + 1), RLX_AGENT);
+                    }
+                }
+#pragma unroll
+                for (int u = 0; u < U; ++u) {
+                    if (j0 + u >= nj) continue;
+                    double val = 0.0;   // the diagonal: subtracting +0.0 is the identity
+                    if (nd[u] == 0) {
+                        val = a[u] * xv[u];
+                    } else if (nd[u] > 0) {
+                        linked = true;
+                        const unsigned want = tag(nd[u]);
+                        if ((unsigned)(ga[u] >> 32) == want && (unsigned)(gc[u] >> 32) == want)
+                            val = a[u] * __longlong_as_double((long long)((gc[u] << 32) | (ga[u] & 0xffffffffull)));
+                        else {
+                            pend |= 1u << (j0 + u);
+                            if (ovl) val = __longlong_as_double((long long)c[u]);   // its column, until resolved
+                        }
+                    }
+                    mine[gl + G * (j0 + u)] = val;
+                }
+            }
+            if (!ovl) {
+                while (pend) {   // (B)
+                    const int j = __builtin_ctz(pend);
+                    pend &= pend - 1;
+                    const int t = gl + G * j;
+                    const int c = ci[kb + t];
+                    mine[t] = v[kb + t] * granule_wait(gran + 2 * (size_t)c, tag(fused_need(c, i, s, split)), err, spin);
+                }
+                wave_sync();
+                if (gl == 0 && m > 0) acc = chain_sub_pipe(acc, mine, 0, m);   // (C)
+                wave_sync();
+                continue;
+            }
+            // (B) and (C) interleaved as in gs_flow_group: the chain runs up to the first pending entry
+            wave_sync();
+            int k = 0, idle = 0;
+            for (;;) {
+                int first = pend ? gl + G * __builtin_ctz(pend) : CAP;
+#pragma unroll
+                for (int off = G / 2; off > 0; off >>= 1) first = min(first, __shfl_xor(first, off, 64));
+                const int lim = min(first, m);
+                constexpr int NP = 2;
+                int tp[NP];
+                unsigned want[NP];
+                unsigned long long ga[NP], gc[NP];
+                double ap[NP];
+                {
+                    unsigned qq = pend;
+#pragma unroll
+                    for (int h = 0; h < NP; ++h) {
+                        tp[h] = -1;
+                        want[h] = 0;
+                        ga[h] = gc[h] = 0;
+                        ap[h] = 0.0;
+                        if (qq) {
+                            tp[h] = gl + G * __builtin_ctz(qq);
+                            qq &= qq - 1;
+                            const int cp = (int)__double_as_longlong(mine[tp[h]]);
+                            want[h] = tag(fused_need(cp, i, s, split));
+                            const unsigned long long *gg = gran + 2 * (size_t)cp;
+                            ga[h] = __hip_atomic_load(const_cast<unsigned long long *>(gg), RLX_AGENT);
+                            gc[h] = __hip_atomic_load(const_cast<unsigned long long *>(gg + 1), RLX_AGENT);
+                            ap[h] = v[kb + tp[h]];
+                        }
+                    }
+                }
+                const bool advance = gl == 0 && k < lim;
+                if (advance) acc = chain_sub_pipe(acc, mine, k, lim);
+                if (gl == 0) k = max(k, lim);
+                bool got = false;
+#pragma unroll
+                for (int h = 0; h < NP; ++h)
+                    if (tp[h] >= 0 && (unsigned)(ga[h] >> 32) == want[h] && (unsigned)(gc[h] >> 32) == want[h]) {
+                        mine[tp[h]] = ap[h] * __longlong_as_double((long long)((gc[h] << 32) | (ga[h] & 0xffffffffull)));
+                        pend &= ~(1u << ((tp[h] - gl) / G));
+                        got = true;
+                    }
+                const bool rowdone = gl != 0 || k >= m;
+                if (__all(rowdone && !pend)) break;
+                wave_sync();
+                if (__any(got || advance)) {
+                    idle = 0;
+                } else {
+                    if (++idle >= spin || ((idle & 63) == 63 && __hip_atomic_load(err, RLX_AGENT))) {
+                        if (gl == 0) __hip_atomic_store(err, 1u, RLX_AGENT);
+                        while (pend) {
+                            mine[gl + G * __builtin_ctz(pend)] = 0.0;
+                            pend &= pend - 1;
+                        }
+                        wave_sync();
+                        if (gl == 0 && k < m) acc = chain_sub_pipe(acc, mine, k, m);
+                        if (gl == 0) k = m;
+                        break;
+                    }
+                    if (idle < 16) __builtin_amdgcn_s_sleep(1);
+                    else __builtin_amdgcn_s_sleep(8);
+                }
+            }
+            wave_sync();
+        }
+        // any lane of the row group staged an off-diagonal entry
+#pragma unroll
+        for (int off = G / 2; off > 0; off >>= 1) linked = linked || __shfl_xor((int)linked, off, 64);
+        if (active && gl == 0) {
+            unsigned long long *own = gran + 2 * (size_t)i;
+            double xn;
+            if (fabs(dr) > SMALLFLOAT) xn = acc / dr;
+            else xn = s == 0 ? x_own(x, i) : granule_wait(own, tag(s), err, spin);   // unchanged
+            // a row without neighbours is ordered after its previous update only here
+            if (s > 0 && !linked) (void)granule_wait(own, tag(s), err, spin);
+            granule_put(own, tag(s + 1), xn);
+            if (s == last) x[i] = xn;   // x holds version 0 until the last sweep
+        }
+    }
+    flow_exit(ctl, epoch, err, spin);
+}
+
 // ---- single-CU engine --------------------------------------------------------------------------
 // One workgroup of kCuWaves waves.  h_off[d] .. h_off[d+1]: positions of depth d in `rows`.
 __global__ __launch_bounds__(64 * kCuWaves) void gs_cu(int nrows, int ndepth, const int *__restrict__ rows,
@@ -540,6 +740,160 @@ void gs_persist_free(PassSchedule &ps)
     g = GsPersist();
 }
 
+// Fused plan.  Requires F rows [0, split) and C rows [split, n) (relabeled level) and a structurally
+// symmetric level (checked here; otherwise no plan and the per-pass engines run).  Fused depth:
+// fd(i, s) = 1 + max(fd(i, s - 1), fd of the version of every neighbour that node (i, s) reads),
+// computed pass by pass over each pass's own depth groups (rows of one group are independent).
+int gs_fused_build(GsFused &f, const SSS_MAT &A, const int *cls, const int *pdepth, int sweeps)
+{
+    f = GsFused();
+    const int n = A.num_rows;
+    const int *rp = A.row_ptr, *ci = A.col_idx;
+    if (n <= 0 || sweeps < 1 || sweeps > 14 || A.num_cols != n || (long long)n * sweeps >= (1ll << 31)) return 0;
+    int split = 0;
+    while (split < n && cls[split] == 0) ++split;
+    for (int i = split; i < n; ++i)
+        if (cls[i] != 1) return 0;
+    {   // structural symmetry: every off-diagonal (i, j) has (j, i)
+        std::vector<long long> off((size_t)n + 1, 0);
+        for (int i = 0; i < n; ++i) off[i + 1] = off[i] + (rp[i + 1] - rp[i]);
+        std::vector<int> cols((size_t)off[n]);
+        parallel_chunks(n, 4096, [&](int a, int e) {
+            for (int i = a; i < e; ++i) {
+                std::copy(ci + rp[i], ci + rp[i + 1], cols.begin() + off[i]);
+                std::sort(cols.begin() + off[i], cols.begin() + off[i + 1]);
+            }
+        });
+        std::atomic<bool> bad{false};
+        parallel_chunks(n, 4096, [&](int a, int e) {
+            for (int i = a; i < e && !bad; ++i)
+                for (long long t = off[i]; t < off[i + 1]; ++t) {
+                    const int j = cols[(size_t)t];
+                    if (j == i) continue;
+                    if (j < 0 || j >= n || !std::binary_search(cols.begin() + off[j], cols.begin() + off[j + 1], i)) {
+                        bad = true;
+                        break;
+                    }
+                }
+        });
+        if (bad) return 0;
+    }
+    // rows of each class grouped by their pass depth
+    int maxd[2] = {0, 0};
+    for (int i = 0; i < n; ++i) maxd[cls[i]] = std::max(maxd[cls[i]], pdepth[i] + 1);
+    std::vector<int> goff[2], grows[2];
+    for (int c = 0; c < 2; ++c) {
+        goff[c].assign((size_t)maxd[c] + 1, 0);
+        for (int i = 0; i < n; ++i)
+            if (cls[i] == c) goff[c][pdepth[i] + 1]++;
+        for (int d = 0; d < maxd[c]; ++d) goff[c][d + 1] += goff[c][d];
+        grows[c].resize((size_t)goff[c][maxd[c]]);
+        std::vector<int> fill(goff[c].begin(), goff[c].end() - 1);
+        for (int i = 0; i < n; ++i)
+            if (cls[i] == c) grows[c][(size_t)fill[pdepth[i]]++] = i;
+    }
+    std::vector<int> fd((size_t)n * sweeps, 0);   // fd[s * n + i]
+    auto ver_depth = [&](int j, int ver) { return ver == 0 ? 0 : fd[(size_t)(ver - 1) * n + j]; };
+    for (int s = 0; s < sweeps; ++s)
+        for (int c = 0; c < 2; ++c)
+            for (int d = 0; d < maxd[c]; ++d)
+                parallel_chunks(goff[c][d + 1] - goff[c][d], 2048, [&](int a, int e) {
+                    for (int q = goff[c][d] + a; q < goff[c][d] + e; ++q) {
+                        const int i = grows[c][(size_t)q];
+                        int dep = s > 0 ? fd[(size_t)(s - 1) * n + i] : 0;
+                        for (int k = rp[i]; k < rp[i + 1]; ++k) {
+                            const int j = ci[k];
+                            if (j != i) {
+                                const int need = (cls[j] == cls[i]) ? (j < i ? s + 1 : s) : (cls[j] ? s : s + 1);
+                                dep = std::max(dep, ver_depth(j, need));
+                            }
+                        }
+                        fd[(size_t)s * n + i] = dep + 1;
+                    }
+                });
+    int depth = 0;
+    for (int x : fd) depth = std::max(depth, x);
+    std::vector<int> doff((size_t)depth + 2, 0);
+    for (int x : fd) doff[(size_t)x]++;
+    for (int d = 0; d <= depth; ++d) doff[(size_t)d + 1] += doff[(size_t)d];
+    std::vector<int> order(fd.size());
+    {
+        std::vector<int> fill(doff.begin(), doff.end() - 1);
+        for (size_t t = 0; t < fd.size(); ++t) order[(size_t)fill[(size_t)fd[t] - 1]++] = (int)t;
+    }
+    long long nnz = rp[n];
+    const double avg = (double)nnz / n;
+    f.G = avg <= 24 ? 4 : avg <= 48 ? 8 : avg <= 96 ? 16 : avg <= 192 ? 32 : 64;
+    f.overlap = avg >= 300;
+    const int R = 64 / f.G;
+    std::vector<int> ck;
+    for (int d = 0; d < depth; ++d)
+        for (int s0 = doff[(size_t)d]; s0 < doff[(size_t)d + 1]; s0 += R) ck.push_back(s0);
+    ck.push_back((int)order.size());
+    f.nchunks = (int)ck.size() - 1;
+    f.depth = depth;
+    f.sweeps = sweeps;
+    f.n = n;
+    f.split = split;
+    f.spin = kFlowSpinLimit;
+    if (const char *sp = getenv("SSS_HIP_GS_SPIN")) f.spin = atoi(sp);
+    f.ck = dev_alloc<int>(ck.size());
+    f.nodes = dev_alloc<int>(order.size());
+    f.gran = dev_alloc<unsigned long long>(2 * (size_t)n);
+    f.ctl = dev_alloc<unsigned>(kCtlWords);
+    if (!f.ck || !f.nodes || !f.gran || !f.ctl) {
+        gs_fused_free(f);
+        return hip_fail(hipErrorOutOfMemory, "hipMalloc(gs fused)", __FILE__, __LINE__);
+    }
+    SSS_HIP(hipMemcpy(f.ck, ck.data(), sizeof(int) * ck.size(), hipMemcpyHostToDevice));
+    SSS_HIP(hipMemcpy(f.nodes, order.data(), sizeof(int) * order.size(), hipMemcpyHostToDevice));
+    SSS_HIP(hipMemset(f.gran, 0, sizeof(unsigned long long) * 2 * (size_t)n));
+    SSS_HIP(hipMemset(f.ctl, 0, sizeof(unsigned) * kCtlWords));
+    f.err = f.ctl + kCtlErr;
+    int cus = 256;
+    {
+        int dev = 0;
+        hipDeviceProp_t prop;
+        if (hipGetDevice(&dev) == hipSuccess && hipGetDeviceProperties(&prop, dev) == hipSuccess)
+            cus = prop.multiProcessorCount;
+    }
+    const double per_depth = (double)f.nchunks / std::max(1, depth);
+    int waves = (int)std::min<double>(1024.0, std::max(32.0, 4.0 * per_depth));
+    waves = std::min(waves, std::min(f.nchunks, cus * 8));
+    f.grid = std::max(1, (waves + 3) / 4);
+    f.engine = 1;
+    return 0;
+}
+
+void gs_fused_free(GsFused &f)
+{
+    dev_free(f.ck);
+    dev_free(f.nodes);
+    dev_free(f.gran);
+    dev_free(f.ctl);
+    f = GsFused();
+}
+
+int gs_fused_run(const GsFused &f, const DevCSR &A, const double *b, double *x, const double *d_first,
+                 const double *d_later, hipStream_t s)
+{
+    if (!f.engine) return ERROR_INPUT_PAR;
+    auto go = [&](auto kern) {
+        hipLaunchKernelGGL(kern, dim3(f.grid), dim3(kBlock), 0, s, f.nchunks, f.ck, f.nodes, f.n, f.split,
+                           f.sweeps - 1, A.rp, A.ci, A.v, b, x, d_first, d_later, f.gran, f.ctl, f.err, f.spin,
+                           f.overlap ? 1 : 0);
+    };
+    switch (f.G) {
+    case 4: go(gs_fused_group<4>); break;
+    case 8: go(gs_fused_group<8>); break;
+    case 16: go(gs_fused_group<16>); break;
+    case 32: go(gs_fused_group<32>); break;
+    default: go(gs_fused_group<64>); break;
+    }
+    SSS_HIP(hipGetLastError());
+    return 0;
+}
+
 
 // Diagnostic builds only (make EXTRA=-DSSS_GS_TRACE): each flow pass writes its rows' stamps to a
 // buffer that gs_trace_dump appends, with the pass's depth offsets, to $SSS_GS_TRACE_FILE.
@@ -628,6 +982,7 @@ void smoother_set_err(SmootherPlan &sp, unsigned *err)
 {
     for (auto &ps : sp.pass)
         if (ps.gp.engine && err) ps.gp.err = err;
+    if (sp.fz.engine && err) sp.fz.err = err;
 }
 
 // the error word as a double (1.0 if any pass of the hierarchy stalled since the last read, else

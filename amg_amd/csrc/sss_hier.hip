@@ -1314,11 +1314,13 @@ extern "C" int sss_hip_level_info_get(sss_hip_hier *h, int level, sss_hip_level_
     out->dag_c = L.sm.pass[1].depth;
     out->smoother_kind = L.sm.kind;
     out->inner = L.sm.inner;
-    out->gs_engine_f = L.sm.pass[0].gp.engine;
-    out->gs_engine_c = L.sm.pass[1].gp.engine;
-    unsigned ef = 0, ec = 0;
+    out->gs_engine_f = L.sm.fz.engine ? 3 : L.sm.pass[0].gp.engine;   // 3: all passes in one launch
+    out->gs_engine_c = L.sm.fz.engine ? 3 : L.sm.pass[1].gp.engine;
+    unsigned ef = 0, ec = 0, ez = 0;
     if (gs_persist_error(L.sm.pass[0], &ef) || gs_persist_error(L.sm.pass[1], &ec)) return ERROR_MISC;
-    out->gs_stall = (int)(ef | ec);
+    if (L.sm.fz.err && hipMemcpy(&ez, L.sm.fz.err, sizeof(unsigned), hipMemcpyDeviceToHost) != hipSuccess)
+        return ERROR_MISC;
+    out->gs_stall = (int)(ef | ec | ez);
     auto fmt = [](const DevCSR &M) {
         return (M.pk ? 1 : 0) | (has_dict(M) ? 2 : 0) | (M.vec_rows ? 4 : 0) | (M.mg_G ? 8 : 0) | (M.wave_rows ? 16 : 0) |
                (M.dv_ell ? 64 : 0) | (M.dv_xell ? 128 : 0);

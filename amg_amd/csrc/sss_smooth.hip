@@ -226,6 +226,14 @@ int smoother_build(SmootherPlan &sp, const SSS_MAT &A, const int *mark, int kind
             if (contiguous && (rc = gs_persist_build(ps, A, lo, hi, sp.long_rows))) return rc;
         }
     }
+    {   // every pass of a call in one launch (exact GS-CF, both passes on the flow engine; 2 sweeps,
+        // SSS_amg_pars_init's pre/post count)
+        const char *fe = getenv("SSS_HIP_GS_FUSED");   // 0: per-pass launches (tests compare both)
+        if (!(fe && *fe == '0') && kind == SSS_HIP_SMOOTH_EXACT && !gcls && A.num_cols == n && mark &&
+            sp.pass[0].gp.engine == 1 && sp.pass[1].gp.engine == 1 &&
+            (rc = gs_fused_build(sp.fz, A, cls.data(), depth.data(), 2)))
+            return rc;
+    }
     t_persist = now();
     if (kind == SSS_HIP_SMOOTH_JACOBI && inner > 0 && sp.pass[0].range == (sp.pass[0].nrows > 0) &&
         sp.pass[1].range == (sp.pass[1].nrows > 0)) {
@@ -379,6 +387,7 @@ void smoother_free(SmootherPlan &sp)
         dev_free(ps.ts_P);
         gs_persist_free(ps);
     }
+    gs_fused_free(sp.fz);
     if (sp.d_later != sp.d_first) dev_free(sp.d_later);
     dev_free(sp.d_first);
     dev_free(sp.nd_first);
@@ -1329,6 +1338,11 @@ int smoother_run(const SmootherPlan &sp, const DevCSR &A, const double *b, doubl
     }
     if (rf) rf->done = false;
     if (pre_f && (!sp.pend_ok || hk || sweeps < 1)) return ERROR_INPUT_PAR;
+    if (sp.fz.engine && sweeps == sp.fz.sweeps && !hk && !pre_f) {
+        for (int sw = 0; sw < sweeps; ++sw)
+            for (const auto &ps : sp.pass) ledger_pass(A, ps, 24.0);
+        return gs_fused_run(sp.fz, A, b, x, sp.d_first, sp.d_later, s);
+    }
     const int n = A.n;
     if (n == 0) return 0;
     int rc;

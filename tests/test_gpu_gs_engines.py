@@ -20,7 +20,13 @@ from conftest import build_hierarchy, oracle_solve, vec
 
 pytestmark = pytest.mark.gpu
 
-ENGINES = {"launch": 0, "flow": 1, "cu": 2}
+# "fused": the flow engine with every pass of a smoother call in one launch (level_info reports 3)
+ENGINES = {"launch": 0, "flow": 1, "cu": 2, "fused": 3}
+
+
+def _set_engine(mp, name):
+    mp.setenv("SSS_HIP_GS_ENGINE", "flow" if name == "fused" else name)
+    mp.setenv("SSS_HIP_GS_FUSED", "1" if name == "fused" else "0")
 
 
 @pytest.fixture(scope="module")
@@ -45,7 +51,7 @@ def p64_h(quiet):
 
 @pytest.fixture(params=list(ENGINES))
 def engine(request, monkeypatch):
-    monkeypatch.setenv("SSS_HIP_GS_ENGINE", request.param)
+    _set_engine(monkeypatch, request.param)
     return request.param
 
 
@@ -70,9 +76,12 @@ def _check_engines(D, H, engine):
         for e, depth in ((info.gs_engine_f, info.dag_f), (info.gs_engine_c, info.dag_c)):
             if depth > 1:
                 used.add(e)
-    if engine != "launch":
+    if engine == "fused":   # a level whose passes are not both flow passes keeps them
+        assert used <= {0, 1, 3}
+    elif engine != "launch":
         assert used <= {0, ENGINES[engine]}
         assert ENGINES[engine] in used or not used
+    return used
 
 
 @pytest.mark.parametrize("hname", ["bus_h", "p32_h", "a27_h"])
@@ -129,7 +138,7 @@ def test_repeated_launches_stay_bitwise(p32_h, monkeypatch):
     n = p32_h.level(0).A.num_rows
     out = {}
     for eng in ENGINES:
-        monkeypatch.setenv("SSS_HIP_GS_ENGINE", eng)
+        _set_engine(monkeypatch, eng)
         D = A.DeviceHierarchy(p32_h, smoother="exact", coarse="direct")
         try:
             D.upload(0, "b", np.ones(n))
@@ -137,10 +146,12 @@ def test_repeated_launches_stay_bitwise(p32_h, monkeypatch):
             for _ in range(12):
                 D.cycle()
             out[eng] = D.download(0, "x")
-            _check_engines(D, p32_h, eng)
+            used = _check_engines(D, p32_h, eng)
+            if eng == "fused":
+                assert 3 in used, used
         finally:
             D.close()
-    for eng in ("flow", "cu"):
+    for eng in ("flow", "cu", "fused"):
         assert np.array_equal(out[eng].view(np.uint64), out["launch"].view(np.uint64)), eng
 
 

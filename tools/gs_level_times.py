@@ -1,6 +1,6 @@
 """Lab tool (GPU box): time the exact GS-CF pre-smoother (2 sweeps) of every level per engine.
 
-    python tools/gs_level_times.py --n 256 --engines launch,flow,cu [--reps 3]
+    python tools/gs_level_times.py --n 256 --engines launch,flow,fused,cu [--reps 3]
 
 Prints one line per (engine, level): rows, F/C depth, chosen engines, ms per smoother call.
 """
@@ -38,7 +38,8 @@ def main():
     levels = [int(x) for x in a.levels.split(",")] if a.levels else list(range(1, H.num_levels - 1))
     out = []
     for eng in a.engines.split(","):
-        os.environ["SSS_HIP_GS_ENGINE"] = eng
+        os.environ["SSS_HIP_GS_ENGINE"] = "flow" if eng == "fused" else eng   # fused: all passes in one launch
+        os.environ["SSS_HIP_GS_FUSED"] = "1" if eng == "fused" else "0"
         D = A.DeviceHierarchy(H, smoother="exact", coarse="direct", device=0)
         rng = np.random.default_rng(1)
         for l in levels:
