@@ -606,6 +606,40 @@ __global__ __launch_bounds__(64 * kCuWaves) void gs_cu(int nrows, int ndepth, co
 }
 
 // ---- planning ----------------------------------------------------------------------------------
+// Structural symmetry of the entries (i, j), i in [r0, r1), j != i, that keep(i, j) selects: every
+// such (i, j) has its (j, i).  One streaming pass (no per-row sort, no lookups in other rows): the
+// sums over entries of sign(j - i) * H(min(i, j), max(i, j)) for two independent 64-bit mixes H
+// vanish (mod 2^64) for a symmetric pattern and, for an unsymmetric one, only by a collision of
+// probability ~2^-128.  Even then nothing is silent: the one-launch engines rely on the symmetry
+// for progress, and a pass that waits for a value never published gives up and reports a stall.
+static inline unsigned long long mix64(unsigned long long z)
+{
+    z += 0x9e3779b97f4a7c15ull;
+    z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
+    z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
+    return z ^ (z >> 31);
+}
+template <class Keep>
+static bool pattern_symmetric(const int *rp, const int *ci, int r0, int r1, Keep keep)
+{
+    std::atomic<unsigned long long> h1{0}, h2{0};
+    parallel_chunks(r1 - r0, 1 << 14, [&](int a, int e) {
+        unsigned long long s1 = 0, s2 = 0;
+        for (int i = r0 + a; i < r0 + e; ++i)
+            for (int k = rp[i]; k < rp[i + 1]; ++k) {
+                const int j = ci[k];
+                if (j == i || !keep(i, j)) continue;
+                const unsigned long long key = ((unsigned long long)(unsigned)std::min(i, j) << 32) | (unsigned)std::max(i, j);
+                const unsigned long long u1 = mix64(key), u2 = mix64(key ^ 0x5851f42d4c957f2dull);
+                if (j > i) s1 += u1, s2 += u2;
+                else s1 -= u1, s2 -= u2;
+            }
+        h1 += s1;
+        h2 += s2;
+    });
+    return h1.load() == 0 && h2.load() == 0;
+}
+
 static const char *gs_engine_env()
 {
     const char *e = getenv("SSS_HIP_GS_ENGINE");
@@ -636,36 +670,7 @@ int gs_persist_build(PassSchedule &ps, const SSS_MAT &A, int lo, int hi, bool lo
     if (engine == 2 && ps.depth > kCuMaxDepth) engine = 1;
     if (engine == 1) {
         // the flow engine needs every same-class coupling in both directions (see the header)
-        bool sym = true;
-        // each row's same-class columns, sorted, then every coupling looked up in its partner row
-        const int m = hi - lo;
-        std::vector<long long> off((size_t)m + 1, 0);
-        for (int q = 0; q < m; ++q) {
-            long long c = 0;
-            for (int k = rp[lo + q]; k < rp[lo + q + 1]; ++k) c += (ci[k] >= lo && ci[k] < hi && ci[k] != lo + q);
-            off[q + 1] = off[q] + c;
-        }
-        std::vector<int> cols((size_t)off[m]);
-        parallel_chunks(m, 4096, [&](int a, int e) {
-            for (int q = a; q < e; ++q) {
-                long long o = off[q];
-                for (int k = rp[lo + q]; k < rp[lo + q + 1]; ++k)
-                    if (ci[k] >= lo && ci[k] < hi && ci[k] != lo + q) cols[(size_t)o++] = ci[k];
-                std::sort(cols.begin() + off[q], cols.begin() + off[q + 1]);
-            }
-        });
-        std::vector<char> bad(1, 0);
-        parallel_chunks(m, 4096, [&](int a, int e) {
-            for (int q = a; q < e && !bad[0]; ++q)
-                for (long long t = off[q]; t < off[q + 1]; ++t) {
-                    const int j = cols[(size_t)t] - lo;
-                    if (!std::binary_search(cols.begin() + off[j], cols.begin() + off[j + 1], lo + q)) {
-                        bad[0] = 1;
-                        break;
-                    }
-                }
-        });
-        sym = !bad[0];
+        const bool sym = pattern_symmetric(rp, ci, lo, hi, [&](int, int j) { return j >= lo && j < hi; });
         if (!sym) {
             // the single-CU engine divides by the stale GS-CF divisor; a natural-order pass
             // multiplies by the carried reciprocal (Solve/SSS_smooth.c:112), so it keeps the
@@ -740,11 +745,39 @@ void gs_persist_free(PassSchedule &ps)
     g = GsPersist();
 }
 
+// Fused depth of the nodes of one pass-depth group (rows of one class, one depth of its own pass:
+// independent of each other): fd(i, s) = 1 + max(fd(i, s - 1), fd of each version node (i, s) reads).
+// G lanes per row.
+template <int G>
+__global__ __launch_bounds__(kBlock) void fused_depth_group(int cnt, const int *__restrict__ grows,
+                                                            const int *__restrict__ rp, const int *__restrict__ ci,
+                                                            int n, int split, int s, int *fd)
+{
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    const int r = t / G, gl = t % G;
+    int dep = 0, i = -1;
+    if (r < cnt) {
+        i = grows[r];
+        if (gl == 0 && s > 0) dep = fd[(size_t)(s - 1) * n + i];
+        for (int k = rp[i] + gl; k < rp[i + 1]; k += G) {
+            const int j = ci[k];
+            if (j == i) continue;
+            const int need = fused_need(j, i, s, split);
+            if (need > 0) dep = max(dep, fd[(size_t)(need - 1) * n + j]);
+        }
+    }
+#pragma unroll
+    for (int off = G / 2; off > 0; off >>= 1) dep = max(dep, __shfl_xor(dep, off, 64));
+    if (r < cnt && gl == 0) fd[(size_t)s * n + i] = dep + 1;
+}
+
 // Fused plan.  Requires F rows [0, split) and C rows [split, n) (relabeled level) and a structurally
 // symmetric level (checked here; otherwise no plan and the per-pass engines run).  Fused depth:
 // fd(i, s) = 1 + max(fd(i, s - 1), fd of the version of every neighbour that node (i, s) reads),
-// computed pass by pass over each pass's own depth groups (rows of one group are independent).
-int gs_fused_build(GsFused &f, const SSS_MAT &A, const int *cls, const int *pdepth, int sweeps)
+// computed pass by pass over each pass's own depth groups (rows of one group are independent) --
+// on the GPU over the uploaded level (dA) and the passes' depth-ordered rows, else on the host.
+int gs_fused_build(GsFused &f, const SSS_MAT &A, const DevCSR *dA, const PassSchedule *pass, const int *cls,
+                   const int *pdepth, int sweeps)
 {
     f = GsFused();
     const int n = A.num_rows;
@@ -754,63 +787,70 @@ int gs_fused_build(GsFused &f, const SSS_MAT &A, const int *cls, const int *pdep
     while (split < n && cls[split] == 0) ++split;
     for (int i = split; i < n; ++i)
         if (cls[i] != 1) return 0;
-    {   // structural symmetry: every off-diagonal (i, j) has (j, i)
-        std::vector<long long> off((size_t)n + 1, 0);
-        for (int i = 0; i < n; ++i) off[i + 1] = off[i] + (rp[i + 1] - rp[i]);
-        std::vector<int> cols((size_t)off[n]);
-        parallel_chunks(n, 4096, [&](int a, int e) {
-            for (int i = a; i < e; ++i) {
-                std::copy(ci + rp[i], ci + rp[i + 1], cols.begin() + off[i]);
-                std::sort(cols.begin() + off[i], cols.begin() + off[i + 1]);
-            }
-        });
-        std::atomic<bool> bad{false};
-        parallel_chunks(n, 4096, [&](int a, int e) {
-            for (int i = a; i < e && !bad; ++i)
-                for (long long t = off[i]; t < off[i + 1]; ++t) {
-                    const int j = cols[(size_t)t];
-                    if (j == i) continue;
-                    if (j < 0 || j >= n || !std::binary_search(cols.begin() + off[j], cols.begin() + off[j + 1], i)) {
-                        bad = true;
-                        break;
+    if (!pattern_symmetric(rp, ci, 0, n, [&](int, int j) { return j >= 0 && j < n; })) return 0;
+    const long long nnz = rp[n];
+    const double avg = (double)nnz / n;
+    f.G = avg <= 24 ? 4 : avg <= 48 ? 8 : avg <= 96 ? 16 : avg <= 192 ? 32 : 64;
+    std::vector<int> fd((size_t)n * sweeps, 0);   // fd[s * n + i]
+    if (dA && dA->rp && dA->ci && dA->n == n && pass[0].rows && pass[1].rows) {
+        int *d_fd = dev_alloc<int>(fd.size());
+        if (!d_fd) return hip_fail(hipErrorOutOfMemory, "hipMalloc(fused depth)", __FILE__, __LINE__);
+        auto go = [&](auto kern, int cnt, const int *grows, int sw) {
+            const long long threads = (long long)cnt * f.G;
+            hipLaunchKernelGGL(kern, dim3((unsigned)((threads + kBlock - 1) / kBlock)), dim3(kBlock), 0, nullptr, cnt,
+                               grows, dA->rp, dA->ci, n, split, sw, d_fd);
+        };
+        for (int sw = 0; sw < sweeps; ++sw)
+            for (int c = 0; c < 2; ++c)
+                for (int d = 0; d < pass[c].depth; ++d) {
+                    const int cnt = pass[c].h_off[d + 1] - pass[c].h_off[d];
+                    const int *grows = pass[c].rows + pass[c].h_off[d];
+                    if (cnt <= 0) continue;
+                    switch (f.G) {
+                    case 4: go(fused_depth_group<4>, cnt, grows, sw); break;
+                    case 8: go(fused_depth_group<8>, cnt, grows, sw); break;
+                    case 16: go(fused_depth_group<16>, cnt, grows, sw); break;
+                    case 32: go(fused_depth_group<32>, cnt, grows, sw); break;
+                    default: go(fused_depth_group<64>, cnt, grows, sw); break;
                     }
                 }
-        });
-        if (bad) return 0;
-    }
-    // rows of each class grouped by their pass depth
-    int maxd[2] = {0, 0};
-    for (int i = 0; i < n; ++i) maxd[cls[i]] = std::max(maxd[cls[i]], pdepth[i] + 1);
-    std::vector<int> goff[2], grows[2];
-    for (int c = 0; c < 2; ++c) {
-        goff[c].assign((size_t)maxd[c] + 1, 0);
-        for (int i = 0; i < n; ++i)
-            if (cls[i] == c) goff[c][pdepth[i] + 1]++;
-        for (int d = 0; d < maxd[c]; ++d) goff[c][d + 1] += goff[c][d];
-        grows[c].resize((size_t)goff[c][maxd[c]]);
-        std::vector<int> fill(goff[c].begin(), goff[c].end() - 1);
-        for (int i = 0; i < n; ++i)
-            if (cls[i] == c) grows[c][(size_t)fill[pdepth[i]]++] = i;
-    }
-    std::vector<int> fd((size_t)n * sweeps, 0);   // fd[s * n + i]
-    auto ver_depth = [&](int j, int ver) { return ver == 0 ? 0 : fd[(size_t)(ver - 1) * n + j]; };
-    for (int s = 0; s < sweeps; ++s)
-        for (int c = 0; c < 2; ++c)
-            for (int d = 0; d < maxd[c]; ++d)
-                parallel_chunks(goff[c][d + 1] - goff[c][d], 2048, [&](int a, int e) {
-                    for (int q = goff[c][d] + a; q < goff[c][d] + e; ++q) {
-                        const int i = grows[c][(size_t)q];
-                        int dep = s > 0 ? fd[(size_t)(s - 1) * n + i] : 0;
-                        for (int k = rp[i]; k < rp[i + 1]; ++k) {
-                            const int j = ci[k];
-                            if (j != i) {
-                                const int need = (cls[j] == cls[i]) ? (j < i ? s + 1 : s) : (cls[j] ? s : s + 1);
-                                dep = std::max(dep, ver_depth(j, need));
+        const hipError_t e1 = hipGetLastError();
+        const hipError_t e2 = hipMemcpy(fd.data(), d_fd, sizeof(int) * fd.size(), hipMemcpyDeviceToHost);
+        dev_free(d_fd);
+        if (e1 != hipSuccess) return hip_fail(e1, "fused_depth_group", __FILE__, __LINE__);
+        if (e2 != hipSuccess) return hip_fail(e2, "hipMemcpy(fused depth)", __FILE__, __LINE__);
+    } else {
+        // rows of each class grouped by their pass depth
+        int maxd[2] = {0, 0};
+        for (int i = 0; i < n; ++i) maxd[cls[i]] = std::max(maxd[cls[i]], pdepth[i] + 1);
+        std::vector<int> goff[2], grows[2];
+        for (int c = 0; c < 2; ++c) {
+            goff[c].assign((size_t)maxd[c] + 1, 0);
+            for (int i = 0; i < n; ++i)
+                if (cls[i] == c) goff[c][pdepth[i] + 1]++;
+            for (int d = 0; d < maxd[c]; ++d) goff[c][d + 1] += goff[c][d];
+            grows[c].resize((size_t)goff[c][maxd[c]]);
+            std::vector<int> fill(goff[c].begin(), goff[c].end() - 1);
+            for (int i = 0; i < n; ++i)
+                if (cls[i] == c) grows[c][(size_t)fill[pdepth[i]]++] = i;
+        }
+        for (int sw = 0; sw < sweeps; ++sw)
+            for (int c = 0; c < 2; ++c)
+                for (int d = 0; d < maxd[c]; ++d)
+                    parallel_chunks(goff[c][d + 1] - goff[c][d], 2048, [&](int a, int e) {
+                        for (int q = goff[c][d] + a; q < goff[c][d] + e; ++q) {
+                            const int i = grows[c][(size_t)q];
+                            int dep = sw > 0 ? fd[(size_t)(sw - 1) * n + i] : 0;
+                            for (int k = rp[i]; k < rp[i + 1]; ++k) {
+                                const int j = ci[k];
+                                if (j == i) continue;
+                                const int need = (cls[j] == cls[i]) ? (j < i ? sw + 1 : sw) : (cls[j] ? sw : sw + 1);
+                                if (need > 0) dep = std::max(dep, fd[(size_t)(need - 1) * n + j]);
                             }
+                            fd[(size_t)sw * n + i] = dep + 1;
                         }
-                        fd[(size_t)s * n + i] = dep + 1;
-                    }
-                });
+                    });
+    }
     int depth = 0;
     for (int x : fd) depth = std::max(depth, x);
     std::vector<int> doff((size_t)depth + 2, 0);
@@ -821,9 +861,6 @@ int gs_fused_build(GsFused &f, const SSS_MAT &A, const int *cls, const int *pdep
         std::vector<int> fill(doff.begin(), doff.end() - 1);
         for (size_t t = 0; t < fd.size(); ++t) order[(size_t)fill[(size_t)fd[t] - 1]++] = (int)t;
     }
-    long long nnz = rp[n];
-    const double avg = (double)nnz / n;
-    f.G = avg <= 24 ? 4 : avg <= 48 ? 8 : avg <= 96 ? 16 : avg <= 192 ? 32 : 64;
     f.overlap = avg >= 300;
     const int R = 64 / f.G;
     std::vector<int> ck;

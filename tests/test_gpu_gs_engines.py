@@ -443,3 +443,81 @@ def test_stall_exits_drop_in_cli(tmp_path):
     rows = [l for l in r.stdout.splitlines() if l[:6].strip().isdigit() and "|" in l]
     assert len(rows) <= 1, rows   # only the iteration-0 row
     assert "AMG solve time" not in r.stdout
+
+
+# ---------------------------------------------------------------- fused engine edge cases
+def _sym_two_class(n: int, nf: int, seed: int):
+    """Structurally symmetric random operator with F rows [0, nf) and C rows [nf, n) (the relabeled
+    layout the one-launch engines need), couplings inside and across the classes, rows without a
+    diagonal (stale divisor, Solve/SSS_smooth.c:30,46), a zero diagonal (|d| <= 1e-20: x_i kept)
+    and a row with no off-diagonal entry at all."""
+    rng = np.random.default_rng(seed)
+    cols = [set() for _ in range(n)]
+    for i in range(n):
+        for j in rng.integers(0, n, 5).tolist():
+            if j != i and i != 11 and j != 11:
+                cols[i].add(j)
+                cols[j].add(i)
+    rp, ci, v = [0], [], []
+    for i in range(n):
+        ent = sorted(cols[i] | ({i} if i % 7 else set()))
+        for c in ent:
+            ci.append(c)
+            v.append((0.0 if i == 40 else 6.0 + rng.random()) if c == i else -0.4 * rng.random() - 0.1)
+        rp.append(len(ci))
+    mark = np.array([0] * nf + [1] * (n - nf), np.int32)
+    return A.NumpyCSR(np.array(rp), np.array(ci), np.array(v)), mark
+
+
+@pytest.mark.parametrize("fused", ["0", "1"])
+def test_fused_engine_edge_rows_bitwise(fused, monkeypatch):
+    """Host smoother entry (no uploaded level: the fused depth is computed on the host) over a
+    relabeled two-class operator with missing and zero diagonals and an isolated row: 1, 2 and 3
+    sweeps (the fused plan serves the 2-sweep calls), both directions, bitwise the oracle."""
+    monkeypatch.setenv("SSS_HIP_GS_ENGINE", "flow")
+    monkeypatch.setenv("SSS_HIP_GS_FUSED", fused)
+    ora = oracle.load()
+    M, mark = _sym_two_class(600, 350, 9)
+    n = M.mat.num_rows
+    rng = np.random.default_rng(17)
+    for sweeps in (1, 2, 3):
+        for post in (False, True):
+            b = rng.standard_normal(n)
+            x0 = rng.standard_normal(n)
+            xg, xr = x0.copy(), x0.copy()
+            sg = _smtr(M.mat, b, xg, mark.ctypes.data_as(C.POINTER(C.c_int)), sweeps, post)
+            sr = _smtr(M.mat, b, xr, mark.ctypes.data_as(C.POINTER(C.c_int)), sweeps, post)
+            assert A.lib().sss_hip_host_smooth(C.byref(sg), int(post)) == 0
+            (ora.ora_smoother_post if post else ora.ora_smoother_pre)(C.byref(sr))
+            assert np.array_equal(xg.view(np.uint64), xr.view(np.uint64)), (sweeps, post, fused)
+
+
+def test_fused_engine_used_and_matches_per_pass(p64_h, monkeypatch):
+    """On 7-pt 64^3 every level whose two passes are flow passes runs fused (level_info 3/3), and a
+    V-cycle sequence gives the per-pass engine's iterate and residual norms bit for bit."""
+    n = p64_h.level(0).A.num_rows
+    out = {}
+    for fused in ("0", "1"):
+        monkeypatch.setenv("SSS_HIP_GS_ENGINE", "flow")
+        monkeypatch.setenv("SSS_HIP_GS_FUSED", fused)
+        D = A.DeviceHierarchy(p64_h, smoother="exact", coarse="krylov")
+        try:
+            eng = [(D.level_info(l).gs_engine_f, D.level_info(l).gs_engine_c) for l in range(p64_h.num_levels - 1)]
+            D.upload(0, "b", np.ones(n))
+            D.upload(0, "x", np.ones(n))
+            rel = []
+            for _ in range(5):
+                D.cycle()
+                rel.append(D.residual_norm())
+            out[fused] = (D.download(0, "x"), rel, eng)
+            assert all(D.level_info(l).gs_stall == 0 for l in range(p64_h.num_levels - 1))
+        finally:
+            D.close()
+    assert any(e == (3, 3) for e in out["1"][2]), out["1"][2]
+    assert all(e != (3, 3) for e in out["0"][2])
+    for e0, e1 in zip(out["0"][2], out["1"][2]):
+        assert e1 == (3, 3) or e1 == e0
+        if e0 == (1, 1):
+            assert e1 == (3, 3)
+    assert np.array_equal(out["0"][0].view(np.uint64), out["1"][0].view(np.uint64))
+    assert out["0"][1] == out["1"][1]
