@@ -862,6 +862,11 @@ int gs_fused_build(GsFused &f, const SSS_MAT &A, const DevCSR *dA, const PassSch
         for (size_t t = 0; t < fd.size(); ++t) order[(size_t)fill[(size_t)fd[t] - 1]++] = (int)t;
     }
     f.overlap = avg >= 300;
+    // the levels of the shortest rows are bound by the ticket counter's atomic throughput (one
+    // ticket per chunk of 64 / G rows): two lanes per row there (7-pt 256^3 level 1, 18.9 entries
+    // per row: 13.3 ms per 2-sweep call at G = 4, 9.4 at G = 2, 14.0 at G = 1; level 2, 34.7 per
+    // row: 5.6 ms at G = 8, 6.6 at G = 4, 9.6 at G = 2 -- profiles/r05_gs_fused/)
+    if (avg <= 24) f.G = 2;
     const int R = 64 / f.G;
     std::vector<int> ck;
     for (int d = 0; d < depth; ++d)
@@ -921,7 +926,7 @@ int gs_fused_run(const GsFused &f, const DevCSR &A, const double *b, double *x, 
                            f.overlap ? 1 : 0);
     };
     switch (f.G) {
-    case 4: go(gs_fused_group<4>); break;
+    case 2: go(gs_fused_group<2>); break;
     case 8: go(gs_fused_group<8>); break;
     case 16: go(gs_fused_group<16>); break;
     case 32: go(gs_fused_group<32>); break;

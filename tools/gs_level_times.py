@@ -38,6 +38,11 @@ def main():
     levels = [int(x) for x in a.levels.split(",")] if a.levels else list(range(1, H.num_levels - 1))
     out = []
     for eng in a.engines.split(","):
+        lab = ""
+        if "+" in eng:   # lab: engine+VAR=VALUE sets an environment variable for that engine's run
+            eng, lab = eng.split("+", 1)
+            k, v = lab.split("=", 1)
+            os.environ[k] = v
         os.environ["SSS_HIP_GS_ENGINE"] = "flow" if eng == "fused" else eng   # fused: all passes in one launch
         os.environ["SSS_HIP_GS_FUSED"] = "1" if eng == "fused" else "0"
         D = A.DeviceHierarchy(H, smoother="exact", coarse="direct", device=0)
@@ -55,14 +60,16 @@ def main():
                 D.sync()
                 ts.append(time.perf_counter() - t1)
             info = D.level_info(l)
-            rec = {"engine": eng, "level": l, "rows": n, "nnz": H.level(l).A.num_nnzs, "dag_f": info.dag_f,
+            rec = {"engine": eng + ("+" + lab if lab else ""), "level": l, "rows": n, "nnz": H.level(l).A.num_nnzs, "dag_f": info.dag_f,
                    "dag_c": info.dag_c, "eng_f": info.gs_engine_f, "eng_c": info.gs_engine_c,
                    "stall": info.gs_stall, "ms": float(np.median(ts) * 1e3)}
             out.append(rec)
-            print(f"[gs] {eng:6s} L{l} rows {n:9d} nnz/row {rec['nnz'] / n:7.1f} depth F/C {info.dag_f:5d}/{info.dag_c:5d} "
+            print(f"[gs] {rec['engine']:6s} L{l} rows {n:9d} nnz/row {rec['nnz'] / n:7.1f} depth F/C {info.dag_f:5d}/{info.dag_c:5d} "
                   f"eng {info.gs_engine_f}/{info.gs_engine_c} stall {info.gs_stall}  {rec['ms']:9.2f} ms", file=sys.stderr,
                   flush=True)
         D.close()
+        if lab:
+            os.environ.pop(lab.split("=", 1)[0], None)
     if a.json:
         Path(a.json).write_text(json.dumps(out))
 
