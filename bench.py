@@ -669,6 +669,7 @@ def main():
     # the drop-in default (parity mode) on the same problem: V-cycles/s of the engine whose x is
     # bitwise the reference's after every cycle
     parity = None
+    converge_parity = bool(args.parity_converge) and args.converge_max > 0
     if D.world == 1 and args.parity_cycles > 0 and args.mode == "throughput":
         DH.close()   # one mirror at a time
         t0 = time.perf_counter()
@@ -681,11 +682,11 @@ def main():
         PD.upload(0, "x", np.ones(N))
         t0 = time.perf_counter()
         prel = []
-        ncyc = args.converge_max if args.parity_converge else args.parity_cycles
+        ncyc = args.converge_max if converge_parity else args.parity_cycles
         for _ in range(ncyc):
             PD.cycle()
             prel.append(PD.residual_norm() / float(np.sqrt(N)))
-            if args.parity_converge and prel[-1] < pars["tol"]:
+            if converge_parity and prel[-1] < pars["tol"]:
                 break
         pdt = (time.perf_counter() - t0) / len(prel)
         info = [PD.level_info(l) for l in range(len(table) - 1)]
@@ -693,14 +694,14 @@ def main():
         parity = {"value": 1.0 / pdt, "unit": "V-cycle iter/s", "ms_per_step": pdt * 1e3, "upload_s": up,
                   "relres_first_cycles": prel[:4], "gs_engines": [[i.gs_engine_f, i.gs_engine_c] for i in info],
                   "gs_stall": any(i.gs_stall for i in info)}
-        if args.parity_converge:
+        if converge_parity:
             parity.update(iterations_to_tol=len(prel), final_relres=prel[-1], time_to_solution_s=pdt * len(prel))
         print(f"[bench] parity mode: {pdt * 1e3:.1f} ms per V-cycle (upload {up:.1f} s)", file=sys.stderr, flush=True)
     # reference-semantics iteration counts measured with the parity engine (tools/conv_study.py; the
     # parity engine's printed history equals the reference's, tests/test_gpu_at_size.py)
     ref_conv = None
     conv = ROOT / "profiles" / f"r02_conv{n}_parity_vs_throughput.json"
-    if parity and args.parity_converge:
+    if parity and converge_parity:
         ref_conv = {"iterations_to_tol_reference": parity["iterations_to_tol"],
                     "iterations_to_tol_throughput_same_run": its,
                     "parity_ms_per_cycle_same_run": parity["ms_per_step"],
