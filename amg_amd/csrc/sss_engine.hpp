@@ -22,6 +22,8 @@
 
 #include "../../include/sss_hip.h"
 
+extern "C" void sss_huge_hint(void *p, size_t bytes);   // amg_amd/host/sss_util.c
+
 namespace sss {
 
 constexpr int kBlock = 256;        // threads per workgroup for streaming kernels (4 waves)
@@ -57,6 +59,7 @@ struct HostBuf {
     void resize(size_t m)
     {
         p.reset(m ? new T[m] : nullptr);
+        sss_huge_hint(p.get(), m * sizeof(T));   // large, untouched: transparent huge pages
         n = m;
     }
     T *data() { return p.get(); }

@@ -22,6 +22,15 @@ sss_hip_hier *sss_dev_mirror_for(SSS_AMG *mg);
 /* Fatal HIP/RCCL failure in the product path: print in the reference's style and exit. */
 void sss_fatal(const char *where, const char *what);
 
+/* Ask for transparent huge pages on a large, not yet touched allocation (madvise MADV_HUGEPAGE on
+ * its page-aligned interior; a no-op below 8 MiB).  The setup's random-access passes (the RS first
+ * pass, transposes, RAP) walk gigabytes of per-point records and CSR rows: with 4 KiB pages nearly
+ * every access also misses the TLB. */
+void sss_huge_hint(void *p, size_t bytes);
+/* malloc / calloc followed by sss_huge_hint */
+void *sss_big_malloc(size_t bytes);
+void *sss_big_calloc(size_t n, size_t size);
+
 #ifdef __cplusplus
 }
 #endif

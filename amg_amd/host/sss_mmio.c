@@ -165,14 +165,14 @@ static int read_triplets(const char *path, mtx_triplets *t)
     fseek(f, 0, SEEK_END);
     end = ftell(f);
     fseek(f, pos, SEEK_SET);
-    buf = (char *)malloc((size_t)(end - pos) + 1);
+    buf = (char *)sss_big_malloc((size_t)(end - pos) + 1);
     if (fread(buf, 1, (size_t)(end - pos), f) != (size_t)(end - pos)) { /* short read: parse what we got */ }
     buf[end - pos] = '\0';
     fclose(f);
 
-    t->ri = (int *)malloc(sizeof(int) * (size_t)(t->nentries > 0 ? t->nentries : 1));
-    t->ci = (int *)malloc(sizeof(int) * (size_t)(t->nentries > 0 ? t->nentries : 1));
-    t->v = (double *)malloc(sizeof(double) * (size_t)(t->nentries > 0 ? t->nentries : 1));
+    t->ri = (int *)sss_big_malloc(sizeof(int) * (size_t)(t->nentries > 0 ? t->nentries : 1));
+    t->ci = (int *)sss_big_malloc(sizeof(int) * (size_t)(t->nentries > 0 ? t->nentries : 1));
+    t->v = (double *)sss_big_malloc(sizeof(double) * (size_t)(t->nentries > 0 ? t->nentries : 1));
     if (parse_parallel(buf, (size_t)(end - pos), t)) {
         free(buf);
         return 0;
@@ -252,7 +252,7 @@ int mmio_info(int *m, int *n, int *nnz, int *isSymmetric, char *filename)
     int rc = read_triplets(filename, &t);
     int *rp;
     if (rc != 0) return rc;
-    rp = (int *)malloc(sizeof(int) * ((size_t)t.nrows + 1));
+    rp = (int *)sss_big_malloc(sizeof(int) * ((size_t)t.nrows + 1));
     *m = t.nrows;
     *n = t.ncols;
     *nnz = build_row_ptr(&t, rp);
@@ -286,7 +286,7 @@ int mmio_data(int *csrRowPtr, int *csrColIdx, double *csrAx, char *filename)
     }
     if (rc != 0) return rc;
     build_row_ptr(&t, csrRowPtr);
-    next = (int *)malloc(sizeof(int) * ((size_t)t.nrows + 1));
+    next = (int *)sss_big_malloc(sizeof(int) * ((size_t)t.nrows + 1));
     memcpy(next, csrRowPtr, sizeof(int) * ((size_t)t.nrows + 1));
     for (int k = 0; k < t.nentries; ++k) {
         int r = t.ri[k], c = t.ci[k], dst = next[r]++;
@@ -310,9 +310,9 @@ void SSS_mat_read(char *filemat, SSS_MAT *A)
     printf("filename: %s\n", filemat);
     rc = mmio_info(&A->num_rows, &A->num_cols, &A->num_nnzs, &sym, filemat);
     if (rc != 0) SSS_exit_on_errcode(rc == -1 ? ERROR_OPEN_FILE : ERROR_WRONG_FILE, __func__);
-    A->row_ptr = (int *)malloc(((size_t)A->num_rows + 1) * sizeof(int));
-    A->col_idx = (int *)malloc((size_t)(A->num_nnzs > 0 ? A->num_nnzs : 1) * sizeof(int));
-    A->val = (double *)malloc((size_t)(A->num_nnzs > 0 ? A->num_nnzs : 1) * sizeof(double));
+    A->row_ptr = (int *)sss_big_malloc(((size_t)A->num_rows + 1) * sizeof(int));
+    A->col_idx = (int *)sss_big_malloc((size_t)(A->num_nnzs > 0 ? A->num_nnzs : 1) * sizeof(int));
+    A->val = (double *)sss_big_malloc((size_t)(A->num_nnzs > 0 ? A->num_nnzs : 1) * sizeof(double));
     mmio_data(A->row_ptr, A->col_idx, A->val, filemat);
     printf("A: m = %d, n = %d, nnz = %d\n", A->num_rows, A->num_cols, A->num_nnzs);
 }

@@ -59,7 +59,7 @@ int sss_gen_stencil(int kind, int nx, int ny, int nz, int z0, int z1, SSS_MAT *A
     int *rp;
 
     if ((kind != 7 && kind != 27) || nrows <= 0 || ncols > INT32_MAX) return ERROR_MAT_SIZE;
-    rp = (int *)malloc(sizeof(int) * (size_t)(nrows + 1));
+    rp = (int *)sss_big_malloc(sizeof(int) * (size_t)(nrows + 1));
     rp[0] = 0;
     /* row lengths depend only on the boundary position: count in parallel, scan serially */
 #pragma omp parallel for schedule(static)
@@ -77,8 +77,8 @@ int sss_gen_stencil(int kind, int nx, int ny, int nz, int z0, int z1, SSS_MAT *A
     A->num_cols = (int)ncols;
     A->num_nnzs = (int)nnz;
     A->row_ptr = rp;
-    A->col_idx = (int *)malloc(sizeof(int) * (size_t)(nnz > 0 ? nnz : 1));
-    A->val = (double *)malloc(sizeof(double) * (size_t)(nnz > 0 ? nnz : 1));
+    A->col_idx = (int *)sss_big_malloc(sizeof(int) * (size_t)(nnz > 0 ? nnz : 1));
+    A->val = (double *)sss_big_malloc(sizeof(double) * (size_t)(nnz > 0 ? nnz : 1));
 #pragma omp parallel for schedule(static)
     for (int64_t r = 0; r < nrows; ++r)
         stencil_row(kind, nx, ny, nz, r0 + r, A->col_idx + rp[r], A->val + rp[r]);

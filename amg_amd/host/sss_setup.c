@@ -769,8 +769,8 @@ void interp_DIR(SSS_MAT *A, SSS_IVEC *vertices, SSS_MAT *P, SSS_AMG_PARS *pars)
     const int *mark = vertices->d;
     const int *ia = A->row_ptr, *ja = A->col_idx;
     const double *a = A->val;
-    double *aii_row = (double *)malloc(sizeof(double) * (size_t)(n > 0 ? n : 1));
-    int *diag_pos = (int *)malloc(sizeof(int) * (size_t)(n > 0 ? n : 1));
+    double *aii_row = (double *)sss_big_malloc(sizeof(double) * (size_t)(n > 0 ? n : 1));
+    int *diag_pos = (int *)sss_big_malloc(sizeof(int) * (size_t)(n > 0 ? n : 1));
     int *cmap;
     double t0 = SSS_get_time(), carried = 0.0;
     int ncoarse = 0;
@@ -983,7 +983,7 @@ SSS_MAT SSS_blas_mat_rap(const SSS_MAT *R, const SSS_MAT *A, const SSS_MAT *P)
     const int *ri = R->row_ptr, *rj = R->col_idx, *ai = A->row_ptr, *aj = A->col_idx;
     const int *pi = P->row_ptr, *pj = P->col_idx;
     const double *rv = R->val, *av = A->val, *pv = P->val;
-    int64_t *start = (int64_t *)calloc((size_t)nc + 1, sizeof(int64_t));
+    int64_t *start = (int64_t *)sss_big_calloc((size_t)nc + 1, sizeof(int64_t));
     SSS_MAT C;
     int too_big = 0;
 
@@ -999,9 +999,9 @@ SSS_MAT SSS_blas_mat_rap(const SSS_MAT *R, const SSS_MAT *A, const SSS_MAT *P)
      * pass, so the second pass needs no reset. */
 #pragma omp parallel
     {
-        int *seen_f = (int *)malloc(sizeof(int) * (size_t)(nf > 0 ? nf : 1));
-        int *seen_c = (int *)malloc(sizeof(int) * (size_t)(nc > 0 ? nc : 1));
-        int *slot = (int *)malloc(sizeof(int) * (size_t)(nc > 0 ? nc : 1));
+        int *seen_f = (int *)sss_big_malloc(sizeof(int) * (size_t)(nf > 0 ? nf : 1));
+        int *seen_c = (int *)sss_big_malloc(sizeof(int) * (size_t)(nc > 0 ? nc : 1));
+        int *slot = (int *)sss_big_malloc(sizeof(int) * (size_t)(nc > 0 ? nc : 1));
         for (int i = 0; i < nf; ++i) seen_f[i] = -1;
         for (int i = 0; i < nc; ++i) seen_c[i] = -1;
 #pragma omp for schedule(dynamic, 256)

@@ -15,7 +15,9 @@
 #include <stdlib.h>
 #include <string.h>
 #include <strings.h>
+#include <sys/mman.h>
 #include <sys/time.h>
+#include <stdint.h>
 
 #include <omp.h>
 
@@ -136,11 +138,33 @@ void SSS_blas_array_ax(int n, double a, double *x)
 }
 
 /* ---- allocation and copies (SSS_matvec.c) ------------------------------------------------ */
+void sss_huge_hint(void *p, size_t bytes)
+{
+    if (!p || bytes < ((size_t)8 << 20) || getenv("SSS_NO_HUGEPAGE")) return;
+    const uintptr_t pg = 4096, a = ((uintptr_t)p + pg - 1) & ~(pg - 1), e = ((uintptr_t)p + bytes) & ~(pg - 1);
+    if (e > a) (void)madvise((void *)a, e - a, MADV_HUGEPAGE);
+}
+
+void *sss_big_malloc(size_t bytes)
+{
+    void *p = malloc(bytes);
+    sss_huge_hint(p, bytes);
+    return p;
+}
+
+void *sss_big_calloc(size_t n, size_t size)
+{
+    void *p = calloc(n, size);
+    sss_huge_hint(p, n * size);
+    return p;
+}
+
 void *SSS_calloc(size_t size, int type)
 {
     size_t bytes = size * (size_t)type;
     void *mem = bytes > 0 ? calloc(size, (size_t)type) : NULL;
     if (mem == NULL) printf("### WARNING: Cannot allocate %.3lf MB RAM!\n", (double)bytes / 1048576);
+    sss_huge_hint(mem, bytes);
     return mem;
 }
 
@@ -148,6 +172,7 @@ void *SSS_realloc(void *oldmem, size_t tsize)
 {
     void *mem = tsize > 0 ? realloc(oldmem, tsize) : NULL;
     if (mem == NULL) printf("### WARNING: Cannot allocate %.3lfMB RAM!\n", (double)tsize / 1048576);
+    sss_huge_hint(mem, tsize);
     return mem;
 }
 
@@ -326,9 +351,9 @@ static int cmp_int(const void *a, const void *b)
 static void transpose_pattern_par(int nrows, int ncols, int nnz, const int *ia, const int *ja,
                                   const void *val, size_t vsize, int *tia, int *tja, void *tval)
 {
-    int *fill = (int *)calloc((size_t)ncols + 1, sizeof(int));
-    int *src = (int *)malloc(sizeof(int) * (size_t)nnz);
-    int *rowof = (int *)malloc(sizeof(int) * (size_t)nnz);
+    int *fill = (int *)sss_big_calloc((size_t)ncols + 1, sizeof(int));
+    int *src = (int *)sss_big_malloc(sizeof(int) * (size_t)nnz);
+    int *rowof = (int *)sss_big_malloc(sizeof(int) * (size_t)nnz);
     memset(tia, 0, ((size_t)ncols + 1) * sizeof(int));
 #pragma omp parallel for schedule(static)
     for (int i = 0; i < nrows; ++i)
@@ -413,7 +438,7 @@ static int transpose_pattern_chunked(int nrows, int ncols, int nnz, const int *i
     int failed = 0;
 #pragma omp parallel for schedule(static, 1) num_threads(T) reduction(| : failed)
     for (int t = 0; t < T; ++t) {
-        cnt[t] = (int *)calloc(hi[t] >= lo[t] ? (size_t)(hi[t] - lo[t] + 1) : 1, sizeof(int));
+        cnt[t] = (int *)sss_big_calloc(hi[t] >= lo[t] ? (size_t)(hi[t] - lo[t] + 1) : 1, sizeof(int));
         if (!cnt[t]) {
             failed = 1;
             continue;
@@ -464,7 +489,7 @@ static void transpose_pattern(int nrows, int ncols, int nnz, const int *ia, cons
         transpose_pattern_par(nrows, ncols, nnz, ia, ja, val, vsize, tia, tja, tval);
         return;
     }
-    int *fill = (int *)calloc((size_t)ncols + 1, sizeof(int));
+    int *fill = (int *)sss_big_calloc((size_t)ncols + 1, sizeof(int));
     memset(tia, 0, ((size_t)ncols + 1) * sizeof(int));
     for (int i = 0; i < nrows; ++i)
         for (int k = ia[i]; k < ia[i + 1]; ++k) tia[ja[k] + 1]++;
