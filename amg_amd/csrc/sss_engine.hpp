@@ -444,9 +444,9 @@ void gs_persist_free(PassSchedule &ps);
 int gs_persist_run(const PassSchedule &ps, const DevCSR &A, const double *b, double *x, const double *deff,
                    hipStream_t s);
 int gs_persist_error(const PassSchedule &ps, unsigned *out);
-// cls: per row 1 = C; pdepth: per row its depth within its class pass (same-class lower couplings)
+// cls: per row 1 = C
 int gs_fused_build(GsFused &f, const SSS_MAT &A, const DevCSR *dA, const PassSchedule *pass, const int *cls,
-                   const int *pdepth, int sweeps);
+                   int sweeps);
 int gs_fused_run(const GsFused &f, const DevCSR &A, const double *b, double *x, const double *d_first,
                  const double *d_later, hipStream_t s);
 void gs_fused_free(GsFused &f);

@@ -774,10 +774,10 @@ __global__ __launch_bounds__(kBlock) void fused_depth_group(int cnt, const int *
 // Fused plan.  Requires F rows [0, split) and C rows [split, n) (relabeled level) and a structurally
 // symmetric level (checked here; otherwise no plan and the per-pass engines run).  Fused depth:
 // fd(i, s) = 1 + max(fd(i, s - 1), fd of the version of every neighbour that node (i, s) reads),
-// computed pass by pass over each pass's own depth groups (rows of one group are independent) --
-// on the GPU over the uploaded level (dA) and the passes' depth-ordered rows, else on the host.
+// on the GPU pass by pass over each pass's own depth groups (rows of one group are independent,
+// the uploaded level dA and the passes' depth-ordered rows), or on the host in one serial pass.
 int gs_fused_build(GsFused &f, const SSS_MAT &A, const DevCSR *dA, const PassSchedule *pass, const int *cls,
-                   const int *pdepth, int sweeps)
+                   int sweeps)
 {
     f = GsFused();
     const int n = A.num_rows;
@@ -792,7 +792,14 @@ int gs_fused_build(GsFused &f, const SSS_MAT &A, const DevCSR *dA, const PassSch
     const double avg = (double)nnz / n;
     f.G = avg <= 24 ? 4 : avg <= 48 ? 8 : avg <= 96 ? 16 : avg <= 192 ? 32 : 64;
     std::vector<int> fd((size_t)n * sweeps, 0);   // fd[s * n + i]
-    if (dA && dA->rp && dA->ci && dA->n == n && pass[0].rows && pass[1].rows) {
+    // on the GPU, one launch per depth group of each pass (~40 us each with the plan's other host
+    // work around), or on the host, one serial pass (~2.5 ns per entry and sweep): whichever is
+    // cheaper (400^3: level 1, 32M rows, GPU; levels 5-10, thousands of groups, host)
+    const double gpu_s = 40e-6 * sweeps * (double)(pass[0].depth + pass[1].depth);
+    const double host_s = 2.5e-9 * sweeps * (double)nnz;
+    const char *fde = getenv("SSS_HIP_FUSED_DEPTH");   // gpu | host: force one form (tests)
+    const bool on_gpu = fde && *fde ? std::string(fde) == "gpu" : gpu_s < host_s;
+    if (dA && dA->rp && dA->ci && dA->n == n && pass[0].rows && pass[1].rows && on_gpu) {
         int *d_fd = dev_alloc<int>(fd.size());
         if (!d_fd) return hip_fail(hipErrorOutOfMemory, "hipMalloc(fused depth)", __FILE__, __LINE__);
         auto go = [&](auto kern, int cnt, const int *grows, int sw) {
@@ -820,36 +827,20 @@ int gs_fused_build(GsFused &f, const SSS_MAT &A, const DevCSR *dA, const PassSch
         if (e1 != hipSuccess) return hip_fail(e1, "fused_depth_group", __FILE__, __LINE__);
         if (e2 != hipSuccess) return hip_fail(e2, "hipMemcpy(fused depth)", __FILE__, __LINE__);
     } else {
-        // rows of each class grouped by their pass depth
-        int maxd[2] = {0, 0};
-        for (int i = 0; i < n; ++i) maxd[cls[i]] = std::max(maxd[cls[i]], pdepth[i] + 1);
-        std::vector<int> goff[2], grows[2];
-        for (int c = 0; c < 2; ++c) {
-            goff[c].assign((size_t)maxd[c] + 1, 0);
-            for (int i = 0; i < n; ++i)
-                if (cls[i] == c) goff[c][pdepth[i] + 1]++;
-            for (int d = 0; d < maxd[c]; ++d) goff[c][d + 1] += goff[c][d];
-            grows[c].resize((size_t)goff[c][maxd[c]]);
-            std::vector<int> fill(goff[c].begin(), goff[c].end() - 1);
-            for (int i = 0; i < n; ++i)
-                if (cls[i] == c) grows[c][(size_t)fill[pdepth[i]]++] = i;
-        }
+        // one serial pass in the sequential smoother's own order (every dependency of a node comes
+        // earlier in it), the rows streamed in order
         for (int sw = 0; sw < sweeps; ++sw)
             for (int c = 0; c < 2; ++c)
-                for (int d = 0; d < maxd[c]; ++d)
-                    parallel_chunks(goff[c][d + 1] - goff[c][d], 2048, [&](int a, int e) {
-                        for (int q = goff[c][d] + a; q < goff[c][d] + e; ++q) {
-                            const int i = grows[c][(size_t)q];
-                            int dep = sw > 0 ? fd[(size_t)(sw - 1) * n + i] : 0;
-                            for (int k = rp[i]; k < rp[i + 1]; ++k) {
-                                const int j = ci[k];
-                                if (j == i) continue;
-                                const int need = (cls[j] == cls[i]) ? (j < i ? sw + 1 : sw) : (cls[j] ? sw : sw + 1);
-                                if (need > 0) dep = std::max(dep, fd[(size_t)(need - 1) * n + j]);
-                            }
-                            fd[(size_t)sw * n + i] = dep + 1;
-                        }
-                    });
+                for (int i = c ? split : 0; i < (c ? n : split); ++i) {
+                    int dep = sw > 0 ? fd[(size_t)(sw - 1) * n + i] : 0;
+                    for (int k = rp[i]; k < rp[i + 1]; ++k) {
+                        const int j = ci[k];
+                        if (j == i) continue;
+                        const int need = (cls[j] == c) ? (j < i ? sw + 1 : sw) : (cls[j] ? sw : sw + 1);
+                        if (need > 0) dep = std::max(dep, fd[(size_t)(need - 1) * n + j]);
+                    }
+                    fd[(size_t)sw * n + i] = dep + 1;
+                }
     }
     int depth = 0;
     for (int x : fd) depth = std::max(depth, x);

@@ -231,7 +231,7 @@ int smoother_build(SmootherPlan &sp, const SSS_MAT &A, const int *mark, int kind
         const char *fe = getenv("SSS_HIP_GS_FUSED");   // 0: per-pass launches (tests compare both)
         if (!(fe && *fe == '0') && kind == SSS_HIP_SMOOTH_EXACT && !gcls && A.num_cols == n && mark &&
             sp.pass[0].gp.engine == 1 && sp.pass[1].gp.engine == 1 &&
-            (rc = gs_fused_build(sp.fz, A, dA, sp.pass, cls.data(), depth.data(), 2)))
+            (rc = gs_fused_build(sp.fz, A, dA, sp.pass, cls.data(), 2)))
             return rc;
     }
     t_persist = now();

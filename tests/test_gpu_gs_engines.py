@@ -492,6 +492,29 @@ def test_fused_engine_edge_rows_bitwise(fused, monkeypatch):
             assert np.array_equal(xg.view(np.uint64), xr.view(np.uint64)), (sweeps, post, fused)
 
 
+@pytest.mark.parametrize("depth_form", ["gpu", "host"])
+def test_fused_depth_forms(p32_h, depth_form, monkeypatch):
+    """The fused plan's ticket order (fused-DAG depth) computed on the GPU per depth group or on the
+    host in one serial pass: either is a topological order -- no stall, the reference's x bit for bit."""
+    monkeypatch.setenv("SSS_HIP_GS_ENGINE", "flow")
+    monkeypatch.setenv("SSS_HIP_GS_FUSED", "1")
+    monkeypatch.setenv("SSS_HIP_FUSED_DEPTH", depth_form)
+    n = p32_h.level(0).A.num_rows
+    rtn, rel_r, _ = oracle_solve(p32_h, np.ones(n), x_r := np.ones(n))
+    D = A.DeviceHierarchy(p32_h, smoother="exact", coarse="krylov")
+    try:
+        D.upload(0, "b", np.ones(n))
+        D.upload(0, "x", np.ones(n))
+        for _ in range(len(rel_r)):
+            D.cycle()
+        x_g = D.download(0, "x")
+        used = _check_engines(D, p32_h, "fused")
+        assert 3 in used
+    finally:
+        D.close()
+    assert np.array_equal(x_g.view(np.uint64), x_r.view(np.uint64))
+
+
 def test_fused_engine_used_and_matches_per_pass(p64_h, monkeypatch):
     """On 7-pt 64^3 every level whose two passes are flow passes runs fused (level_info 3/3), and a
     V-cycle sequence gives the per-pass engine's iterate and residual norms bit for bit."""
