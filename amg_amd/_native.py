@@ -78,7 +78,9 @@ class SSS_HIP_OPTS(C.Structure):
     _fields_ = [("device", C.c_int), ("smoother", C.c_int), ("coarse", C.c_int), ("row_cap", C.c_int),
                 ("use_graph", C.c_int), ("verbose", C.c_int),
                 ("inner", C.c_int), ("inner_from", C.c_int), ("relabel", C.c_int),
-                ("sorted_tiles", C.c_int), ("sum_order", C.c_int), ("inner_long", C.c_int)]
+                ("sorted_tiles", C.c_int), ("sum_order", C.c_int), ("inner_long", C.c_int), ("formats", C.c_int)]
+
+FORMATS = {"auto": -1, "full": 0, "lean": 1}
 
 
 class SSS_HIP_LEVEL_INFO(C.Structure):
@@ -350,7 +352,8 @@ class DeviceHierarchy:
     def __init__(self, H: Hierarchy | None, smoother: str = "exact", coarse: str = "krylov", row_cap: int = 0,
                  device: int = -1, verbose: int = 0, relabel: int | None = None, graph: int | None = None,
                  inner: int | None = None, inner_from: int | None = None, sorted_tiles: int | None = None,
-                 sum_order: int | None = None, setup_from: SSS_MAT | None = None, inner_long: int | None = None):
+                 sum_order: int | None = None, setup_from: SSS_MAT | None = None, inner_long: int | None = None,
+                 formats: str | None = None):
         """setup_from: build the Hierarchy from this operator here, with the levels uploaded while
         the setup is still running (sss_hip_setup_create); H must then be None and self.H is the
         new Hierarchy.  self.times = (setup s, mirror s after the setup, of which waiting)."""
@@ -371,6 +374,8 @@ class DeviceHierarchy:
             o.inner_from = inner_from
         if inner_long is not None:
             o.inner_long = inner_long
+        if formats is not None:
+            o.formats = FORMATS[formats]
         if setup_from is not None:
             if H is not None:
                 raise ValueError("setup_from builds its own Hierarchy: pass H=None")
@@ -657,10 +662,12 @@ class DistHierarchy:
     def __init__(self, H: "Hierarchy | None", comm: Comm, smoother: str = "hybrid", coarse: str = "direct",
                  device: int = -1, agg_rows: int = 0, inner: int | None = None, inner_from: int | None = None,
                  sorted_tiles: int | None = None, sum_order: int | None = None, parts=None,
-                 inner_long: int | None = None):
+                 inner_long: int | None = None, formats: str | None = None):
         o = SSS_HIP_OPTS()
         lib().sss_hip_opts_default(C.byref(o))
         o.smoother, o.coarse, o.device = SMOOTH[smoother], COARSE[coarse], device
+        if formats is not None:
+            o.formats = FORMATS[formats]
         if sorted_tiles is not None:
             o.sorted_tiles = sorted_tiles
         if sum_order is not None:

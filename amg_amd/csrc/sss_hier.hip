@@ -105,6 +105,12 @@ extern "C" void sss_hip_opts_default(sss_hip_opts *o)
     o->inner_long = env_int("SSS_HIP_INNER_LONG", 1);
     o->sorted_tiles = env_int("SSS_HIP_SORTED_TILES", 1);
     o->sum_order = env_int("SSS_HIP_SUM_ORDER", 0);
+    o->formats = -1;
+    if (const char *f = getenv("SSS_HIP_FORMATS")) {
+        const std::string v(f);
+        if (v == "full") o->formats = 0;
+        else if (v == "lean") o->formats = 1;
+    }
     if (const char *s = getenv("SSS_HIP_SMOOTHER")) {
         std::string v(s);
         if (v == "hybrid") o->smoother = SSS_HIP_SMOOTH_HYBRID;
@@ -150,6 +156,10 @@ static int level_inner(const sss_hip_opts &o, int l, long long rows, long long n
 int sss::level_kind_of(const sss_hip_opts &o, int l) { return level_smoother_kind(o, l); }
 int sss::level_encoding(const sss_hip_opts &o)
 {
+    // plain CSR tiles only: asked for, or (auto) the exact smoother -- its cycle waits on the GS-CF
+    // chains (7-pt 400^3: ~1.2 s per cycle), and the formats' host builders were ~40 % of its mirror
+    if (o.formats == 1 || (o.formats < 0 && o.smoother == SSS_HIP_SMOOTH_EXACT))
+        return o.sum_order == 1 ? kEncFreeOrder : 0;
     // dictionary tiles (kEncDict) are offered for the level matrices A_l; uploads of P, R and the
     // two-stage split copies mask them out (their column offsets are not row-relative)
     const char *dz = getenv("SSS_HIP_DICT");
@@ -814,9 +824,10 @@ extern "C" sss_hip_hier *sss_hip_setup_create(SSS_AMG *mg, SSS_MAT *A, SSS_AMG_P
 }
 
 // The mirror of a hierarchy already set up: its level tasks (relabel + A_l + smoother plan, P_l /
-// R_l) are independent once their inputs exist, so the calling thread and three helpers take them
+// R_l) are independent once their inputs exist, so the calling thread and five helpers take them
 // side by side (the parity mirror at 7-pt 400^3 took 18.8 s with the tasks in sequence, its largest
-// task ~2 s).  A distributed engine's replicated tail (level_base > 0) keeps the sequence.
+// task ~2 s; 3.6 s with three helpers, 3.0 s with five -- profiles/r05_lean_formats/).  A distributed
+// engine's replicated tail (level_base > 0) keeps the sequence.
 sss_hip_hier *sss::hier_create_impl(const SSS_AMG *mg, const sss_hip_opts *o, int level_base, hipStream_t stream)
 {
     Pipeline P;
@@ -838,7 +849,7 @@ sss_hip_hier *sss::hier_create_impl(const SSS_AMG *mg, const sss_hip_opts *o, in
     P.finished = true;
     (void)hipGetDevice(&P.device);
     std::vector<std::thread> helpers;
-    for (int k = 0; k < 3; ++k)
+    for (int k = 0; k < 5; ++k)
         helpers.emplace_back([&] {
             (void)hipSetDevice(P.device);
             P.loop(false);

@@ -61,6 +61,11 @@ typedef struct sss_hip_opts {
                           SSS_HIP_LONG_ROW_MIN = 300 entries per row on average over the whole level):
                           their lower triangles are the densest, and the extra step keeps throughput
                           mode within the reference's iteration count + 2 at 7-pt 512^3 (default 1) */
+    int formats;       /* storage formats of the uploaded operators (all bitwise-neutral): 0 = every
+                          format a level qualifies for (dictionary / column ELL, dictionary and
+                          column-sorted tiles); 1 = plain CSR tiles only (cheapest to build); -1 = auto
+                          (default): 1 for the exact smoother, whose cycle is bound by the GS-CF chains,
+                          so the formats would only lengthen the mirror's construction, else 0 */
 } sss_hip_opts;
 
 #define SSS_HIP_LONG_ROW_MIN 300
@@ -68,7 +73,8 @@ typedef struct sss_hip_opts {
  * SSS_HIP_COARSE=krylov|direct, SSS_HIP_ROWCAP=<n>, SSS_HIP_GRAPH=0|1, SSS_HIP_DEVICE=<n>,
  * SSS_HIP_VERBOSE=0|1, SSS_HIP_RELABEL=0|1|2 (default 1), SSS_HIP_INNER=<k> (default 1),
  * SSS_HIP_SORTED_TILES=0|1 (default 1), SSS_HIP_SUM_ORDER=0|1 (default 0),
- * SSS_HIP_INNER_FROM=<level> (default 2), SSS_HIP_INNER_LONG=<k> (default 1). */
+ * SSS_HIP_INNER_FROM=<level> (default 2), SSS_HIP_INNER_LONG=<k> (default 1),
+ * SSS_HIP_FORMATS=auto|full|lean (default auto). */
 void sss_hip_opts_default(sss_hip_opts *o);
 
 /* Number of usable HIP devices (0 when none; never exits). */

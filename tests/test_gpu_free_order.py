@@ -128,7 +128,7 @@ def test_sorted_tiles_bitwise_neutral(request, hname):
     for smoother, coarse in (("exact", "krylov"), ("hybrid", "direct")):
         xs = []
         for st in (0, 1):
-            D = A.DeviceHierarchy(H, smoother=smoother, coarse=coarse, sorted_tiles=st)
+            D = A.DeviceHierarchy(H, smoother=smoother, coarse=coarse, sorted_tiles=st, formats="full")
             D.upload(0, "b", np.ones(n))
             D.upload(0, "x", np.ones(n))
             for _ in range(3):

@@ -339,6 +339,7 @@ def test_dictionary_tiles_bitwise(request, hname, smoother, coarse, monkeypatch)
     H = request.getfixturevalue(hname)
     n = H.level(0).A.num_rows
     out, fmt = {}, {}
+    monkeypatch.setenv("SSS_HIP_FORMATS", "full")   # (the exact smoother's own default is plain tiles)
     for mode, env in (("ell", {"SSS_HIP_DICT": "1", "SSS_HIP_ELL": "1", "SSS_HIP_XELL": "1"}),
                       ("xell", {"SSS_HIP_DICT": "1", "SSS_HIP_ELL": "0", "SSS_HIP_XELL": "1"}),
                       ("tiles", {"SSS_HIP_DICT": "1", "SSS_HIP_ELL": "0", "SSS_HIP_XELL": "0"}),
@@ -544,3 +545,29 @@ def test_fused_engine_used_and_matches_per_pass(p64_h, monkeypatch):
             assert e1 == (3, 3)
     assert np.array_equal(out["0"][0].view(np.uint64), out["1"][0].view(np.uint64))
     assert out["0"][1] == out["1"][1]
+
+
+@pytest.mark.parametrize("hname", ["p32_h", "a27_h"])
+def test_exact_mirror_formats_lean_by_default(request, hname, monkeypatch):
+    """The exact smoother's mirror stores every operator as plain CSR tiles (formats auto = lean:
+    its cycle waits on the GS-CF chains, the formats only cost build time); full formats give the
+    same iterates bit for bit."""
+    monkeypatch.delenv("SSS_HIP_FORMATS", raising=False)
+    H = request.getfixturevalue(hname)
+    n = H.level(0).A.num_rows
+    out, fmt = {}, {}
+    for formats in (None, "full"):
+        D = A.DeviceHierarchy(H, smoother="exact", coarse="krylov", formats=formats)
+        try:
+            fmt[formats] = [(D.level_info(l).a_format, D.level_info(l).r_format, D.level_info(l).p_format)
+                            for l in range(H.num_levels - 1)]
+            D.upload(0, "b", np.ones(n))
+            D.upload(0, "x", np.ones(n))
+            for _ in range(4):
+                D.cycle()
+            out[formats] = D.download(0, "x")
+        finally:
+            D.close()
+    assert all((a | r | p) & 0xC3 == 0 for a, r, p in fmt[None]), fmt[None]   # no ELL / dictionary / sorted tiles
+    assert any((a | r | p) & 0xC3 for a, r, p in fmt["full"]), fmt["full"]
+    assert np.array_equal(out[None].view(np.uint64), out["full"].view(np.uint64))

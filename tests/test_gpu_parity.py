@@ -48,12 +48,15 @@ def test_device_present():
 
 
 # ---------------------------------------------------------------- SpMV family, bitwise
-@pytest.fixture(params=["tile", "tile-sorted", "tile-unsorted", "wave"])
+@pytest.fixture(params=["tile", "tile-sorted", "tile-unsorted", "wave", "lean"])
 def row_path(request, monkeypatch):
-    """Run a test with the default kernel choice (dictionary tiles where every block qualifies,
-    else column-sorted tiles), with the column-sorted tiles only (SSS_HIP_DICT=0), with the tiles
-    staged in stored order (SSS_HIP_SORTED_TILES=0 too), and with every matrix forced onto the
-    wave-per-row kernels (SSS_HIP_WAVE_MIN=1), so every row path is checked bitwise."""
+    """Run a test with every storage format a level qualifies for (dictionary tiles where every
+    block qualifies, else column-sorted tiles; SSS_HIP_FORMATS=full, since the exact smoother's
+    own default is plain tiles), with the column-sorted tiles only (SSS_HIP_DICT=0), with the tiles
+    staged in stored order (SSS_HIP_SORTED_TILES=0 too), with every matrix forced onto the
+    wave-per-row kernels (SSS_HIP_WAVE_MIN=1), and with the exact smoother's default plain tiles
+    (lean), so every row path is checked bitwise."""
+    monkeypatch.setenv("SSS_HIP_FORMATS", "lean" if request.param == "lean" else "full")
     if request.param == "wave":
         monkeypatch.setenv("SSS_HIP_WAVE_MIN", "1")
     if request.param in ("tile-sorted", "tile-unsorted"):
