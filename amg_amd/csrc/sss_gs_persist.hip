@@ -853,11 +853,44 @@ int gs_fused_build(GsFused &f, const SSS_MAT &A, const DevCSR *dA, const PassSch
         for (size_t t = 0; t < fd.size(); ++t) order[(size_t)fill[(size_t)fd[t] - 1]++] = (int)t;
     }
     f.overlap = avg >= 300;
-    // the levels of the shortest rows are bound by the ticket counter's atomic throughput (one
-    // ticket per chunk of 64 / G rows): two lanes per row there (7-pt 256^3 level 1, 18.9 entries
-    // per row: 13.3 ms per 2-sweep call at G = 4, 9.4 at G = 2, 14.0 at G = 1; level 2, 34.7 per
-    // row: 5.6 ms at G = 8, 6.6 at G = 4, 9.6 at G = 2 -- profiles/r05_gs_fused/)
-    if (avg <= 24) f.G = 2;
+    // Lanes per row G: the cheapest by a latency model fitted to 2-sweep calls on 7-pt 256^3 and
+    // the circuit stand-in at G = 2 ... 64 (tools/gpu/r05_g_sweep.sh, profiles/r05_gs_fused/):
+    //  * each fused depth step costs the larger of its tickets -- one device-wide counter hands out
+    //    chunks of 64 / G rows at ~13 ns each, so npd * G / 64 * 13 ns for npd nodes per depth --
+    //    and a node's latency, ~2 us + 1 us per group of 8 loads a lane issues for an average row
+    //    + 20 ns per entry a lane stages;
+    //  * hub rows (longer than 4x the average and than one staging round of 32 G entries) add
+    //    ~2 us per further round, each sweep.
+    // 7-pt level 1 (19 entries, ~14K nodes per depth): G = 2 (9.4 ms; 13.3 at 4, 24.7 at 8); level
+    // 2 (35 entries, ~2K): 8 (5.7; 9.0 at 16); level 3 (64, ~280): 32 (4.3; 19.2 at 2); the long-row
+    // levels 64; the circuit stand-in's level 1 (7 entries, hub rows up to 11K): 8-16 (8.9 / 8.3
+    // ms against 13.3 at 4 and 20.8 at 64).
+    int maxlen = 0;
+    for (int i = 0; i < n; ++i) maxlen = std::max(maxlen, rp[i + 1] - rp[i]);
+    {
+        const double npd = (double)n * sweeps / std::max(1, depth);
+        double best = 0.0;
+        for (int g = 2; g <= 64; g *= 2) {
+            const double tick = npd * g / 64.0 * 13e-9;
+            const double lat = 2e-6 + std::ceil(std::min(avg, 32.0 * g) / (8.0 * g)) * 1e-6 + avg / g * 20e-9;
+            double hub = 0.0;
+            const double hub_min = std::max(4.0 * avg, 32.0 * g);
+            if (maxlen > hub_min)
+                for (int i = 0; i < n; ++i) {
+                    const int len = rp[i + 1] - rp[i];
+                    if (len > hub_min) hub += std::ceil(len / (32.0 * g)) - 1.0;
+                }
+            const double est = depth * std::max(tick, lat) + sweeps * hub * 2e-6;
+            if (g == 2 || est < best) best = est, f.G = g;
+        }
+    }
+    if (const char *e = getenv("SSS_HIP_FUSED_G")) {   // test hook: lanes per row 2 ... 64
+        const int g = atoi(e);
+        if (g == 2 || g == 4 || g == 8 || g == 16 || g == 32 || g == 64) f.G = g;
+    }
+    if (getenv("SSS_HIP_TIMING"))
+        fprintf(stderr, "[sss_hip]   fused GS-CF plan n=%d: depth %d (%.0f nodes per depth), rows %.1f avg / %d max, G = %d\n",
+                n, depth, (double)n * sweeps / std::max(1, depth), avg, maxlen, f.G);
     const int R = 64 / f.G;
     std::vector<int> ck;
     for (int d = 0; d < depth; ++d)
@@ -916,12 +949,14 @@ int gs_fused_run(const GsFused &f, const DevCSR &A, const double *b, double *x, 
                            f.sweeps - 1, A.rp, A.ci, A.v, b, x, d_first, d_later, f.gran, f.ctl, f.err, f.spin,
                            f.overlap ? 1 : 0);
     };
-    switch (f.G) {
+    switch (f.G) {   // (every G the planner can choose; the chunk table holds 64 / G rows per ticket)
     case 2: go(gs_fused_group<2>); break;
+    case 4: go(gs_fused_group<4>); break;
     case 8: go(gs_fused_group<8>); break;
     case 16: go(gs_fused_group<16>); break;
     case 32: go(gs_fused_group<32>); break;
-    default: go(gs_fused_group<64>); break;
+    case 64: go(gs_fused_group<64>); break;
+    default: return ERROR_INPUT_PAR;
     }
     SSS_HIP(hipGetLastError());
     return 0;

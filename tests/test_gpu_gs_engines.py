@@ -516,6 +516,30 @@ def test_fused_depth_forms(p32_h, depth_form, monkeypatch):
     assert np.array_equal(x_g.view(np.uint64), x_r.view(np.uint64))
 
 
+@pytest.mark.parametrize("lanes", ["2", "4", "16", "64"])
+@pytest.mark.parametrize("hname", ["p32_h", "a27_h"])
+def test_fused_lanes_per_row(request, hname, lanes, monkeypatch):
+    """Every lanes-per-row width of the fused engine (the planner picks 2 only on the widest levels
+    of short rows, which the test sizes never reach): the reference's x bit for bit, no stall."""
+    monkeypatch.setenv("SSS_HIP_GS_ENGINE", "flow")
+    monkeypatch.setenv("SSS_HIP_GS_FUSED", "1")
+    monkeypatch.setenv("SSS_HIP_FUSED_G", lanes)
+    H = request.getfixturevalue(hname)
+    n = H.level(0).A.num_rows
+    rtn, rel_r, _ = oracle_solve(H, np.ones(n), x_r := np.ones(n))
+    D = A.DeviceHierarchy(H, smoother="exact", coarse="krylov")
+    try:
+        D.upload(0, "b", np.ones(n))
+        D.upload(0, "x", np.ones(n))
+        for _ in range(len(rel_r)):
+            D.cycle()
+        x_g = D.download(0, "x")
+        assert 3 in _check_engines(D, H, "fused")
+    finally:
+        D.close()
+    assert np.array_equal(x_g.view(np.uint64), x_r.view(np.uint64))
+
+
 def test_fused_engine_used_and_matches_per_pass(p64_h, monkeypatch):
     """On 7-pt 64^3 every level whose two passes are flow passes runs fused (level_info 3/3), and a
     V-cycle sequence gives the per-pass engine's iterate and residual norms bit for bit."""

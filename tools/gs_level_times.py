@@ -28,12 +28,19 @@ def main():
     p.add_argument("--reps", type=int, default=3)
     p.add_argument("--levels", default="")
     p.add_argument("--json", default=None)
+    p.add_argument("--workload", default="stencil", choices=["stencil", "circuit"])
+    p.add_argument("--rows", type=int, default=0, help="circuit stand-in rows (default: G3_circuit's)")
     a = p.parse_args()
     import amg_amd as A
     t0 = time.perf_counter()
-    M = A.generate(a.stencil, a.n)
-    H = A.Hierarchy(M)
-    A.lib().SSS_mat_destroy(C.byref(M))
+    if a.workload == "circuit":
+        from amg_amd import workloads as W
+        keep = W.circuit_csr(a.rows or W.G3_CIRCUIT_ROWS)
+        H = A.Hierarchy(keep.mat)
+    else:
+        M = A.generate(a.stencil, a.n)
+        H = A.Hierarchy(M)
+        A.lib().SSS_mat_destroy(C.byref(M))
     print(f"[gs] setup {time.perf_counter() - t0:.1f} s", file=sys.stderr, flush=True)
     levels = [int(x) for x in a.levels.split(",")] if a.levels else list(range(1, H.num_levels - 1))
     out = []
