@@ -12,6 +12,7 @@
 //   hipcc -O3 --offload-arch=gfx950 -ffp-contract=off tools/l0_lab.hip -o tools/l0_lab
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -250,6 +251,88 @@ __global__ __launch_bounds__(B) void kpipe(const unsigned char *__restrict__ ell
         bq = nq;
         wc[0] = wn[0], wc[1] = wn[1];
         bc = bn;
+    }
+}
+
+// ---- x staged in LDS by offset ranges (round 5 lab; measured and rejected) --------------------------
+// 7-pt 400^3 (profiles/r05_l0_lab_lds_stage.txt): 3-4 merged ranges, 1,167-1,423 staged doubles per
+// block against 1,792 gathered values, yet the F pass took 487 us against 283 us and the residual 984
+// against 574 us -- the range loads, the LDS stores and the second barrier lengthen each workgroup's
+// chain of dependent steps, which is what bounds these kernels, and cut its occupancy.
+// A 256-row block's rows read x at r + o for the block's few distinct offsets o; the host merges the
+// intervals [r0 + o, r0 + o + 256) into at most SR ranges, which the workgroup loads coalesced into
+// LDS; each entry then reads its x from LDS at lofs[d] + (r - r0) instead of a scattered gather.
+constexpr int SR = 8, SBUD = 3072;   // ranges per block, staged doubles per block
+struct StagePlan {
+    int nr;                 // ranges (-1: not staged, gather)
+    int gs[SR], len[SR], lb[SR];
+    int lofs[32];           // per offset index: LDS position of row r0's value (-1: not staged)
+};
+template <int MODE>
+__global__ __launch_bounds__(B) void kstage(const unsigned char *__restrict__ ell, const int *__restrict__ ddf,
+                                            const double *__restrict__ vdf, const StagePlan *__restrict__ plan,
+                                            const double *__restrict__ b, double *x, double *__restrict__ y, int lo, int hi)
+{
+    __shared__ int dd[32];
+    __shared__ double vd[8];
+    __shared__ StagePlan sp;
+    __shared__ double xl[SBUD];
+    const int blk = lo / B + blockIdx.x;
+    const int t = threadIdx.x;
+    if (t < 32) dd[t] = ddf[(size_t)blk * 32 + t];
+    if (t < 8) vd[t] = vdf[(size_t)blk * 8 + t];
+    {
+        const int *src = reinterpret_cast<const int *>(plan + blk);
+        int *dst = reinterpret_cast<int *>(&sp);
+        constexpr int NW = sizeof(StagePlan) / 4;
+        if (t < NW) dst[t] = src[t];
+    }
+    const int r = lo + blockIdx.x * B + t;
+    const bool live = r < hi;
+    unsigned w[2] = {0xffffffffu, 0xffffffffu};
+    double br = 0.0;
+    if (live) {
+        const uint2 q = *reinterpret_cast<const uint2 *>(ell + (size_t)r * 8);
+        w[0] = q.x, w[1] = q.y;
+        br = b[r];
+    }
+    __syncthreads();
+    const int nr = sp.nr;
+    for (int k = 0; k < nr; ++k)   // coalesced range loads
+        for (int e = t; e < sp.len[k]; e += B) xl[sp.lb[k] + e] = x[sp.gs[k] + e];
+    __syncthreads();
+    if (!live) return;
+    int d[8], len = 8, ds = -1;
+    double a[8], dv = 0.0;
+#pragma unroll
+    for (int s = 0; s < 8; ++s) {
+        const unsigned byte = (w[s >> 2] >> (8 * (s & 3))) & 0xffu;
+        if (byte == 0xffu && len == 8) len = s;
+        d[s] = byte & 31u;
+        a[s] = vd[byte >> 5];
+    }
+#pragma unroll
+    for (int s = 0; s < 8; ++s)
+        if (s < len && dd[d[s]] == 0) ds = s, dv = a[s];
+    double xv[8];
+    const int tl = r - (lo + blockIdx.x * B);
+#pragma unroll
+    for (int s = 0; s < 8; ++s) {
+        const bool need = s < len && (MODE == 1 || s != ds);
+        xv[s] = need ? (nr >= 0 ? xl[sp.lofs[d[s]] + tl] : x[r + dd[d[s]]]) : 0.0;
+    }
+    if constexpr (MODE == 0) {
+        double tt = br;
+#pragma unroll
+        for (int s = 0; s < 8; ++s)
+            if (s < len && s != ds) tt -= a[s] * xv[s];
+        x[r] = fabs(dv) > 1e-20 ? tt / dv : x[r];
+    } else {
+        double tt = 0.0;
+#pragma unroll
+        for (int s = 0; s < 8; ++s)
+            if (s < len) tt += a[s] * xv[s];
+        y[r] = br + tt * -1.0;
     }
 }
 
@@ -497,6 +580,81 @@ int main(int argc, char **argv)
     run("resid R2 pair", 1, rbytes, RS(2, true));
     run("resid R4 scalar", 1, rbytes, RS(4, false));
     run("resid R4 pair", 1, rbytes, RS(4, true));
+    {   // LDS-staged x: plans for the F pass (diagonal offset not staged) and the residual
+        auto build = [&](bool with_diag, int lo_r, int hi_r) {
+            std::vector<StagePlan> pl(nb);
+            int staged = 0, maxr = 0, tot = 0;
+            for (int q = 0; q < nb; ++q) {
+                StagePlan &P = pl[q];
+                memset(&P, 0, sizeof P);
+                for (int d = 0; d < 32; ++d) P.lofs[d] = -1;
+                const int r0 = q * B, r1 = std::min(n, r0 + B);
+                if (r1 <= lo_r || r0 >= hi_r) { P.nr = -1; continue; }
+                // offsets used by the block's rows
+                bool used[32] = {};
+                for (int r = r0; r < r1; ++r)
+                    for (int sl = 0; sl < 8; ++sl) {
+                        const unsigned char by = ell[(size_t)r * 8 + sl];
+                        if (by == 0xff) break;
+                        const int dgi = by & 31;
+                        if (!with_diag && ddf[(size_t)q * 32 + dgi] == 0) continue;
+                        used[dgi] = true;
+                    }
+                std::vector<std::pair<int, int>> iv;   // [start, end) global, per used offset
+                std::vector<int> ofd;
+                for (int dgi = 0; dgi < 32; ++dgi)
+                    if (used[dgi]) {
+                        const int o = ddf[(size_t)q * 32 + dgi];
+                        iv.push_back({std::max(0, r0 + o), std::min(n, r1 + o)});
+                        ofd.push_back(dgi);
+                    }
+                std::vector<int> ord(iv.size());
+                for (size_t k = 0; k < ord.size(); ++k) ord[k] = (int)k;
+                std::sort(ord.begin(), ord.end(), [&](int a2, int b2) { return iv[a2].first < iv[b2].first; });
+                int nr = 0, lb = 0;
+                bool ok = true;
+                for (size_t k = 0; k < ord.size() && ok; ++k) {
+                    const auto &I = iv[ord[k]];
+                    if (nr > 0 && I.first <= P.gs[nr - 1] + P.len[nr - 1] + 16) {   // merge
+                        const int e = std::max(P.gs[nr - 1] + P.len[nr - 1], I.second);
+                        lb += e - (P.gs[nr - 1] + P.len[nr - 1]);
+                        P.len[nr - 1] = e - P.gs[nr - 1];
+                    } else {
+                        if (nr == SR) { ok = false; break; }
+                        P.gs[nr] = I.first, P.len[nr] = I.second - I.first, P.lb[nr] = lb;
+                        lb += P.len[nr];
+                        ++nr;
+                    }
+                }
+                if (!ok || lb > SBUD) { P.nr = -1; continue; }
+                for (size_t k = 0; k < iv.size(); ++k) {   // lofs: LDS index of row r0's value
+                    const int o = ddf[(size_t)q * 32 + ofd[k]];
+                    for (int m = 0; m < nr; ++m)
+                        if (r0 + o >= P.gs[m] - B && r0 + o < P.gs[m] + P.len[m] &&
+                            std::max(0, r0 + o) >= P.gs[m] && std::min(n, r1 + o) <= P.gs[m] + P.len[m]) {
+                            P.lofs[ofd[k]] = P.lb[m] + (r0 + o - P.gs[m]);
+                            break;
+                        }
+                }
+                P.nr = nr;
+                ++staged;
+                maxr = std::max(maxr, nr);
+                tot += lb;
+            }
+            printf("stage plan (%s): %d of %d blocks staged, max ranges %d, avg staged doubles %.0f\n",
+                   with_diag ? "resid" : "F pass", staged, nb, maxr, staged ? (double)tot / staged : 0.0);
+            StagePlan *dp;
+            CK(hipMalloc(&dp, pl.size() * sizeof(StagePlan)));
+            CK(hipMemcpy(dp, pl.data(), pl.size() * sizeof(StagePlan), hipMemcpyHostToDevice));
+            return dp;
+        };
+        StagePlan *pf = build(false, 0, nF), *pr = build(true, 0, n);
+        ref.clear();
+        run("F pass R1 (again, reference)", 2, fbytes, FP(1, false));
+        run("F pass staged", 0, fbytes, [&] { hipLaunchKernelGGL(kstage<0>, dim3(nF / B), dim3(B), 0, 0, d_ell, d_ddf, d_vdf, pf, b, x, y, 0, nF); });
+        run("resid R1 (again, reference)", 3, rbytes, RS(1, false));
+        run("resid staged", 1, rbytes, [&] { hipLaunchKernelGGL(kstage<1>, dim3(nb), dim3(B), 0, 0, d_ell, d_ddf, d_vdf, pr, b, x, y, 0, n); });
+    }
     run("stream floor (codes,b,x,y)", -1, rbytes, [&] { hipLaunchKernelGGL(kstream, dim3(nb), dim3(B), 0, 0, d_ell, x, b, y, n); });
     return 0;
 }
