@@ -93,3 +93,39 @@ def test_spmv_entry_fails_loudly_without_gpu():
             "print('returned')\n") % str(ROOT)
     r = subprocess.run(["python", "-c", code], capture_output=True, text=True, timeout=120)
     assert r.returncode == (-14) % 256 and "returned" not in r.stdout
+
+
+@pytest.mark.parametrize("env,want", [(None, -1), ("full", 0), ("lean", 1), ("bogus", -1)])
+def test_opts_formats_default_and_env(env, want, monkeypatch):
+    """sss_hip_opts.formats: auto (-1) by default -- plain tiles for the exact smoother, every
+    qualifying format otherwise -- SSS_HIP_FORMATS=full|lean force either; the struct's size and the
+    field's offset are the C header's (sss_hip.h)."""
+    if env is None:
+        monkeypatch.delenv("SSS_HIP_FORMATS", raising=False)
+    else:
+        monkeypatch.setenv("SSS_HIP_FORMATS", env)
+    o = N.SSS_HIP_OPTS()
+    A.lib().sss_hip_opts_default(C.byref(o))
+    assert o.formats == want
+    # the ctypes mirror matches the C header's layout (compiled here)
+    import subprocess as sp
+    import tempfile
+    with tempfile.TemporaryDirectory() as d:
+        src = Path(d) / "o.c"
+        src.write_text('#include "sss_hip.h"\n#include <stddef.h>\n'
+                       '_Static_assert(sizeof(sss_hip_opts) == %d, "size");\n'
+                       '_Static_assert(offsetof(sss_hip_opts, formats) == %d, "formats");\n'
+                       % (C.sizeof(N.SSS_HIP_OPTS), N.SSS_HIP_OPTS.formats.offset))
+        sp.run(["gcc", "-std=c11", "-I", str(ROOT / "include"), "-c", str(src), "-o", str(Path(d) / "o.o")], check=True)
+
+
+def test_huge_page_hint_is_harmless():
+    """sss_huge_hint (transparent huge pages for the large host arrays) accepts any pointer and size:
+    small and unaligned ranges are ignored, a large one is advised, and the memory stays intact."""
+    import numpy as np
+    A.lib().sss_huge_hint.argtypes = [C.c_void_p, C.c_size_t]
+    a = np.arange(3 << 20, dtype=np.float64)   # 24 MiB
+    A.lib().sss_huge_hint(a.ctypes.data, a.nbytes)
+    A.lib().sss_huge_hint(a.ctypes.data + 3, 1000)
+    A.lib().sss_huge_hint(None, 0)
+    assert a[12345] == 12345.0 and a[-1] == (3 << 20) - 1
