@@ -46,10 +46,11 @@ def main():
     out = []
     for eng in a.engines.split(","):
         lab = ""
-        if "+" in eng:   # lab: engine+VAR=VALUE sets an environment variable for that engine's run
+        if "+" in eng:   # lab: engine+VAR=VALUE[+VAR=VALUE...] sets environment variables for that run
             eng, lab = eng.split("+", 1)
-            k, v = lab.split("=", 1)
-            os.environ[k] = v
+            for kv in lab.split("+"):
+                k, v = kv.split("=", 1)
+                os.environ[k] = v
         os.environ["SSS_HIP_GS_ENGINE"] = "flow" if eng == "fused" else eng   # fused: all passes in one launch
         os.environ["SSS_HIP_GS_FUSED"] = "1" if eng == "fused" else "0"
         D = A.DeviceHierarchy(H, smoother="exact", coarse="direct", device=0)
@@ -75,8 +76,8 @@ def main():
                   f"eng {info.gs_engine_f}/{info.gs_engine_c} stall {info.gs_stall}  {rec['ms']:9.2f} ms", file=sys.stderr,
                   flush=True)
         D.close()
-        if lab:
-            os.environ.pop(lab.split("=", 1)[0], None)
+        for kv in lab.split("+") if lab else []:
+            os.environ.pop(kv.split("=", 1)[0], None)
     if a.json:
         Path(a.json).write_text(json.dumps(out))
 
