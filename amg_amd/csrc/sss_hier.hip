@@ -977,6 +977,9 @@ static int walk_cycle(sss_hip_hier *h, CoarseFn coarse, bool pend = false)
     int visits[kMaxLevels] = {0};
     int l = 0, rc;
     hipStream_t s = h->stream;
+    // x_l is zero only on arrival by the descent (restricted into, then cleared): a W-cycle's level
+    // re-descended after its post-smoother starts its pre-smoother from that iterate
+    bool zeroed = false;
     for (;;) {
         while (l < nl - 1) {
             if (g_ledger) g_ledger->slot = l;
@@ -988,12 +991,14 @@ static int walk_cycle(sss_hip_hier *h, CoarseFn coarse, bool pend = false)
             auto &L = h->L[l];
             visits[l]++;
             const bool first = l == 0 && visits[0] == 1;
-            // levels >= 1 were just zeroed by the descent: the first pass may skip its products
-            if ((rc = smooth_then_residual(h, l, 0, nullptr, pend && first ? h->pend_f : nullptr, l > 0))) return rc;
+            // levels >= 1 just zeroed by the descent: the first pass may skip its products
+            if ((rc = smooth_then_residual(h, l, 0, nullptr, pend && first ? h->pend_f : nullptr, zeroed && l > 0)))
+                return rc;
             if ((rc = launch_spmv(L.R, SSS_HIP_SPMV_MXY, 1.0, L.wp, nullptr, h->L[l + 1].b, 0, nullptr, s))) return rc;
             l++;
             ledger_add(8.0 * h->L[l].A.n);
             SSS_HIP(hipMemsetAsync(h->L[l].x, 0, sizeof(double) * (size_t)h->L[l].A.n, s));
+            zeroed = true;
         }
         if (g_ledger) g_ledger->slot = kMaxLevels + 1;
         if ((rc = coarse(h))) return rc;
@@ -1030,6 +1035,7 @@ static int walk_cycle(sss_hip_hier *h, CoarseFn coarse, bool pend = false)
             visits[l] = 0;
         }
         if (l <= 0) break;
+        zeroed = false;   // re-descending from level l: x_l holds its post-smoothed iterate
     }
     return 0;
 }

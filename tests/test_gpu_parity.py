@@ -367,6 +367,27 @@ def test_solve_hybrid_jacobi_converges(p32_h, inner, inner_from):
     assert len(rel_g) <= len(rel_ref) + 2
 
 
+@pytest.mark.parametrize("hname", ["p32_h", "a27_h"])
+@pytest.mark.parametrize("inner", [0, 1])
+def test_w_cycle_throughput_matches_oracle(request, hname, inner):
+    """cycle_type = 2 in throughput mode: a level re-descended after its post-smoother (the W-cycle's
+    second visit, Solve/SSS_cycle.cu:959-966) starts its pre-smoother from that iterate, not from
+    the zero the first descent left -- so the zero-iterate first pass (t = b, no matrix read) must
+    not be taken there.  The history follows the oracle's W-cycle in the same per-level
+    configuration."""
+    H = request.getfixturevalue(hname)
+    H.mg.pars.cycle_type = 2
+    try:
+        kw = device_mode_oracle_opts(H, smoother="hybrid", coarse="direct", inner=inner, inner_from=1)
+        rel_o, x_o = _oracle_history(H, **kw)
+        rel_g, x_g = _gpu_history(H, smoother="hybrid", coarse="direct", inner=inner, inner_from=1)
+    finally:
+        H.mg.pars.cycle_type = 1
+    assert len(rel_g) == len(rel_o)
+    assert np.allclose(rel_g, rel_o, rtol=1e-6)
+    assert np.linalg.norm(x_g - x_o) <= 1e-8 * np.linalg.norm(x_o)
+
+
 @pytest.mark.parametrize("hname", ["bus_h", "p32_h", "a27_h"])
 @pytest.mark.parametrize("smoother,coarse", [("exact", "krylov"), ("hybrid", "direct"), ("jacobi", "direct")])
 def test_relabel_is_bitwise_neutral(request, hname, smoother, coarse):
