@@ -406,6 +406,12 @@ struct GsFused {
     int depth = 0, nchunks = 0, grid = 0;
     int *ck = nullptr;                  // chunk -> first position in nodes (nchunks + 1)
     int *nodes = nullptr;               // sweep * n + row, by fused depth
+    // Sweep 0 of a call on a zero iterate (the pre-smoother of a level the descent just cleared):
+    // each row's entries whose version-0 value it would read are exactly zero, so with finite
+    // values (and b_i != -0.0) their products can be dropped from the stored-order chain without
+    // changing a bit -- rows of only the entries read at a later version, in stored order.
+    int *rp0 = nullptr, *ci0 = nullptr;
+    double *v0 = nullptr;
     unsigned *ctl = nullptr;            // epoch, ticket, exit count, error
     unsigned *err = nullptr;
     int spin = 0;
@@ -448,7 +454,7 @@ int gs_persist_error(const PassSchedule &ps, unsigned *out);
 int gs_fused_build(GsFused &f, const SSS_MAT &A, const DevCSR *dA, const PassSchedule *pass, const int *cls,
                    int sweeps);
 int gs_fused_run(const GsFused &f, const DevCSR &A, const double *b, double *x, const double *d_first,
-                 const double *d_later, hipStream_t s);
+                 const double *d_later, bool x_zero, hipStream_t s);
 void gs_fused_free(GsFused &f);
 struct SmootherPlan;
 // Report the one-launch passes' stalls into *err (a word of the owning hierarchy).

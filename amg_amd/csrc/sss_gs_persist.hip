@@ -344,7 +344,9 @@ __global__ __launch_bounds__(kBlock) void gs_fused_group(int nchunks, const int 
                                                          const double *__restrict__ v, const double *__restrict__ b,
                                                          double *x, const double *__restrict__ d_first,
                                                          const double *__restrict__ d_later, unsigned long long *gran,
-                                                         unsigned *ctl, unsigned *err, int spin, int ovl)
+                                                         unsigned *ctl, unsigned *err, int spin, int ovl,
+                                                         const int *__restrict__ rp0, const int *__restrict__ ci0,
+                                                         const double *__restrict__ v0)
 {
     constexpr int R = 64 / G, CAP = kGroupBuf / R, U = 8;
     static_assert(CAP / G == 32, "one pending bit per staged entry of a lane");
@@ -360,14 +362,22 @@ __global__ __launch_bounds__(kBlock) void gs_fused_group(int nchunks, const int 
         const bool active = p < ck[q + 1];
         int i = -1, s = 0, k0 = 0, len = 0;
         double acc = 0.0, dr = 0.0;
+        const int *cr = ci;        // this row's stored entries: all of them, or (rp0 set: the sweep-0
+        const double *vr = v;      // call on a zero iterate) those read at a later version
         if (active) {
             const int node = nodes[p];
             s = node / n;
             i = node - s * n;
-            k0 = rp[i];
-            len = rp[i + 1] - k0;
             acc = b[i];
             dr = (s == 0 ? d_first : d_later)[i];
+            if (rp0 && s == 0 && __double_as_longlong(acc) != (long long)0x8000000000000000ull) {
+                k0 = rp0[i];
+                len = rp0[i + 1] - k0;
+                cr = ci0, vr = v0;
+            } else {
+                k0 = rp[i];
+                len = rp[i + 1] - k0;
+            }
         }
         bool linked = false;   // an off-diagonal entry: some neighbour orders version s of x_i first
         int maxlen = len;
@@ -383,9 +393,9 @@ __global__ __launch_bounds__(kBlock) void gs_fused_group(int nchunks, const int 
                 double a[U], xv[U];
                 unsigned long long ga[U], gc[U];
 #pragma unroll
-                for (int u = 0; u < U; ++u) c[u] = ci[kb + (j0 + u < nj ? gl + G * (j0 + u) : gl)];
+                for (int u = 0; u < U; ++u) c[u] = cr[kb + (j0 + u < nj ? gl + G * (j0 + u) : gl)];
 #pragma unroll
-                for (int u = 0; u < U; ++u) a[u] = v[kb + (j0 + u < nj ? gl + G * (j0 + u) : gl)];
+                for (int u = 0; u < U; ++u) a[u] = vr[kb + (j0 + u < nj ? gl + G * (j0 + u) : gl)];
 #pragma unroll
                 for (int u = 0; u < U; ++u) nd[u] = (j0 + u < nj && c[u] != i) ? fused_need(c[u], i, s, split) : -1;
                 // the group's loads issued together and read after the loop
@@ -425,8 +435,8 @@ __global__ __launch_bounds__(kBlock) void gs_fused_group(int nchunks, const int 
                     const int j = __builtin_ctz(pend);
                     pend &= pend - 1;
                     const int t = gl + G * j;
-                    const int c = ci[kb + t];
-                    mine[t] = v[kb + t] * granule_wait(gran + 2 * (size_t)c, tag(fused_need(c, i, s, split)), err, spin);
+                    const int c = cr[kb + t];
+                    mine[t] = vr[kb + t] * granule_wait(gran + 2 * (size_t)c, tag(fused_need(c, i, s, split)), err, spin);
                 }
                 wave_sync();
                 if (gl == 0 && m > 0) acc = chain_sub_pipe(acc, mine, 0, m);   // (C)
@@ -462,7 +472,7 @@ __global__ __launch_bounds__(kBlock) void gs_fused_group(int nchunks, const int 
                             const unsigned long long *gg = gran + 2 * (size_t)cp;
                             ga[h] = __hip_atomic_load(const_cast<unsigned long long *>(gg), RLX_AGENT);
                             gc[h] = __hip_atomic_load(const_cast<unsigned long long *>(gg + 1), RLX_AGENT);
-                            ap[h] = v[kb + tp[h]];
+                            ap[h] = vr[kb + tp[h]];
                         }
                     }
                 }
@@ -915,6 +925,46 @@ int gs_fused_build(GsFused &f, const SSS_MAT &A, const DevCSR *dA, const PassSch
     SSS_HIP(hipMemcpy(f.nodes, order.data(), sizeof(int) * order.size(), hipMemcpyHostToDevice));
     SSS_HIP(hipMemset(f.gran, 0, sizeof(unsigned long long) * 2 * (size_t)n));
     SSS_HIP(hipMemset(f.ctl, 0, sizeof(unsigned) * kCtlWords));
+    {   // sweep-0 rows on a zero iterate (finite values only): the entries read at version 1
+        const double *av = A.val;
+        std::atomic<bool> fin{true};
+        parallel_chunks(n, 1 << 16, [&](int a, int e) {
+            for (long long k = rp[a]; k < rp[e] && fin; ++k)
+                if (!std::isfinite(av[k])) fin = false;
+        });
+        if (fin) {
+            std::vector<int> r0((size_t)n + 1, 0);
+            auto keep = [&](int i, int j) { return j != i && ((cls[j] == cls[i]) ? j < i : cls[j] == 0); };
+            parallel_chunks(n, 4096, [&](int a, int e) {
+                for (int i = a; i < e; ++i) {
+                    int c = 0;
+                    for (int k = rp[i]; k < rp[i + 1]; ++k) c += keep(i, ci[k]);
+                    r0[(size_t)i + 1] = c;
+                }
+            });
+            for (int i = 0; i < n; ++i) r0[(size_t)i + 1] += r0[(size_t)i];
+            HostBuf<int> c0;
+            HostBuf<double> w0;
+            c0.resize((size_t)std::max(r0[(size_t)n], 1)), w0.resize((size_t)std::max(r0[(size_t)n], 1));
+            parallel_chunks(n, 4096, [&](int a, int e) {
+                for (int i = a; i < e; ++i) {
+                    int o = r0[(size_t)i];
+                    for (int k = rp[i]; k < rp[i + 1]; ++k)
+                        if (keep(i, ci[k])) c0[(size_t)o] = ci[k], w0[(size_t)o] = av[k], ++o;
+                }
+            });
+            f.rp0 = dev_alloc<int>(r0.size());
+            f.ci0 = dev_alloc<int>(c0.size());
+            f.v0 = dev_alloc<double>(w0.size());
+            if (!f.rp0 || !f.ci0 || !f.v0) {
+                gs_fused_free(f);
+                return hip_fail(hipErrorOutOfMemory, "hipMalloc(gs fused rows)", __FILE__, __LINE__);
+            }
+            SSS_HIP(hipMemcpy(f.rp0, r0.data(), sizeof(int) * r0.size(), hipMemcpyHostToDevice));
+            SSS_HIP(hipMemcpy(f.ci0, c0.data(), sizeof(int) * c0.size(), hipMemcpyHostToDevice));
+            SSS_HIP(hipMemcpy(f.v0, w0.data(), sizeof(double) * w0.size(), hipMemcpyHostToDevice));
+        }
+    }
     f.err = f.ctl + kCtlErr;
     int cus = 256;
     {
@@ -937,6 +987,9 @@ int gs_fused_build(GsFused &f, const SSS_MAT &A, const DevCSR *dA, const PassSch
 
 void gs_fused_free(GsFused &f)
 {
+    dev_free(f.rp0);
+    dev_free(f.ci0);
+    dev_free(f.v0);
     dev_free(f.ck);
     dev_free(f.nodes);
     dev_free(f.gran);
@@ -945,13 +998,13 @@ void gs_fused_free(GsFused &f)
 }
 
 int gs_fused_run(const GsFused &f, const DevCSR &A, const double *b, double *x, const double *d_first,
-                 const double *d_later, hipStream_t s)
+                 const double *d_later, bool x_zero, hipStream_t s)
 {
     if (!f.engine) return ERROR_INPUT_PAR;
     auto go = [&](auto kern) {
         hipLaunchKernelGGL(kern, dim3(f.grid), dim3(kBlock), 0, s, f.nchunks, f.ck, f.nodes, f.n, f.split,
                            f.sweeps - 1, A.rp, A.ci, A.v, b, x, d_first, d_later, f.gran, f.ctl, f.err, f.spin,
-                           f.overlap ? 1 : 0);
+                           f.overlap ? 1 : 0, x_zero ? f.rp0 : (const int *)nullptr, f.ci0, f.v0);
     };
     switch (f.G) {   // (every G the planner can choose; the chunk table holds 64 / G rows per ticket)
     case 2: go(gs_fused_group<2>); break;

@@ -1341,7 +1341,7 @@ int smoother_run(const SmootherPlan &sp, const DevCSR &A, const double *b, doubl
     if (sp.fz.engine && sweeps == sp.fz.sweeps && !hk && !pre_f) {
         for (int sw = 0; sw < sweeps; ++sw)
             for (const auto &ps : sp.pass) ledger_pass(A, ps, 24.0);
-        return gs_fused_run(sp.fz, A, b, x, sp.d_first, sp.d_later, s);
+        return gs_fused_run(sp.fz, A, b, x, sp.d_first, sp.d_later, x_zero, s);
     }
     const int n = A.n;
     if (n == 0) return 0;
