@@ -56,20 +56,15 @@ struct CoarseKrylov {
 // Sequential-order sums inside one workgroup.  Up to three independent sums run concurrently
 // (lanes 0, 64, 128 — three waves); each region holds one chunk of products.
 struct SeqSmem {
-    double reg[3][kSeqChunk];
+    alignas(16) double reg[3][kSeqChunk];
     double bcast[4];
 };
 
+// s + buf[0] + buf[1] + ... in order; the pipelined chain hides the LDS read latency (the
+// additions and their order are unchanged; k_cg_step at 400^3 77.6 -> 72.0 us, k_mgs 469 -> 367)
 __device__ __forceinline__ double seq_add_chunk(double s, const double *buf, int m)
 {
-    int k = 0;
-    for (; k + 8 <= m; k += 8) {
-        const double a0 = buf[k], a1 = buf[k + 1], a2 = buf[k + 2], a3 = buf[k + 3];
-        const double a4 = buf[k + 4], a5 = buf[k + 5], a6 = buf[k + 6], a7 = buf[k + 7];
-        s += a0; s += a1; s += a2; s += a3; s += a4; s += a5; s += a6; s += a7;
-    }
-    for (; k < m; ++k) s += buf[k];
-    return s;
+    return chain_pipe16<false>(s, buf, 0, m);
 }
 
 // returns sum_i x_i*y_i in index order (valid in every thread)
@@ -179,6 +174,45 @@ __global__ __launch_bounds__(kSeqBlock) void k_cg_init(int n, const double *__re
     }
 }
 
+// The step's scalar part (thread 0): iteration counters, best-so-far, check I and the II/III
+// triggers.  flags[0]: copy u to u_best; flags[1]: p = z + p now (no residual check pending).
+__device__ void cg_step_state(CgState *st, int k, double alpha, const double (&sq)[3], double infnormu, int *flags)
+{
+    CgState s = *st;
+    s.iter = k;
+    s.alpha = alpha;
+    s.absres = sqrt(sq[0]);
+    s.relres = s.absres / s.normr0;
+    int copy_best = 0;
+    if (s.absres < s.absres_best - s.maxdiff) {
+        s.absres_best = s.absres;
+        s.iter_best = k;
+        copy_best = 1;
+    }
+    s.flag_resid = 0;
+    s.stag_fire = 0;
+    if (infnormu <= SMALLFLOAT) {
+        s.iter = ERROR_SOLVER_SOLSTAG;
+        s.mode = CG_STOP;
+    } else {
+        const double normu = sqrt(sq[1]);
+        const double reldiff = fabs(alpha) * sqrt(sq[2]) / normu;
+        s.stag_fire = (s.stag <= max_STAG) & (reldiff < s.maxdiff);
+        s.flag_resid = s.stag_fire || s.relres < s.tol;
+    }
+    const int finish_here = s.mode == CG_RUN && !s.flag_resid;
+    if (finish_here) {
+        s.absres0 = s.absres;
+        if (k >= s.maxit) {               // while (iter++ < matrix) ends: iter = matrix + 1
+            s.mode = CG_STOP;
+            s.iter = s.maxit + 1;
+        }
+    }
+    *st = s;
+    flags[0] = copy_best;
+    flags[1] = finish_here;
+}
+
 // The CG step after t += A*p: alpha, updates, norms, best-so-far, checks I and II/III triggers.
 __global__ __launch_bounds__(kSeqBlock) void k_cg_step(int n, int k, double *__restrict__ u, double *__restrict__ r,
                                                        double *__restrict__ p, const double *__restrict__ t,
@@ -202,46 +236,93 @@ __global__ __launch_bounds__(kSeqBlock) void k_cg_step(int n, int k, double *__r
     double sq[3];
     seq_dots<3>(n, xs, ys, sq, sm);
     const double infnormu = block_absmax(n, u, sm);
-    if (threadIdx.x == 0) {
-        CgState s = *st;
-        s.iter = k;
-        s.alpha = alpha;
-        s.absres = sqrt(sq[0]);
-        s.relres = s.absres / s.normr0;
-        int copy_best = 0;
-        if (s.absres < s.absres_best - s.maxdiff) {
-            s.absres_best = s.absres;
-            s.iter_best = k;
-            copy_best = 1;
-        }
-        s.flag_resid = 0;
-        s.stag_fire = 0;
-        if (infnormu <= SMALLFLOAT) {
-            s.iter = ERROR_SOLVER_SOLSTAG;
-            s.mode = CG_STOP;
-        } else {
-            const double normu = sqrt(sq[1]);
-            const double reldiff = fabs(alpha) * sqrt(sq[2]) / normu;
-            s.stag_fire = (s.stag <= max_STAG) & (reldiff < s.maxdiff);
-            s.flag_resid = s.stag_fire || s.relres < s.tol;
-        }
-        const int finish_here = s.mode == CG_RUN && !s.flag_resid;
-        if (finish_here) {
-            s.absres0 = s.absres;
-            if (k >= s.maxit) {               // while (iter++ < matrix) ends: iter = matrix + 1
-                s.mode = CG_STOP;
-                s.iter = s.maxit + 1;
-            }
-        }
-        *st = s;
-        s_flags[0] = copy_best;
-        s_flags[1] = finish_here;
-    }
+    if (threadIdx.x == 0) cg_step_state(st, k, alpha, sq, infnormu, s_flags);
     __syncthreads();
     if (s_flags[0])
         for (int i = threadIdx.x; i < n; i += blockDim.x) u_best[i] = u[i];
     if (s_flags[1])
         for (int i = threadIdx.x; i < n; i += blockDim.x) p[i] = 1.0 * r[i] + 1.0 * p[i];
+}
+
+// k_cg_step for n <= kRegVec * kSeqBlock (the usual coarsest grid): t, p, u, r are read once into
+// registers with every load in flight, the updated u / r / p are written from registers, and the
+// infinity norm of u is reduced while lanes 0 / 64 / 128 run the three chains.  The arithmetic
+// and every sum's order are those of k_cg_step (tests/test_gpu_parity.py::test_cg_step_forms).
+constexpr int kRegVec = 4;
+__global__ __launch_bounds__(kSeqBlock) void k_cg_step_reg(int n, int k, double *__restrict__ u,
+                                                           double *__restrict__ r, double *__restrict__ p,
+                                                           const double *__restrict__ t,
+                                                           double *__restrict__ u_best, CgState *st)
+{
+    __shared__ SeqSmem sm;
+    __shared__ double s_absw[kSeqBlock / 64];
+    __shared__ int s_flags[2];
+    if (st->mode != CG_RUN) return;
+    const int tid = threadIdx.x, lane = tid & 63;
+    double tv[kRegVec], pv[kRegVec], uv[kRegVec], rv[kRegVec];
+#pragma unroll
+    for (int j = 0; j < kRegVec; ++j) {
+        const int i = tid + j * kSeqBlock;
+        const bool in = i < n;
+        tv[j] = in ? t[i] : 0.0;
+        pv[j] = in ? p[i] : 0.0;
+        uv[j] = in ? u[i] : 0.0;
+        rv[j] = in ? r[i] : 0.0;
+    }
+#pragma unroll
+    for (int j = 0; j < kRegVec; ++j) {
+        const int i = tid + j * kSeqBlock;
+        if (i < n) sm.reg[0][i] = tv[j] * pv[j];
+    }
+    __syncthreads();
+    if (tid == 0) sm.bcast[0] = chain_pipe16<false>(0.0, sm.reg[0], 0, n);
+    __syncthreads();
+    const double temp2 = sm.bcast[0];
+    if (!(fabs(temp2) > SMALLFLOAT2)) {                 // possible breakdown: goto RESTORE_BESTSOL
+        if (tid == 0) { st->mode = CG_STOP; st->iter = k; }
+        return;
+    }
+    const double alpha = st->temp1 / temp2;
+    double m = 0.0;
+#pragma unroll
+    for (int j = 0; j < kRegVec; ++j) {
+        const int i = tid + j * kSeqBlock;
+        if (i < n) {
+            uv[j] = uv[j] + alpha * pv[j];
+            rv[j] = rv[j] + -alpha * tv[j];
+            u[i] = uv[j];
+            r[i] = rv[j];
+            sm.reg[0][i] = rv[j] * rv[j];
+            sm.reg[1][i] = uv[j] * uv[j];
+            sm.reg[2][i] = pv[j] * pv[j];
+            m = fmax(m, fabs(uv[j]));
+        }
+    }
+    for (int off = 32; off > 0; off >>= 1) m = fmax(m, __shfl_xor(m, off, 64));
+    if (lane == 0) s_absw[tid >> 6] = m;
+    __syncthreads();
+    if (tid < 192 && lane == 0) {
+        sm.bcast[tid >> 6] = chain_pipe16<false>(0.0, sm.reg[tid >> 6], 0, n);
+    } else if (tid == 192) {
+        double a = 0.0;
+        for (int w = 0; w < kSeqBlock / 64; ++w) a = fmax(a, s_absw[w]);
+        sm.bcast[3] = a;
+    }
+    __syncthreads();
+    if (tid == 0) {
+        const double sq[3] = {sm.bcast[0], sm.bcast[1], sm.bcast[2]};
+        cg_step_state(st, k, alpha, sq, sm.bcast[3], s_flags);
+    }
+    __syncthreads();
+    const int copy_best = s_flags[0], finish_here = s_flags[1];
+#pragma unroll
+    for (int j = 0; j < kRegVec; ++j) {
+        const int i = tid + j * kSeqBlock;
+        if (i < n) {
+            if (copy_best) u_best[i] = uv[j];
+            if (finish_here) p[i] = 1.0 * rv[j] + 1.0 * pv[j];
+        }
+    }
 }
 
 // After the gated residual re-computation: checks II (stagnation) and III (false convergence).
@@ -430,6 +511,8 @@ static int run_cg(CoarseKrylov *k, const DevCSR &A, const double *b, double *u, 
                   int *status)
 {
     const int n = k->n, nblk = A.nblk;
+    const char *cr = getenv("SSS_HIP_CG_REG");   // "0": the LDS-chunked step at every size (test hook)
+    const bool reg_step = !(cr && cr[0] == '0') && n <= kRegVec * kSeqBlock;
     SSS_HIP(hipMemsetAsync(k->t, 0, sizeof(double) * n, s));
     SSS_HIP(hipMemsetAsync(k->u_best, 0, sizeof(double) * n, s));
     hipLaunchKernelGGL(k_resid, dim3(nblk), dim3(kBlock), 0, s, A.blk, A.rp, A.ci, A.v, u, b, k->r, k->cap,
@@ -438,7 +521,12 @@ static int run_cg(CoarseKrylov *k, const DevCSR &A, const double *b, double *u, 
     for (int it = 1; it <= maxit; ++it) {
         hipLaunchKernelGGL(k_acc, dim3(nblk), dim3(kBlock), 0, s, A.blk, A.rp, A.ci, A.v, k->p, k->t, k->cap,
                            (const CgState *)k->st);
-        hipLaunchKernelGGL(k_cg_step, dim3(1), dim3(kSeqBlock), 0, s, n, it, u, k->r, k->p, k->t, k->u_best, k->st);
+        if (reg_step)
+            hipLaunchKernelGGL(k_cg_step_reg, dim3(1), dim3(kSeqBlock), 0, s, n, it, u, k->r, k->p, k->t, k->u_best,
+                               k->st);
+        else
+            hipLaunchKernelGGL(k_cg_step, dim3(1), dim3(kSeqBlock), 0, s, n, it, u, k->r, k->p, k->t, k->u_best,
+                               k->st);
         hipLaunchKernelGGL(k_resid, dim3(nblk), dim3(kBlock), 0, s, A.blk, A.rp, A.ci, A.v, u, b, k->r, k->cap,
                            (const CgState *)k->st, 1);
         hipLaunchKernelGGL(k_cg_fix, dim3(1), dim3(kSeqBlock), 0, s, n, it, k->r, k->p, k->st);

@@ -16,7 +16,7 @@ namespace sss {
 __device__ __forceinline__ int xcd_bid() { return blockIdx.x; }
 
 struct SpmvSmem {
-    double v[kTileEntries];    // products a_k * x_{c_k} of the tile
+    alignas(16) double v[kTileEntries];    // products a_k * x_{c_k} of the tile (chain_pipe16 reads pairs)
     double red[kBlock / 64];
     double d[kBlock];          // sorted tiles: the raw diagonal value of each row of the block
 };
@@ -353,6 +353,7 @@ __device__ __forceinline__ double chain_sub(double s, const double *p, int a, in
 // 16-byte pairs while the current 16 are added -- tools/chain_lab.hip on MI355X: 10.0 cycles per
 // entry against 13.4 for eight 8-byte reads ahead, the dependent fp64 subtraction alone 8.5.  p must
 // be 16-byte aligned.
+constexpr int kPipeRowMin = 64;   // csr_block_rows: rows from this length chain with chain_pipe16
 template <bool SUB>
 __device__ __forceinline__ double chain_pipe16(double s, const double *p, int a, int e)
 {
@@ -702,7 +703,9 @@ __device__ __forceinline__ double csr_block_rows(const BlkT *__restrict__ blk, c
         else stage_products(sm.v, k0, k1, ci, v, x);
         __syncthreads();
         if (r < r1) {
-            const double s = chain_add(0.0, sm.v, ra - k0, re - k0);
+            // rows of 64+ entries: the pipelined chain (same additions in the same order)
+            const double s = re - ra >= kPipeRowMin ? chain_pipe16<false>(0.0, sm.v, ra - k0, re - k0)
+                                                    : chain_add(0.0, sm.v, ra - k0, re - k0);
             contrib = epi(r, s);
         }
     } else {
@@ -717,7 +720,7 @@ __device__ __forceinline__ double csr_block_rows(const BlkT *__restrict__ blk, c
                 const double c = block_tree_sum(sm.v, 0, m, sm.red);
                 if (threadIdx.x == 0) s += c;
             } else if (threadIdx.x == 0) {
-                s = chain_add(s, sm.v, 0, m);
+                s = chain_pipe16<false>(s, sm.v, 0, m);
             }
             __syncthreads();
         }

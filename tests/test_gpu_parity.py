@@ -260,8 +260,11 @@ def test_cf_jacobi_bitwise(request, hname, row_path):
 
 
 # ---------------------------------------------------------------- coarse solve
+@pytest.mark.parametrize("step", ["reg", "lds"])
 @pytest.mark.parametrize("hname", ["bus_h", "p32_h", "a27_h"])
-def test_coarse_krylov_matches_oracle(request, hname):
+def test_coarse_krylov_matches_oracle(request, hname, step, monkeypatch):
+    """Both CG step kernels (register-resident, n <= 4096; LDS-chunked, SSS_HIP_CG_REG=0)."""
+    monkeypatch.setenv("SSS_HIP_CG_REG", "1" if step == "reg" else "0")
     H = request.getfixturevalue(hname)
     Lc = H.level(H.num_levels - 1)
     n = Lc.A.num_rows
@@ -270,6 +273,22 @@ def test_coarse_krylov_matches_oracle(request, hname):
     xg, xr = np.zeros(n), np.zeros(n)
     assert _lib().sss_hip_host_coarse_solve(C.byref(Lc.A), C.byref(vec(b)), C.byref(vec(xg)), 1e-7, 0, 0) == 0
     oracle.load().ora_coarest_solve(C.byref(Lc.A), C.byref(vec(b)), C.byref(vec(xr)), 1e-7,
+                                    C.byref(oracle.opts()))
+    assert np.array_equal(xg.view(np.uint64), xr.view(np.uint64))
+
+
+@pytest.mark.parametrize("step", ["reg", "lds"])
+@pytest.mark.parametrize("lo,hi", [(1025, 4096), (4097, 40000)])
+def test_coarse_krylov_larger_grids(p32_h, lo, hi, step, monkeypatch):
+    """A finer level as the 'coarsest' matrix: several entries per thread in the register step
+    (1025..4096 rows), the LDS-chunked step past 4096 rows and its multi-chunk sequential sums."""
+    monkeypatch.setenv("SSS_HIP_CG_REG", "1" if step == "reg" else "0")
+    L = next(p32_h.level(l) for l in range(p32_h.num_levels) if lo <= p32_h.level(l).A.num_rows <= hi)
+    n = L.A.num_rows
+    b = np.random.default_rng(4).standard_normal(n)
+    xg, xr = np.zeros(n), np.zeros(n)
+    assert _lib().sss_hip_host_coarse_solve(C.byref(L.A), C.byref(vec(b)), C.byref(vec(xg)), 1e-7, 0, 0) == 0
+    oracle.load().ora_coarest_solve(C.byref(L.A), C.byref(vec(b)), C.byref(vec(xr)), 1e-7,
                                     C.byref(oracle.opts()))
     assert np.array_equal(xg.view(np.uint64), xr.view(np.uint64))
 
