@@ -461,6 +461,31 @@ __device__ __forceinline__ void stage_products(double *__restrict__ sm, int k0, 
     }
 }
 
+// As stage_products, by `nt` threads of the block (this one is thread `t` of them).
+__device__ __forceinline__ void stage_products_part(double *__restrict__ sm, int k0, int k1,
+                                                    const int *__restrict__ ci, const double *__restrict__ v,
+                                                    const double *x, int t, int nt)
+{
+    constexpr int U = 8;
+    for (int kb = k0 + t; kb < k1; kb += U * nt) {
+        int j[U];
+        double a[U], xv[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int k = kb + u * nt;
+            j[u] = k < k1 ? ci[k] : -1;
+            a[u] = k < k1 ? v[k] : 0.0;
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) xv[u] = j[u] >= 0 ? x[j[u]] : 0.0;
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int k = kb + u * nt;
+            if (k < k1) sm[k - k0] = j[u] >= 0 ? a[u] * xv[u] : 0.0;
+        }
+    }
+}
+
 // As stage_products, with the x value of each (possibly encoded) column supplied by `fetch`.
 template <class Fetch>
 __device__ __forceinline__ void stage_products_f(double *__restrict__ sm, int k0, int k1, const int *__restrict__ ci,
@@ -708,6 +733,22 @@ __device__ __forceinline__ double csr_block_rows(const BlkT *__restrict__ blk, c
                                                     : chain_add(0.0, sm.v, ra - k0, re - k0);
             contrib = epi(r, s);
         }
+    } else if (!ds && !pk) {
+        // one long row, plain CSR: halves of the tile as a double buffer -- wave 0's lane 0 chains
+        // one half while waves 1-3 stage the next (the same additions in the same order)
+        constexpr int H = kTileEntries / 2;
+        double s = 0.0;
+        stage_products(sm.v, k0, min(k0 + H, k1), ci, v, x);
+        __syncthreads();
+        for (int base = k0, c = 0; base < k1; base += H, ++c) {
+            const int m = min(H, k1 - base), nb = base + H;
+            double *cur = sm.v + (c & 1) * H, *nxt = sm.v + ((c + 1) & 1) * H;
+            if (threadIdx.x == 0) s = chain_pipe16<false>(s, cur, 0, m);
+            else if (threadIdx.x >= 64 && nb < k1)
+                stage_products_part(nxt, nb, min(nb + H, k1), ci, v, x, (int)threadIdx.x - 64, kBlock - 64);
+            __syncthreads();
+        }
+        if (threadIdx.x == 0) contrib = epi(r0, s);
     } else {
         double s = 0.0;
         for (int base = k0; base < k1; base += kTileEntries) {

@@ -293,6 +293,28 @@ def test_coarse_krylov_larger_grids(p32_h, lo, hi, step, monkeypatch):
     assert np.array_equal(xg.view(np.uint64), xr.view(np.uint64))
 
 
+def test_coarse_krylov_long_rows():
+    """Rows longer than one tile (2,048 entries) -- the double-buffered block-row chain -- in the
+    coarse CG / GMRES SpMVs: a 2,600-row matrix whose first 24 rows and columns are dense."""
+    import scipy.sparse as sp
+    n, k = 2600, 24
+    rng = np.random.default_rng(12)
+    S = sp.random(n, n, density=6.0 / n, random_state=rng, format="csr")
+    D = sp.lil_matrix((n, n))
+    D[:k, :] = rng.uniform(-1.0, 1.0, (k, n))
+    M = S + S.T + D + D.T
+    M = (M + sp.diags(np.asarray(abs(M).sum(axis=1)).ravel() + 1.0)).tocsr()
+    M.sort_indices()
+    assert np.diff(M.indptr).max() > 2048
+    hold = A.NumpyCSR(M.indptr, M.indices, M.data)
+    b = rng.standard_normal(n)
+    xg, xr = np.zeros(n), np.zeros(n)
+    assert _lib().sss_hip_host_coarse_solve(C.byref(hold.mat), C.byref(vec(b)), C.byref(vec(xg)), 1e-7, 0, 0) == 0
+    oracle.load().ora_coarest_solve(C.byref(hold.mat), C.byref(vec(b)), C.byref(vec(xr)), 1e-7,
+                                    C.byref(oracle.opts()))
+    assert np.array_equal(xg.view(np.uint64), xr.view(np.uint64))
+
+
 @pytest.mark.parametrize("cap", [0, 40])
 def test_coarse_krylov_row_cap(bus_h, cap):
     """The as-shipped <<<64,64>>> row cap (rows >= cap untouched by the coarse SpMVs)."""
