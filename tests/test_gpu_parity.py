@@ -293,6 +293,23 @@ def test_coarse_krylov_larger_grids(p32_h, lo, hi, step, monkeypatch):
     assert np.array_equal(xg.view(np.uint64), xr.view(np.uint64))
 
 
+@pytest.mark.parametrize("n", [1, 2, 1024, 4095, 4096, 4097])
+def test_coarse_krylov_step_sizes(n):
+    """The register CG step at its size edges (one entry per thread up to four; 4097 rows take the
+    LDS-chunked step): a shifted 1-D Laplacian with a random right-hand side."""
+    import scipy.sparse as sp
+    M = sp.diags([-np.ones(n - 1), np.full(n, 2.05), -np.ones(n - 1)], [-1, 0, 1], format="csr") \
+        if n > 1 else sp.csr_matrix(np.array([[2.05]]))
+    M.sort_indices()
+    hold = A.NumpyCSR(M.indptr, M.indices, M.data)
+    b = np.random.default_rng(n).standard_normal(n)
+    xg, xr = np.zeros(n), np.zeros(n)
+    assert _lib().sss_hip_host_coarse_solve(C.byref(hold.mat), C.byref(vec(b)), C.byref(vec(xg)), 1e-7, 0, 0) == 0
+    oracle.load().ora_coarest_solve(C.byref(hold.mat), C.byref(vec(b)), C.byref(vec(xr)), 1e-7,
+                                    C.byref(oracle.opts()))
+    assert np.array_equal(xg.view(np.uint64), xr.view(np.uint64))
+
+
 def test_coarse_krylov_long_rows():
     """Rows longer than one tile (2,048 entries) -- the double-buffered block-row chain -- in the
     coarse CG / GMRES SpMVs: a 2,600-row matrix whose first 24 rows and columns are dense."""
