@@ -175,7 +175,8 @@ __global__ __launch_bounds__(kSeqBlock) void k_cg_init(int n, const double *__re
 }
 
 // The step's scalar part (thread 0): iteration counters, best-so-far, check I and the II/III
-// triggers.  flags[0]: copy u to u_best; flags[1]: p = z + p now (no residual check pending).
+// triggers.  flags[0]: copy u to u_best; flags[1]: p = z + p now (no residual check pending);
+// flags[2]: a residual check is pending (k_resid gate 1 + k_cg_fix).
 __device__ void cg_step_state(CgState *st, int k, double alpha, const double (&sq)[3], double infnormu, int *flags)
 {
     CgState s = *st;
@@ -211,7 +212,11 @@ __device__ void cg_step_state(CgState *st, int k, double alpha, const double (&s
     *st = s;
     flags[0] = copy_best;
     flags[1] = finish_here;
+    flags[2] = s.mode == CG_RUN && s.flag_resid;
 }
+
+__device__ void cg_fix_body(int n, int k, const double *__restrict__ r, double *__restrict__ p, CgState *st,
+                            SeqSmem &sm, int &s_pmode);
 
 // The CG step after t += A*p: alpha, updates, norms, best-so-far, checks I and II/III triggers.
 __global__ __launch_bounds__(kSeqBlock) void k_cg_step(int n, int k, double *__restrict__ u, double *__restrict__ r,
@@ -219,7 +224,7 @@ __global__ __launch_bounds__(kSeqBlock) void k_cg_step(int n, int k, double *__r
                                                        double *__restrict__ u_best, CgState *st)
 {
     __shared__ SeqSmem sm;
-    __shared__ int s_flags[2];
+    __shared__ int s_flags[3];
     if (st->mode != CG_RUN) return;
     const double temp2 = seq_dot1(n, t, p, sm);
     if (!(fabs(temp2) > SMALLFLOAT2)) {                 // possible breakdown: goto RESTORE_BESTSOL
@@ -246,17 +251,24 @@ __global__ __launch_bounds__(kSeqBlock) void k_cg_step(int n, int k, double *__r
 
 // k_cg_step for n <= kRegVec * kSeqBlock (the usual coarsest grid): t, p, u, r are read once into
 // registers with every load in flight, the updated u / r / p are written from registers, and the
-// infinity norm of u is reduced while lanes 0 / 64 / 128 run the three chains.  The arithmetic
-// and every sum's order are those of k_cg_step (tests/test_gpu_parity.py::test_cg_step_forms).
+// infinity norm of u is reduced while lanes 0 / 64 / 128 run the three chains.  When the step asks
+// for a residual check (rare: checks II / III), this workgroup recomputes r = b - A*u itself (one
+// thread per row, stored order from 0.0, as k_resid) and runs k_cg_fix's body, so an iteration is
+// two launches instead of four.  The arithmetic and every sum's order are those of k_cg_step +
+// k_resid + k_cg_fix (tests/test_gpu_parity.py, SSS_HIP_CG_REG=0 / 1).
 constexpr int kRegVec = 4;
 __global__ __launch_bounds__(kSeqBlock) void k_cg_step_reg(int n, int k, double *__restrict__ u,
                                                            double *__restrict__ r, double *__restrict__ p,
                                                            const double *__restrict__ t,
-                                                           double *__restrict__ u_best, CgState *st)
+                                                           double *__restrict__ u_best, CgState *st,
+                                                           const int *__restrict__ rp, const int *__restrict__ ci,
+                                                           const double *__restrict__ v,
+                                                           const double *__restrict__ b, int cap)
 {
     __shared__ SeqSmem sm;
     __shared__ double s_absw[kSeqBlock / 64];
-    __shared__ int s_flags[2];
+    __shared__ int s_flags[3];
+    __shared__ int s_pmode;
     if (st->mode != CG_RUN) return;
     const int tid = threadIdx.x, lane = tid & 63;
     double tv[kRegVec], pv[kRegVec], uv[kRegVec], rv[kRegVec];
@@ -323,15 +335,38 @@ __global__ __launch_bounds__(kSeqBlock) void k_cg_step_reg(int n, int k, double 
             if (finish_here) p[i] = 1.0 * rv[j] + 1.0 * pv[j];
         }
     }
+    if (!s_flags[2]) return;
+    // k_resid gate 1: r = b - A*u on rows < cap (u as written above; the barriers since order it)
+    for (int row = tid; row < n; row += kSeqBlock) {
+        if (cap > 0 && row >= cap) {
+            r[row] = b[row];
+            continue;
+        }
+        const int e = rp[row + 1];
+        double acc = 0.0;
+        int kk = rp[row];
+        for (; kk + 4 <= e; kk += 4) {
+            int c[4];
+            double a[4], xv[4];
+#pragma unroll
+            for (int h = 0; h < 4; ++h) c[h] = ci[kk + h], a[h] = v[kk + h];
+#pragma unroll
+            for (int h = 0; h < 4; ++h) xv[h] = c[h] >= 0 ? u[c[h]] : 0.0;
+#pragma unroll
+            for (int h = 0; h < 4; ++h) acc += c[h] >= 0 ? a[h] * xv[h] : 0.0;
+        }
+        for (; kk < e; ++kk) acc += ci[kk] >= 0 ? v[kk] * u[ci[kk]] : 0.0;
+        r[row] = b[row] + acc * -1.0;
+    }
+    __syncthreads();
+    cg_fix_body(n, k, r, p, st, sm, s_pmode);
 }
 
 // After the gated residual re-computation: checks II (stagnation) and III (false convergence).
-__global__ __launch_bounds__(kSeqBlock) void k_cg_fix(int n, int k, const double *__restrict__ r,
-                                                      double *__restrict__ p, CgState *st)
+// Every thread of the workgroup calls it; s_pmode is a __shared__ int.
+__device__ void cg_fix_body(int n, int k, const double *__restrict__ r, double *__restrict__ p, CgState *st,
+                            SeqSmem &sm, int &s_pmode)
 {
-    __shared__ SeqSmem sm;
-    __shared__ int s_pmode;   // 0: no p update, 1: p = z + p, 2: p = z + 0
-    if (st->mode != CG_RUN || !st->flag_resid) return;
     const double a3 = sqrt(seq_dot1(n, r, r, sm));
     if (threadIdx.x == 0) {
         CgState s = *st;
@@ -364,6 +399,15 @@ __global__ __launch_bounds__(kSeqBlock) void k_cg_fix(int n, int k, const double
     __syncthreads();
     if (s_pmode)
         for (int i = threadIdx.x; i < n; i += blockDim.x) p[i] = 1.0 * r[i] + 1.0 * (s_pmode == 2 ? 0.0 : p[i]);
+}
+
+__global__ __launch_bounds__(kSeqBlock) void k_cg_fix(int n, int k, const double *__restrict__ r,
+                                                      double *__restrict__ p, CgState *st)
+{
+    __shared__ SeqSmem sm;
+    __shared__ int s_pmode;   // 0: no p update, 1: p = z + p, 2: p = z + 0
+    if (st->mode != CG_RUN || !st->flag_resid) return;
+    cg_fix_body(n, k, r, p, st, sm, s_pmode);
 }
 
 __global__ __launch_bounds__(kSeqBlock) void k_cg_restore(int n, double *__restrict__ u,
@@ -521,15 +565,16 @@ static int run_cg(CoarseKrylov *k, const DevCSR &A, const double *b, double *u, 
     for (int it = 1; it <= maxit; ++it) {
         hipLaunchKernelGGL(k_acc, dim3(nblk), dim3(kBlock), 0, s, A.blk, A.rp, A.ci, A.v, k->p, k->t, k->cap,
                            (const CgState *)k->st);
-        if (reg_step)
+        if (reg_step) {
             hipLaunchKernelGGL(k_cg_step_reg, dim3(1), dim3(kSeqBlock), 0, s, n, it, u, k->r, k->p, k->t, k->u_best,
-                               k->st);
-        else
+                               k->st, A.rp, A.ci, A.v, b, k->cap);
+        } else {
             hipLaunchKernelGGL(k_cg_step, dim3(1), dim3(kSeqBlock), 0, s, n, it, u, k->r, k->p, k->t, k->u_best,
                                k->st);
-        hipLaunchKernelGGL(k_resid, dim3(nblk), dim3(kBlock), 0, s, A.blk, A.rp, A.ci, A.v, u, b, k->r, k->cap,
-                           (const CgState *)k->st, 1);
-        hipLaunchKernelGGL(k_cg_fix, dim3(1), dim3(kSeqBlock), 0, s, n, it, k->r, k->p, k->st);
+            hipLaunchKernelGGL(k_resid, dim3(nblk), dim3(kBlock), 0, s, A.blk, A.rp, A.ci, A.v, u, b, k->r, k->cap,
+                               (const CgState *)k->st, 1);
+            hipLaunchKernelGGL(k_cg_fix, dim3(1), dim3(kSeqBlock), 0, s, n, it, k->r, k->p, k->st);
+        }
         if (it % kPoll == 0 || it == maxit || it == 1) {
             SSS_HIP(hipMemcpyAsync(k->h_st, k->st, sizeof(CgState), hipMemcpyDeviceToHost, s));
             SSS_HIP(hipStreamSynchronize(s));
