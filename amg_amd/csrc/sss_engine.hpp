@@ -403,6 +403,7 @@ struct GsFused {
     int n = 0, split = 0;               // rows; F rows [0, split), C rows [split, n)
     int G = 64;                         // lanes per row
     bool overlap = false;               // the chain runs while pending granules are polled
+    int shards = 8;                     // ticket counters (SSS_HIP_FUSED_SHARDS; 1 = one device-wide)
     int depth = 0, nchunks = 0, grid = 0;
     int *ck = nullptr;                  // chunk -> first position in nodes (nchunks + 1)
     int *nodes = nullptr;               // sweep * n + row, by fused depth

@@ -51,8 +51,11 @@ constexpr int kSpinLimit = 1 << 22;        // LDS polls before a cu wave gives u
 constexpr int kFlowSpinLimit = 1 << 18;    // granule polls before a flow wave gives up (~0.5 s)
 
 // control words of a flow pass: [0] epoch of the last completed launch, [1] ticket, [2] waves that
-// have exited, [3] error (stall) flag
-enum { kCtlEpoch = 0, kCtlTicket = 1, kCtlExit = 2, kCtlErr = 3, kCtlWords = 4 };
+// have exited, [3] error (stall) flag; from word kCtlShard0 the fused engine's ticket shards, one per
+// 128-byte line
+constexpr int kTicketShards = 8, kCtlShardStride = 32;
+enum { kCtlEpoch = 0, kCtlTicket = 1, kCtlExit = 2, kCtlErr = 3, kCtlShard0 = 32,
+       kCtlWords = kCtlShard0 + kTicketShards * kCtlShardStride };
 
 #define RLX_AGENT __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT
 
@@ -101,6 +104,7 @@ __device__ __forceinline__ void flow_exit(unsigned *ctl, unsigned epoch, unsigne
     const unsigned total = gridDim.x * (blockDim.x >> 6);
     if ((threadIdx.x & 63) == 0 && __hip_atomic_fetch_add(&ctl[kCtlExit], 1u, RLX_AGENT) == total - 1) {
         __hip_atomic_store(&ctl[kCtlTicket], 0u, RLX_AGENT);
+        for (int c = 0; c < kTicketShards; ++c) __hip_atomic_store(&ctl[kCtlShard0 + c * kCtlShardStride], 0u, RLX_AGENT);
         __hip_atomic_store(&ctl[kCtlExit], 0u, RLX_AGENT);
         __hip_atomic_store(&ctl[kCtlEpoch], epoch, RLX_AGENT);
     }
@@ -114,6 +118,16 @@ __device__ __forceinline__ int flow_ticket(unsigned *ctl)
 {
     const unsigned inc = (threadIdx.x & 63) == 0 ? 1u : 0u;
     return __builtin_amdgcn_readfirstlane((int)__hip_atomic_fetch_add(&ctl[kCtlTicket], inc, RLX_AGENT));
+}
+
+// Next local ticket of a shard counter: one lane's atomic (the others add nothing and issue
+// nothing), its result read back from lane 0 -- the wave is converged at every call site (a loop head
+// whose exit depends on this uniform value only).
+__device__ __forceinline__ int flow_ticket_at(unsigned *w)
+{
+    unsigned t = 0;
+    if ((threadIdx.x & 63) == 0) t = __hip_atomic_fetch_add(w, 1u, RLX_AGENT);
+    return __builtin_amdgcn_readfirstlane((int)t);
 }
 
 // s - p[a] - p[a+1] - ... - p[e-1] in order (chain_pipe16: the next 16 products read as 16-byte
@@ -346,9 +360,16 @@ __global__ __launch_bounds__(kBlock) void gs_fused_group(int nchunks, const int 
                                                          const double *__restrict__ d_later, unsigned long long *gran,
                                                          unsigned *ctl, unsigned *err, int spin, int ovl,
                                                          const int *__restrict__ rp0, const int *__restrict__ ci0,
-                                                         const double *__restrict__ v0)
+                                                         const double *__restrict__ v0, int shards)
 {
     constexpr int R = 64 / G, CAP = kGroupBuf / R, U = 8;
+    // tickets from `nt` counters: shard c hands out chunks c, c + nt, c + 2 nt, ... in order, each
+    // to the waves of the workgroups blockIdx = c mod nt.  Every shard's sequence is a subsequence of
+    // the topological order and every shard has waves, so the lowest unfinished chunk is always held
+    // by a wave whose inputs are final (or is next in its shard, whose waves then hold only finished
+    // chunks): no deadlock, as with one counter, at up to nt times its atomic throughput.
+    const int nt = min(shards, (int)gridDim.x), shard = (int)blockIdx.x % nt;
+    unsigned *tick = ctl + kCtlShard0 + shard * kCtlShardStride;
     static_assert(CAP / G == 32, "one pending bit per staged entry of a lane");
     __shared__ __attribute__((aligned(16))) double buf[kBlock / 64][kGroupBuf];
     const int lane = threadIdx.x & 63, grp = lane / G, gl = lane % G;
@@ -356,7 +377,7 @@ __global__ __launch_bounds__(kBlock) void gs_fused_group(int nchunks, const int 
     const unsigned epoch = __hip_atomic_load(&ctl[kCtlEpoch], RLX_AGENT) + 1u;
     auto tag = [&](int ver) { return (epoch << 4) | (unsigned)ver; };
     for (;;) {
-        const int q = flow_ticket(ctl);
+        const int q = flow_ticket_at(tick) * nt + shard;
         if (q >= nchunks) break;
         const int p = ck[q] + grp;
         const bool active = p < ck[q + 1];
@@ -898,6 +919,8 @@ int gs_fused_build(GsFused &f, const SSS_MAT &A, const DevCSR *dA, const PassSch
         const int g = atoi(e);
         if (g == 2 || g == 4 || g == 8 || g == 16 || g == 32 || g == 64) f.G = g;
     }
+    f.shards = kTicketShards;
+    if (const char *e = getenv("SSS_HIP_FUSED_SHARDS")) f.shards = std::min(kTicketShards, std::max(1, atoi(e)));
     if (getenv("SSS_HIP_TIMING"))
         fprintf(stderr, "[sss_hip]   fused GS-CF plan n=%d: depth %d (%.0f nodes per depth), rows %.1f avg / %d max, G = %d\n",
                 n, depth, (double)n * sweeps / std::max(1, depth), avg, maxlen, f.G);
@@ -1004,7 +1027,7 @@ int gs_fused_run(const GsFused &f, const DevCSR &A, const double *b, double *x, 
     auto go = [&](auto kern) {
         hipLaunchKernelGGL(kern, dim3(f.grid), dim3(kBlock), 0, s, f.nchunks, f.ck, f.nodes, f.n, f.split,
                            f.sweeps - 1, A.rp, A.ci, A.v, b, x, d_first, d_later, f.gran, f.ctl, f.err, f.spin,
-                           f.overlap ? 1 : 0, x_zero ? f.rp0 : (const int *)nullptr, f.ci0, f.v0);
+                           f.overlap ? 1 : 0, x_zero ? f.rp0 : (const int *)nullptr, f.ci0, f.v0, f.shards);
     };
     switch (f.G) {   // (every G the planner can choose; the chunk table holds 64 / G rows per ticket)
     case 2: go(gs_fused_group<2>); break;

@@ -516,14 +516,17 @@ def test_fused_depth_forms(p32_h, depth_form, monkeypatch):
     assert np.array_equal(x_g.view(np.uint64), x_r.view(np.uint64))
 
 
+@pytest.mark.parametrize("shards", ["1", "3", "8"])
 @pytest.mark.parametrize("lanes", ["2", "4", "16", "64"])
 @pytest.mark.parametrize("hname", ["p32_h", "a27_h"])
-def test_fused_lanes_per_row(request, hname, lanes, monkeypatch):
+def test_fused_lanes_per_row(request, hname, lanes, shards, monkeypatch):
     """Every lanes-per-row width of the fused engine (the planner picks 2 only on the widest levels
-    of short rows, which the test sizes never reach): the reference's x bit for bit, no stall."""
+    of short rows, which the test sizes never reach), with one, three or eight ticket counters: the
+    reference's x bit for bit, no stall."""
     monkeypatch.setenv("SSS_HIP_GS_ENGINE", "flow")
     monkeypatch.setenv("SSS_HIP_GS_FUSED", "1")
     monkeypatch.setenv("SSS_HIP_FUSED_G", lanes)
+    monkeypatch.setenv("SSS_HIP_FUSED_SHARDS", shards)
     H = request.getfixturevalue(hname)
     n = H.level(0).A.num_rows
     rtn, rel_r, _ = oracle_solve(H, np.ones(n), x_r := np.ones(n))
