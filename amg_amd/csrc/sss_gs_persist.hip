@@ -886,8 +886,9 @@ int gs_fused_build(GsFused &f, const SSS_MAT &A, const DevCSR *dA, const PassSch
     f.overlap = avg >= 300;
     // Lanes per row G: the cheapest by a latency model fitted to 2-sweep calls on 7-pt 256^3 and
     // the circuit stand-in at G = 2 ... 64 (tools/gpu/r05_g_sweep.sh, profiles/r05_gs_fused/):
-    //  * each fused depth step costs the larger of its tickets -- one device-wide counter hands out
-    //    chunks of 64 / G rows at ~13 ns each, so npd * G / 64 * 13 ns for npd nodes per depth --
+    //  * each fused depth step costs the larger of its tickets -- the eight ticket shards hand out
+    //    chunks of 64 / G rows at ~4.5 ns each (one device-wide counter: ~13 ns; re-fitted at 400^3,
+    //    profiles/r05_shards/), so npd * G / 64 * 4.5 ns for npd nodes per depth --
     //    and a node's latency, ~2 us + 1 us per group of 8 loads a lane issues for an average row
     //    + 20 ns per entry a lane stages;
     //  * hub rows (longer than 4x the average and than one staging round of 32 G entries) add
@@ -902,7 +903,7 @@ int gs_fused_build(GsFused &f, const SSS_MAT &A, const DevCSR *dA, const PassSch
         const double npd = (double)n * sweeps / std::max(1, depth);
         double best = 0.0;
         for (int g = 2; g <= 64; g *= 2) {
-            const double tick = npd * g / 64.0 * 13e-9;
+            const double tick = npd * g / 64.0 * 4.5e-9;
             const double lat = 2e-6 + std::ceil(std::min(avg, 32.0 * g) / (8.0 * g)) * 1e-6 + avg / g * 20e-9;
             double hub = 0.0;
             const double hub_min = std::max(4.0 * avg, 32.0 * g);
