@@ -19,7 +19,7 @@ LIBDIR  ?= amg_amd/lib
 EXTRA   ?=
 BINDIR  := amg_amd/bin
 
-CFLAGS   := -O3 -fPIC -ffp-contract=off -fopenmp -std=gnu11 -Wall -Wno-unused-result
+CFLAGS   := -O3 -fPIC -ffp-contract=off -fopenmp -std=gnu11 -Wall -Wno-unused-result -I$(ROCM)/include
 HIPFLAGS := -O3 -fPIC -std=c++17 --offload-arch=$(ARCH) -ffp-contract=off -Wall -Wno-unused-result $(EXTRA)
            
 
@@ -46,7 +46,7 @@ $(BUILD)/hip/%.o: amg_amd/csrc/%.hip $(HEADERS)
 
 $(LIB): $(HOST_OBJ) $(HIP_OBJ)
 	@mkdir -p $(LIBDIR)
-	$(HIPCC) -shared -fPIC -o $@ $^ -Wl,-Bsymbolic-functions -lgomp -L$(ROCM)/lib -lrccl -Wl,-rpath,$(ROCM)/lib
+	$(HIPCC) -shared -fPIC -o $@ $^ -Wl,-Bsymbolic-functions -lgomp -L$(ROCM)/lib -lrccl -lrocprofiler-sdk-roctx -Wl,-rpath,$(ROCM)/lib
 
 $(BIN): amg_amd/host/sss_main.c $(LIB) $(HEADERS)
 	@mkdir -p $(BINDIR)

@@ -611,19 +611,12 @@ static sss_hip_dist *dist_new(const SSS_AMG_PARS &pars, const sss_hip_opts *o, s
     return d;
 }
 
-static int agg_rows_or_default(int agg_rows)
-{
-    if (agg_rows > 0) return agg_rows;
-    const char *e = getenv("SSS_HIP_AGG_ROWS");
-    return (e && *e) ? atoi(e) : 20000;
-}
-
 extern "C" sss_hip_dist *sss_hip_dist_create(const SSS_AMG *mg, const sss_hip_opts *o, sss_hip_comm *c, int agg_rows)
 {
     if (!mg || !c || sss_hip_device_count() <= 0) return nullptr;
     PartPlan plan;
     const char *err = nullptr;
-    if (part_plan_build(plan, mg, c->nranks, c->rank, agg_rows_or_default(agg_rows))) {
+    if (part_plan_build(plan, mg, c->nranks, c->rank, part_agg_rows(agg_rows))) {
         err = "partition";
         plan = PartPlan();
     }
@@ -759,6 +752,7 @@ static int dist_cycle_enqueue(sss_hip_dist *d)
     int rc;
     d->resid_c_ready = false;
     for (int l = 0; l < nagg; ++l) {   // descent
+        TraceRange tr("rank %d level %d descent", d->comm->rank, l);
         DLevel &L = d->L[l];
         ResidFuse rf;   // the last C pass may form the residual's C rows (then only F rows remain)
         rf.r = L.wp;
@@ -789,8 +783,12 @@ static int dist_cycle_enqueue(sss_hip_dist *d)
             SSS_HIP(hipMemsetAsync(tx, 0, sizeof(double) * (size_t)d->nc_all, s));
         }
     }
-    if ((rc = sss_hip_cycle(d->tail))) return rc;   // replicated levels, same stream
+    {
+        TraceRange tr("rank %d replicated tail", d->comm->rank);
+        if ((rc = sss_hip_cycle(d->tail))) return rc;   // replicated levels, same stream
+    }
     for (int l = nagg - 1; l >= 0; --l) {           // ascent
+        TraceRange tr("rank %d level %d ascent", d->comm->rank, l);
         DLevel &L = d->L[l];
         double *xc = l + 1 < nagg ? d->L[l + 1].x : hier_vec(d->tail, 0, SSS_HIP_VEC_X);
         // dead F-row correction (see walk_cycle in sss_hier.hip): prolong into the C rows only

@@ -22,6 +22,19 @@
 
 #include "../../include/sss_hip.h"
 
+// roctx ranges (amg_amd/host/sss_util.c; rocprofv3 --marker-trace)
+extern "C" void sss_trace_push(const char *fmt, ...) __attribute__((format(printf, 1, 2)));
+extern "C" void sss_trace_pop(void);
+namespace sss {
+struct TraceRange {
+    template <class... Args>
+    explicit TraceRange(const char *fmt, Args... a) { sss_trace_push(fmt, a...); }
+    ~TraceRange() { sss_trace_pop(); }
+    TraceRange(const TraceRange &) = delete;
+    TraceRange &operator=(const TraceRange &) = delete;
+};
+}  // namespace sss
+
 extern "C" void sss_huge_hint(void *p, size_t bytes);   // amg_amd/host/sss_util.c
 
 namespace sss {
@@ -457,6 +470,8 @@ int gs_fused_build(GsFused &f, const SSS_MAT &A, const DevCSR *dA, const PassSch
 int gs_fused_run(const GsFused &f, const DevCSR &A, const double *b, double *x, const double *d_first,
                  const double *d_later, bool x_zero, hipStream_t s);
 void gs_fused_free(GsFused &f);
+// *out = the fused engine's stall word (0 when the plan has no fused engine); cleared if set and clear
+int gs_fused_error(const GsFused &f, unsigned *out, bool clear);
 struct SmootherPlan;
 // Report the one-launch passes' stalls into *err (a word of the owning hierarchy).
 void smoother_set_err(SmootherPlan &sp, unsigned *err);

@@ -945,10 +945,19 @@ int gs_fused_build(GsFused &f, const SSS_MAT &A, const DevCSR *dA, const PassSch
         gs_fused_free(f);
         return hip_fail(hipErrorOutOfMemory, "hipMalloc(gs fused)", __FILE__, __LINE__);
     }
-    SSS_HIP(hipMemcpy(f.ck, ck.data(), sizeof(int) * ck.size(), hipMemcpyHostToDevice));
-    SSS_HIP(hipMemcpy(f.nodes, order.data(), sizeof(int) * order.size(), hipMemcpyHostToDevice));
-    SSS_HIP(hipMemset(f.gran, 0, sizeof(unsigned long long) * 2 * (size_t)n));
-    SSS_HIP(hipMemset(f.ctl, 0, sizeof(unsigned) * kCtlWords));
+    // an upload failure frees what this plan holds (as the allocation failures do)
+#define SSS_FUSED_HIP(call)                                          \
+    do {                                                             \
+        hipError_t e_ = (call);                                      \
+        if (e_ != hipSuccess) {                                      \
+            gs_fused_free(f);                                        \
+            return hip_fail(e_, #call, __FILE__, __LINE__);          \
+        }                                                            \
+    } while (0)
+    SSS_FUSED_HIP(hipMemcpy(f.ck, ck.data(), sizeof(int) * ck.size(), hipMemcpyHostToDevice));
+    SSS_FUSED_HIP(hipMemcpy(f.nodes, order.data(), sizeof(int) * order.size(), hipMemcpyHostToDevice));
+    SSS_FUSED_HIP(hipMemset(f.gran, 0, sizeof(unsigned long long) * 2 * (size_t)n));
+    SSS_FUSED_HIP(hipMemset(f.ctl, 0, sizeof(unsigned) * kCtlWords));
     {   // sweep-0 rows on a zero iterate (finite values only): the entries read at version 1
         const double *av = A.val;
         std::atomic<bool> fin{true};
@@ -984,11 +993,12 @@ int gs_fused_build(GsFused &f, const SSS_MAT &A, const DevCSR *dA, const PassSch
                 gs_fused_free(f);
                 return hip_fail(hipErrorOutOfMemory, "hipMalloc(gs fused rows)", __FILE__, __LINE__);
             }
-            SSS_HIP(hipMemcpy(f.rp0, r0.data(), sizeof(int) * r0.size(), hipMemcpyHostToDevice));
-            SSS_HIP(hipMemcpy(f.ci0, c0.data(), sizeof(int) * c0.size(), hipMemcpyHostToDevice));
-            SSS_HIP(hipMemcpy(f.v0, w0.data(), sizeof(double) * w0.size(), hipMemcpyHostToDevice));
+            SSS_FUSED_HIP(hipMemcpy(f.rp0, r0.data(), sizeof(int) * r0.size(), hipMemcpyHostToDevice));
+            SSS_FUSED_HIP(hipMemcpy(f.ci0, c0.data(), sizeof(int) * c0.size(), hipMemcpyHostToDevice));
+            SSS_FUSED_HIP(hipMemcpy(f.v0, w0.data(), sizeof(double) * w0.size(), hipMemcpyHostToDevice));
         }
     }
+#undef SSS_FUSED_HIP
     f.err = f.ctl + kCtlErr;
     int cus = 256;
     {
@@ -997,6 +1007,25 @@ int gs_fused_build(GsFused &f, const SSS_MAT &A, const DevCSR *dA, const PassSch
         if (hipGetDevice(&dev) == hipSuccess && hipGetDeviceProperties(&prop, dev) == hipSuccess)
             cus = prop.multiProcessorCount;
     }
+    // Progress needs every workgroup that takes tickets to be resident (a waiting wave spins until its
+    // producers finish), and with sharded tickets at least one resident workgroup per shard: cap the
+    // grid at what the occupancy API says can be co-resident on the device (the kernel takes
+    // min(shards, grid) counters, so every shard then has a resident workgroup).
+    int per_cu = 0;
+    {
+        auto occ = [&](auto kern) {
+            if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, kBlock, 0) != hipSuccess) per_cu = 0;
+        };
+        switch (f.G) {
+        case 2: occ(gs_fused_group<2>); break;
+        case 4: occ(gs_fused_group<4>); break;
+        case 8: occ(gs_fused_group<8>); break;
+        case 16: occ(gs_fused_group<16>); break;
+        case 32: occ(gs_fused_group<32>); break;
+        default: occ(gs_fused_group<64>); break;
+        }
+    }
+    const int resident = per_cu > 0 ? per_cu * cus : 2 * cus;
     const double per_depth = (double)f.nchunks / std::max(1, depth);
     // waves in flight: at least 512 (1,024 on the long-row levels), so that nodes several fused
     // depths ahead are staged before their dependencies finish (7-pt 400^3, 2-sweep calls,
@@ -1004,7 +1033,7 @@ int gs_fused_build(GsFused &f, const SSS_MAT &A, const DevCSR *dA, const PassSch
     // waves, 28.9 / 56.1 / 120.6 with 1,024; 2,048 slower everywhere)
     int waves = (int)std::min<double>(1024.0, std::max(f.overlap ? 1024.0 : 512.0, 4.0 * per_depth));
     waves = std::min(waves, std::min(f.nchunks, cus * 8));
-    f.grid = std::max(1, (waves + 3) / 4);
+    f.grid = std::max(1, std::min((waves + 3) / 4, resident));
     f.engine = 1;
     return 0;
 }
@@ -1124,6 +1153,17 @@ int gs_persist_error(const PassSchedule &ps, unsigned *out)
     unsigned e = 0;
     SSS_HIP(hipMemcpy(&e, ps.gp.err, sizeof(unsigned), hipMemcpyDeviceToHost));
     *out = e;
+    return 0;
+}
+
+int gs_fused_error(const GsFused &f, unsigned *out, bool clear)
+{
+    *out = 0;
+    if (!f.engine || !f.err) return 0;
+    unsigned e = 0;
+    SSS_HIP(hipMemcpy(&e, f.err, sizeof(unsigned), hipMemcpyDeviceToHost));
+    *out = e;
+    if (e && clear) SSS_HIP(hipMemset(f.err, 0, sizeof(unsigned)));
     return 0;
 }
 

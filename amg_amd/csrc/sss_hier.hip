@@ -399,6 +399,7 @@ static void hb_perm(HierBuild &b, int l)
 // A_l (+ its smoother plan unless coarsest) and the level vectors
 static bool hb_level_a(HierBuild &b, int l, bool coarsest)
 {
+    TraceRange tr("mirror level %d: A + smoother plan", l);
     sss_hip_hier *h = b.h;
     const SSS_AMG_COMP &C = b.mg->cg[l];
     auto &L = h->L[l];
@@ -458,6 +459,7 @@ static bool hb_level_a(HierBuild &b, int l, bool coarsest)
 // run, or l + 1 is the coarsest)
 static bool hb_level_pr(HierBuild &b, int l)
 {
+    TraceRange tr("mirror level %d: P, R", l);
     sss_hip_hier *h = b.h;
     const SSS_AMG_COMP &C = b.mg->cg[l];
     auto &L = h->L[l];
@@ -985,9 +987,13 @@ static int walk_cycle(sss_hip_hier *h, CoarseFn coarse, bool pend = false)
             if (g_ledger) g_ledger->slot = l;
             if (h->tail.from > 0 && l == h->tail.from && cycle_type == 1) {
                 // levels tail.from .. nl-1: descent, coarsest solve and ascent in one launch
-                if ((rc = tail_launch(h->tail, s))) return rc;
+                {
+                    TraceRange tr("levels %d-%d tail", l, nl - 1);
+                    if ((rc = tail_launch(h->tail, s))) return rc;
+                }
                 goto ascent;
             }
+            TraceRange tr("level %d descent", l);
             auto &L = h->L[l];
             visits[l]++;
             const bool first = l == 0 && visits[0] == 1;
@@ -1001,11 +1007,16 @@ static int walk_cycle(sss_hip_hier *h, CoarseFn coarse, bool pend = false)
             zeroed = true;
         }
         if (g_ledger) g_ledger->slot = kMaxLevels + 1;
-        if ((rc = coarse(h))) return rc;
+        {
+            TraceRange tr("coarse solve (level %d)", nl - 1);
+            rc = coarse(h);
+        }
+        if (rc) return rc;
     ascent:
         while (l > 0) {
             l--;
             if (g_ledger) g_ledger->slot = l;
+            TraceRange tr("level %d ascent", l);
             auto &L = h->L[l];
             // x_l += P e.  When the post-smoother's first pass overwrites every F row from C values
             // only (depth-1 GS F pass, all |d| > 1e-20), the F rows' correction is dead: prolong
@@ -1618,16 +1629,32 @@ extern "C" int sss_hip_host_smooth(const SSS_SMTR *s, int post)
     int rc = (!dx || !db) ? ERROR_ALLOC_MEM : 0;
     if (!rc && hipMemcpy(dx, s->x->d, sizeof(double) * n, hipMemcpyHostToDevice) != hipSuccess) rc = ERROR_MISC;
     if (!rc && hipMemcpy(db, s->b->d, sizeof(double) * n, hipMemcpyHostToDevice) != hipSuccess) rc = ERROR_MISC;
-    if (!rc) rc = smoother_run(M->sp, M->d, db, dx, s->nsweeps, nullptr, nullptr, nullptr, nullptr, false, natural && desc);
+    // a caller's iterate of +0.0 everywhere (every bit zero) takes the zero-iterate forms the cycle uses
+    // on a just-cleared level (the fused engine's reduced sweep-0 rows, the C/F-Jacobi first pass
+    // without the matrix): bitwise the full sweep on finite values, with b_i = -0.0 handled
+    bool x_zero = !natural;
+    for (int i = 0; x_zero && i < n; ++i) {
+        unsigned long long u;
+        memcpy(&u, s->x->d + i, sizeof u);
+        x_zero = u == 0ull;
+    }
+    if (!rc) rc = smoother_run(M->sp, M->d, db, dx, s->nsweeps, nullptr, nullptr, nullptr, nullptr, x_zero, natural && desc);
     if (!rc && hipMemcpy(s->x->d, dx, sizeof(double) * n, hipMemcpyDeviceToHost) != hipSuccess) rc = ERROR_MISC;
-    for (auto &ps : M->sp.pass) {   // a stalled one-launch pass: fail (and clear its word for the next call)
+    // a stalled one-launch pass or fused call: fail, and clear its word for the next call (read every
+    // word even after a failure, so none stays set)
+    bool stalled = false;
+    for (auto &ps : M->sp.pass) {
         unsigned e = 0;
-        if (!rc && gs_persist_error(ps, &e)) rc = ERROR_MISC;
-        if (!rc && e) {
+        if (gs_persist_error(ps, &e)) rc = rc ? rc : ERROR_MISC;
+        if (e) {
             (void)hipMemset(ps.gp.err, 0, sizeof(unsigned));
-            rc = stall_error("SSS_amg_smoother_pre/post");
+            stalled = true;
         }
     }
+    unsigned ez = 0;
+    if (gs_fused_error(M->sp.fz, &ez, true)) rc = rc ? rc : ERROR_MISC;
+    if (ez) stalled = true;
+    if (stalled && !rc) rc = stall_error("SSS_amg_smoother_pre/post");
     dev_free(dx);
     dev_free(db);
     return rc;

@@ -224,6 +224,14 @@ static int part_plan_build_impl(PartPlan &p, const SSS_AMG *mg, int nranks, int 
     return 0;
 }
 
+int part_agg_rows(int agg_rows)
+{
+    if (agg_rows > 0) return agg_rows;
+    const char *e = getenv("SSS_HIP_AGG_ROWS");
+    const int v = (e && *e) ? atoi(e) : 0;
+    return v > 0 ? v : kAggRowsDefault;
+}
+
 int part_plan_build(PartPlan &p, const SSS_AMG *mg, int nranks, int rank, int agg_rows)
 {
     return part_plan_build_impl(p, mg, nranks, rank, agg_rows, nullptr);
@@ -443,7 +451,7 @@ struct sss_part_plan {
 extern "C" int sss_part_save(const SSS_AMG *mg, int nranks, int agg_rows, const char *prefix)
 {
     if (!mg || nranks < 1 || !prefix) return ERROR_INPUT_PAR;
-    if (agg_rows <= 0) agg_rows = 20000;
+    agg_rows = sss::part_agg_rows(agg_rows);
     int nagg = -1;
     if (int rc = sss::part_save_all(mg, nranks, agg_rows, prefix, nagg)) return rc;
     SSS_AMG tail = *mg;   // the replicated levels, as their own hierarchy
@@ -466,7 +474,7 @@ extern "C" sss_part_plan *sss_part_plan_load(const char *path)
 extern "C" sss_part_plan *sss_part_plan_create(const SSS_AMG *mg, int nranks, int rank, int agg_rows)
 {
     auto *pp = new sss_part_plan();
-    if (sss::part_plan_build(pp->p, mg, nranks, rank, agg_rows > 0 ? agg_rows : 20000)) {
+    if (sss::part_plan_build(pp->p, mg, nranks, rank, sss::part_agg_rows(agg_rows))) {
         delete pp;
         return nullptr;
     }

@@ -60,6 +60,9 @@ struct PartPlan {
 
 // agg_rows: the first level l >= 1 with at most agg_rows rows, and every level below it, is
 // replicated (the coarsest always is).  Returns 0 or an SSS error code.
+constexpr int kAggRowsDefault = 20000;
+// agg_rows if > 0, else SSS_HIP_AGG_ROWS, else kAggRowsDefault
+int part_agg_rows(int agg_rows);
 int part_plan_build(PartPlan &p, const SSS_AMG *mg, int nranks, int rank, int agg_rows);
 
 // Partition file of one rank (sss_part_save): its PartPlan plus the solve parameters (format 2:

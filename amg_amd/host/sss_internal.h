@@ -31,6 +31,12 @@ void sss_huge_hint(void *p, size_t bytes);
 void *sss_big_malloc(size_t bytes);
 void *sss_big_calloc(size_t n, size_t size);
 
+/* roctx ranges (rocprofv3 --marker-trace shows them; near-free without a profiler): the solve's
+ * outer iterations, the setup's levels, the mirror's level tasks, and per level the descent and
+ * ascent of a V-cycle as it is enqueued (eager launches, or once at the graph capture). */
+void sss_trace_push(const char *fmt, ...) __attribute__((format(printf, 1, 2)));
+void sss_trace_pop(void);
+
 #ifdef __cplusplus
 }
 #endif

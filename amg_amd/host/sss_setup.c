@@ -1139,18 +1139,23 @@ void sss_amg_setup_hooked(SSS_AMG *mg, SSS_MAT *A, SSS_AMG_PARS *pars, sss_setup
         memset(&S, 0, sizeof(S));
 
         const double tc0 = SSS_get_time();
+        sss_trace_push("SSS_amg_setup level %d", lvl);
+        sss_trace_push("coarsen");
         status = SSS_amg_coarsen(&L->A, &vertices, &L->P, &S, pars);
+        sss_trace_pop();
         const double tc1 = SSS_get_time();
         if (status < 0) {
             free(S.row_ptr);
             free(S.col_idx);
             printf("### WARNING: Could not find any C-variables!\n");
             printf("### WARNING: RS coarsening on level-%d failed!\n", lvl);
+            sss_trace_pop();
             break;
         }
         if (L->P.num_cols < min_cdof) {
             free(S.row_ptr);
             free(S.col_idx);
+            sss_trace_pop();
             break;
         }
         if (L->P.num_rows > L->P.num_cols * 10) {
@@ -1163,10 +1168,15 @@ void sss_amg_setup_hooked(SSS_AMG *mg, SSS_MAT *A, SSS_AMG_PARS *pars, sss_setup
         L->cfmark = SSS_ivec_create(L->A.num_rows);
         memcpy(L->cfmark.d, vertices.d, (size_t)L->A.num_rows * sizeof(int));
 
+        sss_trace_push("interpolation");
         SSS_amg_interp(&L->A, &vertices, &L->P, &S, pars);
+        sss_trace_pop();
         const double tc2 = SSS_get_time();
+        sss_trace_push("R = P^T");
         L->R = SSS_mat_trans(&L->P);
+        sss_trace_pop();
         const double tc3 = SSS_get_time();
+        sss_trace_push("RAP");
         /* the device walks each coarse row's (R entry, A entry) steps in order, so it wins on the
          * wide levels of short rows (7-pt 400^3 levels 0-2: 3.1 -> 1.1, 2.0 -> 0.75, 0.59 -> 0.37 s)
          * and loses on the narrow levels of long rows (level 3 and below: 0.75 -> 1.2 s) */
@@ -1174,6 +1184,8 @@ void sss_amg_setup_hooked(SSS_AMG *mg, SSS_MAT *A, SSS_AMG_PARS *pars, sss_setup
                              (double)L->A.num_nnzs <= (double)gpu_rap_maxrow * L->A.num_rows;
         if (!(gpu_here && sss_hip_rap(&L->R, &L->A, &L->P, &mg->cg[lvl + 1].A) == 0))
             mg->cg[lvl + 1].A = SSS_blas_mat_rap(&L->R, &L->A, &L->P);
+        sss_trace_pop();
+        sss_trace_pop();   /* the level */
         if (getenv("SSS_SETUP_TIMING"))   /* phase times on stderr (stdout stays the reference's) */
             fprintf(stderr, "[setup] level %d: coarsen %.3f s, interp %.3f s, transpose %.3f s, RAP %.3f s\n", lvl,
                     tc1 - tc0, tc2 - tc1, tc3 - tc2, SSS_get_time() - tc3);

@@ -93,12 +93,14 @@ SSS_RTN SSS_amg_solve(SSS_AMG *mg, SSS_VEC *x, SSS_VEC *b)
      * (Solve/SSS_SOLVE.c:31,82-83).  Their time goes to stderr, so stdout stays the reference's. */
     if (fabs(sumb) != 0.0) {
         const double tu = SSS_get_time();
+        sss_trace_push("SSS_amg_solve upload");
         mg->cg[0].x = *x;
         mg->cg[0].b = *b;
         h = sss_dev_mirror_for(mg);
         check(sss_hip_upload_vec(h, 0, SSS_HIP_VEC_B, b->d, b->n), __func__);
         check(sss_hip_upload_vec(h, 0, SSS_HIP_VEC_X, x->d, x->n), __func__);
         check(sss_hip_sync(h), __func__);
+        sss_trace_pop();
         fprintf(stderr, "AMG device upload time: %g s\n", SSS_get_time() - tu);
     }
     t0 = SSS_get_time();
@@ -111,8 +113,14 @@ SSS_RTN SSS_amg_solve(SSS_AMG *mg, SSS_VEC *x, SSS_VEC *b)
 
     for (int iter = 1; iter <= max_it; ++iter) {
         double absres, relres, factor;
+        sss_trace_push("SSS_amg_solve iteration %d", iter);
+        sss_trace_push("V-cycle");
         check(sss_hip_cycle(h), __func__);
+        sss_trace_pop();
+        sss_trace_push("residual + norm");
         check(sss_hip_residual_norm(h, &absres), __func__);   /* one 8-byte D2H per iteration */
+        sss_trace_pop();
+        sss_trace_pop();
         relres = absres / sumb;
         factor = absres / absres0;
         absres0 = absres;

@@ -10,6 +10,11 @@
  */
 #include "sss_internal.h"
 
+struct hsa_agent_s;   /* (named in roctx.h's prototypes; declared here so C sees one type) */
+struct ihipStream_t;
+#include <rocprofiler-sdk-roctx/roctx.h>
+#include <stdarg.h>
+
 #include <math.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -532,3 +537,16 @@ SSS_IMAT SSS_imat_trans(SSS_IMAT *A)
                       sizeof(int), T.row_ptr, T.col_idx, T.val);
     return T;
 }
+
+/* ---- roctx ranges (tracing row) --------------------------------------------- */
+void sss_trace_push(const char *fmt, ...)
+{
+    char buf[128];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    roctxRangePushA(buf);
+}
+
+void sss_trace_pop(void) { roctxRangePop(); }

@@ -20,6 +20,11 @@ import threading
 import time
 from pathlib import Path
 
+# The partition file layout's version (sss_part.hip kPartVersion; readers reject any other).  A set on
+# disk records it in its manifest and bench.py puts it in the set's directory name, so a set written
+# by an older layout is regenerated instead of failing the run with ERROR_WRONG_FILE.
+PART_FORMAT = 2
+
 
 def level_table(H) -> list:
     out = []
@@ -77,7 +82,8 @@ def build(stencil: int, n: int, ranks: int, prefix: Path, agg_rows: int = 0, sum
     phase[0] = "writing the partition set"
     N.part_save(H, ranks, prefix, agg_rows)
     t2 = time.perf_counter()
-    man = {"stencil": stencil, "n": n, "ranks": ranks, "agg_rows": agg_rows, "levels": level_table(H),
+    man = {"format": PART_FORMAT, "stencil": stencil, "n": n, "ranks": ranks, "agg_rows": agg_rows,
+           "levels": level_table(H),
            "pars": {"pre_iter": H.pars.pre_iter, "post_iter": H.pars.post_iter, "tol": H.pars.tol},
            "setup_s": t1 - t0, "partition_s": t2 - t1,
            "peak_rss_gb": resource.getrusage(resource.RUSAGE_SELF).ru_maxrss / 2**20}

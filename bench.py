@@ -61,6 +61,11 @@ def parse():
     p.add_argument("--workload", default="stencil", choices=["stencil", "circuit"],
                    help="stencil: the --stencil operator on an --n grid; circuit: the G3_circuit stand-in "
                         "(BASELINE.json configs[3], amg_amd/workloads.py; --n = rows, default 1,585,478; 1 GPU)")
+    p.add_argument("--mtx", default=None,
+                   help="a Matrix Market file read by the reference's ingest (SSS_mat_read: SSS_main.c:12-22, "
+                        "mmio_highlevel.h:10-305) instead of a generated operator, b = x0 = 1 as ./amg sets them "
+                        "(SSS_main.c:141-145): BASELINE.json configs[0] (nos5) and configs[3] (G3_circuit) when the "
+                        "SuiteSparse file is supplied; 1 GPU")
     p.add_argument("--parity-converge", type=int, default=None,
                    help="run the parity-mode mirror to tol (the reference-semantics iteration count measured in "
                         "this run, beside the throughput count); default 1 at N = 1")
@@ -335,6 +340,23 @@ def select_workload(args, world: int):
     return stencil, 256 if stencil == 27 else 400
 
 
+def workload_name(args, circuit: bool, mtx) -> str:
+    """config.workload of this run: the stencil and grid, the circuit stand-in's rows, or the .mtx
+    file's name (mtx_<stem>)."""
+    if mtx is not None:
+        return f"mtx_{Path(mtx).stem}"
+    return f"g3_circuit_standin_{args.n}" if circuit else f"poisson{args.stencil}_{args.n}^3"
+
+
+def load_mtx(A, path):
+    """The .mtx file as the reference's ./amg reads it (SSS_mat_read -> mmio_info + mmio_data: symmetric
+    expansion, file order within rows, SSS_main.c:12-22); refuses an empty or unreadable matrix."""
+    M = A.read_mtx(path)
+    if M.num_rows <= 0 or M.num_rows != M.num_cols or not M.row_ptr:
+        raise SystemExit(f"bench.py: --mtx {path}: not a square sparse matrix ({M.num_rows} x {M.num_cols})")
+    return M
+
+
 def transport_policy(world: int, devices: int, rccl_ok_everywhere: bool) -> str:
     """The halo transport of a multi-rank run: "rccl" when every rank created its communicator;
     "host" (gloo) only when the ranks share GPUs (fewer visible devices than ranks: RCCL refuses
@@ -345,6 +367,25 @@ def transport_policy(world: int, devices: int, rccl_ok_everywhere: bool) -> str:
     return "host" if devices < world else "fail"
 
 
+def part_set_name(stencil: int, n: int, world: int) -> str:
+    """Directory name of a partition set: the file layout's version (amg_amd.partition.PART_FORMAT)
+    and the replicated-tail threshold are part of it, so a set written by an older layout or for
+    another threshold is never picked up (it would fail the run with ERROR_WRONG_FILE, or silently
+    measure another tail)."""
+    from amg_amd.partition import PART_FORMAT
+    agg = int(os.environ.get("SSS_HIP_AGG_ROWS", "0") or 0)
+    return f"sss_parts_v{PART_FORMAT}_{stencil}pt_{n}_{world}r" + (f"_agg{agg}" if agg > 0 else "")
+
+
+def part_set_usable(manifest: Path) -> bool:
+    """A set on disk is reused only if its manifest records this layout version."""
+    from amg_amd.partition import PART_FORMAT
+    try:
+        return json.loads(manifest.read_text()).get("format") == PART_FORMAT
+    except (OSError, ValueError):
+        return False
+
+
 def part_prefix(stencil: int, n: int, world: int) -> Path:
     """Where the partition set of a multi-rank run lives (reused by later runs of the same
     configuration): SSS_PART_DIR if set; else an existing set of this configuration in any of /tmp,
@@ -352,13 +393,13 @@ def part_prefix(stencil: int, n: int, world: int) -> Path:
     it -- the set takes ~490 B per row for the 7-point operator and ~870 B per row for the 27-point
     one (profiles/r03_partition_*.json: 65 GB at 512^3; r04_partition_p7_400_*.json at 400^3)."""
     import shutil
-    name = f"sss_parts_{stencil}pt_{n}_{world}r"
+    name = part_set_name(stencil, n, world)
     if os.environ.get("SSS_PART_DIR"):
         return Path(os.environ["SSS_PART_DIR"]) / name / "part"
     need = 1.25 * (870 if stencil == 27 else 490) * float(n) ** 3
     cands = [Path("/tmp"), Path("/dev/shm"), Path.home(), ROOT.parent]
     for c in cands:   # an existing set of this configuration anywhere wins over free space
-        if (c / name / "part.json").exists():
+        if part_set_usable(c / name / "part.json"):
             return c / name / "part"
     best, room = None, -1.0
     for c in cands:
@@ -455,10 +496,16 @@ def main():
     circuit = args.workload == "circuit"
     if circuit and D.world > 1:
         raise SystemExit("bench.py: --workload circuit is a single-GPU configuration (BASELINE.json configs[3])")
+    mtx = Path(args.mtx) if args.mtx else None
+    if mtx is not None and D.world > 1:
+        raise SystemExit("bench.py: --mtx runs on one GPU (BASELINE.json configs[0] and configs[3])")
+    if mtx is not None and not mtx.is_file():
+        raise SystemExit(f"bench.py: --mtx {mtx}: no such file")
+    irregular = circuit or mtx is not None   # no stencil: no grid edge, no stencil-only records
     # one problem at every rank count (the metric's 7-pt 400^3 unless --stencil / --n): the driver's
     # --gpus 1, 2, 4, 8 runs form one strong-scaling curve
     args.stencil, args.n = select_workload(args, D.world)
-    workload = f"g3_circuit_standin_{args.n}" if circuit else f"poisson{args.stencil}_{args.n}^3"
+    workload = workload_name(args, circuit, mtx)
     if args.probe_ranks:
         # one write() per line: the ranks share the launcher's stdout pipe
         os.write(json_fd, (json.dumps({"rank": D.rank, "world": D.world, "local_rank": D.local_rank,
@@ -497,6 +544,15 @@ def main():
         if cache is not None and cache.exists():
             H = A.Hierarchy.load(cache)
             hier_src = f"loaded from {cache}"
+        elif mtx is not None:
+            M = load_mtx(A, mtx)
+            if args.sequential_upload:
+                H = quiet_call(A.Hierarchy, M)
+            else:
+                DH = quiet_call(A.DeviceHierarchy, None, setup_from=M, **dh_kw)
+                H = DH.H
+            A.lib().SSS_mat_destroy(C.byref(M))
+            hier_src = f"setup of {mtx.name} (SSS_mat_read)"
         elif circuit:
             from amg_amd.workloads import circuit_csr
             M = circuit_csr(n)
@@ -531,10 +587,11 @@ def main():
         D.dist.broadcast_object_list(box, src=0)
         prefix = Path(box[0])
         manifest = Path(str(prefix) + ".json")
-        if D.rank == 0 and not manifest.exists():
+        if D.rank == 0 and not part_set_usable(manifest):
             import subprocess
             subprocess.run([sys.executable, "-m", "amg_amd.partition", "--stencil", str(args.stencil), "--n", str(n),
-                            "--ranks", str(D.world), "--prefix", str(prefix), "--no-readback"], check=True,
+                            "--ranks", str(D.world), "--prefix", str(prefix), "--no-readback",
+                            "--agg-rows", str(int(os.environ.get("SSS_HIP_AGG_ROWS", "0") or 0))], check=True,
                            cwd=str(ROOT), stdout=sys.stderr)
             hier_src = f"partition set written to {prefix.parent}"
             # a set this run wrote is removed at the end (tens of GB of scratch per rank count)
@@ -709,7 +766,7 @@ def main():
         # throughput mode must converge within the reference's count + 2
         ref_conv["ladder"] = ("ok" if parity["final_relres"] < pars["tol"] and relres < pars["tol"]
                               and its <= parity["iterations_to_tol"] + 2 else "violated")
-    elif conv.exists() and args.stencil == 7 and not circuit:
+    elif conv.exists() and args.stencil == 7 and not irregular:
         try:
             cj = json.loads(conv.read_text())["modes"]
             ref_conv = {"iterations_to_tol_reference": cj["parity"]["iters"],
@@ -730,7 +787,7 @@ def main():
     # inside this process), with the commit it was measured at
     traffic, traffic_src = None, None
     pmcs = sorted((ROOT / "profiles").glob("r*_level0_spmv_pmc.json"))
-    if pmcs and D.world == 1 and not circuit:
+    if pmcs and D.world == 1 and not irregular:
         try:
             rec = json.loads(pmcs[-1].read_text())
             if rec.get("n") == n and rec.get("a_format") == a_format:
@@ -748,11 +805,12 @@ def main():
         hb_stop = threading.Event()
         threading.Thread(target=heartbeat, args=(hb_stop, time.perf_counter()), daemon=True).start()
         Hc = H
-        if args.cpu_n and args.cpu_n != n and not circuit:
+        if args.cpu_n and args.cpu_n != n and not irregular:
             Mc = A.generate(args.stencil, args.cpu_n)
             Hc = quiet_call(A.Hierarchy, Mc)
-        cpu_n = n if circuit else (args.cpu_n or n)
-        wname = f"G3_circuit stand-in ({n} rows)" if circuit else f"{args.stencil}-pt {cpu_n}^3"
+        cpu_n = n if irregular else (args.cpu_n or n)
+        wname = (f"{mtx.name} ({N} rows)" if mtx is not None else f"G3_circuit stand-in ({n} rows)" if circuit
+                 else f"{args.stencil}-pt {cpu_n}^3")
         hostinfo = host_cpus()
         a0_bytes = 12 * nnz + 4 * (N + 1) + 24 * N
         print("[bench] CPU baseline: reference semantics, 1 thread", file=sys.stderr, flush=True)
@@ -801,9 +859,10 @@ def main():
         "ms_per_step": ms_per_step, "higher_is_better": True,
         "scaling": "strong" if D.world > 1 else None, "vs_baseline": None,
         "dtype": "f64",
-        "data": ("synthetic (G3_circuit stand-in: weighted graph Laplacian + shift, amg_amd/workloads.py; b = x0 = 1)"
+        "data": (f"{mtx} read by SSS_mat_read (the reference's .mtx ingest), b = x0 = 1" if mtx is not None else
+                 "synthetic (G3_circuit stand-in: weighted graph Laplacian + shift, amg_amd/workloads.py; b = x0 = 1)"
                  if circuit else f"synthetic ({args.stencil}-pt Poisson generated in memory, b = x0 = 1)"),
-        "config": {"workload": f"g3_circuit_standin_{n}" if circuit else f"poisson{args.stencil}_{n}^3", "rows": N, "nnz": nnz, "levels": len(levels),
+        "config": {"workload": workload, "rows": N, "nnz": nnz, "levels": len(levels),
                    "hierarchy": [list(t) for t in levels],
                    "mode": args.mode, "smoother": smoother, "coarse": coarse,
                    "inner": inner if smoother != "exact" else None,
@@ -835,6 +894,8 @@ def main():
                    "transport": transport},
         "roofline": {"bound": "hbm", "kernel": "spmv_adaptive<RESID> level 0 from its CSR arrays (y = b - A0 x)",
                      "achieved": achieved, "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": achieved / PEAK_HBM_GBS,
+                     # the same residual as the V-cycle runs it, from its own (compressed) storage
+                     "cycle_storage_frac": format_gbps / PEAK_HBM_GBS,
                      "frac_of_copy_peak": achieved / COPY_PEAK_GBS, "avg_launch_ms": csr_ms,
                      "bytes_per_launch": csr_bytes, "traffic": traffic.get("csr") if traffic else None,
                      "traffic_source": traffic_src,
@@ -875,7 +936,7 @@ def main():
         "cpu_baseline": cpu_baseline,
         "cpu_baseline_same_mode": cpu_mt,
     }
-    if D.world == 1 and not circuit:
+    if D.world == 1 and not irregular:
         # left for the N > 1 runs of the same workload on this host (parallel_efficiency)
         try:
             single_ref_path(workload, args.mode).write_text(
@@ -887,10 +948,13 @@ def main():
         ref = single_gpu_reference(args.single_ref, rec["config"])
         rec["single_gpu_reference"] = ref
         rec["parallel_efficiency"] = value / (D.world * ref["value"]) if ref else None
-    if cpu_baseline:
-        rec["speedup_vs_cpu"] = value / cpu_baseline["value"]
+    # speed-ups on the same basis only: the drop-in default (parity mode, x bitwise the
+    # reference's) against the reference semantics on 1 host thread, and this line's throughput mode
+    # against the CPU running that same mode on every usable core
+    if cpu_baseline and parity:
+        rec["speedup_parity_vs_cpu_reference_semantics_1_thread"] = parity["value"] / cpu_baseline["value"]
     if cpu_mt:
-        rec["speedup_vs_cpu_same_mode"] = value / cpu_mt["value"]
+        rec["speedup_throughput_vs_cpu_same_mode_all_cores"] = value / cpu_mt["value"]
     DH.close()
     if comm is not None:
         comm.close()

@@ -289,3 +289,30 @@ def test_bench_single_gpu_reference_matches_configuration(tmp_path):
     # same workload, other smoother: not a denominator
     assert bench.single_gpu_reference(str(thr), dict(cfg, workload="poisson7_63^3", smoother="jacobi")) is None
     assert bench.single_ref_path("poisson7_64^3", "parity") != bench.single_ref_path("poisson7_64^3", "throughput")
+
+
+def test_partition_set_versioned(tmp_path, monkeypatch):
+    """A partition set names its file layout: the C writer's version word equals
+    amg_amd.partition.PART_FORMAT, bench.py puts it (and a non-default tail threshold) in the set's
+    directory name, and a manifest of another layout is not reused (it would abort the run with
+    ERROR_WRONG_FILE instead of being regenerated)."""
+    import json
+    import struct
+    import amg_amd as A
+    import bench
+    from amg_amd.partition import PART_FORMAT
+    from conftest import build_hierarchy, quiet_ctx
+    H = build_hierarchy(A.generate(7, 12), quiet_ctx)
+    A.part_save(H, 2, tmp_path / "part", 60)
+    raw = (tmp_path / "part.r0").read_bytes()
+    assert raw[:8] == b"SSSPART1" and struct.unpack("<i", raw[8:12])[0] == PART_FORMAT
+    monkeypatch.delenv("SSS_HIP_AGG_ROWS", raising=False)
+    assert bench.part_set_name(7, 512, 8) == f"sss_parts_v{PART_FORMAT}_7pt_512_8r"
+    monkeypatch.setenv("SSS_HIP_AGG_ROWS", "80000")
+    assert bench.part_set_name(7, 512, 8).endswith("_agg80000")
+    man = tmp_path / "part.json"
+    man.write_text(json.dumps({"format": PART_FORMAT - 1}))
+    assert not bench.part_set_usable(man)
+    man.write_text(json.dumps({"format": PART_FORMAT}))
+    assert bench.part_set_usable(man)
+    assert not bench.part_set_usable(tmp_path / "missing.json")

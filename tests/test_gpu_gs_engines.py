@@ -493,6 +493,67 @@ def test_fused_engine_edge_rows_bitwise(fused, monkeypatch):
             assert np.array_equal(xg.view(np.uint64), xr.view(np.uint64)), (sweeps, post, fused)
 
 
+@pytest.mark.parametrize("nonfinite", [False, True])
+@pytest.mark.parametrize("smoother", [2, 1])   # SSS_SM_GS (exact GS-CF), SSS_SM_JACOBI (C/F-Jacobi)
+@pytest.mark.parametrize("fused", ["0", "1"])
+def test_host_smooth_zero_iterate(fused, smoother, nonfinite, monkeypatch):
+    """A zero iterate (every bit of x zero) takes the zero-iterate forms: the fused engine's reduced
+    sweep-0 rows and the C/F-Jacobi first pass without the matrix.  Their exactness rests on two
+    guards, both forced here: b_i = -0.0 on many rows (the dropped products (+-0) would otherwise
+    turn -0.0 into +0.0 in the reference's chain) and, in the second case, a non-finite entry
+    (inf * 0 = NaN must reach the rows that read it: the plans then keep every product).  Bitwise
+    the oracle's smoother for 1, 2 and 3 sweeps, both directions."""
+    monkeypatch.setenv("SSS_HIP_GS_ENGINE", "flow")
+    monkeypatch.setenv("SSS_HIP_GS_FUSED", fused)
+    ora = oracle.load()
+    M, mark = _sym_two_class(600, 350, 9)
+    n = M.mat.num_rows
+    if nonfinite:
+        rp = M.rp
+        M.v[rp[100] + (1 if M.ci[rp[100]] == 100 else 0)] = np.inf   # an off-diagonal entry of row 100
+    rng = np.random.default_rng(23)
+    mk = mark.ctypes.data_as(C.POINTER(C.c_int))
+    for sweeps in (1, 2, 3):
+        for post in (False, True):
+            b = rng.standard_normal(n)
+            b[::5] = -0.0
+            b[1::11] = 0.0
+            xg, xr = np.zeros(n), np.zeros(n)
+            assert A.lib().sss_hip_host_smooth(C.byref(_smtr(M.mat, b, xg, mk, sweeps, post, smoother)), int(post)) == 0
+            (ora.ora_smoother_post if post else ora.ora_smoother_pre)(C.byref(_smtr(M.mat, b, xr, mk, sweeps, post,
+                                                                                     smoother)))
+            # NaNs at the same rows (their sign bit is the hardware's: x86 and gfx950 differ), every
+            # other value bitwise
+            ng, nr = np.isnan(xg), np.isnan(xr)
+            assert np.array_equal(ng, nr), (sweeps, post, fused, smoother)
+            assert np.array_equal(xg[~ng].view(np.uint64), xr[~nr].view(np.uint64)), (sweeps, post, fused, smoother)
+            assert (~np.isfinite(xr)).any() == nonfinite
+
+
+@pytest.mark.parametrize("fused", ["0", "1"])
+def test_host_smooth_stall_fails(fused, monkeypatch):
+    """The host smoother entry (SSS_amg_smoother_pre/post) on a stalled one-launch pass or fused
+    call (forced: SSS_HIP_GS_SPIN < 0) returns the stall error instead of a wrong x, and the stall
+    word is cleared: the same call without the hook succeeds and is bitwise the oracle."""
+    monkeypatch.setenv("SSS_HIP_GS_ENGINE", "flow")
+    monkeypatch.setenv("SSS_HIP_GS_FUSED", fused)
+    ora = oracle.load()
+    M, mark = _sym_two_class(600, 350, 9)
+    n = M.mat.num_rows
+    rng = np.random.default_rng(5)
+    b = rng.standard_normal(n)
+    x0 = rng.standard_normal(n)
+    mk = mark.ctypes.data_as(C.POINTER(C.c_int))
+    monkeypatch.setenv("SSS_HIP_GS_SPIN", "-1")
+    xg = x0.copy()
+    assert A.lib().sss_hip_host_smooth(C.byref(_smtr(M.mat, b, xg, mk, 2, False)), 0) == -14   # ERROR_MISC
+    monkeypatch.delenv("SSS_HIP_GS_SPIN")
+    xg, xr = x0.copy(), x0.copy()
+    assert A.lib().sss_hip_host_smooth(C.byref(_smtr(M.mat, b, xg, mk, 2, False)), 0) == 0
+    ora.ora_smoother_pre(C.byref(_smtr(M.mat, b, xr, mk, 2, False)))
+    assert np.array_equal(xg.view(np.uint64), xr.view(np.uint64))
+
+
 @pytest.mark.parametrize("depth_form", ["gpu", "host"])
 def test_fused_depth_forms(p32_h, depth_form, monkeypatch):
     """The fused plan's ticket order (fused-DAG depth) computed on the GPU per depth group or on the

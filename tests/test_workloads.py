@@ -48,3 +48,48 @@ def test_circuit_oracle_converges():
     rtn, rel, _ = oracle_solve(H, np.ones(n), np.ones(n))
     assert H.num_levels >= 4
     assert rel[-1] < H.pars.tol and len(rel) < 40
+
+
+# ---- bench.py --mtx (BASELINE.json configs[0] nos5 / configs[3] G3_circuit when the files are supplied)
+def test_bench_mtx_reads_like_the_reference(tmp_path):
+    """bench.py --mtx goes through SSS_mat_read (the reference's ingest; tests/test_ref_units.py pins
+    that reader to the compiled reference one): on 1138_bus the matrix it loads is the reader's CSR,
+    and the workload is named after the file."""
+    import ctypes as C
+    import sys
+    from conftest import BUS_MTX, ROOT
+    sys.path.insert(0, str(ROOT))
+    import amg_amd as A
+    import bench
+    M = bench.load_mtx(A, BUS_MTX)
+    R = A.read_mtx(BUS_MTX)
+    try:
+        assert (M.num_rows, M.num_cols, M.num_nnzs) == (1138, 1138, 4054)
+        n, z = M.num_rows, M.num_nnzs
+        for f, k in (("row_ptr", n + 1), ("col_idx", z), ("val", z)):
+            a = np.ctypeslib.as_array(getattr(M, f), shape=(k,))
+            b = np.ctypeslib.as_array(getattr(R, f), shape=(k,))
+            assert np.array_equal(a, b), f
+    finally:
+        A.lib().SSS_mat_destroy(C.byref(M))
+        A.lib().SSS_mat_destroy(C.byref(R))
+
+    class Args:
+        n, stencil = None, 7
+    assert bench.workload_name(Args, False, BUS_MTX) == "mtx_1138_bus"
+
+
+def test_bench_mtx_cli(tmp_path):
+    """The --mtx flag on the command line: the rank probe names the file's workload; a missing file
+    and a multi-rank request fail before anything touches the GPU."""
+    import json
+    import subprocess
+    import sys
+    from conftest import BUS_MTX, ROOT
+    r = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--probe-ranks", "--mtx", str(BUS_MTX)],
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    assert json.loads(r.stdout.strip())["workload"] == "mtx_1138_bus"
+    r = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--mtx", str(tmp_path / "nos5.mtx")],
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode != 0 and "no such file" in r.stderr
