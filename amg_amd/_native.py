@@ -115,13 +115,13 @@ ABI_SYMBOLS = [
     "sss_hip_cycle_launches", "sss_hip_cycle_bytes",
     "sss_hip_spmv_plan_create", "sss_hip_spmv_plan_destroy", "sss_hip_spmv", "sss_hip_host_spmv",
     "sss_hip_host_smooth", "sss_hip_host_coarse_solve", "sss_hip_host_cache_clear", "sss_hip_time_level0_spmv", "sss_hip_time_iterations",
-    "sss_hip_time_level0_spmv_csr",
+    "sss_hip_time_level0_spmv_csr", "sss_hip_time_levels", "sss_hip_dist_time_tail_levels",
     "sss_gen_stencil",
-    "sss_hip_rccl_unique_id", "sss_hip_comm_rccl", "sss_hip_comm_host", "sss_hip_comm_destroy",
+    "sss_hip_rccl_unique_id", "sss_hip_comm_rccl", "sss_hip_comm_host", "sss_hip_comm_timing", "sss_hip_comm_destroy",
     "sss_hip_dist_create", "sss_hip_dist_destroy", "sss_hip_dist_info", "sss_hip_dist_level_flags",
     "sss_hip_dist_upload_vec",
     "sss_hip_dist_download_vec", "sss_hip_dist_cycle", "sss_hip_dist_residual_norm", "sss_hip_dist_sync",
-    "sss_hip_dist_time_level0_spmv",
+    "sss_hip_dist_time_level0_spmv", "sss_hip_dist_time_levels", "sss_hip_dist_halo_stats",
     "sss_part_plan_create", "sss_part_plan_destroy", "sss_part_save", "sss_part_plan_load",
     "sss_hip_dist_create_from_files", "sss_hip_dist_level_size", "sss_part_plan_nagg", "sss_part_plan_level",
     "sss_part_plan_matrix", "sss_part_plan_ids", "sss_part_plan_halo",
@@ -205,10 +205,13 @@ def _declare(lib):
                                                 C.c_int]),
         "sss_hip_time_level0_spmv": (C.c_int, [C.c_void_p, C.c_int, _dbl_p]),
         "sss_hip_time_level0_spmv_csr": (C.c_int, [C.c_void_p, C.c_int, _dbl_p]),
+        "sss_hip_time_levels": (C.c_int, [C.c_void_p, C.c_int, _dbl_p, C.c_int]),
+        "sss_hip_dist_time_tail_levels": (C.c_int, [C.c_void_p, C.c_int, _dbl_p, C.c_int]),
         "sss_hip_time_iterations": (C.c_int, [C.c_void_p, C.c_int, _dbl_p, _dbl_p]),
         "sss_hip_rccl_unique_id": (C.c_int, [C.c_char_p]),
         "sss_hip_comm_rccl": (C.c_void_p, [C.c_int, C.c_int, C.c_char_p, C.c_int]),
         "sss_hip_comm_host": (C.c_void_p, [C.c_int, C.c_int, P(SSS_HIP_HOST_TRANSPORT)]),
+        "sss_hip_comm_timing": (C.c_void_p, [C.c_int, C.c_int]),
         "sss_hip_comm_destroy": (None, [C.c_void_p]),
         "sss_hip_dist_create": (C.c_void_p, [P(SSS_AMG), P(SSS_HIP_OPTS), C.c_void_p, C.c_int]),
         "sss_hip_dist_destroy": (None, [C.c_void_p]),
@@ -221,6 +224,9 @@ def _declare(lib):
         "sss_hip_dist_residual_norm": (C.c_int, [C.c_void_p, _dbl_p]),
         "sss_hip_dist_sync": (C.c_int, [C.c_void_p]),
         "sss_hip_dist_time_level0_spmv": (C.c_int, [C.c_void_p, C.c_int, _dbl_p]),
+        "sss_hip_dist_time_levels": (C.c_int, [C.c_void_p, C.c_int, _dbl_p, _dbl_p, C.c_int]),
+        "sss_hip_dist_halo_stats": (C.c_int, [C.c_void_p, P(C.c_longlong), P(C.c_longlong), C.c_int, C.c_int,
+                                              _int_p, _int_p, _int_p]),
         "sss_part_plan_create": (C.c_void_p, [P(SSS_AMG), C.c_int, C.c_int, C.c_int]),
         "sss_part_save": (C.c_int, [P(SSS_AMG), C.c_int, C.c_int, C.c_char_p]),
         "sss_part_plan_load": (C.c_void_p, [C.c_char_p]),
@@ -456,6 +462,12 @@ class DeviceHierarchy:
         self._check(lib().sss_hip_time_level0_spmv_csr(self.h, reps, C.byref(ms)), "time_level0_spmv_csr")
         return ms.value
 
+    def time_levels(self, reps: int) -> list:
+        """ms per level of an eager cycle (sss_hip_time_levels); advances the iterate"""
+        lv = (C.c_double * self.H.num_levels)() if self.H is not None else (C.c_double * 32)()
+        self._check(lib().sss_hip_time_levels(self.h, reps, lv, len(lv)), "time_levels")
+        return list(lv)
+
     def time_iterations(self, reps: int):
         ms, ares = C.c_double(), C.c_double()
         self._check(lib().sss_hip_time_iterations(self.h, reps, C.byref(ms), C.byref(ares)), "time_iterations")
@@ -623,7 +635,8 @@ class TorchHostTransport:
 
 
 class Comm:
-    """sss_hip_comm: RCCL (one GPU per rank) or the host transport (tests)."""
+    """sss_hip_comm: RCCL (one GPU per rank), the host transport (tests), or "timing": no transfer at all
+    (the per-rank compute floor, tools/n8_floor.py; iterates meaningless)."""
 
     def __init__(self, nranks: int, rank: int, kind: str = "rccl", device: int = -1):
         self.kind = kind
@@ -642,6 +655,8 @@ class Comm:
                 raise RuntimeError("communicator (rccl) creation failed: no unique id on rank 0")
             uid = C.create_string_buffer(raw[:128], 128)
             self.c = lib().sss_hip_comm_rccl(nranks, rank, uid, device)
+        elif kind == "timing":
+            self.c = lib().sss_hip_comm_timing(nranks, rank)
         else:
             self.transport = TorchHostTransport()
             self.c = lib().sss_hip_comm_host(nranks, rank, C.byref(self.transport.t))
@@ -731,6 +746,28 @@ class DistHierarchy:
         ms = C.c_double()
         self._check(lib().sss_hip_dist_time_level0_spmv(self.d, reps, C.byref(ms)), "dist spmv timing")
         return ms.value
+
+    def time_levels(self, reps: int):
+        """(cycle ms as it runs, [per partitioned level ms of an eager cycle] + [replicated tail ms])"""
+        cyc = C.c_double()
+        lv = (C.c_double * (self.nagg + 1))()
+        self._check(lib().sss_hip_dist_time_levels(self.d, reps, C.byref(cyc), lv, self.nagg + 1), "dist level timing")
+        return cyc.value, list(lv)
+
+    def time_tail_levels(self, reps: int) -> list:
+        """ms per replicated level (global levels nagg, nagg + 1, ...) of the tail's own eager cycle"""
+        lv = (C.c_double * 32)()
+        self._check(lib().sss_hip_dist_time_tail_levels(self.d, reps, lv, 32), "tail level timing")
+        return list(lv)
+
+    def halo_stats(self, reset: bool = True) -> dict:
+        calls = (C.c_longlong * self.nagg)()
+        dbl = (C.c_longlong * self.nagg)()
+        own, allr, tl = C.c_int(), C.c_int(), C.c_int()
+        self._check(lib().sss_hip_dist_halo_stats(self.d, calls, dbl, self.nagg, int(reset), C.byref(own), C.byref(allr),
+                                                  C.byref(tl)), "dist halo stats")
+        return {"exchanges": list(calls), "doubles_sent": list(dbl), "gather_own": own.value, "gather_all": allr.value,
+                "tail_levels": tl.value}
 
     def close(self):
         if self.d:

@@ -31,6 +31,10 @@ using namespace sss;
 struct sss_hip_comm {
     int nranks = 1, rank = 0;
     bool host = false;
+    // timing only (sss_hip_comm_timing): every collective and halo transfer is skipped, the rest of
+    // the rank's cycle -- its kernels, halo packs, the graph -- runs as over RCCL: the per-rank compute
+    // floor of a multi-GPU run, measured one rank at a time on one GPU (its results are meaningless)
+    bool timing = false;
     ncclComm_t nccl = nullptr;
     sss_hip_host_transport t{};
 };
@@ -131,6 +135,11 @@ struct sss_hip_dist {
     int use_graph = 0;
     hipGraphExec_t cycle_exec = nullptr;
     bool graph_resid_ready = false;   // resid_c_ready as the captured cycle leaves it
+    // halo statistics as enqueued (sss_hip_dist_halo_stats): exchanges and doubles sent per level
+    long long ex_calls[kMaxLevels] = {}, ex_doubles[kMaxLevels] = {};
+    // per-level timing of an eager cycle (sss_hip_dist_time_levels): events after each level's
+    // descent, the tail and each level's ascent
+    std::vector<hipEvent_t> lev_ev;
 };
 
 namespace {
@@ -147,10 +156,13 @@ int exchange_begin(sss_hip_dist *d, int l, double *vec)
     const hipStream_t s = d->stream;
     if (H.nsend == 0 && H.nrecv == 0) return 0;
     const int ns = H.soff.empty() ? 0 : H.soff.back();
+    d->ex_calls[l]++;
+    d->ex_doubles[l] += ns;
     if (ns > 0) {
         hipLaunchKernelGGL(pack_kernel, dim3((ns + 255) / 256), dim3(256), 0, s, ns, H.d_sidx, vec, H.d_sbuf);
         SSS_HIP(hipGetLastError());
     }
+    if (c->timing) return 0;
     if (!c->host) {
         SSS_HIP(hipEventRecord(d->ev_packed, s));
         SSS_HIP(hipStreamWaitEvent(d->cstream, d->ev_packed, 0));
@@ -181,7 +193,7 @@ int exchange_begin(sss_hip_dist *d, int l, double *vec)
 int exchange_end(sss_hip_dist *d, int l)
 {
     const Halo &H = d->L[l].halo;
-    if (d->comm->host || (H.nsend == 0 && H.nrecv == 0)) return 0;
+    if (d->comm->host || d->comm->timing || (H.nsend == 0 && H.nrecv == 0)) return 0;
     SSS_HIP(hipStreamWaitEvent(d->stream, d->ev_halo, 0));
     return 0;
 }
@@ -276,6 +288,7 @@ int smooth(sss_hip_dist *d, int l, int post, ResidFuse *rf = nullptr, bool x_zer
 int allreduce_host(sss_hip_dist *d, double *v, int n)
 {
     sss_hip_comm *c = d->comm;
+    if (c->timing) return 0;
     if (c->host) return c->t.allreduce_sum(c->t.ctx, v, n) ? ERROR_MISC : 0;
     double *dv = dev_alloc<double>((size_t)n);
     if (!dv) return ERROR_MISC;
@@ -329,6 +342,12 @@ int allgather_coarse(sss_hip_dist *d)
     sss_hip_comm *c = d->comm;
     const hipStream_t s = d->stream;
     if (!c->host) {
+        if (c->timing) {   // this rank's own part only
+            if (d->nc_own > 0)
+                SSS_HIP(hipMemcpyAsync(d->d_call + d->displs[c->rank], d->d_cown, sizeof(double) * d->nc_own,
+                                       hipMemcpyDeviceToDevice, s));
+            return 0;
+        }
         SSS_NCCL(ncclGroupStart());
         for (int q = 0; q < c->nranks; ++q) {
             if (q == c->rank) continue;
@@ -360,7 +379,7 @@ int allreduce_norm(sss_hip_dist *d)
 {
     sss_hip_comm *c = d->comm;
     if (int rc = launch_err_flag(d->d_err, d->d_norm + 1, d->stream)) return rc;
-    if (!c->host) SSS_NCCL(ncclAllReduce(d->d_norm, d->d_norm, 2, ncclDouble, ncclSum, c->nccl, d->stream));
+    if (!c->host && !c->timing) SSS_NCCL(ncclAllReduce(d->d_norm, d->d_norm, 2, ncclDouble, ncclSum, c->nccl, d->stream));
     SSS_HIP(hipMemcpyAsync(d->h_norm, d->d_norm, 2 * sizeof(double), hipMemcpyDeviceToHost, d->stream));
     SSS_HIP(hipStreamSynchronize(d->stream));
     if (c->host && c->t.allreduce_sum(c->t.ctx, d->h_norm, 2)) return ERROR_MISC;
@@ -400,6 +419,7 @@ void release(sss_hip_dist *d)
     dev_free(d->d_norm);
     dev_free(d->d_err);
     if (d->h_norm) (void)hipHostFree(d->h_norm);
+    for (hipEvent_t e : d->lev_ev) (void)hipEventDestroy(e);
     if (d->stream) (void)hipStreamDestroy(d->stream);
     if (d->cstream) (void)hipStreamDestroy(d->cstream);
     if (d->ev_packed) (void)hipEventDestroy(d->ev_packed);
@@ -450,6 +470,16 @@ extern "C" sss_hip_comm *sss_hip_comm_host(int nranks, int rank, const sss_hip_h
     c->rank = rank;
     c->host = true;
     c->t = *t;
+    return c;
+}
+
+extern "C" sss_hip_comm *sss_hip_comm_timing(int nranks, int rank)
+{
+    if (nranks < 1 || rank < 0 || rank >= nranks) return nullptr;
+    auto *c = new sss_hip_comm();
+    c->nranks = nranks;
+    c->rank = rank;
+    c->timing = true;
     return c;
 }
 
@@ -751,7 +781,17 @@ static int dist_cycle_enqueue(sss_hip_dist *d)
     const int nagg = d->nagg;
     int rc;
     d->resid_c_ready = false;
+    // per-level timing (eager cycles only): event k marks the end of step k -- descent of level
+    // 0 .. nagg-1, the replicated tail, ascent of level nagg-1 .. 0
+    const bool tev = !d->lev_ev.empty();
+    int ek = 0;
+    auto mark = [&]() -> int {
+        if (tev) SSS_HIP(hipEventRecord(d->lev_ev[(size_t)++ek], s));
+        return 0;
+    };
+    if (tev) SSS_HIP(hipEventRecord(d->lev_ev[0], s));
     for (int l = 0; l < nagg; ++l) {   // descent
+        if (l > 0 && (rc = mark())) return rc;
         TraceRange tr("rank %d level %d descent", d->comm->rank, l);
         DLevel &L = d->L[l];
         ResidFuse rf;   // the last C pass may form the residual's C rows (then only F rows remain)
@@ -783,11 +823,14 @@ static int dist_cycle_enqueue(sss_hip_dist *d)
             SSS_HIP(hipMemsetAsync(tx, 0, sizeof(double) * (size_t)d->nc_all, s));
         }
     }
+    if ((rc = mark())) return rc;
     {
         TraceRange tr("rank %d replicated tail", d->comm->rank);
         if ((rc = sss_hip_cycle(d->tail))) return rc;   // replicated levels, same stream
     }
+    if ((rc = mark())) return rc;
     for (int l = nagg - 1; l >= 0; --l) {           // ascent
+        if (l < nagg - 1 && (rc = mark())) return rc;
         TraceRange tr("rank %d level %d ascent", d->comm->rank, l);
         DLevel &L = d->L[l];
         double *xc = l + 1 < nagg ? d->L[l + 1].x : hier_vec(d->tail, 0, SSS_HIP_VEC_X);
@@ -817,6 +860,82 @@ static int dist_cycle_enqueue(sss_hip_dist *d)
             return rc;
         }
     }
+    return mark();
+}
+
+// Timing of this rank's cycle (for the per-rank compute floor with sss_hip_comm_timing): *cycle_ms =
+// the cycle as it runs (the captured graph when there is one), averaged over reps; level_ms[l] (l <
+// nagg) = level l's descent + ascent and level_ms[nagg] = the replicated tail, from reps eager cycles
+// with an event between the steps (launch gaps included).  Advances the iterate.
+extern "C" int sss_hip_dist_time_levels(sss_hip_dist *d, int reps, double *cycle_ms, double *level_ms, int nslots)
+{
+    if (!d || reps < 1 || nslots < d->nagg + 1) return ERROR_INPUT_PAR;
+    const int nagg = d->nagg;
+    const hipStream_t s = d->stream;
+    hipEvent_t e0, e1;
+    SSS_HIP(hipEventCreate(&e0));
+    SSS_HIP(hipEventCreate(&e1));
+    int rc = sss_hip_dist_cycle(d);   // (captures the graph on first use)
+    if (!rc && hipStreamSynchronize(s) != hipSuccess) rc = ERROR_MISC;
+    if (!rc && hipEventRecord(e0, s) != hipSuccess) rc = ERROR_MISC;
+    for (int r = 0; r < reps && !rc; ++r) rc = sss_hip_dist_cycle(d);
+    float ms = 0.0f;
+    if (!rc && (hipEventRecord(e1, s) != hipSuccess || hipEventSynchronize(e1) != hipSuccess ||
+                hipEventElapsedTime(&ms, e0, e1) != hipSuccess))
+        rc = ERROR_MISC;
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+    if (rc) return rc;
+    *cycle_ms = ms / reps;
+    d->lev_ev.assign((size_t)2 * nagg + 2, nullptr);
+    for (auto &e : d->lev_ev)
+        if (hipEventCreate(&e) != hipSuccess) rc = ERROR_MISC;
+    std::vector<double> acc((size_t)nagg + 1, 0.0);
+    for (int r = 0; r < reps && !rc; ++r) {
+        rc = dist_cycle_enqueue(d);
+        if (!rc && hipStreamSynchronize(s) != hipSuccess) rc = ERROR_MISC;
+        auto seg = [&](int a, int b) {
+            float t = 0.0f;
+            if (hipEventElapsedTime(&t, d->lev_ev[(size_t)a], d->lev_ev[(size_t)b]) != hipSuccess) rc = ERROR_MISC;
+            return (double)t;
+        };
+        for (int l = 0; l < nagg && !rc; ++l) {
+            acc[(size_t)l] += seg(l, l + 1);                                       // descent
+            const int k = nagg + 1 + (nagg - 1 - l);                               // ascent of level l
+            acc[(size_t)l] += seg(k, k + 1);
+        }
+        if (!rc) acc[(size_t)nagg] += seg(nagg, nagg + 1);
+    }
+    for (hipEvent_t e : d->lev_ev)
+        if (e) (void)hipEventDestroy(e);
+    d->lev_ev.clear();
+    if (rc) return rc;
+    for (int l = 0; l <= nagg; ++l) level_ms[l] = acc[(size_t)l] / reps;
+    return 0;
+}
+
+// The replicated tail's own per-level times (sss_hip_time_levels on it; the rank's iterate advances)
+extern "C" int sss_hip_dist_time_tail_levels(sss_hip_dist *d, int reps, double *level_ms, int nslots)
+{
+    if (!d || !d->tail) return ERROR_INPUT_PAR;
+    return sss_hip_time_levels(d->tail, reps, level_ms, nslots);
+}
+
+// Halo exchanges enqueued per partitioned level since the last reset, and the doubles this rank
+// sent in them (a captured cycle counts once, at its capture); nc_own / nc_all: the all-gather
+// into the replicated tail (own and all rows of its first level); tail_levels: the replicated levels.
+extern "C" int sss_hip_dist_halo_stats(sss_hip_dist *d, long long *calls, long long *doubles, int nslots, int reset,
+                                       int *nc_own, int *nc_all, int *tail_levels)
+{
+    if (!d || nslots < d->nagg) return ERROR_INPUT_PAR;
+    for (int l = 0; l < d->nagg; ++l) {
+        calls[l] = d->ex_calls[l];
+        doubles[l] = d->ex_doubles[l];
+        if (reset) d->ex_calls[l] = d->ex_doubles[l] = 0;
+    }
+    *nc_own = d->nc_own;
+    *nc_all = d->nc_all;
+    *tail_levels = sss_hip_num_levels(d->tail);
     return 0;
 }
 

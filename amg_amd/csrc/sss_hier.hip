@@ -82,6 +82,11 @@ struct sss_hip_hier {
     double *pcg_s = nullptr;     // device scalars
     double *pcg_h = nullptr;     // pinned host mirror
     TailPlan tail;               // the small coarse levels as one single-workgroup launch (sss_tail.hip)
+    // per-level timing of an eager cycle (sss_hip_time_levels): an event after each step of the
+    // walk, tagged with the level the step belonged to
+    std::vector<hipEvent_t> lev_ev;
+    std::vector<int> lev_tag;
+    int lev_n = 0;
 };
 
 static int env_int(const char *name, int dflt)
@@ -979,6 +984,14 @@ static int walk_cycle(sss_hip_hier *h, CoarseFn coarse, bool pend = false)
     int visits[kMaxLevels] = {0};
     int l = 0, rc;
     hipStream_t s = h->stream;
+    // per-level timing (sss_hip_time_levels): an event at the end of each step, tagged with its level
+    auto mark = [&](int level) -> int {
+        if (h->lev_ev.empty() || h->lev_n >= (int)h->lev_ev.size()) return 0;
+        h->lev_tag[(size_t)h->lev_n] = level;
+        SSS_HIP(hipEventRecord(h->lev_ev[(size_t)h->lev_n++], s));
+        return 0;
+    };
+    if ((rc = mark(-1))) return rc;
     // x_l is zero only on arrival by the descent (restricted into, then cleared): a W-cycle's level
     // re-descended after its post-smoother starts its pre-smoother from that iterate
     bool zeroed = false;
@@ -991,6 +1004,7 @@ static int walk_cycle(sss_hip_hier *h, CoarseFn coarse, bool pend = false)
                     TraceRange tr("levels %d-%d tail", l, nl - 1);
                     if ((rc = tail_launch(h->tail, s))) return rc;
                 }
+                if ((rc = mark(l))) return rc;
                 goto ascent;
             }
             TraceRange tr("level %d descent", l);
@@ -1005,13 +1019,14 @@ static int walk_cycle(sss_hip_hier *h, CoarseFn coarse, bool pend = false)
             ledger_add(8.0 * h->L[l].A.n);
             SSS_HIP(hipMemsetAsync(h->L[l].x, 0, sizeof(double) * (size_t)h->L[l].A.n, s));
             zeroed = true;
+            if ((rc = mark(l - 1))) return rc;
         }
         if (g_ledger) g_ledger->slot = kMaxLevels + 1;
         {
             TraceRange tr("coarse solve (level %d)", nl - 1);
             rc = coarse(h);
         }
-        if (rc) return rc;
+        if (rc || (rc = mark(nl - 1))) return rc;
     ascent:
         while (l > 0) {
             l--;
@@ -1042,6 +1057,7 @@ static int walk_cycle(sss_hip_hier *h, CoarseFn coarse, bool pend = false)
             } else if ((rc = sss_hip_smooth(h, l, 1))) {
                 return rc;
             }
+            if ((rc = mark(l))) return rc;
             if (visits[l] < cycle_type) break;
             visits[l] = 0;
         }
@@ -1357,6 +1373,43 @@ extern "C" int sss_hip_level_info_get(sss_hip_hier *h, int level, sss_hip_level_
     out->r_format = level + 1 < h->nl ? fmt(L.R) : 0;
     out->p_format = level + 1 < h->nl ? fmt(L.P) : 0;
     out->a_stream_bytes = L.A.stream_bytes;
+    return 0;
+}
+
+// Per-level time of the cycle: level_ms[l] = level l's steps (pre-smoothing, residual, restriction,
+// zero fill; prolongation, post-smoothing; the coarsest level: its solve; a single-workgroup tail:
+// at its first level), averaged over reps eager cycles with an event between the steps (launch gaps
+// included, unlike the graph-replayed cycle).  Advances the iterate.  nslots >= num levels.
+extern "C" int sss_hip_time_levels(sss_hip_hier *h, int reps, double *level_ms, int nslots)
+{
+    if (!h || reps < 1 || nslots < h->nl) return ERROR_INPUT_PAR;
+    const size_t nev = (size_t)4 * h->nl + 4;
+    h->lev_ev.assign(nev, nullptr);
+    h->lev_tag.assign(nev, -1);
+    int rc = 0;
+    for (auto &e : h->lev_ev)
+        if (hipEventCreate(&e) != hipSuccess) rc = ERROR_MISC;
+    std::vector<double> acc((size_t)h->nl, 0.0);
+    for (int r = 0; r < reps && !rc; ++r) {
+        h->lev_n = 0;
+        h->resid_c_ready = h->pending_f = false;
+        rc = walk_cycle(h, [](sss_hip_hier *hh) { return sss_hip_coarse_solve(hh); }, false);
+        if (!rc && hipStreamSynchronize(h->stream) != hipSuccess) rc = ERROR_MISC;
+        for (int k = 1; k < h->lev_n && !rc; ++k) {
+            float t = 0.0f;
+            if (hipEventElapsedTime(&t, h->lev_ev[(size_t)k - 1], h->lev_ev[(size_t)k]) != hipSuccess) rc = ERROR_MISC;
+            const int lv = h->lev_tag[(size_t)k];
+            if (lv >= 0 && lv < h->nl) acc[(size_t)lv] += t;
+        }
+    }
+    for (hipEvent_t e : h->lev_ev)
+        if (e) (void)hipEventDestroy(e);
+    h->lev_ev.clear();
+    h->lev_tag.clear();
+    h->lev_n = 0;
+    h->resid_c_ready = h->pending_f = false;
+    if (rc) return rc;
+    for (int l = 0; l < h->nl; ++l) level_ms[l] = acc[(size_t)l] / reps;
     return 0;
 }
 

@@ -199,6 +199,10 @@ int sss_hip_host_coarse_solve(SSS_MAT *A, SSS_VEC *b, SSS_VEC *x, double ctol, i
 /* Engine event timer around `reps` launches of the level-0 residual SpMV on the engine
  * stream: average kernel milliseconds (roofline measurement in bench.py). */
 int sss_hip_time_level0_spmv(sss_hip_hier *h, int reps, double *avg_ms);
+/* level_ms[l] (nslots >= levels): level l's share of an eager cycle -- pre-smoothing, residual,
+ * restriction, zero fill, prolongation, post-smoothing (the coarsest: its solve; a single-workgroup
+ * tail: at its first level) -- averaged over reps, events between the steps.  Advances the iterate. */
+int sss_hip_time_levels(sss_hip_hier *h, int reps, double *level_ms, int nslots);
 /* The same launch from level 0's plain CSR arrays (whatever storage the cycle uses for A_0). */
 int sss_hip_time_level0_spmv_csr(sss_hip_hier *h, int reps, double *avg_ms);
 /* Average milliseconds of `reps` full iterations (cycle + residual + norm) on the engine
@@ -230,6 +234,10 @@ int sss_hip_rccl_unique_id(unsigned char *id);
 /* device >= 0: hipSetDevice(device) first (the communicator binds the current device) */
 sss_hip_comm *sss_hip_comm_rccl(int nranks, int rank, const unsigned char *id, int device);
 sss_hip_comm *sss_hip_comm_host(int nranks, int rank, const sss_hip_host_transport *t);
+/* Timing only: every collective and halo transfer is skipped, the rest of the rank's cycle (its
+ * kernels, halo packs, graph capture) runs as over RCCL -- the per-rank compute floor of a multi-GPU
+ * run measured one rank at a time on one GPU (tools/n8_floor.py).  The iterates are meaningless. */
+sss_hip_comm *sss_hip_comm_timing(int nranks, int rank);
 void sss_hip_comm_destroy(sss_hip_comm *c);
 
 /* mg: the global hierarchy (every rank runs the same host setup).  V-cycles only.
@@ -257,6 +265,17 @@ int sss_hip_dist_residual_norm(sss_hip_dist *d, double *absres);
 int sss_hip_dist_sync(sss_hip_dist *d);
 /* average ms of `reps` local level-0 residual SpMVs (no exchange): the per-rank roofline */
 int sss_hip_dist_time_level0_spmv(sss_hip_dist *d, int reps, double *avg_ms);
+/* *cycle_ms: this rank's cycle as it runs (captured graph), averaged over reps; level_ms[l] (l < nagg)
+ * one partitioned level's descent + ascent and level_ms[nagg] the replicated tail, from reps eager
+ * cycles with events between the steps (nslots >= nagg + 1).  Advances the iterate. */
+int sss_hip_dist_time_levels(sss_hip_dist *d, int reps, double *cycle_ms, double *level_ms, int nslots);
+/* the replicated tail's per-level times (sss_hip_time_levels on it) */
+int sss_hip_dist_time_tail_levels(sss_hip_dist *d, int reps, double *level_ms, int nslots);
+/* Per partitioned level: halo exchanges enqueued since the last reset and the doubles this rank sent
+ * in them (a captured cycle counts at its capture); the tail all-gather's own / all rows and the
+ * number of replicated levels. */
+int sss_hip_dist_halo_stats(sss_hip_dist *d, long long *calls, long long *doubles, int nslots, int reset,
+                            int *nc_own, int *nc_all, int *tail_levels);
 
 /* Host-only view of the partition (no device needed; used by the CPU multi-process tests).
  * which: 0 = A_l (m x (m+g)), 1 = P_l (m x next-level local), 2 = R_l (own coarse rows x (m+g)).

@@ -199,3 +199,45 @@ def _run(world, transport, kind, n, smoother, inner_from, agg, sum_order=0, part
         errs.append(errq.get())
     assert not errs, "\n".join(errs)
     assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
+
+
+def test_timing_comm_floor_and_level_times():
+    """The floor instruments (tools/n8_floor.py): a rank built with the timing-only communicator
+    (no transfer, no peer process) runs its whole cycle alone -- graph captured -- and reports its
+    halo exchanges (rank 0 of 2 has a level-0 peer) and per-level times; the single-GPU engine's
+    per-level times cover every level and add up to about one eager cycle."""
+    import amg_amd as A
+    from conftest import build_hierarchy, quiet_ctx
+    H = build_hierarchy(A.generate(7, 32), quiet_ctx)
+    comm = A.Comm(2, 0, "timing", device=0)
+    D = A.DistHierarchy(H, comm, smoother="hybrid", coarse="direct", device=0, agg_rows=60)
+    try:
+        own = D.hi - D.lo
+        D.upload("b", np.ones(own))
+        D.upload("x", np.ones(own))
+        D.halo_stats(reset=True)
+        D.cycle()
+        D.residual_norm()
+        hs = D.halo_stats(reset=True)
+        assert hs["exchanges"][0] > 0 and hs["doubles_sent"][0] >= hs["exchanges"][0] * 32 * 32
+        assert hs["gather_all"] == H.level(D.nagg).A.num_rows and 0 < hs["gather_own"] < hs["gather_all"]
+        assert hs["tail_levels"] == H.num_levels - D.nagg
+        assert D.level_flags(0)["cycle_graph"]
+        cyc, lv = D.time_levels(3)
+        assert cyc > 0 and len(lv) == D.nagg + 1 and all(t > 0 for t in lv)
+        tl = D.time_tail_levels(2)[:hs["tail_levels"]]
+        assert tl[0] > 0 and all(t >= 0 for t in tl)   # (a single-workgroup tail counts at its first level)
+    finally:
+        D.close()
+        comm.close()
+    S = A.DeviceHierarchy(H, smoother="hybrid", coarse="direct")
+    try:
+        n = H.level(0).A.num_rows
+        S.upload(0, "b", np.ones(n))
+        S.upload(0, "x", np.ones(n))
+        lv = S.time_levels(3)
+        assert len(lv) == H.num_levels and lv[0] > 0 and all(t >= 0 for t in lv)
+        S.cycle()   # the graph-replayed cycle is unaffected by the timing walk
+        assert np.isfinite(S.residual_norm())
+    finally:
+        S.close()
