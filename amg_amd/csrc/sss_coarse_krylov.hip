@@ -28,6 +28,9 @@
 #include "sss_spmv_dev.hpp"
 
 #include <cmath>
+#include <cstdio>
+#include <algorithm>
+#include <queue>
 #include <cstring>
 #include <vector>
 
@@ -46,6 +49,13 @@ struct CgState {
 struct CoarseKrylov {
     int n = 0, cap = 0;
     double *p = nullptr, *r = nullptr, *t = nullptr, *u_best = nullptr;
+    // the one-launch CG (k_cg_persist): {tag, half} granules of p (2 n) and t (2 n), the command
+    // word and the stall word (pctl), the launch counter that makes every launch's tags fresh
+    unsigned long long *gp_p = nullptr, *gp_t = nullptr, *pctl = nullptr;
+    unsigned epoch = 0;
+    int persist_grid = -1;  // workgroups of the one-launch CG; -1: it does not fit (two kernels per iteration)
+    int *wl_ptr = nullptr, *wl_rows = nullptr;   // each worker wave's rows (cg_persist_plan)
+    double *tw = nullptr;                        // t_{k-1}, t_k by parity of k (the worker's own rows)
     CgState *st = nullptr;
     CgState *h_st = nullptr;   // pinned
     double *gp = nullptr, *gw = nullptr, *gx_best = nullptr, *hcol = nullptr, *rs_dev = nullptr, *scal = nullptr;
@@ -427,6 +437,481 @@ __global__ __launch_bounds__(kSeqBlock) void k_cg_restore(int n, double *__restr
 }
 
 // ---------------------------------------------------------------------------------------------
+// The whole CG loop in one launch (k_cg_persist; n <= kRegVec * kSeqBlock).  Workgroup 0 runs every
+// step as k_cg_step_reg does (same arithmetic, same sequential sums); workgroups 1 .. G-1 run the
+// SpMVs t_k = t_{k-1} + A p_k, one wave per row at a time, each row summed from 0.0 in stored order
+// and added to t_{k-1} as k_acc does.  A row's sum is one dependent chain of adds issued by one lane,
+// so what bounds the SpMV is the chain work each SIMD issues: the host deals the rows to the waves
+// longest first onto the least-loaded SIMD (cg_persist_plan; the coarsest level of 7-pt 400^3 has
+// rows of 2 to 2,907 entries, 767 on average), and each wave works through its list.  The two sides hand over through {tag, half} granules (8-byte agent-scope
+// atomics, the 8 XCD L2s are not coherent): p_k from workgroup 0 (all rows; two buffers by command
+// parity), t_k from the wave that owns the row.  A command (tag, k, exit) in a ring of four words
+// starts each SpMV: a word is rewritten only after every worker has answered the command two back.
+//   Speculation: with beta == 1, p_{k+1} = 1.0 r + 1.0 p_k is known as soon as alpha has updated r --
+// before the step's three norm chains decide whether a residual check (rare) rewrites it.  Workgroup
+// 0 publishes it right away, so SpMV k+1 overlaps the rest of step k; when the check fires, the fixed
+// p_{k+1} goes out under a new tag and the workers redo SpMV k+1 from t_k: t_k lives in tw[k & 1],
+// written and read only by the lane that owns the row.
+//   Progress: every workgroup is co-resident (the grid is capped by the occupancy API) and every wait
+// is bounded (spin polls; past the limit the stall word is set and every workgroup leaves).
+#define CGP_RLX __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT
+constexpr int kCgpWaves = kSeqBlock / 64;
+constexpr int kCgpSpin = 1 << 20;    // polls before a waiting wave gives up (~1 s with the back-off)
+constexpr int kCgpTraceIts = 256, kCgpTraceK = 10;
+constexpr int kCgpChainWaves = kCgpWaves;   // chaining waves per worker
+
+__device__ __forceinline__ void cgp_put(unsigned long long *g, unsigned tag, double v)
+{
+    const unsigned long long u = (unsigned long long)__double_as_longlong(v);
+    __hip_atomic_store(g, ((unsigned long long)tag << 32) | (u & 0xffffffffull), CGP_RLX);
+    __hip_atomic_store(g + 1, ((unsigned long long)tag << 32) | (u >> 32), CGP_RLX);
+}
+// the granule's value once both halves carry `tag` (bounded wait; 0.0 and the stall word set past it)
+__device__ __forceinline__ double cgp_wait(const unsigned long long *g, unsigned tag, unsigned long long *err)
+{
+    for (int s = 0;; ++s) {
+        const unsigned long long a = __hip_atomic_load(const_cast<unsigned long long *>(g), CGP_RLX);
+        const unsigned long long c = __hip_atomic_load(const_cast<unsigned long long *>(g + 1), CGP_RLX);
+        if ((unsigned)(a >> 32) == tag && (unsigned)(c >> 32) == tag)
+            return __longlong_as_double((long long)((c << 32) | (a & 0xffffffffull)));
+        if (s >= kCgpSpin || ((s & 63) == 63 && __hip_atomic_load(err, CGP_RLX))) {
+            __hip_atomic_store(err, 1ull, CGP_RLX);
+            return 0.0;
+        }
+        if (s < 32) __builtin_amdgcn_s_sleep(1);
+        else __builtin_amdgcn_s_sleep(4);
+    }
+}
+// s + p[0] + ... + p[m-1] in order (chain_pipe16's additions, 8 products read ahead instead of 16: the
+// step workgroup of k_cg_persist keeps its vectors in registers around its chains)
+__device__ __forceinline__ double chain_pipe8(double s, const double *p, int m)
+{
+    int k = 0;
+    if (m >= 16) {
+        double2 c[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) c[u] = *reinterpret_cast<const double2 *>(p + 2 * u);
+        for (k = 8; k + 8 <= m; k += 8) {
+            double2 nx[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) nx[u] = *reinterpret_cast<const double2 *>(p + k + 2 * u);
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                s += c[u].x;
+                s += c[u].y;
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u) c[u] = nx[u];
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            s += c[u].x;
+            s += c[u].y;
+        }
+    }
+    for (; k < m; ++k) s += p[k];
+    return s;
+}
+
+// Granules i0 + j * stride (j < N, those below n) of base, all loads in flight before any check;
+// out[j] = 0.0 past n
+template <int N>
+__device__ __forceinline__ void cgp_wait_n(const unsigned long long *base, int i0, int stride, int n, unsigned tag,
+                                           unsigned long long *err, double (&out)[N])
+{
+    bool done[N];
+#pragma unroll
+    for (int j = 0; j < N; ++j) done[j] = i0 + j * stride >= n, out[j] = 0.0;
+    for (int s = 0;; ++s) {
+        unsigned long long a[N], c[N];
+#pragma unroll
+        for (int j = 0; j < N; ++j) {
+            unsigned long long *g = const_cast<unsigned long long *>(base) + 2 * (size_t)(i0 + j * stride);
+            a[j] = done[j] ? 0ull : __hip_atomic_load(g, CGP_RLX);
+            c[j] = done[j] ? 0ull : __hip_atomic_load(g + 1, CGP_RLX);
+        }
+        bool all = true;
+#pragma unroll
+        for (int j = 0; j < N; ++j) {
+            if (done[j]) continue;
+            if ((unsigned)(a[j] >> 32) == tag && (unsigned)(c[j] >> 32) == tag) {
+                out[j] = __longlong_as_double((long long)((c[j] << 32) | (a[j] & 0xffffffffull)));
+                done[j] = true;
+            } else {
+                all = false;
+            }
+        }
+        if (all) return;
+        if (s >= kCgpSpin || ((s & 63) == 63 && __hip_atomic_load(err, CGP_RLX))) {
+            __hip_atomic_store(err, 1ull, CGP_RLX);
+            return;
+        }
+        if (s < 32) __builtin_amdgcn_s_sleep(1);
+        else __builtin_amdgcn_s_sleep(4);
+    }
+}
+__device__ __forceinline__ unsigned cgp_tag(unsigned epoch, int seq) { return (epoch << 12) | (unsigned)seq; }
+
+// k_cg_persist's rare residual check (k_resid gate 1 + k_cg_fix): r = b - A u on rows < cap, one
+// thread per row as k_cg_step_reg; u and p_k in global memory; ends with every thread past a barrier.
+__device__ __forceinline__ void cgp_check(int n, int k, const int *__restrict__ rp, const int *__restrict__ ci,
+                                       const double *__restrict__ v, const double *__restrict__ b, int cap,
+                                       const double *u, double *r, double *p, CgState *ss, SeqSmem &sm, int &s_pmode)
+{
+    for (int row = threadIdx.x; row < n; row += kSeqBlock) {
+        if (cap > 0 && row >= cap) {
+            r[row] = b[row];
+            continue;
+        }
+        const int e = rp[row + 1];
+        double acc = 0.0;
+        int kk = rp[row];
+        for (; kk + 4 <= e; kk += 4) {
+            int cc[4];
+            double a[4], xv[4];
+#pragma unroll
+            for (int h = 0; h < 4; ++h) cc[h] = ci[kk + h], a[h] = v[kk + h];
+#pragma unroll
+            for (int h = 0; h < 4; ++h) xv[h] = cc[h] >= 0 ? u[cc[h]] : 0.0;
+#pragma unroll
+            for (int h = 0; h < 4; ++h) acc += cc[h] >= 0 ? a[h] * xv[h] : 0.0;
+        }
+        for (; kk < e; ++kk) acc += ci[kk] >= 0 ? v[kk] * u[ci[kk]] : 0.0;
+        r[row] = b[row] + acc * -1.0;
+    }
+    __syncthreads();
+    cg_fix_body(n, k, r, p, ss, sm, s_pmode);
+    __syncthreads();
+}
+
+// 0.0 + a_k p_{c_k} over the row's entries [k0, k1) in stored order, by one wave (valid in lane 0):
+// wave_row_chain's additions, with the next strip's column / value loads in flight while lane 0 chains
+// the current one (two strips per wave) -- on the coarsest level of 7-pt 400^3 a row of 2,907 entries
+// is the SpMV's critical path.  x from LDS (the workers' copy of p).
+__device__ __forceinline__ double cgp_row_chain(int k0, int k1, const int *__restrict__ ci, const double *__restrict__ v,
+                                                const double *x, double *strip0, double *strip1,
+                                                unsigned long long *tacc = nullptr)
+{
+    constexpr int U = kWaveStage / 64;
+    const int lane = threadIdx.x & 63;
+    double acc = 0.0;
+    if (k1 <= k0) return acc;
+    int c[U];
+    double a[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {   // strip 0 (clamped: a lane past the row loads its last entry, value 0.0)
+        const int q = lane + 64 * u, kc = min(k0 + q, k1 - 1);
+        c[u] = ci[kc];
+        a[u] = k0 + q < k1 ? v[kc] : 0.0;
+    }
+    int cur = 0;
+    unsigned long long tw_load = 0, tw_chain = 0;
+    for (int base = k0; base < k1; base += kWaveStage) {
+        const int m = min(kWaveStage, k1 - base);
+        double *buf = cur ? strip1 : strip0;
+        const unsigned long long ta = tacc ? wall_clock64() : 0;
+        {   // branch-free: past the row a = 0.0 and the column is clamped (those slots are never summed)
+            double xv[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) xv[u] = x[c[u]];
+#pragma unroll
+            for (int u = 0; u < U; ++u) buf[lane + 64 * u] = a[u] * xv[u];
+        }
+        wave_sync();
+        const unsigned long long tb = tacc ? wall_clock64() : 0;
+        const int nb = base + kWaveStage;
+        if (nb < k1) {   // the next strip's loads, in flight during the chain below
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int q = lane + 64 * u, kc = min(nb + q, k1 - 1);
+                c[u] = ci[kc];
+                a[u] = nb + q < k1 ? v[kc] : 0.0;
+            }
+        }
+        if (lane == 0) acc = chain_fixed<false, 16>(acc, buf, m);
+        if (tacc) {
+            __builtin_amdgcn_s_waitcnt(0xc07f);   // lgkmcnt(0)
+            const unsigned long long tc = wall_clock64();
+            tw_load += tb - ta, tw_chain += tc - tb;
+        }
+        cur ^= 1;
+    }
+    if (tacc && lane == 0) tacc[0] = tw_load, tacc[1] = tw_chain;
+    return acc;
+}
+
+__global__ __launch_bounds__(kSeqBlock) void k_cg_persist(int n, int maxit, const int *__restrict__ rp,
+                                                          const int *__restrict__ ci, const double *__restrict__ v,
+                                                          const double *__restrict__ b, int cap, double *u, double *r,
+                                                          double *p, double *__restrict__ u_best, CgState *st,
+                                                          unsigned long long *gpp, unsigned long long *gpt,
+                                                          unsigned long long *ctl, unsigned epoch,
+                                                          const int *__restrict__ wl_ptr, const int *__restrict__ wl_rows,
+                                                          double *tw, unsigned long long *trc)
+{
+    // diagnostics (SSS_HIP_CG_TRACE): 100 MHz timestamps, plain stores -- workgroup 0's phases of
+    // iterations k < kCgpTraceIts (trc[16 k + j]), and for SpMV kCgpTraceK each worker's command / p
+    // (trc_w[4 b + j]) and each row's start, end, strip-load and chain time (trc_r[4 row + j])
+    unsigned long long *trc_w = trc ? trc + 16 * kCgpTraceIts : nullptr, *trc_r = trc ? trc_w + 4 * gridDim.x : nullptr;
+    auto ts0 = [&](int k, int j) {
+        if (trc && k < kCgpTraceIts) trc[16 * k + j] = wall_clock64();
+    };
+    __shared__ __attribute__((aligned(16))) double lds[3 * kSeqChunk + 32];   // (+ chain_fixed's over-read)
+    __shared__ double s_absw[kCgpWaves];
+    __shared__ int s_flags[3];
+    __shared__ int s_pmode;
+    __shared__ unsigned long long s_cmd;
+    __shared__ CgState ss;
+    // command ring: slot (seq & 3), one 128-byte line each; then the stall word
+    auto cmd_of = [&](int sq) { return ctl + 16 * (sq & 3); };
+    unsigned long long *err = ctl + 64;
+    const size_t pbuf = 2 * (size_t)n;   // p granules of commands of parity 1 at gpp + pbuf
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    if (blockIdx.x > 0) {   // ---- a worker: SpMVs of the rows the plan gives each wave
+        // p in LDS (n <= kSeqChunk), then two strips of kWaveStage per wave
+        double *pl = lds, *strip0 = lds + kSeqChunk + wave * 2 * kWaveStage, *strip1 = strip0 + kWaveStage;
+        const int gw = (int)(blockIdx.x - 1) * kCgpWaves + wave, q0 = wl_ptr[gw], q1 = wl_ptr[gw + 1];
+        for (int seq = 1;; ++seq) {
+            const unsigned tag = cgp_tag(epoch, seq);
+            if (tid == 0) {   // the next command: tag in the high word, k << 1 | exit in the low
+                unsigned long long c = 0;
+                for (int s = 0;; ++s) {
+                    c = __hip_atomic_load(cmd_of(seq), CGP_RLX);
+                    if ((unsigned)(c >> 32) == tag) break;
+                    if (s >= kCgpSpin || ((s & 63) == 63 && __hip_atomic_load(err, CGP_RLX))) {
+                        __hip_atomic_store(err, 1ull, CGP_RLX);
+                        c = ((unsigned long long)tag << 32) | 1ull;
+                        break;
+                    }
+                    if (s < 32) __builtin_amdgcn_s_sleep(1);
+                    else __builtin_amdgcn_s_sleep(4);
+                }
+                s_cmd = c;
+            }
+            __syncthreads();
+            const unsigned long long c = s_cmd;
+            if ((c & 1ull) || __hip_atomic_load(err, CGP_RLX)) break;
+            const int k = (int)((c & 0xffffffffull) >> 1);
+            const bool tr = trc && k == kCgpTraceK;
+            if (tr && tid == 0) trc_w[4 * blockIdx.x] = wall_clock64();
+            {
+                double pw[kRegVec];
+                cgp_wait_n<kRegVec>(gpp + (seq & 1) * pbuf, tid, kSeqBlock, n, tag, err, pw);
+#pragma unroll
+                for (int q = 0; q < kRegVec; ++q)
+                    if (tid + q * kSeqBlock < n) pl[tid + q * kSeqBlock] = pw[q];
+            }
+            __syncthreads();
+            if (tr && tid == 0) trc_w[4 * blockIdx.x + 1] = wall_clock64();
+            for (int q = q0; q < q1; ++q) {
+                const int row = wl_rows[q];
+                const bool capped = cap > 0 && row >= cap;   // t stays t_0 = 0 (k_acc's row cap)
+                const unsigned long long t_row = wall_clock64();
+                const double s = capped ? 0.0
+                                        : cgp_row_chain(rp[row], rp[row + 1], ci, v, pl, strip0, strip1,
+                                                        tr ? trc_r + 4 * row + 2 : nullptr);
+                if (lane == 0) {
+                    const double tprev = k > 1 ? tw[(size_t)((k - 1) & 1) * n + row] : 0.0;
+                    const double tcur = capped ? tprev : tprev + s;
+                    tw[(size_t)(k & 1) * n + row] = tcur;
+                    cgp_put(gpt + 2 * (size_t)row, tag, tcur);
+                    if (tr) {
+                        trc_r[4 * row] = t_row;
+                        trc_r[4 * row + 1] = wall_clock64();
+                        // HW_ID: wave [3:0], SIMD [5:4], CU [11:8], SE [15:13]
+                        trc_r[4 * n + row] = (unsigned)__builtin_amdgcn_s_getreg(4 | (15 << 11)) | ((unsigned long long)gw << 32);
+                    }
+                }
+            }
+        }
+        return;
+    }
+    // ---- workgroup 0: the CG steps (k_cg_step_reg + k_resid gate 1 + k_cg_fix), p and t via granules.
+    // Step k's three norm chains (waves 0-2) run while waves 4-15 collect t_{k+1} of the speculative
+    // SpMV chunk by chunk in index order, each chunk as t_{k+1} p_{k+1} into LDS with a ready flag, and
+    // wave 3 chains the chunks as they turn ready: the chain runs behind the SpMV's rows instead of
+    // after the last of them, and the next step's (t, p) starts ready.
+    SeqSmem &sm = *reinterpret_cast<SeqSmem *>(lds);
+    constexpr int kTpChunk = 128, kTpChunks = kSeqChunk / kTpChunk, kTpPollers = kCgpWaves - 4;
+    __shared__ __attribute__((aligned(16))) double tp[kSeqChunk + 16];   // p_{k+1}, then t_{k+1} * p_{k+1}
+    __shared__ int s_rdy[kTpChunks];   // chunk c of round r summed-ready when s_rdy[c] == r
+    __shared__ double s_temp2;
+    const int ntp = (n + kTpChunk - 1) / kTpChunk;
+    if (tid == 0) ss = *st;
+    if (tid < kTpChunks) s_rdy[tid] = 0;
+    __syncthreads();
+    // u and r stay in global memory (each thread reads and writes its own entries: L2 hits), p_{k+1}
+    // and t_k in registers -- the step's chains then run without spilling the vectors
+    double tv[kRegVec], pv[kRegVec];
+#pragma unroll
+    for (int j = 0; j < kRegVec; ++j) {
+        const int i = tid + j * kSeqBlock;
+        pv[j] = i < n ? p[i] : 0.0;
+    }
+    int seq = 1;
+    auto publish = [&](int sq, int k, const double (&pp)[kRegVec], bool exit, int ti) {
+        const unsigned tag = cgp_tag(epoch, sq);
+        if (!exit)
+#pragma unroll
+            for (int j = 0; j < kRegVec; ++j) {
+                const int i = ti + j * kSeqBlock;
+                if (i < n) cgp_put(gpp + (sq & 1) * pbuf + 2 * (size_t)i, tag, pp[j]);
+            }
+        if (tid == 0)
+            __hip_atomic_store(cmd_of(sq), ((unsigned long long)tag << 32) | ((unsigned long long)k << 1) | (exit ? 1ull : 0ull),
+                               CGP_RLX);
+    };
+    if (ss.mode != CG_RUN) {
+        publish(seq, 0, pv, true, tid);
+        return;
+    }
+    publish(seq, 1, pv, false, tid);   // SpMV 1 from p_1 (k_cg_init)
+    bool spec_out = false;        // a command past `seq` is out (the speculative SpMV k + 1)
+    bool have_temp2 = false;      // (t_k, p_k) already summed (behind the previous step's norms)
+    double temp2 = 0.0;
+    int rounds = 0;               // speculative rounds completed (chunk flags of the next one: rounds + 1)
+    for (int k = 1;; ++k) {
+        // the thread's index, opaque to the compiler inside the loop: the addresses of its entries
+        // (u, r, p, u_best, the granules: 7 arrays x 4 entries x 64 bits) are recomputed in the
+        // iteration instead of held -- and spilled -- across it
+        int tid_k = tid;
+        asm volatile("" : "+v"(tid_k));
+        spec_out = false;   // the command at `seq` is this iteration's SpMV; none past it yet
+        if (tid == 0) ts0(k, 0);
+        cgp_wait_n<kRegVec>(gpt, tid_k, kSeqBlock, n, cgp_tag(epoch, seq), err, tv);
+        if (tid == 0) ts0(k, 1);
+        if (__hip_atomic_load(err, CGP_RLX)) break;
+        if (!have_temp2) {   // -- (t_k, p_k) as k_cg_step_reg sums it
+#pragma unroll
+            for (int j = 0; j < kRegVec; ++j) {
+                const int i = tid_k + j * kSeqBlock;
+                if (i < n) sm.reg[0][i] = tv[j] * pv[j];
+            }
+            __syncthreads();
+            if (tid == 0) s_temp2 = chain_fixed<false, 8>(0.0, sm.reg[0], n);
+            __syncthreads();
+            temp2 = s_temp2;
+        }
+        have_temp2 = false;
+        if (!(fabs(temp2) > SMALLFLOAT2)) {   // possible breakdown: goto RESTORE_BESTSOL
+            if (tid == 0) {
+                ss.mode = CG_STOP;
+                ss.iter = k;
+            }
+            break;
+        }
+        const double alpha = ss.temp1 / temp2;
+        double m = 0.0;
+#pragma unroll
+        for (int j = 0; j < kRegVec; ++j) {
+            const int i = tid_k + j * kSeqBlock;
+            if (i < n) {
+                const double un = u[i] + alpha * pv[j];
+                const double rn = r[i] + -alpha * tv[j];
+                u[i] = un;
+                r[i] = rn;
+                m = fmax(m, fabs(un));
+                sm.reg[0][i] = rn * rn;
+                sm.reg[1][i] = un * un;
+                sm.reg[2][i] = pv[j] * pv[j];
+                p[i] = pv[j];                    // p_k, for a residual check that rewrites p_{k+1}
+                pv[j] = 1.0 * rn + 1.0 * pv[j];  // p_{k+1} if none does
+                tp[i] = pv[j];
+            } else {
+                pv[j] = 0.0;
+            }
+        }
+        if (tid == 0) ts0(k, 2);
+        spec_out = k < ss.maxit;   // (at maxit the step always stops)
+        if (spec_out) publish(seq + 1, k + 1, pv, false, tid_k);
+        if (tid == 0) ts0(k, 3);
+        for (int off = 32; off > 0; off >>= 1) m = fmax(m, __shfl_xor(m, off, 64));
+        if (lane == 0) s_absw[wave] = m;
+        __syncthreads();
+        if (tid < 192) {   // the norms of step k
+            if (lane == 0) sm.bcast[wave] = chain_fixed<false, 8>(0.0, sm.reg[wave], n);
+        } else if (tid < 256) {   // wave 3: the absmax, then t_{k+1} p_{k+1} chunk by chunk as they turn ready
+            if (lane == 0) {
+                double a = 0.0;
+                for (int w = 0; w < kCgpWaves; ++w) a = fmax(a, s_absw[w]);
+                sm.bcast[3] = a;
+                if (spec_out) {
+                    if (trc) ts0(k, 5);
+                    double s = 0.0;
+                    for (int c = 0; c < ntp; ++c) {
+                        for (int sp = 0; __hip_atomic_load(&s_rdy[c], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) <= rounds;
+                             ++sp) {
+                            if (sp >= kCgpSpin) {
+                                __hip_atomic_store(err, 1ull, CGP_RLX);
+                                break;
+                            }
+                            __builtin_amdgcn_s_sleep(1);
+                        }
+                        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+                        if (c == 0 && trc) ts0(k, 6);
+                        s = chain_fixed<false, 8>(s, tp + c * kTpChunk, min(kTpChunk, n - c * kTpChunk));
+                    }
+                    s_temp2 = s;
+                    if (trc) ts0(k, 7);
+                }
+            }
+        } else if (spec_out) {   // waves 4-15: chunks wave - 4, + 12, ... of t_{k+1} (in the chain's order)
+            for (int c = wave - 4; c < ntp; c += kTpPollers) {
+                double tt[kTpChunk / 64];
+                cgp_wait_n<kTpChunk / 64>(gpt, c * kTpChunk + lane, 64, n, cgp_tag(epoch, seq + 1), err, tt);
+#pragma unroll
+                for (int q = 0; q < kTpChunk / 64; ++q) {
+                    const int i = c * kTpChunk + lane + 64 * q;
+                    if (i < n) tp[i] = tt[q] * tp[i];
+                }
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+                if (lane == 0) __hip_atomic_store(&s_rdy[c], rounds + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            }
+        }
+        __syncthreads();
+        if (spec_out) ++rounds;
+        if (tid == 0) {
+            const double sq[3] = {sm.bcast[0], sm.bcast[1], sm.bcast[2]};
+            cg_step_state(&ss, k, alpha, sq, sm.bcast[3], s_flags);
+        }
+        __syncthreads();
+        const int copy_best = s_flags[0], finish_here = s_flags[1], check = s_flags[2];
+        if (tid == 0) ts0(k, 12);
+#pragma unroll
+        for (int j = 0; j < kRegVec; ++j) {
+            const int i = tid_k + j * kSeqBlock;
+            if (i < n && copy_best) u_best[i] = u[i];
+        }
+        if (finish_here) {
+            if (ss.mode != CG_RUN) break;   // maxit reached (no command went out)
+            temp2 = s_temp2;                // (t_{k+1}, p_{k+1}): p_{k+1} = pv, already out
+            have_temp2 = true;
+            seq += 1;
+            continue;
+        }
+        if (!check) break;   // stopped by the step (a speculative command may be out)
+        // -- k_resid gate 1 + k_cg_fix: r = b - A u (rows < cap), checks II / III, p rewritten from
+        // p_k (in p since the update)
+        __syncthreads();
+        cgp_check(n, k, rp, ci, v, b, cap, u, r, p, &ss, sm, s_pmode);
+        if (ss.mode != CG_RUN || !s_pmode) break;
+#pragma unroll
+        for (int j = 0; j < kRegVec; ++j) {
+            const int i = tid_k + j * kSeqBlock;
+            pv[j] = i < n ? p[i] : 0.0;
+        }
+        // the fixed p_{k+1} under a fresh tag: the workers redo SpMV k + 1 from t_k
+        seq += spec_out ? 2 : 1;
+        publish(seq, k + 1, pv, false, tid_k);
+        spec_out = false;
+    }
+    // every worker leaves at the next command
+    publish(seq + (spec_out ? 2 : 1), 0, pv, true, tid);
+    __syncthreads();
+    if (tid == 0) *st = ss;
+}
+
+// ---------------------------------------------------------------------------------------------
 // GMRES kernels (single workgroup unless noted)
 __global__ __launch_bounds__(kSeqBlock) void k_seq_norm(int n, const double *__restrict__ x, double *out)
 {
@@ -499,6 +984,8 @@ __global__ __launch_bounds__(kBlock) void k_gm_recombine(int n, int i, double *_
 }
 
 // ---------------------------------------------------------------------------------------------
+static void cg_persist_plan(CoarseKrylov *k, const DevCSR &A);
+
 CoarseKrylov *coarse_krylov_create(const DevCSR &A, int row_cap, hipStream_t)
 {
     auto *k = new CoarseKrylov();
@@ -516,10 +1003,17 @@ CoarseKrylov *coarse_krylov_create(const DevCSR &A, int row_cap, hipStream_t)
     k->hcol = dev_alloc<double>(max_RESTART + 2);
     k->rs_dev = dev_alloc<double>(max_RESTART + 2);
     k->scal = dev_alloc<double>(2);
+    k->gp_p = dev_alloc<unsigned long long>(4 * (size_t)n);   // two buffers of {tag, half} pairs
+    k->gp_t = dev_alloc<unsigned long long>(2 * (size_t)n);
+    k->pctl = dev_alloc<unsigned long long>(80);
     bool ok = k->p && k->r && k->t && k->u_best && k->st && k->gp && k->gw && k->gx_best && k->hcol && k->rs_dev &&
-              k->scal;
+              k->scal && k->gp_p && k->gp_t && k->pctl;
+    ok = ok && hipMemset(k->gp_p, 0, sizeof(unsigned long long) * 4 * (size_t)n) == hipSuccess &&
+         hipMemset(k->gp_t, 0, sizeof(unsigned long long) * 2 * (size_t)n) == hipSuccess &&
+         hipMemset(k->pctl, 0, sizeof(unsigned long long) * 80) == hipSuccess;
     ok = ok && hipHostMalloc((void **)&k->h_st, sizeof(CgState)) == hipSuccess;
     ok = ok && hipHostMalloc((void **)&k->h_buf, sizeof(double) * 64) == hipSuccess;
+    if (ok) cg_persist_plan(k, A);
     if (!ok) {
         coarse_krylov_destroy(k);
         return nullptr;
@@ -531,7 +1025,9 @@ void coarse_krylov_destroy(CoarseKrylov *k)
 {
     if (!k) return;
     for (void *p : {(void *)k->p, (void *)k->r, (void *)k->t, (void *)k->u_best, (void *)k->st, (void *)k->gp,
-                    (void *)k->gw, (void *)k->gx_best, (void *)k->hcol, (void *)k->rs_dev, (void *)k->scal})
+                    (void *)k->gw, (void *)k->gx_best, (void *)k->hcol, (void *)k->rs_dev, (void *)k->scal,
+                    (void *)k->gp_p, (void *)k->gp_t, (void *)k->pctl, (void *)k->wl_ptr, (void *)k->wl_rows,
+                    (void *)k->tw})
         dev_free(p);
     if (k->h_st) (void)hipHostFree(k->h_st);
     if (k->h_buf) (void)hipHostFree(k->h_buf);
@@ -551,18 +1047,167 @@ static int host_resid_norm(CoarseKrylov *k, const DevCSR &A, const double *u, co
     return 0;
 }
 
+// The one-launch CG's plan: one step workgroup and W workers (every workgroup co-resident: the
+// occupancy API bounds W), and each worker wave's rows.  A row's SpMV is a chain of dependent adds
+// issued by one lane: rows go longest first onto the least-loaded wave (entries + a per-row
+// overhead), each list in ascending row order (the rows of low index are the first the step
+// workgroup's t.p chain needs).  Measured at 400^3 (SSS_HIP_CG_TRACE): four chaining waves per
+// SIMD finish the SpMV sooner than one wave per SIMD working through the same rows in turn (one
+// wave's chain leaves the SIMD idle between its dependent adds), though each row then takes longer.
+// Sets persist_grid = W + 1, or -1 when the one-launch form does not fit.
+static void cg_persist_plan(CoarseKrylov *k, const DevCSR &A)
+{
+    k->persist_grid = -1;
+    const int n = A.n;
+    int dev = 0, per_cu = 0;
+    hipDeviceProp_t prop;
+    if (n < 1 || n > kRegVec * kSeqBlock || hipGetDevice(&dev) != hipSuccess ||
+        hipGetDeviceProperties(&prop, dev) != hipSuccess ||
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_cg_persist, kSeqBlock, 0) != hipSuccess)
+        return;
+    const int resident = per_cu * prop.multiProcessorCount;   // every workgroup must be co-resident
+    if (resident < 2) return;
+    const int workers = std::min(resident - 1, std::max(1, (n + 3) / 4)), nwaves = workers * kCgpWaves;
+    std::vector<int> rp(n + 1);
+    if (hipMemcpy(rp.data(), A.rp, sizeof(int) * (n + 1), hipMemcpyDeviceToHost) != hipSuccess) return;
+    constexpr long long kRowCost = 64;   // per-row overhead in entries (command, strip set-up, publish)
+    auto cost = [&](int r) { return (long long)(rp[r + 1] - rp[r]) + kRowCost; };
+    std::vector<int> order(n);
+    for (int i = 0; i < n; ++i) order[i] = i;
+    std::stable_sort(order.begin(), order.end(), [&](int a, int b) { return cost(a) > cost(b); });
+    using Bin = std::pair<long long, int>;   // (load, chaining wave: worker * 4 + wave)
+    std::priority_queue<Bin, std::vector<Bin>, std::greater<Bin>> bins;
+    for (int b = 0; b < workers * kCgpChainWaves; ++b) bins.push({0, b});
+    std::vector<std::vector<int>> lists(nwaves);
+    for (int r : order) {
+        Bin b = bins.top();
+        bins.pop();
+        lists[(b.second / kCgpChainWaves) * kCgpWaves + b.second % kCgpChainWaves].push_back(r);
+        b.first += cost(r);
+        bins.push(b);
+    }
+    std::vector<int> ptr(nwaves + 1, 0), rows;
+    rows.reserve(n);
+    for (int w = 0; w < nwaves; ++w) {
+        std::sort(lists[w].begin(), lists[w].end());
+        rows.insert(rows.end(), lists[w].begin(), lists[w].end());
+        ptr[w + 1] = (int)rows.size();
+    }
+    k->wl_ptr = dev_alloc<int>(nwaves + 1);
+    k->wl_rows = dev_alloc<int>(n);
+    k->tw = dev_alloc<double>(2 * (size_t)n);
+    if (!k->wl_ptr || !k->wl_rows || !k->tw ||
+        hipMemcpy(k->wl_ptr, ptr.data(), sizeof(int) * (nwaves + 1), hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemcpy(k->wl_rows, rows.data(), sizeof(int) * n, hipMemcpyHostToDevice) != hipSuccess)
+        return;
+    k->persist_grid = workers + 1;
+}
+
+// SSS_HIP_CG_TRACE: mean phase times (us) of k_cg_persist's iterations 2 .. kCgpTraceIts-1, and the
+// workers' SpMV kCgpTraceK, to stderr (diagnostics)
+static size_t cg_trace_words(int n, int grid) { return 16 * (size_t)kCgpTraceIts + 4 * (size_t)grid + 5 * (size_t)n; }
+static void cg_trace_report(unsigned long long *trc, int n, int grid, const int *rp, hipStream_t s)
+{
+    std::vector<unsigned long long> h(cg_trace_words(n, grid));
+    std::vector<int> hrp(n + 1);
+    const bool ok = hipMemcpyAsync(hrp.data(), rp, sizeof(int) * (n + 1), hipMemcpyDeviceToHost, s) == hipSuccess &&
+                    hipMemcpyAsync(h.data(), trc, sizeof(unsigned long long) * h.size(), hipMemcpyDeviceToHost, s) ==
+                        hipSuccess &&
+                    hipStreamSynchronize(s) == hipSuccess;
+    (void)hipFree(trc);
+    if (!ok) return;
+    // relative to iteration k's start (slot 0): t wait done 1, update 2, published 3, norms 4, wave-3 polls 5,
+    // all polls 6, t.p chain 7, step 12
+    const char *nm[13] = {"period", "t_in", "update", "publish", "norm0", "poll_w3", "poll_all", "tp_chain",
+                          "", "", "", "", "step"};
+    double acc[13] = {0};
+    int cnt = 0;
+    for (int k = 2; k + 1 < kCgpTraceIts; ++k) {
+        const unsigned long long *a = &h[16 * k], *nx = &h[16 * (k + 1)];
+        if (!a[0] || !nx[0] || !a[12]) continue;
+        for (int j : {1, 2, 3, 4, 5, 6, 7, 12}) acc[j] += a[j] ? (double)(a[j] - a[0]) * 0.01 : 0.0;
+        acc[0] += (double)(nx[0] - a[0]) * 0.01;
+        ++cnt;
+    }
+    std::fprintf(stderr, "[cg trace] %d iterations, us from the iteration's start:", cnt);
+    for (int j = 0; j < 13; ++j)
+        if (nm[j][0]) std::fprintf(stderr, " %s %.2f", nm[j], cnt ? acc[j] / cnt : 0.0);
+    std::fprintf(stderr, "\n");
+    // SpMV kCgpTraceK, from its (speculative) publish in iteration kCgpTraceK - 1
+    const long long P = (long long)h[16 * (kCgpTraceK - 1) + 3];
+    const unsigned long long *w = &h[16 * kCgpTraceIts], *r = w + 4 * grid;
+    auto rel = [&](unsigned long long t) { return ((long long)t - P) * 0.01; };
+    double cmd_lo = 1e30, cmd_hi = -1e30, p_lo = 1e30, p_hi = -1e30;
+    for (int b = 1; b < grid; ++b)
+        if (w[4 * b])
+            cmd_lo = std::min(cmd_lo, rel(w[4 * b])), cmd_hi = std::max(cmd_hi, rel(w[4 * b])),
+            p_lo = std::min(p_lo, rel(w[4 * b + 1])), p_hi = std::max(p_hi, rel(w[4 * b + 1]));
+    std::vector<int> idx;
+    double sdur = 0, slen = 0;
+    for (int i = 0; i < n; ++i)
+        if (r[4 * i + 1]) idx.push_back(i), sdur += (r[4 * i + 1] - r[4 * i]) * 10.0, slen += hrp[i + 1] - hrp[i];
+    std::sort(idx.begin(), idx.end(), [&](int a, int b) { return r[4 * a + 1] > r[4 * b + 1]; });
+    std::fprintf(stderr, "[cg trace] SpMV %d from its publish: command %.2f..%.2f, p in LDS %.2f..%.2f; rows %zu, "
+                 "%.2f ns per entry; latest rows (row:len start dur [strip loads, chains]):",
+                 kCgpTraceK, cmd_lo, cmd_hi, p_lo, p_hi, idx.size(), slen > 0 ? sdur / slen : 0.0);
+    for (size_t q = 0; q < 12 && q < idx.size(); ++q) {
+        const int i = idx[q];
+        std::fprintf(stderr, " %d:%d %.2f %.2f [%.2f %.2f]", i, hrp[i + 1] - hrp[i], rel(r[4 * i]),
+                     (r[4 * i + 1] - r[4 * i]) * 0.01, r[4 * i + 2] * 0.01, r[4 * i + 3] * 0.01);
+    }
+    std::fprintf(stderr, "\n");
+    // where the rows ran: per (block, SIMD) the entries chained, against the plan's wave % 4
+    std::vector<long long> simd(4 * grid, 0), plan(4 * grid, 0);
+    int mism = 0;
+    for (int i = 0; i < n; ++i) {
+        const unsigned long long x = r[4 * n + i];
+        const int gwv = (int)(x >> 32), hw = (int)(x & 0xffff), sm = (hw >> 4) & 3, b = gwv / kCgpWaves;
+        simd[4 * b + sm] += hrp[i + 1] - hrp[i];
+        plan[4 * b + (gwv % kCgpWaves) % 4] += hrp[i + 1] - hrp[i];
+        mism += sm != (gwv % kCgpWaves) % 4;
+    }
+    std::fprintf(stderr, "[cg trace] rows whose SIMD != wave %% 4: %d; max entries per SIMD: measured %lld, plan %lld; "
+                 "row 0..7 waves/SIMDs:", mism, *std::max_element(simd.begin(), simd.end()),
+                 *std::max_element(plan.begin(), plan.end()));
+    for (int i = 0; i < 8 && i < n; ++i)
+        std::fprintf(stderr, " %d/%d", (int)(r[4 * n + i] >> 32) % kCgpWaves, (int)((r[4 * n + i] >> 4) & 3));
+    std::fprintf(stderr, "\n");
+}
+
 static int run_cg(CoarseKrylov *k, const DevCSR &A, const double *b, double *u, double tol, int maxit, hipStream_t s,
                   int *status)
 {
     const int n = k->n, nblk = A.nblk;
     const char *cr = getenv("SSS_HIP_CG_REG");   // "0": the LDS-chunked step at every size (test hook)
     const bool reg_step = !(cr && cr[0] == '0') && n <= kRegVec * kSeqBlock;
+    // the whole loop in one launch (k_cg_persist); SSS_HIP_CG_PERSIST=0: two kernels per iteration (test hook)
+    const char *cp = getenv("SSS_HIP_CG_PERSIST");
+    const bool persist = reg_step && k->persist_grid > 0 && !(cp && cp[0] == '0');
+    unsigned long long *trc = nullptr;   // SSS_HIP_CG_TRACE=1: phase timestamps of the first launch (diagnostics)
+    static bool traced = false;
+    const char *ct = getenv("SSS_HIP_CG_TRACE");
+    if (persist && ct && ct[0] == '1' && !traced) {
+        traced = true;
+        const size_t words = cg_trace_words(n, k->persist_grid);
+        if (hipMalloc(&trc, sizeof(unsigned long long) * words) != hipSuccess) trc = nullptr;
+        else SSS_HIP(hipMemsetAsync(trc, 0, sizeof(unsigned long long) * words, s));
+    }
     SSS_HIP(hipMemsetAsync(k->t, 0, sizeof(double) * n, s));
     SSS_HIP(hipMemsetAsync(k->u_best, 0, sizeof(double) * n, s));
     hipLaunchKernelGGL(k_resid, dim3(nblk), dim3(kBlock), 0, s, A.blk, A.rp, A.ci, A.v, u, b, k->r, k->cap,
                        (const CgState *)nullptr, 0);
     hipLaunchKernelGGL(k_cg_init, dim3(1), dim3(kSeqBlock), 0, s, n, k->r, k->p, tol, maxit, k->st);
-    for (int it = 1; it <= maxit; ++it) {
+    if (persist) {
+        k->epoch = (k->epoch + 1) & 0xfffffu;   // 20 bits of launch count above 12 bits of command count
+        if (k->epoch == 0) k->epoch = 1;        // (tag 0 is the zeroed granules')
+        SSS_HIP(hipMemsetAsync(k->pctl + 64, 0, sizeof(unsigned long long), s));
+        hipLaunchKernelGGL(k_cg_persist, dim3(k->persist_grid), dim3(kSeqBlock), 0, s, n, maxit, A.rp, A.ci, A.v, b,
+                           k->cap, u, k->r, k->p, k->u_best, k->st, k->gp_p, k->gp_t, k->pctl, k->epoch, k->wl_ptr, k->wl_rows, k->tw, trc);
+        SSS_HIP(hipGetLastError());
+        if (trc) cg_trace_report(trc, n, k->persist_grid, A.rp, s);
+        SSS_HIP(hipMemcpyAsync(k->h_buf + 8, k->pctl + 64, sizeof(unsigned long long), hipMemcpyDeviceToHost, s));
+    }
+    for (int it = 1; it <= maxit && !persist; ++it) {
         hipLaunchKernelGGL(k_acc, dim3(nblk), dim3(kBlock), 0, s, A.blk, A.rp, A.ci, A.v, k->p, k->t, k->cap,
                            (const CgState *)k->st);
         if (reg_step) {
@@ -587,6 +1232,11 @@ static int run_cg(CoarseKrylov *k, const DevCSR &A, const double *b, double *u, 
     SSS_HIP(hipGetLastError());
     SSS_HIP(hipMemcpyAsync(k->h_st, k->st, sizeof(CgState), hipMemcpyDeviceToHost, s));
     SSS_HIP(hipStreamSynchronize(s));
+    if (persist && reinterpret_cast<const unsigned long long *>(k->h_buf)[8] != 0) {
+        fprintf(stderr, "### ERROR: coarse CG: a workgroup of the one-launch CG stalled (spin limit reached); "
+                        "the coarse iterate is invalid\n");
+        return ERROR_MISC;
+    }
     *status = k->h_st->status;
     return 0;
 }

@@ -130,11 +130,13 @@ __device__ __forceinline__ int flow_ticket_at(unsigned *w)
     return __builtin_amdgcn_readfirstlane((int)t);
 }
 
-// s - p[a] - p[a+1] - ... - p[e-1] in order (chain_pipe16: the next 16 products read as 16-byte
-// pairs while the current 16 are subtracted; the chain is one dependent fp64 subtraction per entry)
+// s - p[a] - p[a+1] - ... - p[e-1] in order (chain_fixed: 16-byte pair reads a group of 16 ahead,
+// each group's 16 dependent fp64 subtractions in one asm block; reads up to 16 products past e,
+// inside the workgroup's LDS row buffers or past the allocation's end, values unused)
 __device__ __forceinline__ double chain_sub_pipe(double s, const double *p, int a, int e)
 {
-    return chain_pipe16<true>(s, p, a, e);
+    if ((a & 1) && a < e) s -= p[a++];   // 16-byte alignment of the pair reads
+    return a < e ? chain_fixed<true, 16>(s, p + a, e - a) : s;
 }
 
 constexpr int kGroupBuf = 2048;   // staged products per wave (16 KiB; 64 KiB per workgroup)

@@ -395,6 +395,69 @@ __device__ __forceinline__ double chain_pipe16(double s, const double *p, int a,
     return s;
 }
 
+// The same in-order chain with the schedule fixed: groups of G products read as 16-byte pairs into
+// two register sets in turn, each group's G dependent adds in one asm block, so the compiler neither
+// interleaves copies into the chain nor sinks the next group's reads below it (inside a loop that
+// also keeps global loads in flight it did both: tools/row_chain_lab.hip on MI355X, one wave, a
+// 2,907-entry row in 256-entry strips: 21.3 cycles per entry with chain_pipe16, 13.8 with this at
+// G = 16; bare chain over LDS 10.7 against 8.9).  s + p[0] + ... + p[m-1] (SUB: s - ...), same bits.
+// p 16-byte aligned in LDS; reads up to G entries past m (values unused), which must stay inside
+// the LDS allocation.
+#define SSS_ADD2(i, j) "v_add_f64 %0, %0, %" #i "\n\tv_add_f64 %0, %0, %" #j "\n\t"
+#define SSS_SUB2(i, j) "v_add_f64 %0, %0, -%" #i "\n\tv_add_f64 %0, %0, -%" #j "\n\t"
+#define SSS_OPS8(c) "v"(c[0].x), "v"(c[0].y), "v"(c[1].x), "v"(c[1].y), "v"(c[2].x), "v"(c[2].y), "v"(c[3].x), "v"(c[3].y)
+#define SSS_OPS16(c)                                                                                            \
+    SSS_OPS8(c), "v"(c[4].x), "v"(c[4].y), "v"(c[5].x), "v"(c[5].y), "v"(c[6].x), "v"(c[6].y), "v"(c[7].x), \
+        "v"(c[7].y)
+template <bool SUB, int G>
+__device__ __forceinline__ double chain_group(double s, const double2 (&c)[G / 2])
+{
+    static_assert(G == 8 || G == 16, "group of 8 or 16");
+    if constexpr (G == 8 && !SUB)
+        asm volatile(SSS_ADD2(1, 2) SSS_ADD2(3, 4) SSS_ADD2(5, 6) SSS_ADD2(7, 8) : "+v"(s) : SSS_OPS8(c));
+    else if constexpr (G == 8)
+        asm volatile(SSS_SUB2(1, 2) SSS_SUB2(3, 4) SSS_SUB2(5, 6) SSS_SUB2(7, 8) : "+v"(s) : SSS_OPS8(c));
+    else if constexpr (!SUB)
+        asm volatile(SSS_ADD2(1, 2) SSS_ADD2(3, 4) SSS_ADD2(5, 6) SSS_ADD2(7, 8) SSS_ADD2(9, 10) SSS_ADD2(11, 12)
+                         SSS_ADD2(13, 14) SSS_ADD2(15, 16)
+                     : "+v"(s)
+                     : SSS_OPS16(c));
+    else
+        asm volatile(SSS_SUB2(1, 2) SSS_SUB2(3, 4) SSS_SUB2(5, 6) SSS_SUB2(7, 8) SSS_SUB2(9, 10) SSS_SUB2(11, 12)
+                         SSS_SUB2(13, 14) SSS_SUB2(15, 16)
+                     : "+v"(s)
+                     : SSS_OPS16(c));
+    return s;
+}
+template <bool SUB, int G>
+__device__ __forceinline__ double chain_fixed(double s, const double *p, int m)
+{
+    int k = 0;
+    if (m >= 2 * G) {
+        double2 a[G / 2], b[G / 2];
+#pragma unroll
+        for (int u = 0; u < G / 2; ++u) a[u] = *reinterpret_cast<const double2 *>(p + 2 * u);
+        for (; k + 2 * G <= m; k += 2 * G) {
+#pragma unroll
+            for (int u = 0; u < G / 2; ++u) b[u] = *reinterpret_cast<const double2 *>(p + k + G + 2 * u);
+            s = chain_group<SUB, G>(s, a);
+#pragma unroll
+            for (int u = 0; u < G / 2; ++u) a[u] = *reinterpret_cast<const double2 *>(p + k + 2 * G + 2 * u);
+            s = chain_group<SUB, G>(s, b);
+        }
+        if (k + G <= m) {
+            s = chain_group<SUB, G>(s, a);
+            k += G;
+        }
+    }
+    for (; k < m; ++k) s = SUB ? s - p[k] : s + p[k];
+    return s;
+}
+#undef SSS_ADD2
+#undef SSS_SUB2
+#undef SSS_OPS8
+#undef SSS_OPS16
+
 // Fixed-order block reduction (xor butterfly inside the wave, then waves in order).
 // Result valid in thread 0.  Must be reached by every thread of the block.
 __device__ __forceinline__ double block_sum(double v, double *red)

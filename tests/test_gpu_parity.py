@@ -260,11 +260,18 @@ def test_cf_jacobi_bitwise(request, hname, row_path):
 
 
 # ---------------------------------------------------------------- coarse solve
-@pytest.mark.parametrize("step", ["reg", "lds"])
+def _cg_form(mp, step):
+    """persist: the whole CG loop in one launch (k_cg_persist, the default for n <= 4096); reg: the
+    register step and the SpMV as two kernels per iteration; lds: the LDS-chunked step."""
+    mp.setenv("SSS_HIP_CG_REG", "0" if step == "lds" else "1")
+    mp.setenv("SSS_HIP_CG_PERSIST", "1" if step == "persist" else "0")
+
+
+@pytest.mark.parametrize("step", ["persist", "reg", "lds"])
 @pytest.mark.parametrize("hname", ["bus_h", "p32_h", "a27_h"])
 def test_coarse_krylov_matches_oracle(request, hname, step, monkeypatch):
-    """Both CG step kernels (register-resident, n <= 4096; LDS-chunked, SSS_HIP_CG_REG=0)."""
-    monkeypatch.setenv("SSS_HIP_CG_REG", "1" if step == "reg" else "0")
+    """Every CG form (one launch; register-resident step, n <= 4096; LDS-chunked, SSS_HIP_CG_REG=0)."""
+    _cg_form(monkeypatch, step)
     H = request.getfixturevalue(hname)
     Lc = H.level(H.num_levels - 1)
     n = Lc.A.num_rows
@@ -277,12 +284,12 @@ def test_coarse_krylov_matches_oracle(request, hname, step, monkeypatch):
     assert np.array_equal(xg.view(np.uint64), xr.view(np.uint64))
 
 
-@pytest.mark.parametrize("step", ["reg", "lds"])
+@pytest.mark.parametrize("step", ["persist", "reg", "lds"])
 @pytest.mark.parametrize("lo,hi", [(1025, 4096), (4097, 40000)])
 def test_coarse_krylov_larger_grids(p32_h, lo, hi, step, monkeypatch):
     """A finer level as the 'coarsest' matrix: several entries per thread in the register step
     (1025..4096 rows), the LDS-chunked step past 4096 rows and its multi-chunk sequential sums."""
-    monkeypatch.setenv("SSS_HIP_CG_REG", "1" if step == "reg" else "0")
+    _cg_form(monkeypatch, step)
     L = next(p32_h.level(l) for l in range(p32_h.num_levels) if lo <= p32_h.level(l).A.num_rows <= hi)
     n = L.A.num_rows
     b = np.random.default_rng(4).standard_normal(n)
@@ -293,10 +300,13 @@ def test_coarse_krylov_larger_grids(p32_h, lo, hi, step, monkeypatch):
     assert np.array_equal(xg.view(np.uint64), xr.view(np.uint64))
 
 
-@pytest.mark.parametrize("n", [1, 2, 1024, 4095, 4096, 4097])
-def test_coarse_krylov_step_sizes(n):
-    """The register CG step at its size edges (one entry per thread up to four; 4097 rows take the
-    LDS-chunked step): a shifted 1-D Laplacian with a random right-hand side."""
+@pytest.mark.parametrize("step", ["persist", "reg"])
+@pytest.mark.parametrize("n", [1, 2, 17, 1024, 4095, 4096, 4097])
+def test_coarse_krylov_step_sizes(n, step, monkeypatch):
+    """The register CG step and the one-launch CG at their size edges (one entry per thread up to
+    four; one row per worker wave; 4097 rows take the LDS-chunked step): a shifted 1-D Laplacian with
+    a random right-hand side."""
+    _cg_form(monkeypatch, step)
     import scipy.sparse as sp
     M = sp.diags([-np.ones(n - 1), np.full(n, 2.05), -np.ones(n - 1)], [-1, 0, 1], format="csr") \
         if n > 1 else sp.csr_matrix(np.array([[2.05]]))
@@ -310,7 +320,8 @@ def test_coarse_krylov_step_sizes(n):
     assert np.array_equal(xg.view(np.uint64), xr.view(np.uint64))
 
 
-def test_coarse_krylov_long_rows():
+@pytest.mark.parametrize("step", ["persist", "reg"])
+def test_coarse_krylov_long_rows(step, monkeypatch):
     """Rows longer than one tile (2,048 entries) -- the double-buffered block-row chain -- in the
     coarse CG / GMRES SpMVs: a 2,600-row matrix whose first 24 rows and columns are dense."""
     import scipy.sparse as sp
@@ -323,6 +334,7 @@ def test_coarse_krylov_long_rows():
     M = (M + sp.diags(np.asarray(abs(M).sum(axis=1)).ravel() + 1.0)).tocsr()
     M.sort_indices()
     assert np.diff(M.indptr).max() > 2048
+    _cg_form(monkeypatch, step)
     hold = A.NumpyCSR(M.indptr, M.indices, M.data)
     b = rng.standard_normal(n)
     xg, xr = np.zeros(n), np.zeros(n)
@@ -332,9 +344,11 @@ def test_coarse_krylov_long_rows():
     assert np.array_equal(xg.view(np.uint64), xr.view(np.uint64))
 
 
+@pytest.mark.parametrize("step", ["persist", "reg"])
 @pytest.mark.parametrize("cap", [0, 40])
-def test_coarse_krylov_row_cap(bus_h, cap):
+def test_coarse_krylov_row_cap(bus_h, cap, step, monkeypatch):
     """The as-shipped <<<64,64>>> row cap (rows >= cap untouched by the coarse SpMVs)."""
+    _cg_form(monkeypatch, step)
     Lc = bus_h.level(bus_h.num_levels - 1)
     n = Lc.A.num_rows
     b = np.linspace(-1.0, 2.0, n)

@@ -67,6 +67,158 @@ __device__ double chain16(double s, const double *p, int a, int e)
     for (; k < e; ++k) s -= p[k];
     return s;
 }
+// 16 ahead, two register sets in turn (no copies between them)
+__device__ double chain_pp(double s, const double *p, int a, int e)
+{
+    int k = a;
+    if ((k & 1) && k < e) s -= p[k++];
+    if (e - k >= 32) {
+        double2 c[8], d[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) c[u] = *reinterpret_cast<const double2 *>(p + k + 2 * u);
+        for (; k + 32 <= e; k += 32) {
+#pragma unroll
+            for (int u = 0; u < 8; ++u) d[u] = *reinterpret_cast<const double2 *>(p + k + 16 + 2 * u);
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                s -= c[u].x;
+                s -= c[u].y;
+            }
+            if (k + 48 <= e) {
+#pragma unroll
+                for (int u = 0; u < 8; ++u) c[u] = *reinterpret_cast<const double2 *>(p + k + 32 + 2 * u);
+            }
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                s -= d[u].x;
+                s -= d[u].y;
+            }
+        }
+        if (k + 16 <= e) {
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                s -= c[u].x;
+                s -= c[u].y;
+            }
+            k += 16;
+        }
+    }
+    for (; k < e; ++k) s -= p[k];
+    return s;
+}
+// chain16 with the schedule pinned: the 8 pair reads, then the 16 subtractions, then the copies
+__device__ double chain16_sb(double s, const double *p, int a, int e)
+{
+    int k = a;
+    if ((k & 1) && k < e) s -= p[k++];
+    if (e - k >= 32) {
+        double2 c[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) c[u] = *reinterpret_cast<const double2 *>(p + k + 2 * u);
+        for (k += 16; k + 16 <= e; k += 16) {
+            double2 n[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) n[u] = *reinterpret_cast<const double2 *>(p + k + 2 * u);
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                s -= c[u].x;
+                s -= c[u].y;
+            }
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int u = 0; u < 8; ++u) c[u] = n[u];
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            s -= c[u].x;
+            s -= c[u].y;
+        }
+    }
+    for (; k < e; ++k) s -= p[k];
+    return s;
+}
+// two register sets in turn, schedule pinned (no copies)
+__device__ double chain_pp_sb(double s, const double *p, int a, int e)
+{
+    int k = a;
+    if ((k & 1) && k < e) s -= p[k++];
+    if (e - k >= 32) {
+        double2 c[8], d[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) c[u] = *reinterpret_cast<const double2 *>(p + k + 2 * u);
+        for (; k + 32 <= e; k += 32) {
+#pragma unroll
+            for (int u = 0; u < 8; ++u) d[u] = *reinterpret_cast<const double2 *>(p + k + 16 + 2 * u);
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                s -= c[u].x;
+                s -= c[u].y;
+            }
+            __builtin_amdgcn_sched_barrier(0);
+            // (reads past e stay inside the caller's LDS array: values unused)
+#pragma unroll
+            for (int u = 0; u < 8; ++u) c[u] = *reinterpret_cast<const double2 *>(p + k + 32 + 2 * u);
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                s -= d[u].x;
+                s -= d[u].y;
+            }
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        if (k + 16 <= e) {
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                s -= c[u].x;
+                s -= c[u].y;
+            }
+            k += 16;
+        }
+    }
+    for (; k < e; ++k) s -= p[k];
+    return s;
+}
+// 16 in-order subtractions in one asm block: the compiler waits for all 16 operands first, and
+// cannot move the next group's reads below them
+__device__ __forceinline__ double sub16(double s, const double2 (&c)[8])
+{
+    asm volatile(
+        "v_add_f64 %0, %0, -%1\n\tv_add_f64 %0, %0, -%2\n\tv_add_f64 %0, %0, -%3\n\tv_add_f64 %0, %0, -%4\n\t"
+        "v_add_f64 %0, %0, -%5\n\tv_add_f64 %0, %0, -%6\n\tv_add_f64 %0, %0, -%7\n\tv_add_f64 %0, %0, -%8\n\t"
+        "v_add_f64 %0, %0, -%9\n\tv_add_f64 %0, %0, -%10\n\tv_add_f64 %0, %0, -%11\n\tv_add_f64 %0, %0, -%12\n\t"
+        "v_add_f64 %0, %0, -%13\n\tv_add_f64 %0, %0, -%14\n\tv_add_f64 %0, %0, -%15\n\tv_add_f64 %0, %0, -%16"
+        : "+v"(s)
+        : "v"(c[0].x), "v"(c[0].y), "v"(c[1].x), "v"(c[1].y), "v"(c[2].x), "v"(c[2].y), "v"(c[3].x), "v"(c[3].y),
+          "v"(c[4].x), "v"(c[4].y), "v"(c[5].x), "v"(c[5].y), "v"(c[6].x), "v"(c[6].y), "v"(c[7].x), "v"(c[7].y));
+    return s;
+}
+__device__ double chain_asm(double s, const double *p, int a, int e)
+{
+    int k = a;
+    if ((k & 1) && k < e) s -= p[k++];
+    if (e - k >= 32) {
+        double2 A[8], B[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) A[u] = *reinterpret_cast<const double2 *>(p + k + 2 * u);
+        for (; k + 32 <= e; k += 32) {
+#pragma unroll
+            for (int u = 0; u < 8; ++u) B[u] = *reinterpret_cast<const double2 *>(p + k + 16 + 2 * u);
+            s = sub16(s, A);
+            // (the last pass reads up to 16 entries past e: LDS, values unused)
+#pragma unroll
+            for (int u = 0; u < 8; ++u) A[u] = *reinterpret_cast<const double2 *>(p + k + 32 + 2 * u);
+            s = sub16(s, B);
+        }
+        if (k + 16 <= e) {
+            s = sub16(s, A);
+            k += 16;
+        }
+    }
+    for (; k < e; ++k) s -= p[k];
+    return s;
+}
 // the chain from registers only (the floor: dependent subtractions alone)
 __device__ double chain_reg(double s, const double *p, int a, int e)
 {
@@ -79,23 +231,31 @@ __device__ double chain_reg(double s, const double *p, int a, int e)
     return s;
 }
 
+// every wave of the block chains its own copy (lane 0): waves sharing a SIMD share its issue
 template <int V>
-__global__ __launch_bounds__(64) void kchain(const double *src, double *out, long long *cyc, int m)
+__global__ __launch_bounds__(1024) void kchain(const double *src, double *out, long long *cyc, int m)
 {
-    __shared__ double p[M];
-    for (int t = threadIdx.x; t < M; t += 64) p[t] = src[t];
+    __shared__ __attribute__((aligned(16))) double p[M * 4 + 64];
+    const int w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    for (int t = threadIdx.x; t < M * 4; t += blockDim.x) p[t] = src[t % M];
     __syncthreads();
+    double *q = p + (w % 4) * M;
     double s = 1.0;
     long long t0 = 0, t1 = 0;
-    if (threadIdx.x == 0) {
+    if ((threadIdx.x & 63) == 0) {
         t0 = __builtin_amdgcn_s_memtime();
-        if (V == 0) s = chain8(s, p, 0, m);
-        else if (V == 1) s = chain16(s, p, 0, m);
-        else s = chain_reg(s, p, 0, m);
-        out[0] = s;
+        if (V == 0) s = chain8(s, q, 0, m);
+        else if (V == 1) s = chain16(s, q, 0, m);
+        else if (V == 3) s = chain_pp(s, q, 0, m);
+        else if (V == 4) s = chain16_sb(s, q, 0, m);
+        else if (V == 5) s = chain_pp_sb(s, q, 0, m);
+        else if (V == 6) s = chain_asm(s, q, 0, m);
+        else s = chain_reg(s, q, 0, m);
+        out[w] = s;
         t1 = __builtin_amdgcn_s_memtime();
-        cyc[0] = t1 - t0;
+        cyc[w] = t1 - t0;
     }
+    (void)nw;
 }
 
 int main()
@@ -105,27 +265,38 @@ int main()
     double *src, *out;
     long long *cyc;
     CK(hipMalloc(&src, sizeof h));
-    CK(hipMalloc(&out, 8));
-    CK(hipMalloc(&cyc, 8));
+    CK(hipMalloc(&out, 8 * 16));
+    CK(hipMalloc(&cyc, 8 * 16));
     CK(hipMemcpy(src, h, sizeof h, hipMemcpyHostToDevice));
-    const char *names[3] = {"8 ahead (engine)", "16 ahead, 16-B reads", "registers (floor)"};
+    const char *names[7] = {"8 ahead (engine)", "16 ahead, 16-B reads", "registers (floor)", "16 ahead, two sets",
+                            "16 ahead, pinned", "two sets, pinned", "two sets, asm adds"};
     double ref = 0;
-    for (int v = 0; v < 3; ++v) {
-        long long best = 1LL << 60;
-        double s = 0;
-        for (int rep = 0; rep < 5; ++rep) {
-            if (v == 0) hipLaunchKernelGGL(kchain<0>, dim3(1), dim3(64), 0, 0, src, out, cyc, M);
-            if (v == 1) hipLaunchKernelGGL(kchain<1>, dim3(1), dim3(64), 0, 0, src, out, cyc, M);
-            if (v == 2) hipLaunchKernelGGL(kchain<2>, dim3(1), dim3(64), 0, 0, src, out, cyc, M);
-            CK(hipDeviceSynchronize());
-            long long c;
-            CK(hipMemcpy(&c, cyc, 8, hipMemcpyDeviceToHost));
-            CK(hipMemcpy(&s, out, 8, hipMemcpyDeviceToHost));
-            if (c < best) best = c;
+    for (int waves : {1, 4, 16})
+        for (int v : {0, 1, 6, 2}) {
+            long long best = 1LL << 60;
+            double s[16];
+            for (int rep = 0; rep < 5; ++rep) {
+                const dim3 g(1), b(64 * waves);
+                if (v == 0) hipLaunchKernelGGL(kchain<0>, g, b, 0, 0, src, out, cyc, M);
+                if (v == 1) hipLaunchKernelGGL(kchain<1>, g, b, 0, 0, src, out, cyc, M);
+                if (v == 2) hipLaunchKernelGGL(kchain<2>, g, b, 0, 0, src, out, cyc, M);
+                if (v == 3) hipLaunchKernelGGL(kchain<3>, g, b, 0, 0, src, out, cyc, M);
+                if (v == 4) hipLaunchKernelGGL(kchain<4>, g, b, 0, 0, src, out, cyc, M);
+                if (v == 5) hipLaunchKernelGGL(kchain<5>, g, b, 0, 0, src, out, cyc, M);
+                if (v == 6) hipLaunchKernelGGL(kchain<6>, g, b, 0, 0, src, out, cyc, M);
+                CK(hipDeviceSynchronize());
+                long long c[16];
+                CK(hipMemcpy(c, cyc, 8 * waves, hipMemcpyDeviceToHost));
+                CK(hipMemcpy(s, out, 8 * waves, hipMemcpyDeviceToHost));
+                long long mx = 0;
+                for (int w = 0; w < waves; ++w) mx = c[w] > mx ? c[w] : mx;
+                if (mx < best) best = mx;
+            }
+            if (v == 0 && waves == 1) ref = s[0];
+            bool same = true;
+            for (int w = 0; w < waves; ++w) same = same && !memcmp(&s[w], &ref, 8);
+            printf("%2d waves  %-24s %8lld s_memtime ticks for %d entries (%.2f per entry)%s\n", waves, names[v], best, M,
+                   (double)best / M, v != 2 ? (same ? "  bitwise ok" : "  MISMATCH") : "");
         }
-        if (v == 0) ref = s;
-        printf("%-24s %8lld s_memtime ticks for %d entries (%.2f per entry)%s\n", names[v], best, M, (double)best / M,
-               v < 2 ? (memcmp(&s, &ref, 8) ? "  MISMATCH" : "  bitwise ok") : "");
-    }
     return 0;
 }
