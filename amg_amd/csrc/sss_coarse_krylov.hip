@@ -458,7 +458,7 @@ __global__ __launch_bounds__(kSeqBlock) void k_cg_restore(int n, double *__restr
 constexpr int kCgpWaves = kSeqBlock / 64;
 constexpr int kCgpSpin = 1 << 20;    // polls before a waiting wave gives up (~1 s with the back-off)
 constexpr int kCgpTraceIts = 256, kCgpTraceK = 10;
-constexpr int kCgpChainWaves = kCgpWaves;   // chaining waves per worker
+constexpr int kCgpSimds = 4;         // SIMDs per CU: a worker's 16 waves, four on each
 
 __device__ __forceinline__ void cgp_put(unsigned long long *g, unsigned tag, double v)
 {
@@ -658,6 +658,7 @@ __global__ __launch_bounds__(kSeqBlock) void k_cg_persist(int n, int maxit, cons
     };
     __shared__ __attribute__((aligned(16))) double lds[3 * kSeqChunk + 32];   // (+ chain_fixed's over-read)
     __shared__ double s_absw[kCgpWaves];
+    __shared__ int s_simd[kCgpWaves];
     __shared__ int s_flags[3];
     __shared__ int s_pmode;
     __shared__ unsigned long long s_cmd;
@@ -670,7 +671,21 @@ __global__ __launch_bounds__(kSeqBlock) void k_cg_persist(int n, int maxit, cons
     if (blockIdx.x > 0) {   // ---- a worker: SpMVs of the rows the plan gives each wave
         // p in LDS (n <= kSeqChunk), then two strips of kWaveStage per wave
         double *pl = lds, *strip0 = lds + kSeqChunk + wave * 2 * kWaveStage, *strip1 = strip0 + kWaveStage;
-        const int gw = (int)(blockIdx.x - 1) * kCgpWaves + wave, q0 = wl_ptr[gw], q1 = wl_ptr[gw + 1];
+        // this wave's plan slot: 4 s + (its rank among the waves on SIMD s), by HW_ID [5:4]; the
+        // wave index itself should the 16 waves not sit four to a SIMD
+        if (lane == 0) s_simd[wave] = (__builtin_amdgcn_s_getreg(4 | (15 << 11)) >> 4) & 3;
+        __syncthreads();
+        int rank = 0, cnt[kCgpSimds] = {0, 0, 0, 0};
+        const int mine = s_simd[wave];
+        for (int w = 0; w < kCgpWaves; ++w) {
+            const int sw = s_simd[w];
+            rank += (w < wave && sw == mine);
+            cnt[0] += sw == 0, cnt[1] += sw == 1, cnt[2] += sw == 2, cnt[3] += sw == 3;
+        }
+        constexpr int per = kCgpWaves / kCgpSimds;
+        const bool four = cnt[0] == per && cnt[1] == per && cnt[2] == per && cnt[3] == per;
+        const int gw = (int)(blockIdx.x - 1) * kCgpWaves + (four ? mine * per + rank : wave);
+        const int q0 = wl_ptr[gw], q1 = wl_ptr[gw + 1];
         for (int seq = 1;; ++seq) {
             const unsigned tag = cgp_tag(epoch, seq);
             if (tid == 0) {   // the next command: tag in the high word, k << 1 | exit in the low
@@ -1048,13 +1063,15 @@ static int host_resid_norm(CoarseKrylov *k, const DevCSR &A, const double *u, co
 }
 
 // The one-launch CG's plan: one step workgroup and W workers (every workgroup co-resident: the
-// occupancy API bounds W), and each worker wave's rows.  A row's SpMV is a chain of dependent adds
-// issued by one lane: rows go longest first onto the least-loaded wave (entries + a per-row
-// overhead), each list in ascending row order (the rows of low index are the first the step
-// workgroup's t.p chain needs).  Measured at 400^3 (SSS_HIP_CG_TRACE): four chaining waves per
-// SIMD finish the SpMV sooner than one wave per SIMD working through the same rows in turn (one
-// wave's chain leaves the SIMD idle between its dependent adds), though each row then takes longer.
-// Sets persist_grid = W + 1, or -1 when the one-launch form does not fit.
+// occupancy API bounds W), and the rows of each worker's wave slots, slot 4 s + j being the j-th
+// wave on SIMD s (k_cg_persist reads each wave's SIMD from HW_ID).  A row's SpMV is a chain of
+// dependent adds issued by one lane, and the waves on one SIMD share its issue slots, so rows go
+// longest first onto the SIMD with the least work (entries + a per-row overhead) and within it onto
+// its least-loaded slot; each list runs in ascending row order (the rows of low index are the first
+// the step workgroup's t.p chain needs).  Measured at 400^3 (SSS_HIP_CG_TRACE): four chaining waves
+// per SIMD finish the SpMV sooner than one wave per SIMD working through the same rows in turn, and
+// balancing per SIMD beats balancing per wave (42.6 against 55.0 us per iteration).  Sets
+// persist_grid = W + 1, or -1 when the one-launch form does not fit.
 static void cg_persist_plan(CoarseKrylov *k, const DevCSR &A)
 {
     k->persist_grid = -1;
@@ -1075,16 +1092,23 @@ static void cg_persist_plan(CoarseKrylov *k, const DevCSR &A)
     std::vector<int> order(n);
     for (int i = 0; i < n; ++i) order[i] = i;
     std::stable_sort(order.begin(), order.end(), [&](int a, int b) { return cost(a) > cost(b); });
-    using Bin = std::pair<long long, int>;   // (load, chaining wave: worker * 4 + wave)
-    std::priority_queue<Bin, std::vector<Bin>, std::greater<Bin>> bins;
-    for (int b = 0; b < workers * kCgpChainWaves; ++b) bins.push({0, b});
+    using Bin = std::pair<long long, int>;   // (load, worker * 4 + SIMD)
+    std::priority_queue<Bin, std::vector<Bin>, std::greater<Bin>> simds;
+    for (int b = 0; b < workers * kCgpSimds; ++b) simds.push({0, b});
+    constexpr int per = kCgpWaves / kCgpSimds;
+    std::vector<long long> sload(nwaves, 0);
     std::vector<std::vector<int>> lists(nwaves);
     for (int r : order) {
-        Bin b = bins.top();
-        bins.pop();
-        lists[(b.second / kCgpChainWaves) * kCgpWaves + b.second % kCgpChainWaves].push_back(r);
+        Bin b = simds.top();
+        simds.pop();
+        const int s0 = (b.second / kCgpSimds) * kCgpWaves + (b.second % kCgpSimds) * per;   // the SIMD's slots
+        int best = s0;
+        for (int q = s0 + 1; q < s0 + per; ++q)
+            if (sload[q] < sload[best]) best = q;
+        sload[best] += cost(r);
+        lists[best].push_back(r);
         b.first += cost(r);
-        bins.push(b);
+        simds.push(b);
     }
     std::vector<int> ptr(nwaves + 1, 0), rows;
     rows.reserve(n);
@@ -1163,10 +1187,10 @@ static void cg_trace_report(unsigned long long *trc, int n, int grid, const int 
         const unsigned long long x = r[4 * n + i];
         const int gwv = (int)(x >> 32), hw = (int)(x & 0xffff), sm = (hw >> 4) & 3, b = gwv / kCgpWaves;
         simd[4 * b + sm] += hrp[i + 1] - hrp[i];
-        plan[4 * b + (gwv % kCgpWaves) % 4] += hrp[i + 1] - hrp[i];
-        mism += sm != (gwv % kCgpWaves) % 4;
+        plan[4 * b + (gwv % kCgpWaves) / 4] += hrp[i + 1] - hrp[i];
+        mism += sm != (gwv % kCgpWaves) / 4;
     }
-    std::fprintf(stderr, "[cg trace] rows whose SIMD != wave %% 4: %d; max entries per SIMD: measured %lld, plan %lld; "
+    std::fprintf(stderr, "[cg trace] rows whose SIMD != plan slot / 4: %d; max entries per SIMD: measured %lld, plan %lld; "
                  "row 0..7 waves/SIMDs:", mism, *std::max_element(simd.begin(), simd.end()),
                  *std::max_element(plan.begin(), plan.end()));
     for (int i = 0; i < 8 && i < n; ++i)

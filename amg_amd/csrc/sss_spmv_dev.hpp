@@ -348,53 +348,6 @@ __device__ __forceinline__ double chain_sub(double s, const double *p, int a, in
     return s;
 }
 
-// One lane's in-order chain over a long run of LDS products (the exact GS-CF engines, the parity
-// wave-per-row kernels): s -/+= p[a], p[a+1], ... in order, with the next 16 products read as eight
-// 16-byte pairs while the current 16 are added -- tools/chain_lab.hip on MI355X: 10.0 cycles per
-// entry against 13.4 for eight 8-byte reads ahead, the dependent fp64 subtraction alone 8.5.  p must
-// be 16-byte aligned.
-constexpr int kPipeRowMin = 64;   // csr_block_rows: rows from this length chain with chain_pipe16
-template <bool SUB>
-__device__ __forceinline__ double chain_pipe16(double s, const double *p, int a, int e)
-{
-    int k = a;
-    if ((k & 1) && k < e) s = SUB ? s - p[k++] : s + p[k++];
-    if (e - k >= 32) {
-        double2 c[8];
-#pragma unroll
-        for (int u = 0; u < 8; ++u) c[u] = *reinterpret_cast<const double2 *>(p + k + 2 * u);
-        for (k += 16; k + 16 <= e; k += 16) {
-            double2 nx[8];
-#pragma unroll
-            for (int u = 0; u < 8; ++u) nx[u] = *reinterpret_cast<const double2 *>(p + k + 2 * u);
-#pragma unroll
-            for (int u = 0; u < 8; ++u) {
-                if (SUB) {
-                    s -= c[u].x;
-                    s -= c[u].y;
-                } else {
-                    s += c[u].x;
-                    s += c[u].y;
-                }
-            }
-#pragma unroll
-            for (int u = 0; u < 8; ++u) c[u] = nx[u];
-        }
-#pragma unroll
-        for (int u = 0; u < 8; ++u) {
-            if (SUB) {
-                s -= c[u].x;
-                s -= c[u].y;
-            } else {
-                s += c[u].x;
-                s += c[u].y;
-            }
-        }
-    }
-    for (; k < e; ++k) s = SUB ? s - p[k] : s + p[k];
-    return s;
-}
-
 // The same in-order chain with the schedule fixed: groups of G products read as 16-byte pairs into
 // two register sets in turn, each group's G dependent adds in one asm block, so the compiler neither
 // interleaves copies into the chain nor sinks the next group's reads below it (inside a loop that
@@ -457,6 +410,18 @@ __device__ __forceinline__ double chain_fixed(double s, const double *p, int m)
 #undef SSS_SUB2
 #undef SSS_OPS8
 #undef SSS_OPS16
+
+// One lane's in-order chain over a long run of LDS products (the exact GS-CF engines, the parity
+// wave-per-row kernels, the stored-order block rows): s -/+= p[a], p[a+1], ... in order -- chain_fixed
+// after one entry that aligns the pair reads (p 16-byte aligned).  Reads up to 16 products past e
+// (values unused): every caller's buffer continues in LDS or ends the allocation.
+constexpr int kPipeRowMin = 64;   // csr_block_rows: rows from this length chain with chain_pipe16
+template <bool SUB>
+__device__ __forceinline__ double chain_pipe16(double s, const double *p, int a, int e)
+{
+    if ((a & 1) && a < e) s = SUB ? s - p[a++] : s + p[a++];
+    return a < e ? chain_fixed<SUB, 16>(s, p + a, e - a) : s;
+}
 
 // Fixed-order block reduction (xor butterfly inside the wave, then waves in order).
 // Result valid in thread 0.  Must be reached by every thread of the block.
