@@ -348,12 +348,13 @@ __device__ __forceinline__ double chain_sub(double s, const double *p, int a, in
     return s;
 }
 
-// The same in-order chain with the schedule fixed: groups of G products read as 16-byte pairs into
-// two register sets in turn, each group's G dependent adds in one asm block, so the compiler neither
-// interleaves copies into the chain nor sinks the next group's reads below it (inside a loop that
-// also keeps global loads in flight it did both: tools/row_chain_lab.hip on MI355X, one wave, a
-// 2,907-entry row in 256-entry strips: 21.3 cycles per entry with chain_pipe16, 13.8 with this at
-// G = 16; bare chain over LDS 10.7 against 8.9).  s + p[0] + ... + p[m-1] (SUB: s - ...), same bits.
+// The in-order chain with its schedule fixed: groups of G products read as 16-byte pairs into two
+// register sets in turn, each group's G dependent adds in one asm block, so the compiler neither
+// copies between the sets nor sinks the next group's reads below the current adds.  Written in plain
+// C++ (16 reads ahead, then the adds, then a copy of the sets) inside a loop that also keeps global
+// loads in flight, it did both: tools/row_chain_lab.hip on MI355X, one wave, a 2,907-entry row in
+// 256-entry strips, 21.3 cycles per entry that way, 13.8 with this at G = 16; the bare chain over
+// LDS 10.7 against 8.9, the dependent v_add_f64 floor 8.1 (tools/chain_lab.hip).  s + p[0] + ... + p[m-1] (SUB: s - ...), same bits.
 // p 16-byte aligned in LDS; reads up to G entries past m (values unused), which must stay inside
 // the LDS allocation.
 #define SSS_ADD2(i, j) "v_add_f64 %0, %0, %" #i "\n\tv_add_f64 %0, %0, %" #j "\n\t"
