@@ -404,6 +404,13 @@ __device__ __forceinline__ double chain_fixed(double s, const double *p, int m)
             k += G;
         }
     }
+    // the tail (and rows under 2 G): groups of 8 read together, then added
+    for (; k + 8 <= m; k += 8) {
+        double2 c[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) c[u] = *reinterpret_cast<const double2 *>(p + k + 2 * u);
+        s = chain_group<SUB, 8>(s, c);
+    }
     for (; k < m; ++k) s = SUB ? s - p[k] : s + p[k];
     return s;
 }
