@@ -456,7 +456,8 @@ __global__ __launch_bounds__(kSeqBlock) void k_cg_restore(int n, double *__restr
 // is bounded (spin polls; past the limit the stall word is set and every workgroup leaves).
 #define CGP_RLX __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT
 constexpr int kCgpWaves = kSeqBlock / 64;
-constexpr int kCgpSpin = 1 << 20;    // polls before a waiting wave gives up (~1 s with the back-off)
+constexpr int kCgpSpin = 1 << 20;    // polls before a waiting wave gives up (~1 s with the back-off);
+                                     // SSS_HIP_CG_SPIN: another limit (test hook; negative: every wait fails)
 constexpr int kCgpTraceIts = 256, kCgpTraceK = 10;
 constexpr int kCgpSimds = 4;         // SIMDs per CU: a worker's 16 waves, four on each
 
@@ -465,22 +466,6 @@ __device__ __forceinline__ void cgp_put(unsigned long long *g, unsigned tag, dou
     const unsigned long long u = (unsigned long long)__double_as_longlong(v);
     __hip_atomic_store(g, ((unsigned long long)tag << 32) | (u & 0xffffffffull), CGP_RLX);
     __hip_atomic_store(g + 1, ((unsigned long long)tag << 32) | (u >> 32), CGP_RLX);
-}
-// the granule's value once both halves carry `tag` (bounded wait; 0.0 and the stall word set past it)
-__device__ __forceinline__ double cgp_wait(const unsigned long long *g, unsigned tag, unsigned long long *err)
-{
-    for (int s = 0;; ++s) {
-        const unsigned long long a = __hip_atomic_load(const_cast<unsigned long long *>(g), CGP_RLX);
-        const unsigned long long c = __hip_atomic_load(const_cast<unsigned long long *>(g + 1), CGP_RLX);
-        if ((unsigned)(a >> 32) == tag && (unsigned)(c >> 32) == tag)
-            return __longlong_as_double((long long)((c << 32) | (a & 0xffffffffull)));
-        if (s >= kCgpSpin || ((s & 63) == 63 && __hip_atomic_load(err, CGP_RLX))) {
-            __hip_atomic_store(err, 1ull, CGP_RLX);
-            return 0.0;
-        }
-        if (s < 32) __builtin_amdgcn_s_sleep(1);
-        else __builtin_amdgcn_s_sleep(4);
-    }
 }
 // s + p[0] + ... + p[m-1] in order (chain_pipe16's additions, 8 products read ahead instead of 16: the
 // step workgroup of k_cg_persist keeps its vectors in registers around its chains)
@@ -517,7 +502,7 @@ __device__ __forceinline__ double chain_pipe8(double s, const double *p, int m)
 // out[j] = 0.0 past n
 template <int N>
 __device__ __forceinline__ void cgp_wait_n(const unsigned long long *base, int i0, int stride, int n, unsigned tag,
-                                           unsigned long long *err, double (&out)[N])
+                                           int spin, unsigned long long *err, double (&out)[N])
 {
     bool done[N];
 #pragma unroll
@@ -541,8 +526,8 @@ __device__ __forceinline__ void cgp_wait_n(const unsigned long long *base, int i
                 all = false;
             }
         }
-        if (all) return;
-        if (s >= kCgpSpin || ((s & 63) == 63 && __hip_atomic_load(err, CGP_RLX))) {
+        if (all && spin >= 0) return;
+        if (s >= spin || ((s & 63) == 63 && __hip_atomic_load(err, CGP_RLX))) {
             __hip_atomic_store(err, 1ull, CGP_RLX);
             return;
         }
@@ -647,7 +632,7 @@ __global__ __launch_bounds__(kSeqBlock) void k_cg_persist(int n, int maxit, cons
                                                           unsigned long long *gpp, unsigned long long *gpt,
                                                           unsigned long long *ctl, unsigned epoch,
                                                           const int *__restrict__ wl_ptr, const int *__restrict__ wl_rows,
-                                                          double *tw, unsigned long long *trc)
+                                                          double *tw, int spin, unsigned long long *trc)
 {
     // diagnostics (SSS_HIP_CG_TRACE): 100 MHz timestamps, plain stores -- workgroup 0's phases of
     // iterations k < kCgpTraceIts (trc[16 k + j]), and for SpMV kCgpTraceK each worker's command / p
@@ -692,8 +677,8 @@ __global__ __launch_bounds__(kSeqBlock) void k_cg_persist(int n, int maxit, cons
                 unsigned long long c = 0;
                 for (int s = 0;; ++s) {
                     c = __hip_atomic_load(cmd_of(seq), CGP_RLX);
-                    if ((unsigned)(c >> 32) == tag) break;
-                    if (s >= kCgpSpin || ((s & 63) == 63 && __hip_atomic_load(err, CGP_RLX))) {
+                    if ((unsigned)(c >> 32) == tag && spin >= 0) break;
+                    if (s >= spin || ((s & 63) == 63 && __hip_atomic_load(err, CGP_RLX))) {
                         __hip_atomic_store(err, 1ull, CGP_RLX);
                         c = ((unsigned long long)tag << 32) | 1ull;
                         break;
@@ -711,7 +696,7 @@ __global__ __launch_bounds__(kSeqBlock) void k_cg_persist(int n, int maxit, cons
             if (tr && tid == 0) trc_w[4 * blockIdx.x] = wall_clock64();
             {
                 double pw[kRegVec];
-                cgp_wait_n<kRegVec>(gpp + (seq & 1) * pbuf, tid, kSeqBlock, n, tag, err, pw);
+                cgp_wait_n<kRegVec>(gpp + (seq & 1) * pbuf, tid, kSeqBlock, n, tag, spin, err, pw);
 #pragma unroll
                 for (int q = 0; q < kRegVec; ++q)
                     if (tid + q * kSeqBlock < n) pl[tid + q * kSeqBlock] = pw[q];
@@ -793,7 +778,7 @@ __global__ __launch_bounds__(kSeqBlock) void k_cg_persist(int n, int maxit, cons
         asm volatile("" : "+v"(tid_k));
         spec_out = false;   // the command at `seq` is this iteration's SpMV; none past it yet
         if (tid == 0) ts0(k, 0);
-        cgp_wait_n<kRegVec>(gpt, tid_k, kSeqBlock, n, cgp_tag(epoch, seq), err, tv);
+        cgp_wait_n<kRegVec>(gpt, tid_k, kSeqBlock, n, cgp_tag(epoch, seq), spin, err, tv);
         if (tid == 0) ts0(k, 1);
         if (__hip_atomic_load(err, CGP_RLX)) break;
         if (!have_temp2) {   // -- (t_k, p_k) as k_cg_step_reg sums it
@@ -853,12 +838,14 @@ __global__ __launch_bounds__(kSeqBlock) void k_cg_persist(int n, int maxit, cons
                 if (spec_out) {
                     if (trc) ts0(k, 5);
                     double s = 0.0;
+                    bool gone = false;   // past a stall every later chunk is summed without waiting
                     for (int c = 0; c < ntp; ++c) {
-                        for (int sp = 0; __hip_atomic_load(&s_rdy[c], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) <= rounds;
+                        for (int sp = 0; !gone && __hip_atomic_load(&s_rdy[c], __ATOMIC_RELAXED,
+                                                                    __HIP_MEMORY_SCOPE_WORKGROUP) <= rounds;
                              ++sp) {
-                            if (sp >= kCgpSpin) {
+                            if (sp >= spin || ((sp & 63) == 63 && __hip_atomic_load(err, CGP_RLX))) {
                                 __hip_atomic_store(err, 1ull, CGP_RLX);
-                                break;
+                                gone = true;
                             }
                             __builtin_amdgcn_s_sleep(1);
                         }
@@ -873,7 +860,7 @@ __global__ __launch_bounds__(kSeqBlock) void k_cg_persist(int n, int maxit, cons
         } else if (spec_out) {   // waves 4-15: chunks wave - 4, + 12, ... of t_{k+1} (in the chain's order)
             for (int c = wave - 4; c < ntp; c += kTpPollers) {
                 double tt[kTpChunk / 64];
-                cgp_wait_n<kTpChunk / 64>(gpt, c * kTpChunk + lane, 64, n, cgp_tag(epoch, seq + 1), err, tt);
+                cgp_wait_n<kTpChunk / 64>(gpt, c * kTpChunk + lane, 64, n, cgp_tag(epoch, seq + 1), spin, err, tt);
 #pragma unroll
                 for (int q = 0; q < kTpChunk / 64; ++q) {
                     const int i = c * kTpChunk + lane + 64 * q;
@@ -1207,6 +1194,8 @@ static int run_cg(CoarseKrylov *k, const DevCSR &A, const double *b, double *u, 
     // the whole loop in one launch (k_cg_persist); SSS_HIP_CG_PERSIST=0: two kernels per iteration (test hook)
     const char *cp = getenv("SSS_HIP_CG_PERSIST");
     const bool persist = reg_step && k->persist_grid > 0 && !(cp && cp[0] == '0');
+    int spin = kCgpSpin;
+    if (const char *e = getenv("SSS_HIP_CG_SPIN")) spin = atoi(e);
     unsigned long long *trc = nullptr;   // SSS_HIP_CG_TRACE=1: phase timestamps of the first launch (diagnostics)
     static bool traced = false;
     const char *ct = getenv("SSS_HIP_CG_TRACE");
@@ -1226,7 +1215,7 @@ static int run_cg(CoarseKrylov *k, const DevCSR &A, const double *b, double *u, 
         if (k->epoch == 0) k->epoch = 1;        // (tag 0 is the zeroed granules')
         SSS_HIP(hipMemsetAsync(k->pctl + 64, 0, sizeof(unsigned long long), s));
         hipLaunchKernelGGL(k_cg_persist, dim3(k->persist_grid), dim3(kSeqBlock), 0, s, n, maxit, A.rp, A.ci, A.v, b,
-                           k->cap, u, k->r, k->p, k->u_best, k->st, k->gp_p, k->gp_t, k->pctl, k->epoch, k->wl_ptr, k->wl_rows, k->tw, trc);
+                           k->cap, u, k->r, k->p, k->u_best, k->st, k->gp_p, k->gp_t, k->pctl, k->epoch, k->wl_ptr, k->wl_rows, k->tw, spin, trc);
         SSS_HIP(hipGetLastError());
         if (trc) cg_trace_report(trc, n, k->persist_grid, A.rp, s);
         SSS_HIP(hipMemcpyAsync(k->h_buf + 8, k->pctl + 64, sizeof(unsigned long long), hipMemcpyDeviceToHost, s));

@@ -359,6 +359,25 @@ def test_coarse_krylov_row_cap(bus_h, cap, step, monkeypatch):
     assert np.array_equal(xg.view(np.uint64), xr.view(np.uint64))
 
 
+def test_coarse_krylov_persist_stall_is_reported(bus_h, monkeypatch):
+    """A stalled one-launch CG (SSS_HIP_CG_SPIN=-1: every bounded wait gives up at once) leaves the
+    launch -- every workgroup reaches its exit -- and the coarse solve reports the error instead of
+    returning the garbage iterate; the next launch (fresh tags, stall word cleared) solves bitwise."""
+    _cg_form(monkeypatch, "persist")
+    Lc = bus_h.level(bus_h.num_levels - 1)
+    n = Lc.A.num_rows
+    b = np.random.default_rng(21).standard_normal(n)
+    xg, xr = np.zeros(n), np.zeros(n)
+    monkeypatch.setenv("SSS_HIP_CG_SPIN", "-1")
+    assert _lib().sss_hip_host_coarse_solve(C.byref(Lc.A), C.byref(vec(b)), C.byref(vec(xg)), 1e-7, 0, 0) != 0
+    monkeypatch.delenv("SSS_HIP_CG_SPIN")
+    xg[:] = 0.0
+    assert _lib().sss_hip_host_coarse_solve(C.byref(Lc.A), C.byref(vec(b)), C.byref(vec(xg)), 1e-7, 0, 0) == 0
+    oracle.load().ora_coarest_solve(C.byref(Lc.A), C.byref(vec(b)), C.byref(vec(xr)), 1e-7,
+                                    C.byref(oracle.opts()))
+    assert np.array_equal(xg.view(np.uint64), xr.view(np.uint64))
+
+
 def test_coarse_direct_solves(p32_h):
     Lc = p32_h.level(p32_h.num_levels - 1)
     n = Lc.A.num_rows
