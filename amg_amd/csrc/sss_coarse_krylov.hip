@@ -839,7 +839,7 @@ __global__ __launch_bounds__(kSeqBlock) void k_cg_persist(int n, int maxit, cons
                     if (trc) ts0(k, 5);
                     double s = 0.0;
                     bool gone = false;   // past a stall every later chunk is summed without waiting
-                    for (int c = 0; c < ntp; ++c) {
+                    for (int c = 0; c < ntp;) {
                         for (int sp = 0; !gone && __hip_atomic_load(&s_rdy[c], __ATOMIC_RELAXED,
                                                                     __HIP_MEMORY_SCOPE_WORKGROUP) <= rounds;
                              ++sp) {
@@ -849,9 +849,16 @@ __global__ __launch_bounds__(kSeqBlock) void k_cg_persist(int n, int maxit, cons
                             }
                             __builtin_amdgcn_s_sleep(1);
                         }
+                        // and every chunk after it that is ready already: one chain over the run
+                        int ce = c + 1;
+                        while (ce < ntp && (gone || __hip_atomic_load(&s_rdy[ce], __ATOMIC_RELAXED,
+                                                                      __HIP_MEMORY_SCOPE_WORKGROUP) > rounds))
+                            ++ce;
                         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
                         if (c == 0 && trc) ts0(k, 6);
-                        s = chain_fixed<false, 8>(s, tp + c * kTpChunk, min(kTpChunk, n - c * kTpChunk));
+                        if (trc && k < kCgpTraceIts) ts0(k, 8), trc[16 * k + 9] = min(ce * kTpChunk, n) - c * kTpChunk;
+                        s = chain_fixed<false, 16>(s, tp + c * kTpChunk, min(ce * kTpChunk, n) - c * kTpChunk);
+                        c = ce;
                     }
                     s_temp2 = s;
                     if (trc) ts0(k, 7);
@@ -1143,6 +1150,15 @@ static void cg_trace_report(unsigned long long *trc, int n, int grid, const int 
     std::fprintf(stderr, "[cg trace] %d iterations, us from the iteration's start:", cnt);
     for (int j = 0; j < 13; ++j)
         if (nm[j][0]) std::fprintf(stderr, " %s %.2f", nm[j], cnt ? acc[j] / cnt : 0.0);
+    {   // the last run of ready chunks the t.p chain summed in one call: its length and rate
+        double len = 0, us = 0;
+        int m = 0;
+        for (int k = 2; k + 1 < kCgpTraceIts; ++k)
+            if (h[16 * k + 8] && h[16 * k + 7] > h[16 * k + 8])
+                len += (double)h[16 * k + 9], us += (double)(h[16 * k + 7] - h[16 * k + 8]) * 0.01, ++m;
+        if (m) std::fprintf(stderr, " | last chain run: %.0f entries in %.2f us (%.2f ns per entry)", len / m, us / m,
+                            len > 0 ? us * 1e3 / len : 0.0);
+    }
     std::fprintf(stderr, "\n");
     // SpMV kCgpTraceK, from its (speculative) publish in iteration kCgpTraceK - 1
     const long long P = (long long)h[16 * (kCgpTraceK - 1) + 3];
