@@ -443,9 +443,11 @@ __global__ __launch_bounds__(kSeqBlock) void k_cg_restore(int n, double *__restr
 // and added to t_{k-1} as k_acc does.  A row's sum is one dependent chain of adds issued by one lane,
 // so what bounds the SpMV is the chain work each SIMD issues: the host deals the rows to the waves
 // longest first onto the least-loaded SIMD (cg_persist_plan; the coarsest level of 7-pt 400^3 has
-// rows of 2 to 2,907 entries, 767 on average), and each wave works through its list.  The two sides hand over through {tag, half} granules (8-byte agent-scope
-// atomics, the 8 XCD L2s are not coherent): p_k from workgroup 0 (all rows; two buffers by command
-// parity), t_k from the wave that owns the row.  A command (tag, k, exit) in a ring of four words
+// rows of 2 to 2,907 entries, 767 on average), and each wave works through its list.  The two sides
+// hand over through {tag, half} granules (8-byte agent-scope atomics, the 8 XCD L2s are not
+// coherent): p_k from workgroup 0 (all rows; two buffers by command parity), t_k from the wave that
+// owns the row; workgroup 0's waves 4-15 collect t chunk by chunk and wave 3 sums t.p over each run
+// of ready chunks as it arrives.  A command (tag, k, exit) in a ring of four words
 // starts each SpMV: a word is rewritten only after every worker has answered the command two back.
 //   Speculation: with beta == 1, p_{k+1} = 1.0 r + 1.0 p_k is known as soon as alpha has updated r --
 // before the step's three norm chains decide whether a residual check (rare) rewrites it.  Workgroup
