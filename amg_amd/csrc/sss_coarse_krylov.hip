@@ -1092,6 +1092,9 @@ static void cg_persist_plan(CoarseKrylov *k, const DevCSR &A)
     std::priority_queue<Bin, std::vector<Bin>, std::greater<Bin>> simds;
     for (int b = 0; b < workers * kCgpSimds; ++b) simds.push({0, b});
     constexpr int per = kCgpWaves / kCgpSimds;
+    // chaining waves per SIMD (SSS_HIP_CG_CHAINERS, 1..4): measured against each other at 400^3
+    int chainers = per;
+    if (const char *e = getenv("SSS_HIP_CG_CHAINERS")) chainers = std::max(1, std::min(per, atoi(e)));
     std::vector<long long> sload(nwaves, 0);
     std::vector<std::vector<int>> lists(nwaves);
     for (int r : order) {
@@ -1099,7 +1102,7 @@ static void cg_persist_plan(CoarseKrylov *k, const DevCSR &A)
         simds.pop();
         const int s0 = (b.second / kCgpSimds) * kCgpWaves + (b.second % kCgpSimds) * per;   // the SIMD's slots
         int best = s0;
-        for (int q = s0 + 1; q < s0 + per; ++q)
+        for (int q = s0 + 1; q < s0 + chainers; ++q)
             if (sload[q] < sload[best]) best = q;
         sload[best] += cost(r);
         lists[best].push_back(r);
