@@ -1034,6 +1034,7 @@ int gs_fused_build(GsFused &f, const SSS_MAT &A, const DevCSR *dA, const PassSch
     // profiles/r05_gs_fused/: levels 5 / 6 / 8 31.3 / 60.8 / 128.1 ms with the former minimum of 32
     // waves, 28.9 / 56.1 / 120.6 with 1,024; 2,048 slower everywhere)
     int waves = (int)std::min<double>(1024.0, std::max(f.overlap ? 1024.0 : 512.0, 4.0 * per_depth));
+    if (const char *e = getenv("SSS_HIP_FUSED_WAVES")) waves = std::max(4, atoi(e));   // lab hook
     waves = std::min(waves, std::min(f.nchunks, cus * 8));
     f.grid = std::max(1, std::min((waves + 3) / 4, resident));
     f.engine = 1;
